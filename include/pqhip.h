@@ -1,0 +1,290 @@
+/*
+ * pqhip.h — C-ABI of libpqhip, the MI355X-native Parquet column-chunk page decoder.
+ *
+ * This is the drop-in boundary for ONE hot path of github.com/fraugster/parquet-go
+ * (mounted at /root/reference): decoding the pages of a column chunk.  The reference
+ * decodes a page through the package-internal seam
+ *
+ *     pageReader{ init(dDecoder, rDecoder, values); read(r, ph, codec, crc); readValues(size); numValues() }
+ *                                                     (reference interfaces.go:11-18)
+ *     valuesDecoder{ init(io.Reader); decodeValues([]interface{}) (int, error) }   (interfaces.go:29-33)
+ *     levelDecoder{ next() (int32, error); init/initSize(io.Reader); maxLevel() }   (hybrid_decoder.go:16-27)
+ *
+ * and builds those readers in FileReader.readChunk/readPages (chunk_reader.go:182-362).  A cgo
+ * shim binds the functions below in place of that seam:
+ *
+ *   - pqh_file_*        replace readChunk/readPages + readPageBlock/newBlockReader (host side:
+ *                       thrift page headers, CRC, GZIP/SNAPPY decompression) and emit a page table;
+ *   - pqh_batch_*       replace pageReader.read + readValues(numValues) for every page of a set of
+ *                       column chunks: all hybrid RLE/bit-packed streams, DELTA_BINARY_PACKED,
+ *                       dictionary gathers, PLAIN values and level decoding run as HIP kernels on
+ *                       HBM-resident page images, one launch per kernel kind for the whole batch.
+ *
+ * Conventions: every function returns a pqh_status (0 = PQH_OK) unless stated otherwise, never
+ * aborts, and stores a message retrievable with pqh_last_error / pqh_file_error.  No torch types,
+ * plain pointers and sizes only.  Device pointers are HIP device pointers of the context's device.
+ */
+#ifndef PQHIP_H
+#define PQHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQH_ABI_VERSION 1
+
+/* Bytes of readable slack the device payload buffer must have after its last page image.  The
+ * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
+#define PQH_PAYLOAD_PAD 256
+
+/* parquet.Type (reference parquet/parquet.thrift:32-41) */
+enum pqh_physical_type {
+  PQH_BOOLEAN = 0,
+  PQH_INT32 = 1,
+  PQH_INT64 = 2,
+  PQH_INT96 = 3,
+  PQH_FLOAT = 4,
+  PQH_DOUBLE = 5,
+  PQH_BYTE_ARRAY = 6,
+  PQH_FIXED_LEN_BYTE_ARRAY = 7
+};
+
+/* parquet.Encoding (parquet.thrift:414-470) */
+enum pqh_encoding {
+  PQH_ENC_PLAIN = 0,
+  PQH_ENC_PLAIN_DICTIONARY = 2,
+  PQH_ENC_RLE = 3,
+  PQH_ENC_BIT_PACKED = 4,
+  PQH_ENC_DELTA_BINARY_PACKED = 5,
+  PQH_ENC_DELTA_LENGTH_BYTE_ARRAY = 6,
+  PQH_ENC_DELTA_BYTE_ARRAY = 7,
+  PQH_ENC_RLE_DICTIONARY = 8,
+  PQH_ENC_BYTE_STREAM_SPLIT = 9
+};
+
+/* parquet.PageType (parquet.thrift:498-507) */
+enum pqh_page_type {
+  PQH_DATA_PAGE = 0,
+  PQH_INDEX_PAGE = 1,
+  PQH_DICTIONARY_PAGE = 2,
+  PQH_DATA_PAGE_V2 = 3
+};
+
+/* parquet.CompressionCodec (parquet.thrift:487-496) */
+enum pqh_codec {
+  PQH_CODEC_UNCOMPRESSED = 0,
+  PQH_CODEC_SNAPPY = 1,
+  PQH_CODEC_GZIP = 2,
+  PQH_CODEC_ZSTD = 6
+};
+
+/* Status codes.  Each data-path code names the reference error it stands for. */
+typedef enum pqh_status {
+  PQH_OK = 0,
+  PQH_ERR_EOF = 1,                    /* io.EOF before a needed value (hybrid_decoder.go:142-147, ...) */
+  PQH_ERR_UNEXPECTED_EOF = 2,         /* io.ErrUnexpectedEOF: short fixed-size read (binary.Read, ReadFull) */
+  PQH_ERR_VARINT_OVERFLOW = 3,        /* encoding/binary: varint overflows a 64-bit integer */
+  PQH_ERR_INT32_RANGE = 4,            /* "int32 out of range" (helpers.go:162-164, 181-183) */
+  PQH_ERR_EMPTY_BP_RUN = 5,           /* "rle: empty bit-packed run" (hybrid_decoder.go:151-155) */
+  PQH_ERR_EMPTY_RLE_RUN = 6,          /* "rle: empty RLE run" (hybrid_decoder.go:158-161) */
+  PQH_ERR_RLE_VALUE_TOO_LARGE = 7,    /* "rle: RLE run value is too large" (hybrid_decoder.go:126-128) */
+  PQH_ERR_READER_NOT_INITIALIZED = 8, /* "reader is not initialized" (hybrid_decoder.go:86-88) */
+  PQH_ERR_DICT_BIT_WIDTH = 9,         /* "invalid bitwidth" (type_dict.go:28-30) */
+  PQH_ERR_DICT_INDEX = 10,            /* "dict: invalid index" (type_dict.go:52-54) */
+  PQH_ERR_DELTA_BLOCK_SIZE = 11,      /* "invalid block size" (deltabp_decoder.go:56-58) */
+  PQH_ERR_DELTA_MINIBLOCKS = 12,      /* "invalid number of mini blocks" / zero miniblock values (:64-71) */
+  PQH_ERR_DELTA_VALUE_COUNT = 13,     /* "invalid total value count" (:77-79) */
+  PQH_ERR_DELTA_BIT_WIDTH = 14,       /* "invalid miniblock bit width" (:100-104) */
+  PQH_ERR_DELTA_STREAM = 15,          /* "invalid stream" / negative remaining (:151-154) */
+  PQH_ERR_NEGATIVE_LENGTH = 16,       /* "bytearray/plain: len is negative" (type_bytearray.go:30-34) */
+  PQH_ERR_NEGATIVE_DLBA_LENGTH = 17,  /* negative DELTA_LENGTH length: a runtime panic in the reference */
+  PQH_ERR_DBA_PREFIX = 18,            /* "invalid prefix len in the stream" (type_bytearray.go:223-226) */
+  PQH_ERR_DBA_COUNT = 19,             /* "different number of suffixes and prefixes" (type_bytearray.go:206-208) */
+  PQH_ERR_INT96_SHORT = 20,           /* "not enough byte to read Int96" (type_int96.go:34-36) */
+  PQH_ERR_UNSUPPORTED = 21,           /* getValuesDecoder: unsupported (type, encoding) (chunk_reader.go:106-159) */
+  PQH_ERR_PAGE_HEADER = 22,           /* negative NumValues / sizes, missing sub-header (page_v1.go:88-94 ...) */
+  PQH_ERR_DECOMPRESS = 23,            /* decompression failed or size mismatch (compress.go:131-152) */
+  PQH_ERR_CRC = 24,                   /* "CRC32 check failed" (chunk_reader.go:173-177) */
+  PQH_ERR_THRIFT = 25,                /* malformed thrift compact structure */
+  PQH_ERR_IO = 26,                    /* file I/O */
+  PQH_ERR_ARG = 27,                   /* invalid argument to this API */
+  PQH_ERR_HIP = 28,                   /* HIP runtime failure */
+  PQH_ERR_NOMEM = 29,                 /* allocation failure */
+  PQH_ERR_SCHEMA = 30,                /* schema / column metadata inconsistency (chunk_reader.go:303-312) */
+  PQH_ERR_DICT_PAGE = 31,             /* second dictionary page / dictionary encoding not PLAIN (chunk_reader.go:197-199, page_dict.go:44-46) */
+  PQH_ERR_NO_DEVICE = 32              /* no HIP device present */
+} pqh_status;
+
+/* Decode phases, in the order the reference runs them for one page (page_v1.go:33-122). */
+enum pqh_phase {
+  PQH_PHASE_LOAD = 0,   /* pageReader.read: level initSize, values decoder init      */
+  PQH_PHASE_REP = 1,    /* readValues: repetition levels (decodePackedArray)          */
+  PQH_PHASE_DEF = 2,    /* readValues: definition levels + not-null count             */
+  PQH_PHASE_VALUES = 3  /* readValues: valuesDecoder.decodeValues(notNull)            */
+};
+
+/* ---------------------------------------------------------------------------------------------
+ * Batch decode (device).  Replaces pageReader.read + readValues(numValues) (page_v1.go:33-122,
+ * page_v2.go:31-131, page_dict.go:35-72) for every page of a set of column chunks.
+ * ------------------------------------------------------------------------------------------- */
+
+typedef struct pqh_column {
+  int32_t physical_type; /* enum pqh_physical_type */
+  int32_t type_length;   /* FIXED_LEN_BYTE_ARRAY length (SchemaElement.type_length) */
+  int32_t max_def;       /* Column.MaxDefinitionLevel() (schema.go:904-914) */
+  int32_t max_rep;       /* Column.MaxRepetitionLevel() */
+} pqh_column;
+
+/* One page as the reference page walker sees it (parquet.PageHeader fields + the decompressed
+ * page image).  For DATA_PAGE and DICTIONARY_PAGE the image is the decompressed block; for
+ * DATA_PAGE_V2 it is the raw level bytes followed by the decompressed values section
+ * (page_v2.go:113-125: the values section is always passed through the chunk codec). */
+typedef struct pqh_page {
+  int64_t image_offset;           /* byte offset of the page image in the payload buffer */
+  int32_t image_len;              /* bytes in the image */
+  int32_t page_type;              /* PQH_DATA_PAGE, PQH_DATA_PAGE_V2 or PQH_DICTIONARY_PAGE */
+  int32_t num_values;             /* DataPageHeader(V2).num_values / DictionaryPageHeader.num_values */
+  int32_t encoding;               /* values encoding from the header */
+  int32_t def_levels_byte_length; /* DataPageHeaderV2 only (else 0) */
+  int32_t rep_levels_byte_length; /* DataPageHeaderV2 only (else 0) */
+  int32_t chunk;                  /* index of the owning pqh_chunk */
+  int32_t reserved;
+} pqh_page;
+
+/* A column chunk: a contiguous range of pages; a dictionary page, if any, comes first
+ * (chunk_reader.go:195-227). */
+typedef struct pqh_chunk {
+  pqh_column column;
+  int32_t first_page;  /* index into the page array */
+  int32_t num_pages;   /* including the dictionary page */
+  int32_t host_status; /* page-walker error for this chunk (readPages failed), else PQH_OK */
+  int32_t reserved;
+} pqh_chunk;
+
+/* Device-resident result of one chunk, owned by the batch. */
+typedef struct pqh_chunk_out {
+  int64_t num_values;    /* level slots: Σ num_values of the data pages */
+  int64_t num_non_null;  /* Σ notNull (helpers.go:143-145): number of decoded values */
+  int32_t value_size;    /* bytes per value (bool: 1, INT96: 12, FLBA: type_length), 0 for BYTE_ARRAY */
+  int32_t status;        /* first error of the chunk in page order, or PQH_OK */
+  int32_t error_page;    /* page index (batch-global) of that error, or -1 */
+  int32_t error_phase;   /* enum pqh_phase of that error */
+  int64_t error_index;   /* value / level index of that error inside its page */
+  void* values;          /* dense not-null values, natural width, little endian (device) */
+  int64_t* offsets;      /* BYTE_ARRAY: num_non_null + 1 byte offsets into bytes (device), else NULL */
+  uint8_t* bytes;        /* BYTE_ARRAY data (device), else NULL */
+  int64_t num_bytes;     /* BYTE_ARRAY data size */
+  uint8_t* def_levels;   /* one byte per level slot, NULL when max_def == 0 (device) */
+  uint8_t* rep_levels;   /* one byte per level slot, NULL when max_rep == 0 (device) */
+} pqh_chunk_out;
+
+/* Per-page result (host copy). */
+typedef struct pqh_page_result {
+  int32_t status;       /* pqh_status of the page's first error, PQH_OK if none */
+  int32_t phase;        /* enum pqh_phase of that error */
+  int64_t index;        /* index at which it happened (level slot, value, or load sub-step) */
+  int32_t num_non_null; /* notNull of the page */
+  int32_t reserved;
+  int64_t value_offset; /* first value of this page in pqh_chunk_out.values */
+  int64_t level_offset; /* first level slot of this page in pqh_chunk_out.{def,rep}_levels */
+} pqh_page_result;
+
+typedef struct pqh_kernel_stat {
+  char name[32];
+  int32_t launches;     /* launches timed */
+  int32_t work_items;   /* tiles / pages per launch */
+  double total_ms;      /* summed HIP-event time */
+  double bytes_read;    /* algorithmic bytes read per launch */
+  double bytes_written; /* algorithmic bytes written per launch */
+} pqh_kernel_stat;
+
+typedef struct pqh_ctx pqh_ctx;
+typedef struct pqh_batch pqh_batch;
+
+#define PQH_CTX_PROFILE 1u /* time every kernel launch with HIP events */
+
+int pqh_abi_version(void);
+int pqh_device_count(int32_t* count);
+int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out);
+void pqh_ctx_destroy(pqh_ctx* ctx);
+const char* pqh_last_error(const pqh_ctx* ctx);
+/* The HIP stream all kernels of this context are enqueued on (a hipStream_t). */
+void* pqh_ctx_stream(pqh_ctx* ctx);
+
+int pqh_malloc(pqh_ctx* ctx, void** dptr, size_t bytes);
+int pqh_free(pqh_ctx* ctx, void* dptr);
+int pqh_host_alloc(pqh_ctx* ctx, void** hptr, size_t bytes); /* pinned */
+int pqh_host_free(pqh_ctx* ctx, void* hptr);
+int pqh_memcpy_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes); /* async, ctx stream */
+int pqh_memcpy_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes); /* async, ctx stream */
+int pqh_sync(pqh_ctx* ctx);
+
+/* Plan a batch: copies the page/chunk tables, sizes and allocates scratch and outputs.
+ * d_payload must stay valid and unchanged until the batch is destroyed and must have
+ * PQH_PAYLOAD_PAD readable bytes after payload_bytes. */
+int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks,
+                     const pqh_page* pages, int32_t num_pages, const void* d_payload,
+                     int64_t payload_bytes, pqh_batch** out);
+/* Enqueue the whole decode on the context stream (asynchronous; may be re-run). */
+int pqh_batch_run(pqh_batch* batch);
+/* Wait for the last run and copy back per-page results. */
+int pqh_batch_sync(pqh_batch* batch);
+int pqh_batch_chunk_out(const pqh_batch* batch, int32_t chunk, pqh_chunk_out* out);
+int pqh_batch_page_results(const pqh_batch* batch, pqh_page_result* out, int32_t num_pages);
+/* Kernel timing accumulated since the last reset (requires PQH_CTX_PROFILE). */
+int pqh_batch_kernel_stats(const pqh_batch* batch, pqh_kernel_stat* out, int32_t max_stats,
+                           int32_t* num_stats);
+int pqh_batch_reset_stats(pqh_batch* batch);
+/* Algorithmic bytes of one run: payload bytes read once, dictionary bytes once per chunk, and
+ * decoded bytes written (values, levels, offsets, byte data). */
+int pqh_batch_traffic(const pqh_batch* batch, double* bytes_read, double* bytes_written);
+void pqh_batch_destroy(pqh_batch* batch);
+
+/* ---------------------------------------------------------------------------------------------
+ * Host side: file footer, page walker, decompression.  Replaces NewFileReader's footer read
+ * (file_meta.go:18-73), readChunk/readPages (chunk_reader.go:182-362) and readPageBlock /
+ * newBlockReader (chunk_reader.go:161-180, compress.go:131-152).  No GPU needed.
+ * ------------------------------------------------------------------------------------------- */
+
+typedef struct pqh_file pqh_file;
+typedef struct pqh_host_batch pqh_host_batch;
+
+int pqh_file_open(const char* path, pqh_file** out);
+/* Reads from memory; the caller keeps data alive until pqh_file_close. */
+int pqh_file_open_memory(const void* data, int64_t len, pqh_file** out);
+void pqh_file_close(pqh_file* f);
+const char* pqh_file_error(const pqh_file* f);
+int32_t pqh_file_num_row_groups(const pqh_file* f);
+int64_t pqh_file_num_rows(const pqh_file* f);
+int64_t pqh_file_row_group_num_rows(const pqh_file* f, int32_t row_group);
+int32_t pqh_file_num_columns(const pqh_file* f);
+/* Leaf column metadata; path is the dot-joined schema path (Column.FlatName). */
+int pqh_file_column(const pqh_file* f, int32_t column, pqh_column* out, char* path,
+                    int32_t path_capacity);
+
+/* Walk and decompress the pages of the given leaf columns for row groups [rg_begin, rg_end),
+ * producing a page table and one payload of page images (8-byte aligned images). */
+int pqh_file_load(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns,
+                  int32_t num_columns, int32_t validate_crc, pqh_host_batch** out);
+int32_t pqh_host_batch_num_chunks(const pqh_host_batch* hb);
+int32_t pqh_host_batch_num_pages(const pqh_host_batch* hb);
+const pqh_chunk* pqh_host_batch_chunks(const pqh_host_batch* hb);
+const pqh_page* pqh_host_batch_pages(const pqh_host_batch* hb);
+const uint8_t* pqh_host_batch_payload(const pqh_host_batch* hb);
+int64_t pqh_host_batch_payload_bytes(const pqh_host_batch* hb);
+/* Host time spent in decompression / thrift parsing during pqh_file_load (seconds). */
+double pqh_host_batch_decompress_seconds(const pqh_host_batch* hb);
+void pqh_host_batch_free(pqh_host_batch* hb);
+
+/* Upload a host batch (pinned staging, async H2D on the context stream) and plan it.  The
+ * returned batch owns the device copy of the payload. */
+int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PQHIP_H */

@@ -1,0 +1,87 @@
+"""In-tree build of the native libraries (no JIT cache: the .so files travel with the repo).
+
+  libpqhip.so  — product: HIP kernels for gfx950 + host page walker + C-ABI (include/pqhip.h)
+  libpqgen.so  — tooling: reference-writer-shaped file generator (csrc/tools/pqgen.h)
+
+Usage:  python parquet-go_amd/build.py [--force]
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+INCLUDE = os.path.join(ROOT, "include")
+
+HOST_SRCS = ["host/codec.cpp", "host/file_reader.cpp"]
+HIP_SRCS = ["kernels/decode.hip", "host/batch.hip"]
+GEN_SRCS = ["tools/pqgen.cpp", "host/codec.cpp"]
+HEADERS = ["host/codec.h", "host/thrift_compact.h", "host/file_reader.h", "kernels/decode.h",
+           "tools/pqgen.h", "host/internal.h"]
+
+ARCH = os.environ.get("PQH_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    deps = [os.path.join(CSRC, s) for s in sources + HEADERS] + [os.path.join(INCLUDE, "pqhip.h")]
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError("build failed: " + " ".join(cmd[:3]) + " ...")
+    return r.stdout
+
+
+def build_gen(force=False):
+    out = os.path.join(LIBDIR, "libpqgen.so")
+    if force or _stale(out, GEN_SRCS):
+        os.makedirs(LIBDIR, exist_ok=True)
+        _run(["g++", "-O2", "-g", "-std=c++17", "-shared", "-fPIC", "-Wall", "-I", INCLUDE, "-o", out]
+             + [os.path.join(CSRC, s) for s in GEN_SRCS] + ["-lz", "-lpthread"])
+    return out
+
+
+def build_hip(force=False):
+    out = os.path.join(LIBDIR, "libpqhip.so")
+    if force or _stale(out, HOST_SRCS + HIP_SRCS):
+        os.makedirs(LIBDIR, exist_ok=True)
+        objs = []
+        bdir = os.path.join(PKG, "build")
+        os.makedirs(bdir, exist_ok=True)
+        for s in HIP_SRCS:
+            o = os.path.join(bdir, os.path.basename(s) + ".o")
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                  "-munsafe-fp-atomics", "-I", INCLUDE, "-c", os.path.join(CSRC, s), "-o", o])
+            objs.append(o)
+        for s in HOST_SRCS:
+            o = os.path.join(bdir, os.path.basename(s) + ".o")
+            _run(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-Wall", "-I", INCLUDE,
+                  "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-c", os.path.join(CSRC, s), "-o", o])
+            objs.append(o)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lz", "-lpthread"])
+    return out
+
+
+def build_all(force=False):
+    return build_gen(force), build_hip(force)
+
+
+if __name__ == "__main__":
+    for p in build_all(force="--force" in sys.argv):
+        print(p)

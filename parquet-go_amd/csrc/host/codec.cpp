@@ -1,0 +1,228 @@
+// codec.cpp — see codec.h.
+#include "codec.h"
+
+#include <zlib.h>
+
+#include <cstring>
+
+namespace pqhip {
+
+static bool read_uvarint(const uint8_t*& p, const uint8_t* end, uint64_t& v) {
+  v = 0;
+  for (int s = 0; s < 64 && p < end; s += 7) {
+    uint8_t b = *p++;
+    v |= uint64_t(b & 0x7f) << s;
+    if (b < 0x80) return true;
+  }
+  return false;
+}
+
+// Snappy block decoding (format of golang/snappy decode.go): uvarint length, then literal /
+// copy elements.  Every copy must reference already produced bytes and stay inside the length.
+bool snappy_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
+  const uint8_t* p = src;
+  const uint8_t* end = src + n;
+  uint64_t len;
+  if (!read_uvarint(p, end, len)) return false;
+  if (len > (uint64_t(1) << 32) - 1) return false;
+  dst.resize(size_t(len));
+  uint8_t* out = dst.data();
+  size_t d = 0;
+  while (p < end) {
+    uint8_t tag = *p++;
+    size_t length, offset;
+    switch (tag & 3) {
+      case 0: {
+        size_t x = tag >> 2;
+        if (x >= 60) {
+          int k = int(x) - 59;
+          if (end - p < k) return false;
+          x = 0;
+          for (int i = 0; i < k; i++) x |= size_t(p[i]) << (8 * i);
+          p += k;
+        }
+        length = x + 1;
+        if (size_t(end - p) < length || len - d < length) return false;
+        memcpy(out + d, p, length);
+        p += length;
+        d += length;
+        continue;
+      }
+      case 1:
+        if (end - p < 1) return false;
+        length = 4 + ((tag >> 2) & 7);
+        offset = (size_t(tag >> 5) << 8) | p[0];
+        p += 1;
+        break;
+      case 2:
+        if (end - p < 2) return false;
+        length = 1 + (tag >> 2);
+        offset = size_t(p[0]) | (size_t(p[1]) << 8);
+        p += 2;
+        break;
+      default:
+        if (end - p < 4) return false;
+        length = 1 + (tag >> 2);
+        offset = size_t(p[0]) | (size_t(p[1]) << 8) | (size_t(p[2]) << 16) | (size_t(p[3]) << 24);
+        p += 4;
+        break;
+    }
+    if (offset == 0 || offset > d || len - d < length) return false;
+    for (size_t i = 0; i < length; i++) out[d + i] = out[d + i - offset];  // overlap-safe forward copy
+    d += length;
+  }
+  return d == len;
+}
+
+static inline uint32_t load32(const uint8_t* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+static void emit_literal(std::vector<uint8_t>& o, const uint8_t* p, size_t n) {
+  if (n == 0) return;
+  size_t x = n - 1;
+  if (x < 60) {
+    o.push_back(uint8_t(x << 2));
+  } else {
+    int k = x < (1u << 8) ? 1 : x < (1u << 16) ? 2 : x < (1u << 24) ? 3 : 4;
+    o.push_back(uint8_t((59 + k) << 2));
+    for (int i = 0; i < k; i++) o.push_back(uint8_t(x >> (8 * i)));
+  }
+  o.insert(o.end(), p, p + n);
+}
+
+static void emit_copy(std::vector<uint8_t>& o, size_t offset, size_t len) {
+  while (len > 0) {
+    size_t l = len;
+    if (l > 64) l = (len - 64 < 4) ? 60 : 64;
+    o.push_back(uint8_t(((l - 1) << 2) | 2));
+    o.push_back(uint8_t(offset));
+    o.push_back(uint8_t(offset >> 8));
+    len -= l;
+  }
+}
+
+// Greedy single-probe hash matcher over 64 KiB fragments, emitting snappy block format.
+void snappy_compress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
+  dst.clear();
+  uint64_t v = n;
+  while (v >= 0x80) {
+    dst.push_back(uint8_t(v | 0x80));
+    v >>= 7;
+  }
+  dst.push_back(uint8_t(v));
+  std::vector<int32_t> table(1 << 14);
+  for (size_t start = 0; start < n; start += 65536) {
+    size_t end = start + 65536 < n ? start + 65536 : n;
+    std::fill(table.begin(), table.end(), -1);
+    size_t ip = start, lit = start;
+    while (ip + 4 <= end) {
+      uint32_t cur = load32(src + ip);
+      uint32_t h = (cur * 0x1e35a7bdu) >> 18;
+      int32_t cand = table[h];
+      table[h] = int32_t(ip - start);
+      if (cand >= 0 && load32(src + start + cand) == cur) {
+        size_t c = start + size_t(cand);
+        size_t len = 4;
+        while (ip + len < end && src[c + len] == src[ip + len]) len++;
+        emit_literal(dst, src + lit, ip - lit);
+        emit_copy(dst, ip - c, len);
+        ip += len;
+        lit = ip;
+      } else {
+        ip++;
+      }
+    }
+    emit_literal(dst, src + lit, end - lit);
+  }
+}
+
+bool gzip_decompress(const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst) {
+  dst.clear();
+  dst.resize(expected > 0 ? expected : 64);
+  size_t pos = 0;
+  const uint8_t* in = src;
+  size_t left = n;
+  bool any = false;
+  // Go's gzip.Reader is multistream: concatenated members decode as one stream.
+  while (left > 0) {
+    z_stream s;
+    memset(&s, 0, sizeof(s));
+    if (inflateInit2(&s, 16 + MAX_WBITS) != Z_OK) return false;
+    s.next_in = const_cast<Bytef*>(in);
+    s.avail_in = uInt(left);
+    int rc;
+    do {
+      if (pos == dst.size()) dst.resize(dst.size() * 2);
+      s.next_out = dst.data() + pos;
+      s.avail_out = uInt(dst.size() - pos);
+      rc = inflate(&s, Z_NO_FLUSH);
+      pos = dst.size() - s.avail_out;
+      if (rc != Z_OK && rc != Z_STREAM_END && !(rc == Z_BUF_ERROR && s.avail_out == 0)) {
+        inflateEnd(&s);
+        return false;
+      }
+    } while (rc != Z_STREAM_END);
+    size_t used = left - s.avail_in;
+    inflateEnd(&s);
+    in += used;
+    left -= used;
+    any = true;
+  }
+  if (!any) return false;
+  dst.resize(pos);
+  return true;
+}
+
+bool gzip_compress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
+  z_stream s;
+  memset(&s, 0, sizeof(s));
+  if (deflateInit2(&s, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 16 + MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+    return false;
+  dst.resize(deflateBound(&s, uLong(n)) + 32);
+  s.next_in = const_cast<Bytef*>(src);
+  s.avail_in = uInt(n);
+  s.next_out = dst.data();
+  s.avail_out = uInt(dst.size());
+  int rc = deflate(&s, Z_FINISH);
+  size_t out = dst.size() - s.avail_out;
+  deflateEnd(&s);
+  if (rc != Z_STREAM_END) return false;
+  dst.resize(out);
+  return true;
+}
+
+bool decompress_block(int codec, const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst) {
+  switch (codec) {
+    case 0:
+      dst.assign(src, src + n);
+      return true;
+    case 1:
+      return snappy_decompress(src, n, dst);
+    case 2:
+      return gzip_decompress(src, n, expected, dst);
+    default:
+      return false;
+  }
+}
+
+bool compress_block(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
+  switch (codec) {
+    case 0:
+      dst.assign(src, src + n);
+      return true;
+    case 1:
+      snappy_compress(src, n, dst);
+      return true;
+    case 2:
+      return gzip_compress(src, n, dst);
+    default:
+      return false;
+  }
+}
+
+uint32_t crc32_ieee(const uint8_t* p, size_t n) { return uint32_t(crc32(0L, p, uInt(n))); }
+
+}  // namespace pqhip
