@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded output GB/s of the HIP page decoder + HBM roofline fraction.
+
+A "step" is one full decode pass (every page of every chunk of the rank's row groups) over
+HBM-resident page images: k_prologue -> k_scan -> k_levels / k_copy / k_bool_plain / k_dict.
+Default workload = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16 row
+groups per GPU.  Multi-GPU: one process per GPU (torchrun), row groups sharded (each rank decodes
+its own 16 row groups, different seed), no data-path collective -> "scaling": "weak".
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3] [--rows R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "decoded output GB/s (per GPU and whole node) + fraction of HBM roofline"
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def package():
+    import __graft_entry__ as ge
+
+    return ge._package()
+
+
+def cpu_baseline(data, seconds):
+    """The oracle (plain-C restatement of the reference decoders, 1 core) on a bounded sample of
+    the same file: whole row groups until `seconds` of decode work (walk excluded)."""
+    from oracle import oracle as O
+
+    fr = O.FileReader(data)
+    ncols = len(fr.columns)
+    out_bytes = 0
+    spent = 0.0
+    rgs = 0
+    for rg in range(len(fr.row_groups)):
+        chunks = [fr.read_chunk(rg, ci) for ci in range(ncols)]
+        t0 = time.perf_counter()
+        for ch in chunks:
+            for r in O.decode_chunk(ch):
+                if r.status:
+                    raise RuntimeError(f"oracle failed on rg {rg}: status {r.status}")
+                out_bytes += len(r.values) + (0 if r.def_levels is None else len(r.def_levels)) + \
+                    (0 if r.rep_levels is None else len(r.rep_levels))
+        spent += time.perf_counter() - t0
+        rgs += 1
+        if spent >= seconds:
+            break
+    return {"value": round(out_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{rgs} of {len(fr.row_groups)} row groups ({out_bytes / 1e9:.3f} GB decoded) by oracle/refdecode.c "
+                      f"(C restatement of the reference Go decoders), single thread, {spent:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3"])
+    ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch = dist = None
+    try:
+        import torch  # noqa: F811
+        import torch.distributed as dist  # noqa: F811
+    except Exception:
+        torch = None
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    pkg = package()
+    from parquet_go_amd import datasets, native
+
+    desc, builder = datasets.WORKLOADS[args.workload]
+    kw = {}
+    if args.rows:
+        kw["rows"] = args.rows
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20}[args.workload] + 1000 * rank
+    t0 = time.perf_counter()
+    data = builder(seed=seed_kw, **kw)
+    gen_s = time.perf_counter() - t0
+    log(f"rank {rank}: generated {len(data) / 1e9:.2f} GB file in {gen_s:.1f}s")
+
+    ctx = native.Context(local, profile=True)
+    f = native.File(data)
+    ncols = len(f.columns())
+    t0 = time.perf_counter()
+    hb = f.load(0, f.num_row_groups, list(range(ncols)))
+    walk_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    batch = native.Batch.from_host(ctx, hb)
+    h2d_s = time.perf_counter() - t0
+    log(f"rank {rank}: walked {hb.num_pages} pages / {hb.num_chunks} chunks in {walk_s:.2f}s, "
+        f"payload {hb.payload_bytes / 1e9:.2f} GB uploaded in {h2d_s:.2f}s")
+
+    batch.run()
+    batch.sync()
+    for c in range(hb.num_chunks):
+        o = batch.chunk_out(c)
+        if o.status != native.OK:
+            raise RuntimeError(f"chunk {c} failed: {native.STATUS.get(o.status)} page {o.error_page}")
+    bytes_read, bytes_written = batch.traffic()
+    for _ in range(args.warmup):
+        batch.run()
+    batch.sync()
+    batch.reset_stats()
+
+    def barrier_sync():
+        if world > 1:
+            dist.barrier()
+        ctx.sync()
+        if torch is not None and torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([bytes_written], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        total_written = float(tot.item())
+    else:
+        total_written = bytes_written
+    batch.sync()
+    stats = batch.kernel_stats()
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_written * args.steps / elapsed / 1e9
+
+    kernels = {}
+    dom = None
+    for s in stats:
+        if s.launches == 0:
+            continue
+        avg_ms = s.total_ms / s.launches
+        algo = s.bytes_read + s.bytes_written
+        kernels[s.name.decode()] = {"avg_ms": round(avg_ms, 4), "launches": s.launches, "work_items": s.work_items,
+                                    "algo_bytes": algo,
+                                    "gbps": round(algo / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
+        if dom is None or s.total_ms > dom.total_ms:
+            dom = s
+    roof = None
+    if dom is not None:
+        avg_ms = dom.total_ms / dom.launches
+        ach = (dom.bytes_read + dom.bytes_written) / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom.name.decode(), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written}
+    all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            log("timing the CPU baseline (oracle) ...")
+            cpu = cpu_baseline(data, args.cpu_seconds)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/int64/f32/f64/bool/flba16 (bit-exact integer/byte decode)" if args.workload == "c2"
+            else "int32" if args.workload == "c1" else "int64",
+            "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
+            "config": {"workload": desc, "rows_per_gpu": f.num_rows, "row_groups_per_gpu": f.num_row_groups,
+                       "pages_per_gpu": hb.num_pages, "parallelism": f"row-group sharded x{world}, no collective",
+                       "mode": "HBM-resident"},
+            "per_gpu_gbps": round(bytes_written * args.steps / elapsed / 1e9, 2),
+            "algo_read_bytes_per_step": bytes_read,
+            "decoded_bytes_per_step": bytes_written,
+            "algo_gbps_all_kernels": round((bytes_read + bytes_written) / (all_ms * 1e-3) / 1e9, 1) if all_ms else None,
+            "roofline": roof,
+            "kernels": kernels,
+            "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 2),
+                     "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    batch.close()
+    hb.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

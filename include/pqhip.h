@@ -115,7 +115,8 @@ typedef enum pqh_status {
   PQH_ERR_NOMEM = 29,                 /* allocation failure */
   PQH_ERR_SCHEMA = 30,                /* schema / column metadata inconsistency (chunk_reader.go:303-312) */
   PQH_ERR_DICT_PAGE = 31,             /* second dictionary page / dictionary encoding not PLAIN (chunk_reader.go:197-199, page_dict.go:44-46) */
-  PQH_ERR_NO_DEVICE = 32              /* no HIP device present */
+  PQH_ERR_NO_DEVICE = 32,             /* no HIP device present */
+  PQH_ERR_NOT_IMPLEMENTED = 33        /* decoder kind not (yet) available on the device */
 } pqh_status;
 
 /* Decode phases, in the order the reference runs them for one page (page_v1.go:33-122). */

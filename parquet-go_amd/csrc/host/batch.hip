@@ -1,0 +1,700 @@
+// batch.hip — C-ABI implementation of the device side (include/pqhip.h): contexts, memory, and the
+// batch planner that replaces pageReader.read + readValues for every page of a set of chunks.
+//
+// Planning (host, once per batch): resolve each page's decoder (getValuesDecoder,
+// chunk_reader.go:106-159), header-level errors, level/value output offsets, checkpoint storage and
+// the tile lists of each kernel kind.  Running: one launch per kernel kind for the whole batch on
+// the context stream (k_prologue -> k_scan -> k_levels / k_copy / k_bool_plain / k_dict /
+// k_rle_bool), optionally bracketed by HIP events.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../kernels/launch.h"
+#include "internal.h"
+#include "pqhip.h"
+
+using namespace pqhip;
+
+struct pqh_ctx {
+  int32_t device = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(pqh_ctx* ctx, int code, const std::string& m) {
+  if (ctx) ctx->err = m;
+  g_err = m;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                              \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err(ctx, PQH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct KernelRun {
+  int kind;  // index into kKernelNames
+  hipEvent_t start, stop;
+  int32_t items;
+};
+
+const char* kKernelNames[] = {"k_prologue", "k_scan", "k_levels", "k_copy", "k_bool_plain",
+                              "k_dict",     "k_rle_bool"};
+constexpr int kNumKernels = 7;
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+namespace pqhip {
+
+int32_t resolve_kind(int32_t type, int32_t type_length, int32_t enc, int32_t* vs) {
+  if (enc == PQH_ENC_PLAIN_DICTIONARY) enc = PQH_ENC_RLE_DICTIONARY;
+  int32_t size = 0;
+  switch (type) {
+    case PQH_BOOLEAN: size = 1; break;
+    case PQH_INT32: case PQH_FLOAT: size = 4; break;
+    case PQH_INT64: case PQH_DOUBLE: size = 8; break;
+    case PQH_INT96: size = 12; break;
+    case PQH_FIXED_LEN_BYTE_ARRAY: size = type_length > 0 ? type_length : 0; break;
+    default: size = 0;
+  }
+  *vs = size;
+  switch (type) {
+    case PQH_BOOLEAN:
+      if (enc == PQH_ENC_PLAIN) return K_PLAIN_BOOL;
+      if (enc == PQH_ENC_RLE) return K_RLE_BOOL;
+      return K_UNSUPPORTED;
+    case PQH_BYTE_ARRAY:
+      if (enc == PQH_ENC_PLAIN) return K_PLAIN_BA;
+      if (enc == PQH_ENC_DELTA_LENGTH_BYTE_ARRAY) return K_DLBA;
+      if (enc == PQH_ENC_DELTA_BYTE_ARRAY) return K_DBA;
+      if (enc == PQH_ENC_RLE_DICTIONARY) return K_DICT;
+      return K_UNSUPPORTED;
+    case PQH_FIXED_LEN_BYTE_ARRAY:
+      if (enc == PQH_ENC_PLAIN) return type_length > 0 ? K_PLAIN_FIXED : type_length == 0 ? K_PLAIN_BA : K_FLBA_NEGATIVE;
+      if (enc == PQH_ENC_DELTA_BYTE_ARRAY) {
+        *vs = 0;
+        return K_DBA;
+      }
+      if (enc == PQH_ENC_RLE_DICTIONARY) return K_DICT;
+      return K_UNSUPPORTED;
+    case PQH_FLOAT:
+    case PQH_DOUBLE:
+      if (enc == PQH_ENC_PLAIN) return K_PLAIN_FIXED;
+      if (enc == PQH_ENC_RLE_DICTIONARY) return K_DICT;
+      return K_UNSUPPORTED;
+    case PQH_INT96:
+      if (enc == PQH_ENC_PLAIN) return K_PLAIN_INT96;
+      if (enc == PQH_ENC_RLE_DICTIONARY) return K_DICT;
+      return K_UNSUPPORTED;
+    case PQH_INT32:
+    case PQH_INT64:
+      if (enc == PQH_ENC_PLAIN) return K_PLAIN_FIXED;
+      if (enc == PQH_ENC_DELTA_BINARY_PACKED) return type == PQH_INT32 ? K_DELTA32 : K_DELTA64;
+      if (enc == PQH_ENC_RLE_DICTIONARY) return K_DICT;
+      return K_UNSUPPORTED;
+    default:
+      return K_UNSUPPORTED;
+  }
+}
+
+}  // namespace pqhip
+
+struct TileGroup {
+  int kernel;             // index into kKernelNames
+  int32_t value_size = 0; // dict groups
+  bool lds = false;
+  size_t shm = 0;
+  std::vector<Tile> tiles;
+  size_t offset = 0;      // into the device tile buffer
+};
+
+struct pqh_batch {
+  pqh_ctx* ctx = nullptr;
+  std::vector<pqh_chunk> chunks;
+  std::vector<pqh_page> pages;
+  std::vector<DevPage> hpages;
+  std::vector<DevChunk> hchunks;
+  std::vector<TileGroup> groups;
+  const uint8_t* d_payload = nullptr;
+  void* owned_payload = nullptr;
+  int64_t payload_bytes = 0;
+  DevPage* d_pages = nullptr;
+  DevChunk* d_chunks = nullptr;
+  PageState* d_states = nullptr;
+  Ckpt* d_ckpts = nullptr;
+  Tile* d_tiles = nullptr;
+  std::vector<void*> allocations;
+  std::vector<PageState> states;   // host copy after sync
+  std::vector<int64_t> chunk_n;    // level slots per chunk
+  std::vector<KernelRun> pending;  // events of the last run
+  std::vector<pqh_kernel_stat> stats;
+  bool synced = false;
+  double bytes_read = 0, bytes_written = 0;
+  std::vector<double> k_read, k_written;  // per kernel kind algorithmic bytes of one run
+  std::vector<hipEvent_t> event_pool;
+  size_t event_next = 0;
+};
+
+namespace {
+
+void free_batch(pqh_batch* b) {
+  for (auto& r : b->pending) (void)r;
+  for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
+  for (void* p : b->allocations) hipFree(p);
+  if (b->owned_payload) hipFree(b->owned_payload);
+}
+
+int dalloc(pqh_batch* b, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  b->allocations.push_back(*p);
+  return PQH_OK;
+}
+
+hipEvent_t next_event(pqh_batch* b) {
+  if (b->event_next == b->event_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    b->event_pool.push_back(e);
+  }
+  return b->event_pool[b->event_next++];
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqh_abi_version(void) { return PQH_ABI_VERSION; }
+
+int pqh_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = e == hipSuccess ? n : 0;
+  return e == hipSuccess ? PQH_OK : PQH_ERR_NO_DEVICE;
+}
+
+int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(nullptr, PQH_ERR_NO_DEVICE, "no HIP device");
+  if (device < 0 || device >= n) return set_err(nullptr, PQH_ERR_ARG, "bad device index");
+  pqh_ctx* c = new pqh_ctx();
+  c->device = device;
+  c->flags = flags;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_err(nullptr, PQH_ERR_HIP, "stream creation failed");
+  }
+  *out = c;
+  return PQH_OK;
+}
+
+void pqh_ctx_destroy(pqh_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* pqh_last_error(const pqh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+void* pqh_ctx_stream(pqh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int pqh_malloc(pqh_ctx* ctx, void** dptr, size_t bytes) {
+  hipSetDevice(ctx->device);
+  HIP_TRY(ctx, hipMalloc(dptr, bytes ? bytes : 16));
+  return PQH_OK;
+}
+int pqh_free(pqh_ctx* ctx, void* dptr) {
+  HIP_TRY(ctx, hipFree(dptr));
+  return PQH_OK;
+}
+int pqh_host_alloc(pqh_ctx* ctx, void** hptr, size_t bytes) {
+  HIP_TRY(ctx, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault));
+  return PQH_OK;
+}
+int pqh_host_free(pqh_ctx* ctx, void* hptr) {
+  HIP_TRY(ctx, hipHostFree(hptr));
+  return PQH_OK;
+}
+int pqh_memcpy_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return PQH_OK;
+}
+int pqh_memcpy_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return PQH_OK;
+}
+int pqh_sync(pqh_ctx* ctx) {
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return PQH_OK;
+}
+
+int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, const pqh_page* pages,
+                     int32_t num_pages, const void* d_payload, int64_t payload_bytes, pqh_batch** out) {
+  *out = nullptr;
+  if (!ctx || num_chunks < 0 || num_pages < 0 || (num_pages > 0 && !d_payload))
+    return set_err(ctx, PQH_ERR_ARG, "bad batch arguments");
+  hipSetDevice(ctx->device);
+  pqh_batch* b = new pqh_batch();
+  b->ctx = ctx;
+  b->chunks.assign(chunks, chunks + num_chunks);
+  b->pages.assign(pages, pages + num_pages);
+  b->d_payload = static_cast<const uint8_t*>(d_payload);
+  b->payload_bytes = payload_bytes;
+  b->hpages.resize(size_t(num_pages));
+  b->hchunks.resize(size_t(num_chunks));
+  b->chunk_n.assign(size_t(num_chunks), 0);
+  b->k_read.assign(kNumKernels, 0);
+  b->k_written.assign(kNumKernels, 0);
+
+  // ---- per-page planning ----
+  int64_t ck_cursor = 0;
+  TileGroup levels{2}, copy{3}, bools{4}, rle{6};
+  std::map<std::pair<int, int>, TileGroup> dicts;  // (value size, lds) -> tiles
+  std::map<std::pair<int, int>, size_t> dict_shm;
+  for (int32_t c = 0; c < num_chunks; c++) {
+    const pqh_chunk& C = chunks[c];
+    DevChunk& D = b->hchunks[size_t(c)];
+    memset(&D, 0, sizeof(D));
+    D.physical_type = C.column.physical_type;
+    D.type_length = C.column.type_length;
+    D.max_def = C.column.max_def;
+    D.max_rep = C.column.max_rep;
+    D.first_page = C.first_page;
+    D.num_pages = C.num_pages;
+    D.dict_page = -1;
+    int32_t vs = 0;
+    resolve_kind(C.column.physical_type, C.column.type_length, PQH_ENC_PLAIN, &vs);
+    D.value_size = vs;
+    if (C.first_page < 0 || C.num_pages < 0 || int64_t(C.first_page) + C.num_pages > num_pages) {
+      delete b;
+      return set_err(ctx, PQH_ERR_ARG, "chunk page range out of bounds");
+    }
+    const uint64_t chunk_err = C.host_status != PQH_OK ? err_key(0, 0, C.host_status) : kNoError;
+    int64_t level_base = 0;
+    for (int32_t i = 0; i < C.num_pages; i++) {
+      const int32_t p = C.first_page + i;
+      const pqh_page& Q = pages[p];
+      DevPage& P = b->hpages[size_t(p)];
+      memset(&P, 0, sizeof(P));
+      P.image_off = Q.image_offset;
+      P.image_len = Q.image_len;
+      P.page_type = Q.page_type;
+      P.num_values = Q.num_values;
+      P.encoding = Q.encoding;
+      P.def_len = Q.def_levels_byte_length;
+      P.rep_len = Q.rep_levels_byte_length;
+      P.chunk = c;
+      P.dict_page = -1;
+      P.ck_rep = P.ck_def = P.ck_val = -1;
+      P.host_err = chunk_err;
+      if (Q.image_offset < 0 || Q.image_len < 0 || Q.image_offset + Q.image_len > payload_bytes) {
+        delete b;
+        return set_err(ctx, PQH_ERR_ARG, "page image outside the payload");
+      }
+      if (Q.page_type == PQH_DICTIONARY_PAGE) {
+        // dictPageReader.read (page_dict.go:35-72) + getDictValuesDecoder (chunk_reader.go:17-39)
+        int32_t dvs = 0;
+        int32_t kind = resolve_kind(C.column.physical_type, C.column.type_length, PQH_ENC_PLAIN, &dvs);
+        P.kind = kind;
+        P.value_size = dvs;
+        if (i != 0 || D.dict_page >= 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
+        else if (Q.num_values < 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
+        else if (Q.encoding != PQH_ENC_PLAIN && Q.encoding != PQH_ENC_PLAIN_DICTIONARY)
+          P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
+        else if (C.column.physical_type == PQH_BOOLEAN)
+          P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
+        else if (dvs == 0)
+          P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
+        if (i == 0) D.dict_page = p;
+        b->bytes_read += Q.image_len;
+        continue;
+      }
+      if (Q.page_type != PQH_DATA_PAGE && Q.page_type != PQH_DATA_PAGE_V2)
+        P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
+      int32_t pvs = 0;
+      int32_t kind = resolve_kind(C.column.physical_type, C.column.type_length, Q.encoding, &pvs);
+      P.kind = kind;
+      P.value_size = pvs;
+      P.dict_page = D.dict_page;
+      if (Q.num_values < 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
+      if (Q.page_type == PQH_DATA_PAGE_V2 &&
+          (Q.rep_levels_byte_length < 0 || Q.def_levels_byte_length < 0 ||
+           int64_t(Q.rep_levels_byte_length) + Q.def_levels_byte_length > Q.image_len))
+        P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
+      if (kind == K_UNSUPPORTED) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
+      const bool device_ready = kind == K_PLAIN_FIXED || kind == K_PLAIN_INT96 || kind == K_PLAIN_BOOL ||
+                                kind == K_RLE_BOOL || kind == K_FLBA_NEGATIVE || kind == K_UNSUPPORTED ||
+                                (kind == K_DICT && pvs > 0);
+      if (!device_ready) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
+      const int64_t n = Q.num_values > 0 ? Q.num_values : 0;
+      P.level_base = level_base;
+      level_base += n;
+      b->bytes_read += Q.image_len;
+      if (n == 0) continue;
+      const int64_t nt = ceil_div(n, kHybridTile);
+      if (C.column.max_rep > 0) {
+        P.ck_rep = int32_t(ck_cursor);
+        P.ck_rep_n = int32_t(nt);
+        ck_cursor += nt;
+      }
+      if (C.column.max_def > 0) {
+        P.ck_def = int32_t(ck_cursor);
+        P.ck_def_n = int32_t(nt);
+        ck_cursor += nt;
+      }
+      if (kind == K_DICT || kind == K_RLE_BOOL) {
+        P.ck_val = int32_t(ck_cursor);
+        P.ck_val_n = int32_t(nt);
+        ck_cursor += nt;
+      }
+      if (P.host_err != kNoError) continue;
+      if (C.column.max_rep > 0 || C.column.max_def > 0)
+        for (int32_t k = 0; k < nt; k++) levels.tiles.push_back(Tile{p, k});
+      switch (kind) {
+        case K_PLAIN_FIXED:
+        case K_PLAIN_INT96: {
+          const int64_t ct = ceil_div(n * pvs, kCopyTileBytes);
+          for (int32_t k = 0; k < ct; k++) copy.tiles.push_back(Tile{p, k});
+          break;
+        }
+        case K_PLAIN_BOOL: {
+          const int64_t bt = ceil_div(n, kBoolTile);
+          for (int32_t k = 0; k < bt; k++) bools.tiles.push_back(Tile{p, k});
+          break;
+        }
+        case K_RLE_BOOL:
+          for (int32_t k = 0; k < nt; k++) rle.tiles.push_back(Tile{p, k});
+          break;
+        case K_DICT: {
+          int64_t dict_bytes = 0;
+          if (D.dict_page >= 0) dict_bytes = int64_t(std::max(0, pages[D.dict_page].num_values)) * pvs;
+          const bool lds = dict_bytes <= kDictLdsMax;
+          const int vclass = pvs == 4 ? 4 : pvs == 8 ? 8 : 0;
+          auto key = std::make_pair(vclass, int(lds));
+          TileGroup& g = dicts[key];
+          g.kernel = 5;
+          g.value_size = vclass;
+          g.lds = lds;
+          if (lds) g.shm = std::max<size_t>(g.shm, size_t((dict_bytes + 15) & ~int64_t(15)));
+          for (int32_t k = 0; k < nt; k++) g.tiles.push_back(Tile{p, k});
+          break;
+        }
+        default:
+          break;
+      }
+    }
+    b->chunk_n[size_t(c)] = level_base;
+  }
+  b->groups.push_back(levels);
+  b->groups.push_back(copy);
+  b->groups.push_back(bools);
+  for (auto& kv : dicts) b->groups.push_back(kv.second);
+  b->groups.push_back(rle);
+
+  // ---- device allocations ----
+  int rc;
+  size_t ntiles = 0;
+  for (auto& g : b->groups) {
+    g.offset = ntiles;
+    ntiles += g.tiles.size();
+  }
+  if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_pages), sizeof(DevPage) * size_t(num_pages))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_states), sizeof(PageState) * size_t(num_pages))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ckpts), sizeof(Ckpt) * size_t(ck_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_tiles), sizeof(Tile) * ntiles))) {
+    free_batch(b);
+    delete b;
+    return rc;
+  }
+  for (int32_t c = 0; c < num_chunks; c++) {
+    DevChunk& D = b->hchunks[size_t(c)];
+    const int64_t n = b->chunk_n[size_t(c)];
+    D.values_cap = n;
+    void* p = nullptr;
+    if ((rc = dalloc(b, &p, size_t(n) * size_t(std::max(D.value_size, 1)) + 64))) break;
+    D.values = static_cast<uint8_t*>(p);
+    if (D.max_def > 0) {
+      if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
+      D.def_levels = static_cast<uint8_t*>(p);
+    }
+    if (D.max_rep > 0) {
+      if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
+      D.rep_levels = static_cast<uint8_t*>(p);
+    }
+  }
+  if (rc || (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunks), sizeof(DevChunk) * size_t(std::max(num_chunks, 1))))) {
+    free_batch(b);
+    delete b;
+    return rc;
+  }
+  std::vector<Tile> all;
+  all.reserve(ntiles);
+  for (auto& g : b->groups) all.insert(all.end(), g.tiles.begin(), g.tiles.end());
+  hipStream_t s = ctx->stream;
+  hipError_t e = hipSuccess;
+  if (num_pages) e = hipMemcpyAsync(b->d_pages, b->hpages.data(), sizeof(DevPage) * size_t(num_pages), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && num_chunks)
+    e = hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * size_t(num_chunks), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ntiles) e = hipMemcpyAsync(b->d_tiles, all.data(), sizeof(Tile) * ntiles, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    free_batch(b);
+    delete b;
+    return set_err(ctx, PQH_ERR_HIP, std::string("batch upload: ") + hipGetErrorString(e));
+  }
+  b->stats.resize(kNumKernels);
+  for (int k = 0; k < kNumKernels; k++) {
+    memset(&b->stats[size_t(k)], 0, sizeof(pqh_kernel_stat));
+    snprintf(b->stats[size_t(k)].name, sizeof(b->stats[size_t(k)].name), "%s", kKernelNames[k]);
+  }
+  *out = b;
+  return PQH_OK;
+}
+
+int pqh_batch_run(pqh_batch* b) {
+  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
+  pqh_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  const bool prof = (ctx->flags & PQH_CTX_PROFILE) != 0;
+  hipStream_t s = ctx->stream;
+  DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
+             int32_t(b->chunks.size())};
+  b->synced = false;
+  b->event_next = 0;
+  b->pending.clear();
+  auto timed = [&](int kind, int32_t items, auto&& fn) -> hipError_t {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof) {
+      e0 = next_event(b);
+      e1 = next_event(b);
+      hipEventRecord(e0, s);
+    }
+    hipError_t e = fn();
+    if (prof) {
+      hipEventRecord(e1, s);
+      b->pending.push_back(KernelRun{kind, e0, e1, items});
+    }
+    return e;
+  };
+  hipError_t e;
+  e = timed(0, int32_t(b->pages.size()), [&] { return launch_prologue(d, s); });
+  if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), [&] { return launch_scan(d, s); });
+  for (auto& g : b->groups) {
+    if (e != hipSuccess) break;
+    if (g.tiles.empty()) continue;
+    const Tile* t = b->d_tiles + g.offset;
+    const int32_t n = int32_t(g.tiles.size());
+    switch (g.kernel) {
+      case 2: e = timed(2, n, [&] { return launch_levels(d, t, n, s); }); break;
+      case 3: e = timed(3, n, [&] { return launch_copy(d, t, n, s); }); break;
+      case 4: e = timed(4, n, [&] { return launch_bool_plain(d, t, n, s); }); break;
+      case 5: e = timed(5, n, [&] { return launch_dict(d, t, n, g.value_size, g.lds, g.shm, s); }); break;
+      case 6: e = timed(6, n, [&] { return launch_rle_bool(d, t, n, s); }); break;
+      default: break;
+    }
+  }
+  if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
+  return PQH_OK;
+}
+
+int pqh_batch_sync(pqh_batch* b) {
+  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
+  pqh_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  b->states.resize(b->pages.size());
+  if (!b->pages.empty())
+    HIP_TRY(ctx, hipMemcpyAsync(b->states.data(), b->d_states, sizeof(PageState) * b->pages.size(),
+                                hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (auto& r : b->pending) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess) {
+      pqh_kernel_stat& st = b->stats[size_t(r.kind)];
+      st.launches += 1;
+      st.work_items = r.items;
+      st.total_ms += ms;
+    }
+  }
+  b->pending.clear();
+  // algorithmic bytes of one run: page bytes read once, dictionaries once per
+  // chunk, decoded bytes written; attributed to the kernel that moves them.
+  double wr = 0;
+  std::fill(b->k_read.begin(), b->k_read.end(), 0.0);
+  std::fill(b->k_written.begin(), b->k_written.end(), 0.0);
+  for (size_t p = 0; p < b->pages.size(); p++) {
+    const DevPage& P = b->hpages[p];
+    const PageState& S = b->states[p];
+    const DevChunk& C = b->hchunks[size_t(P.chunk)];
+    if (P.page_type == PQH_DICTIONARY_PAGE) continue;
+    const double n = P.num_values > 0 ? P.num_values : 0;
+    const double levels = (C.max_def > 0 ? n : 0) + (C.max_rep > 0 ? n : 0);
+    const double vals = double(S.nn) * P.value_size;
+    wr += levels + vals;
+    if (levels > 0) {
+      b->k_written[2] += levels;
+      double lb = 0;
+      if (S.rep_s >= 0) lb += S.rep_e - S.rep_s;
+      if (S.def_s >= 0) lb += S.def_e - S.def_s;
+      b->k_read[2] += lb;
+    }
+    switch (P.kind) {
+      case K_PLAIN_FIXED:
+      case K_PLAIN_INT96:
+        b->k_read[3] += vals;
+        b->k_written[3] += vals;
+        break;
+      case K_PLAIN_BOOL:
+        b->k_read[4] += (S.nn + 7) / 8;
+        b->k_written[4] += S.nn;
+        break;
+      case K_DICT:
+        b->k_read[5] += S.val_e - S.val_s;
+        b->k_written[5] += vals;
+        break;
+      case K_RLE_BOOL:
+        b->k_read[6] += S.val_e - S.val_s;
+        b->k_written[6] += S.nn;
+        break;
+      default:
+        break;
+    }
+  }
+  for (size_t c = 0; c < b->hchunks.size(); c++) {  // dictionaries once per chunk
+    const DevChunk& C = b->hchunks[c];
+    if (C.dict_page >= 0) b->k_read[5] += b->pages[size_t(C.dict_page)].image_len;
+  }
+  b->bytes_written = wr;
+  for (int k = 0; k < kNumKernels; k++) {
+    b->stats[size_t(k)].bytes_read = b->k_read[size_t(k)];
+    b->stats[size_t(k)].bytes_written = b->k_written[size_t(k)];
+  }
+  b->synced = true;
+  return PQH_OK;
+}
+
+int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num_pages) {
+  if (!b || !b->synced) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "batch not synced");
+  for (int32_t p = 0; p < num_pages && size_t(p) < b->pages.size(); p++) {
+    const PageState& S = b->states[size_t(p)];
+    pqh_page_result& r = out[p];
+    memset(&r, 0, sizeof(r));
+    if (S.err != kNoError) {
+      r.status = int32_t(S.err & 0xff);
+      r.phase = int32_t(S.err >> 56);
+      r.index = int64_t((S.err >> 8) & 0xffffffffffffull);
+    }
+    r.num_non_null = S.nn;
+    r.value_offset = S.value_base;
+    r.level_offset = b->hpages[size_t(p)].level_base;
+  }
+  return PQH_OK;
+}
+
+int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
+  if (!b || chunk < 0 || size_t(chunk) >= b->chunks.size()) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad chunk");
+  if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
+  const DevChunk& D = b->hchunks[size_t(chunk)];
+  memset(out, 0, sizeof(*out));
+  out->num_values = b->chunk_n[size_t(chunk)];
+  out->value_size = D.value_size;
+  out->values = D.values;
+  out->offsets = D.offsets;
+  out->bytes = D.bytes;
+  out->def_levels = D.def_levels;
+  out->rep_levels = D.rep_levels;
+  out->status = PQH_OK;
+  out->error_page = -1;
+  int64_t nn = 0;
+  for (int32_t i = 0; i < D.num_pages; i++) {
+    const int32_t p = D.first_page + i;
+    const PageState& S = b->states[size_t(p)];
+    if (S.err != kNoError && out->status == PQH_OK) {
+      out->status = int32_t(S.err & 0xff);
+      out->error_page = p;
+      out->error_phase = int32_t(S.err >> 56);
+      out->error_index = int64_t((S.err >> 8) & 0xffffffffffffull);
+    }
+    if (b->hpages[size_t(p)].page_type != PQH_DICTIONARY_PAGE) nn += S.nn;
+  }
+  out->num_non_null = nn;
+  return PQH_OK;
+}
+
+int pqh_batch_kernel_stats(const pqh_batch* b, pqh_kernel_stat* out, int32_t max_stats, int32_t* num_stats) {
+  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
+  int32_t n = 0;
+  for (int k = 0; k < kNumKernels && n < max_stats; k++) out[n++] = b->stats[size_t(k)];
+  *num_stats = n;
+  return PQH_OK;
+}
+
+int pqh_batch_reset_stats(pqh_batch* b) {
+  if (!b) return PQH_ERR_ARG;
+  for (auto& s : b->stats) {
+    s.launches = 0;
+    s.total_ms = 0;
+  }
+  return PQH_OK;
+}
+
+int pqh_batch_traffic(const pqh_batch* b, double* bytes_read, double* bytes_written) {
+  if (!b || !b->synced) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "batch not synced");
+  *bytes_read = b->bytes_read;
+  *bytes_written = b->bytes_written;
+  return PQH_OK;
+}
+
+void pqh_batch_destroy(pqh_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->ctx->device);
+  hipStreamSynchronize(b->ctx->stream);
+  free_batch(b);
+  delete b;
+}
+
+int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out) {
+  *out = nullptr;
+  if (!ctx || !hb) return set_err(ctx, PQH_ERR_ARG, "null argument");
+  hipSetDevice(ctx->device);
+  void* d = nullptr;
+  const size_t bytes = hb->payload.size();
+  HIP_TRY(ctx, hipMalloc(&d, bytes ? bytes : 16));
+  void* src = const_cast<uint8_t*>(hb->payload.data());
+  const bool pinned = bytes && hipHostRegister(src, bytes, hipHostRegisterDefault) == hipSuccess;
+  hipError_t e = bytes ? hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ctx->stream) : hipSuccess;
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (pinned) hipHostUnregister(src);
+  if (e != hipSuccess) {
+    hipFree(d);
+    return set_err(ctx, PQH_ERR_HIP, std::string("payload upload: ") + hipGetErrorString(e));
+  }
+  int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
+                            int32_t(hb->pages.size()), d, hb->payload_bytes, out);
+  if (rc) {
+    hipFree(d);
+    return rc;
+  }
+  (*out)->owned_payload = d;
+  return PQH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// decode.h — device-side tables shared by the host batch planner (host/batch.hip) and the HIP
+// kernels (kernels/decode.hip).  All page bytes stay in one HBM payload buffer; these tables
+// describe where each page image, stream and output lives.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PQH_HD __host__ __device__
+#else
+#define PQH_HD
+#endif
+
+namespace pqhip {
+
+// Value decoder kinds: getValuesDecoder (reference chunk_reader.go:106-159) resolved per page.
+enum DecoderKind : int32_t {
+  K_UNSUPPORTED = 0,
+  K_PLAIN_FIXED = 1,  // int32/int64/float/double/FLBA(L>0): binary.Read / ReadFull(L)
+  K_PLAIN_INT96 = 2,  // type_int96.go:21-39
+  K_PLAIN_BOOL = 3,   // booleanPlainDecoder
+  K_RLE_BOOL = 4,     // booleanRLEDecoder: u32 size + hybrid(1)
+  K_DICT = 5,         // dictDecoder: width byte + hybrid indices + gather
+  K_DELTA32 = 6,      // int32DeltaBPDecoder
+  K_DELTA64 = 7,      // int64DeltaBPDecoder
+  K_PLAIN_BA = 8,     // byteArrayPlainDecoder, variable length
+  K_DLBA = 9,         // byteArrayDeltaLengthDecoder
+  K_DBA = 10,         // byteArrayDeltaDecoder
+  K_FLBA_NEGATIVE = 11,
+  K_DICT_PAGE = 12    // dictionary page (dictPageReader + PLAIN values decoder)
+};
+
+// Tile sizes (values or level slots per work item).
+constexpr int kBlock = 256;          // threads per workgroup
+constexpr int kHybridTile = 8192;    // hybrid-driven tiles (levels, dictionary indices, RLE booleans)
+constexpr int kCopyTileBytes = 65536;
+constexpr int kBoolTile = 32768;     // PLAIN booleans: 256 threads x 16 bytes x 8 bits
+constexpr int kDictLdsMax = 65536;   // dictionaries up to this size are staged in LDS
+constexpr uint64_t kNoError = ~0ull;
+
+// Error key: the reference stops at its FIRST error in decode order; the smallest key wins.
+PQH_HD inline uint64_t err_key(int phase, int64_t index, int code) {
+  uint64_t idx = index < 0 ? 0 : (uint64_t(index) > 0xffffffffffffull ? 0xffffffffffffull : uint64_t(index));
+  return (uint64_t(phase) << 56) | (idx << 8) | uint64_t(code & 0xff);
+}
+
+struct DevPage {
+  int64_t image_off;     // in payload
+  int32_t image_len;
+  int32_t page_type;     // 0 V1, 3 V2, 2 dictionary
+  int32_t num_values;
+  int32_t encoding;
+  int32_t def_len, rep_len;
+  int32_t chunk;
+  int32_t kind;          // DecoderKind
+  int32_t value_size;    // fixed value bytes (FLBA length etc.)
+  int32_t dict_page;     // batch page index of the chunk's dictionary page, -1
+  int64_t level_base;    // first level slot of the page in the chunk's level outputs
+  int32_t ck_rep, ck_def, ck_val;  // checkpoint table offsets (entries), -1 if none
+  int32_t ck_rep_n, ck_def_n, ck_val_n;
+  uint64_t host_err;     // error key found by the host planner (header-level), kNoError if none
+};
+
+struct DevChunk {
+  int32_t physical_type, type_length, max_def, max_rep;
+  int32_t first_page, num_pages;
+  int32_t value_size;    // output bytes per value, 0 = byte array
+  int32_t dict_page;     // batch page index or -1
+  uint8_t* values;
+  int64_t* offsets;
+  uint8_t* bytes;
+  uint8_t* def_levels;
+  uint8_t* rep_levels;
+  int64_t values_cap;    // values capacity (elements)
+  int64_t bytes_cap;
+};
+
+// Written by the prologue (one wave per page) and the scan kernel.
+struct PageState {
+  unsigned long long err;  // min err_key, kNoError if none
+  int32_t nn;              // not-null count
+  int32_t width;           // bit width of the value hybrid stream (dictionary / RLE boolean)
+  int32_t rep_s, rep_e;    // byte ranges in the image; s < 0 = uninitialised decoder
+  int32_t def_s, def_e;
+  int32_t val_s, val_e;    // values section / value hybrid stream
+  int32_t val_limit;       // values before the first phase-3 stream error (== nn if none)
+  int32_t dict_n;          // dictionary pages: entries decoded
+  int64_t value_base;      // first value of the page in the chunk's dense values
+  int64_t byte_base;       // byte arrays: first byte
+};
+
+// Run checkpoint at a tile boundary: the run that contains the tile's first value.
+struct Ckpt {
+  int32_t run_start;  // value index where the run starts
+  int32_t run_len;    // values in the run (clamped to 2^31-1)
+  int32_t data;       // bit-packed: byte offset of the run's first group in the image; RLE: value
+  int32_t next_hdr;   // byte offset of the next run header (clamped); bit 31 = bit-packed run
+};
+
+struct Tile {
+  int32_t page;
+  int32_t k;  // tile index inside the page
+};
+
+}  // namespace pqhip

@@ -1,0 +1,857 @@
+// decode.hip — hand-written HIP kernels (gfx950 / CDNA4) for Parquet page decode.
+//
+// Two-pass design for the sequential chains inside a page (SURVEY.md §7 "Hard parts"):
+//   1. k_prologue   one wave64 per page: page framing (page_v1.go:87-122 / page_v2.go:79-131),
+//                   the hybrid RLE/bit-packed run-header chain of every stream
+//                   (hybrid_decoder.go:81-165) with a run CHECKPOINT at every tile boundary, the
+//                   not-null count (helpers.go:133-149, wave-parallel over bit-packed groups), and
+//                   the exact first-error position of the reference's streaming decoders;
+//   2. k_scan       one workgroup per chunk: dense value offsets = exclusive scan of notNull;
+//   3. expand       data-parallel tiles over HBM-resident page images: level bytes, dictionary
+//                   gathers (dictionary staged in LDS), PLAIN copies and boolean bit expansion.
+// All bandwidth kernels: 16-byte vector loads/stores, no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "launch.h"
+#include "pqhip.h"
+
+namespace pqhip {
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+
+// 8 bytes at p; bytes at or past `end` read as zero (the reference zero-fills a short bit-packed
+// group read: hybrid_decoder.go:132-140).
+__device__ __forceinline__ uint64_t ld64_masked(const uint8_t* p, const uint8_t* end) {
+  if (p + 8 <= end) return ld64u(p);
+  uint64_t v = 0;
+  for (int k = 0; k < 8; k++)
+    if (p + k < end) v |= uint64_t(p[k]) << (8 * k);
+  return v;
+}
+
+__device__ __forceinline__ int bits_len32(uint32_t v) { return v ? 32 - __clz(int(v)) : 0; }
+
+__device__ __forceinline__ int64_t wave_sum(int64_t x) {
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+// binary.ReadUvarint over img[pos, end) (encoding/binary; readUVariant32 helpers.go:151-167).
+__device__ int read_uvarint(const uint8_t* img, int64_t& pos, int64_t end, uint64_t& v) {
+  uint64_t x = 0;
+  int s = 0;
+  for (int i = 0; i < 10; i++) {
+    if (pos >= end) return i ? PQH_ERR_UNEXPECTED_EOF : PQH_ERR_EOF;
+    uint32_t c = img[pos++];
+    if (c < 0x80) {
+      if (i == 9 && c > 1) return PQH_ERR_VARINT_OVERFLOW;
+      v = x | (uint64_t(c) << s);
+      return PQH_OK;
+    }
+    x |= uint64_t(c & 0x7f) << s;
+    s += 7;
+  }
+  return PQH_ERR_VARINT_OVERFLOW;
+}
+
+__device__ __forceinline__ uint32_t mask_w(int w) { return w >= 32 ? 0xffffffffu : ((1u << w) - 1u); }
+
+// Value i of a bit-packed run whose first group starts at byte `data`.
+__device__ __forceinline__ uint32_t bp_value(const uint8_t* img, const uint8_t* end, int32_t data, int64_t rel, int w) {
+  int64_t bit = rel * w;
+  const uint8_t* p = img + data + (bit >> 3);
+  return uint32_t(ld64_masked(p, end) >> (bit & 7)) & mask_w(w);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hybrid run-header walk (one wave, uniform control flow).  Replays hybridDecoder.next for the
+// first N values of a stream: headers, RLE values, the lazy bit-packed group reads and their
+// errors; writes a checkpoint for every tile of kHybridTile values; optionally counts values equal
+// to `match` (definition levels == maxD -> notNull).
+// ------------------------------------------------------------------------------------------------
+struct WalkOut {
+  uint64_t err;
+  int64_t count;
+  int64_t fail_index;
+};
+
+__device__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, int64_t N, int phase, Ckpt* ck,
+                               int match, int lane) {
+  WalkOut o{kNoError, 0, N};
+  if (N <= 0) return o;
+  const int64_t T = kHybridTile;
+  if (w == 0) {  // infinite zeros, no reads (hybrid_decoder.go:82-85)
+    if (ck)
+      for (int64_t k = lane; k * T < N; k += 64) ck[k] = Ckpt{0, 0x7fffffff, 0, 0};
+    o.count = match == 0 ? N : 0;
+    return o;
+  }
+  const uint8_t* end = img + e;
+  const int rle_size = (w + 7) >> 3;
+  const uint32_t m = mask_w(w);
+  int64_t pos = s, produced = 0, next_ck = 0, cnt_lane = 0;
+  while (produced < N) {
+    uint64_t h;
+    int st = read_uvarint(img, pos, e, h);
+    if (st) {
+      o.err = err_key(phase, produced, st);
+      o.fail_index = produced;
+      break;
+    }
+    if (h > 0x7fffffffull) {
+      o.err = err_key(phase, produced, PQH_ERR_INT32_RANGE);
+      o.fail_index = produced;
+      break;
+    }
+    const bool bp = h & 1;
+    int64_t cnt, next, fail = -1;
+    int32_t data;
+    if (bp) {
+      const int64_t groups = int64_t(h >> 1);
+      if (groups == 0) {
+        o.err = err_key(phase, produced, PQH_ERR_EMPTY_BP_RUN);
+        o.fail_index = produced;
+        break;
+      }
+      cnt = groups * 8;
+      data = int32_t(pos);
+      const int64_t need = cnt < N - produced ? cnt : N - produced;
+      const int64_t gneed = (need + 7) >> 3;
+      const int64_t gf = pos >= e ? 0 : (e - pos + w - 1) / w;  // first group read that hits EOF
+      if (gf < gneed) fail = produced + 8 * gf;
+      next = pos + groups * w;
+    } else {
+      cnt = int64_t(h >> 1);
+      if (cnt == 0) {
+        o.err = err_key(phase, produced, PQH_ERR_EMPTY_RLE_RUN);
+        o.fail_index = produced;
+        break;
+      }
+      if (pos >= e || pos + rle_size > e) {  // readRLERunValue: Read -> EOF or short count
+        o.err = err_key(phase, produced, pos >= e ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+        o.fail_index = produced;
+        break;
+      }
+      uint32_t v = 0;
+      for (int k = 0; k < rle_size; k++) v |= uint32_t(img[pos + k]) << (8 * k);
+      if (w < 32 && (v >> w) != 0) {
+        o.err = err_key(phase, produced, PQH_ERR_RLE_VALUE_TOO_LARGE);
+        o.fail_index = produced;
+        break;
+      }
+      data = int32_t(v);
+      next = pos + rle_size;
+    }
+    const int64_t valid_end = fail >= 0 ? fail : produced + cnt;
+    if (ck) {
+      const int32_t nh = int32_t(next < 0x7fffffff ? next : 0x7fffffff) | (bp ? int32_t(0x80000000u) : 0);
+      const int32_t rl = int32_t(cnt < 0x7fffffff ? cnt : 0x7fffffff);
+      while (next_ck * T < N && next_ck * T < valid_end) {
+        if (lane == 0) ck[next_ck] = Ckpt{int32_t(produced), rl, data, nh};
+        next_ck++;
+      }
+    }
+    if (match >= 0) {
+      const int64_t lim = (valid_end < N ? valid_end : N) - produced;
+      if (!bp) {
+        if (lane == 0 && data == match) cnt_lane += lim;
+      } else {
+        for (int64_t g = lane; g * 8 < lim; g += 64) {
+          const uint64_t q = ld64_masked(img + data + g * w, end);
+          const uint64_t q2 = w > 8 ? ld64_masked(img + data + g * w + 8, end) : 0;
+          for (int j = 0; j < 8; j++) {
+            const int bit = j * w;
+            uint32_t v;
+            if (bit + w <= 64) v = uint32_t(q >> bit) & m;
+            else if (bit >= 64) v = uint32_t(q2 >> (bit - 64)) & m;
+            else v = uint32_t((q >> bit) | (q2 << (64 - bit))) & m;
+            cnt_lane += (g * 8 + j < lim) && (int(v) == match);
+          }
+        }
+      }
+    }
+    if (fail >= 0) {
+      o.err = err_key(phase, fail, PQH_ERR_EOF);
+      o.fail_index = fail;
+      break;
+    }
+    produced += cnt;
+    pos = next;
+  }
+  o.count = wave_sum(cnt_lane);
+  return o;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_prologue: one wave64 per page.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= b.num_pages) return;
+  const DevPage P = b.pages[p];
+  const DevChunk C = b.chunks[P.chunk];
+  const uint8_t* img = b.payload + P.image_off;
+  const int64_t L = P.image_len;
+
+  PageState S;
+  S.err = P.host_err;
+  S.nn = 0;
+  S.width = 0;
+  S.rep_s = S.rep_e = S.def_s = S.def_e = -1;
+  S.val_s = S.val_e = 0;
+  S.val_limit = 0;
+  S.dict_n = 0;
+  S.value_base = 0;
+  S.byte_base = 0;
+  uint64_t err = P.host_err;
+
+  if (err == kNoError && P.page_type == PQH_DICTIONARY_PAGE) {
+    // dictPageReader.read: PLAIN decode of num_values entries, no error tolerated (page_dict.go:60-70)
+    const int64_t n = P.num_values;
+    const int vs = P.value_size;
+    if (vs > 0) {
+      const int64_t cap = L / vs, rem = L - cap * vs;
+      if (cap < n) {
+        if (P.kind == K_PLAIN_INT96 && rem != 0)
+          err = cap == n - 1 ? err_key(0, cap, PQH_ERR_INT96_SHORT) : err_key(0, cap + 1, PQH_ERR_EOF);
+        else
+          err = err_key(0, cap, rem == 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+      } else {
+        S.dict_n = int32_t(n);
+      }
+    } else {
+      err = err_key(0, 0, PQH_ERR_UNSUPPORTED);  // byte-array dictionaries: k_ba_chain (next round)
+    }
+  } else if (err == kNoError) {
+    const int64_t n = P.num_values;
+    const int rw = bits_len32(uint32_t(C.max_rep)), dw = bits_len32(uint32_t(C.max_def));
+    int64_t rep_s = -1, rep_e = -1, def_s = -1, def_e = -1, vs, ve = L;
+    // --- pageReader.read: level decoders initSize (V1) / init (V2), then valuesDecoder.init ---
+    if (P.page_type == PQH_DATA_PAGE) {
+      int64_t pos = 0;
+      for (int k = 0; k < 2 && err == kNoError; k++) {
+        if ((k == 0 ? rw : dw) == 0) continue;
+        if (L - pos < 4) {
+          err = err_key(0, 1 + k, L - pos == 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+          break;
+        }
+        const uint32_t size = uint32_t(img[pos]) | (uint32_t(img[pos + 1]) << 8) | (uint32_t(img[pos + 2]) << 16) |
+                              (uint32_t(img[pos + 3]) << 24);
+        const int64_t s0 = pos + 4;
+        const int64_t e0 = s0 + (int64_t(size) < L - s0 ? int64_t(size) : L - s0);
+        if (k == 0) {
+          rep_s = s0;
+          rep_e = e0;
+        } else {
+          def_s = s0;
+          def_e = e0;
+        }
+        pos = e0;
+      }
+      vs = pos;
+    } else {
+      const int64_t rl = P.rep_len, dl = P.def_len;
+      if (rl > 0 && rw > 0) {
+        rep_s = 0;
+        rep_e = rl;
+      }
+      if (dl > 0 && dw > 0) {
+        def_s = rl;
+        def_e = rl + dl;
+      }
+      vs = rl + dl;
+    }
+    int64_t hs = vs, he = ve;  // value hybrid stream
+    if (err == kNoError) {
+      if (P.kind == K_DICT) {  // dictDecoder.init (type_dict.go:22-38)
+        if (vs >= ve) {
+          err = err_key(0, 3, PQH_ERR_EOF);
+        } else {
+          const int w = img[vs];
+          if (w > 32) err = err_key(0, 3, PQH_ERR_DICT_BIT_WIDTH);
+          S.width = w;
+          hs = vs + 1;
+        }
+      } else if (P.kind == K_RLE_BOOL) {  // booleanRLEDecoder.init -> initSize (type_boolean.go:104-107)
+        if (ve - vs < 4) {
+          err = err_key(0, 3, ve - vs == 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+        } else {
+          const uint32_t size = uint32_t(img[vs]) | (uint32_t(img[vs + 1]) << 8) | (uint32_t(img[vs + 2]) << 16) |
+                                (uint32_t(img[vs + 3]) << 24);
+          hs = vs + 4;
+          he = hs + (int64_t(size) < ve - hs ? int64_t(size) : ve - hs);
+          S.width = 1;
+        }
+      }
+    }
+    S.rep_s = int32_t(rep_s);
+    S.rep_e = int32_t(rep_e);
+    S.def_s = int32_t(def_s);
+    S.def_e = int32_t(def_e);
+    S.val_s = int32_t(hs);
+    S.val_e = int32_t(he);
+    // --- readValues(numValues) ---
+    if (err == kNoError && n > 0) {
+      if (rw > 0) {  // decodePackedArray(rDecoder, n)
+        if (rep_s < 0) {
+          err = err_key(1, 0, PQH_ERR_READER_NOT_INITIALIZED);
+        } else {
+          WalkOut r = walk_hybrid(img, rep_s, rep_e, rw, n, 1, P.ck_rep >= 0 ? b.ckpts + P.ck_rep : nullptr, -1, lane);
+          err = r.err;
+        }
+      }
+      int64_t nn = n;
+      if (err == kNoError && dw > 0) {  // decodePackedArray(dDecoder, n) + notNull
+        if (def_s < 0) {
+          err = err_key(2, 0, PQH_ERR_READER_NOT_INITIALIZED);
+        } else {
+          WalkOut r = walk_hybrid(img, def_s, def_e, dw, n, 2, P.ck_def >= 0 ? b.ckpts + P.ck_def : nullptr, C.max_def, lane);
+          err = r.err;
+          nn = r.count;
+        }
+      }
+      if (err == kNoError) {
+        S.nn = int32_t(nn);
+        int64_t limit = nn;
+        if (nn > 0) {
+          const int64_t avail = ve - vs;
+          switch (P.kind) {
+            case K_DICT:
+            case K_RLE_BOOL: {
+              WalkOut r = walk_hybrid(img, hs, he, S.width, nn, 3, P.ck_val >= 0 ? b.ckpts + P.ck_val : nullptr, -1, lane);
+              err = r.err;
+              limit = r.fail_index;
+              break;
+            }
+            case K_PLAIN_FIXED: {  // binary.Read / io.ReadFull per value
+              const int64_t cap = avail / P.value_size, rem = avail - cap * P.value_size;
+              if (cap < nn) {
+                err = err_key(3, cap, rem == 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+                limit = cap;
+              }
+              break;
+            }
+            case K_PLAIN_INT96: {  // type_int96.go:21-39
+              const int64_t cap = avail / 12, rem = avail - cap * 12;
+              if (cap < nn) {
+                if (rem == 0) err = err_key(3, cap, PQH_ERR_EOF);
+                else if (cap == nn - 1) err = err_key(3, cap, PQH_ERR_INT96_SHORT);
+                else err = err_key(3, cap + 1, PQH_ERR_EOF);
+                limit = cap;
+              }
+              break;
+            }
+            case K_PLAIN_BOOL: {  // one io.ReadFull(1 byte) per 8 values (type_boolean.go:43-69)
+              if (avail * 8 < nn) {
+                err = err_key(3, avail * 8, PQH_ERR_EOF);
+                limit = avail * 8;
+              }
+              break;
+            }
+            case K_FLBA_NEGATIVE:
+              err = err_key(3, 0, PQH_ERR_NEGATIVE_LENGTH);
+              limit = 0;
+              break;
+            default:
+              err = err_key(3, 0, PQH_ERR_UNSUPPORTED);
+              limit = 0;
+          }
+        }
+        S.val_limit = int32_t(limit);
+      }
+    }
+  }
+  S.err = err;
+  if (lane == 0) b.states[p] = S;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_scan: one workgroup per chunk; dense value offsets.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool page_failed_before_values(const PageState& s) {
+  return s.err != kNoError && (s.err >> 56) <= 2;
+}
+
+__global__ __launch_bounds__(256) void k_scan(DevBatch b) {
+  const DevChunk C = b.chunks[blockIdx.x];
+  __shared__ int64_t wsum[4];
+  __shared__ int64_t carry;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < C.num_pages; base += 256) {
+    const int i = base + t;
+    const int p = C.first_page + i;
+    int64_t nn = 0;
+    if (i < C.num_pages && b.pages[p].page_type != PQH_DICTIONARY_PAGE) {
+      const PageState s = b.states[p];
+      nn = page_failed_before_values(s) ? 0 : s.nn;
+    }
+    int64_t x = nn;  // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < wv; k++) before += wsum[k];
+    if (i < C.num_pages) b.states[p].value_base = before + x - nn;
+    __syncthreads();
+    if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile expansion of a hybrid stream from a checkpoint.  Thread 0 re-walks the (already validated)
+// run headers of the tile into an LDS run list; every thread then expands 8 consecutive values.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxRuns = 256;
+
+struct RunL {
+  int32_t start, end, data, bp;
+};
+
+struct TileLds {
+  RunL runs[kMaxRuns];
+  int32_t nruns;
+  int32_t seg_end;
+  int32_t next_pos;
+  int32_t pad;
+};
+
+// Build the run list for values [from, t1) starting at run {rs, rl, data, bp} with the next
+// header at `pos`.  Returns via LDS; executed by one thread.
+__device__ void build_runs(const uint8_t* img, int w, int64_t t1, int64_t rs, int64_t rl, int32_t data, int32_t bp,
+                           int64_t pos, TileLds& L) {
+  int n = 0;
+  int64_t cur_end = rs + rl;
+  L.runs[n++] = RunL{int32_t(rs), int32_t(cur_end < t1 ? cur_end : t1), data, bp};
+  const int rle_size = (w + 7) >> 3;
+  while (cur_end < t1 && n < kMaxRuns) {
+    uint64_t h = 0;
+    int64_t pp = pos;
+    read_uvarint(img, pp, int64_t(0x7fffffffffffll), h);  // validated by k_prologue
+    int64_t cnt;
+    int32_t d, isbp;
+    if (h & 1) {
+      cnt = int64_t(h >> 1) * 8;
+      d = int32_t(pp);
+      pos = pp + int64_t(h >> 1) * w;
+      isbp = 1;
+    } else {
+      cnt = int64_t(h >> 1);
+      uint32_t v = 0;
+      for (int k = 0; k < rle_size; k++) v |= uint32_t(img[pp + k]) << (8 * k);
+      d = int32_t(v);
+      pos = pp + rle_size;
+      isbp = 0;
+    }
+    const int64_t e = cur_end + cnt;
+    L.runs[n++] = RunL{int32_t(cur_end), int32_t(e < t1 ? e : t1), d, isbp};
+    cur_end = e;
+  }
+  L.nruns = n;
+  L.seg_end = int32_t(cur_end < t1 ? cur_end : t1);
+  L.next_pos = int32_t(pos < 0x7fffffff ? pos : 0x7fffffff);
+}
+
+__device__ __forceinline__ int find_run(const TileLds& L, int64_t i) {
+  int lo = 0, hi = L.nruns - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.runs[mid].start <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Decode up to 8 values [i0, i0+cnt) into v[].
+__device__ __forceinline__ void decode8(const uint8_t* img, const uint8_t* end, int w, const TileLds& L, int64_t i0,
+                                        int cnt, uint32_t v[8]) {
+  int r = find_run(L, i0);
+  RunL R = L.runs[r];
+  if (i0 + 8 <= R.end) {
+    if (!R.bp) {
+      for (int j = 0; j < 8; j++) v[j] = uint32_t(R.data);
+      return;
+    }
+    const int64_t rel = i0 - R.start;
+    if ((rel & 7) == 0 && w <= 16) {  // whole aligned group: one or two 8-byte loads
+      const uint8_t* p = img + R.data + (rel >> 3) * w;
+      const uint64_t q = ld64_masked(p, end);
+      const uint64_t q2 = w > 8 ? ld64_masked(p + 8, end) : 0;
+      const uint32_t m = mask_w(w);
+      for (int j = 0; j < 8; j++) {
+        const int bit = j * w;
+        if (bit + w <= 64) v[j] = uint32_t(q >> bit) & m;
+        else if (bit >= 64) v[j] = uint32_t(q2 >> (bit - 64)) & m;
+        else v[j] = uint32_t((q >> bit) | (q2 << (64 - bit))) & m;
+      }
+      return;
+    }
+    for (int j = 0; j < 8; j++) v[j] = bp_value(img, end, R.data, rel + j, w);
+    return;
+  }
+  for (int j = 0; j < cnt; j++) {
+    const int64_t i = i0 + j;
+    while (i >= R.end && r + 1 < L.nruns) R = L.runs[++r];
+    v[j] = R.bp ? bp_value(img, end, R.data, i - R.start, w) : uint32_t(R.data);
+  }
+}
+
+// Expand values [t0, t1) of a stream whose tile checkpoint is `c`; calls sink(i0, v, cnt) for
+// every group of up to 8 values.  Must be called by the whole workgroup.
+template <class Sink>
+__device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& c, int64_t t0, int64_t t1,
+                              TileLds& L, Sink& sink) {
+  const uint8_t* end = img + e;
+  int64_t from = t0;
+  int64_t rs = c.run_start, rl = c.run_len, pos = c.next_hdr & 0x7fffffff;
+  int32_t data = c.data, bp = (c.next_hdr >> 31) & 1;
+  if (w == 0) {  // all zeros
+    for (int64_t i0 = t0 + 8 * int64_t(threadIdx.x); i0 < t1; i0 += 8 * kBlock) {
+      uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const int cnt = int(t1 - i0 < 8 ? t1 - i0 : 8);
+      sink(i0, v, cnt);
+    }
+    return;
+  }
+  while (from < t1) {
+    if (threadIdx.x == 0) build_runs(img, w, t1, rs, rl, data, bp, pos, L);
+    __syncthreads();
+    const int64_t seg_end = L.seg_end;
+    for (int64_t i0 = from + 8 * int64_t(threadIdx.x); i0 < seg_end; i0 += 8 * kBlock) {
+      uint32_t v[8];
+      const int cnt = int(seg_end - i0 < 8 ? seg_end - i0 : 8);
+      decode8(img, end, w, L, i0, cnt, v);
+      sink(i0, v, cnt);
+    }
+    // continue after the last listed run
+    const RunL last = L.runs[L.nruns - 1];
+    from = seg_end;
+    rs = last.start;
+    rl = int64_t(seg_end) - last.start;
+    data = last.data;
+    bp = last.bp;
+    pos = L.next_pos;
+    __syncthreads();
+    if (from < t1) {
+      // the last run may continue past seg_end only if it was clipped by t1, which ends the loop;
+      // otherwise the next run starts exactly at seg_end: restart from the header at next_pos with
+      // an empty pseudo-run.
+      rs = from;
+      rl = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_levels: definition / repetition level bytes (decodePackedArray into uint8 slots).
+// ------------------------------------------------------------------------------------------------
+struct LevelSink {
+  uint8_t* out;
+  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+    if (cnt == 8) {
+      uint64_t x = 0;
+      for (int j = 0; j < 8; j++) x |= uint64_t(v[j] & 0xff) << (8 * j);
+      __builtin_memcpy(out + i0, &x, 8);
+    } else {
+      for (int j = 0; j < cnt; j++) out[i0 + j] = uint8_t(v[j]);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_levels(DevBatch b, const Tile* tiles) {
+  __shared__ TileLds L;
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const uint8_t* img = b.payload + P.image_off;
+  const int64_t n = P.num_values;
+  const int64_t t0 = int64_t(t.k) * kHybridTile;
+  const int64_t t1 = t0 + kHybridTile < n ? t0 + kHybridTile : n;
+  if (t0 >= n) return;
+  if (C.max_rep > 0) {
+    LevelSink sink{C.rep_levels + P.level_base};
+    expand_hybrid(img, S.rep_e, bits_len32(uint32_t(C.max_rep)), b.ckpts[P.ck_rep + t.k], t0, t1, L, sink);
+    __syncthreads();
+  }
+  if (C.max_def > 0) {
+    LevelSink sink{C.def_levels + P.level_base};
+    expand_hybrid(img, S.def_e, bits_len32(uint32_t(C.max_def)), b.ckpts[P.ck_def + t.k], t0, t1, L, sink);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_dict: dictDecoder.decodeValues (type_dict.go:40-60): bounds-checked gather of dictionary
+// entries; the dictionary is staged in LDS when it fits (kDictLdsMax).
+// ------------------------------------------------------------------------------------------------
+template <int VS>
+struct DictSink {
+  const uint8_t* dict;  // LDS or global
+  uint8_t* out;         // chunk values + value_base * vs
+  uint32_t K;
+  int vs;               // runtime size when VS == 0
+  int64_t* first_bad;   // per-thread min failing index
+  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+    bool ok = true;
+    for (int j = 0; j < cnt; j++)
+      if (v[j] >= K) {
+        if (i0 + j < *first_bad) *first_bad = i0 + j;
+        ok = false;
+      }
+    if constexpr (VS == 4) {
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(dict);
+      if (ok && cnt == 8) {
+        uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
+        uint4 c = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
+        __builtin_memcpy(out + i0 * 4, &a, 16);
+        __builtin_memcpy(out + i0 * 4 + 16, &c, 16);
+      } else {
+        for (int j = 0; j < cnt; j++)
+          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 4, &d[v[j]], 4);
+      }
+    } else if constexpr (VS == 8) {
+      const uint64_t* d = reinterpret_cast<const uint64_t*>(dict);
+      for (int j = 0; j < cnt; j += 2) {
+        if (ok && j + 1 < cnt) {
+          uint64_t pr[2] = {d[v[j]], d[v[j + 1]]};
+          __builtin_memcpy(out + (i0 + j) * 8, pr, 16);
+        } else {
+          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 8, &d[v[j]], 8);
+          if (j + 1 < cnt && v[j + 1] < K) __builtin_memcpy(out + (i0 + j + 1) * 8, &d[v[j + 1]], 8);
+        }
+      }
+    } else {
+      for (int j = 0; j < cnt; j++) {
+        if (v[j] >= K) continue;
+        const uint8_t* src = dict + int64_t(v[j]) * vs;
+        uint8_t* dst = out + (i0 + j) * vs;
+        int k = 0;
+        for (; k + 4 <= vs; k += 4) {
+          uint32_t x;
+          __builtin_memcpy(&x, src + k, 4);
+          __builtin_memcpy(dst + k, &x, 4);
+        }
+        for (; k < vs; k++) dst[k] = src[k];
+      }
+    }
+  }
+};
+
+template <int VS, bool LDS>
+__global__ __launch_bounds__(256) void k_dict(DevBatch b, const Tile* tiles) {
+  __shared__ TileLds L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dict_lds[];
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const int64_t t0 = int64_t(t.k) * kHybridTile;
+  int64_t t1 = t0 + kHybridTile;
+  if (t1 > S.val_limit) t1 = S.val_limit;
+  if (t0 >= t1) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const int vs = P.value_size;
+  uint32_t K = 0;
+  const uint8_t* dict = nullptr;
+  if (P.dict_page >= 0) {
+    const PageState DS = b.states[P.dict_page];
+    if (DS.err == kNoError) {
+      K = uint32_t(DS.dict_n);
+      dict = b.payload + b.pages[P.dict_page].image_off;
+    }
+  }
+  if constexpr (LDS) {
+    const int64_t bytes = int64_t(K) * vs;
+    const int64_t words = (bytes + 3) >> 2;
+    for (int64_t i = threadIdx.x; i < words; i += kBlock) {
+      uint32_t x = 0;
+      const int64_t o = i * 4;
+      if (o + 4 <= bytes) __builtin_memcpy(&x, dict + o, 4);
+      else for (int k = 0; o + k < bytes; k++) x |= uint32_t(dict[o + k]) << (8 * k);
+      reinterpret_cast<uint32_t*>(dict_lds)[i] = x;
+    }
+    dict = dict_lds;
+    __syncthreads();
+  }
+  const uint8_t* img = b.payload + P.image_off;
+  int64_t first_bad = INT64_MAX;
+  DictSink<VS> sink{dict, C.values + S.value_base * vs, K, vs, &first_bad};
+  expand_hybrid(img, S.val_e, S.width, b.ckpts[P.ck_val + t.k], t0, t1, L, sink);
+  if (first_bad != INT64_MAX)
+    atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, PQH_ERR_DICT_INDEX));
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_rle_bool: booleanRLEDecoder.decodeValues (type_boolean.go:109-120): value == 1.
+// ------------------------------------------------------------------------------------------------
+struct BoolSink {
+  uint8_t* out;
+  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+    if (cnt == 8) {
+      uint64_t x = 0;
+      for (int j = 0; j < 8; j++) x |= uint64_t(v[j] == 1) << (8 * j);
+      __builtin_memcpy(out + i0, &x, 8);
+    } else {
+      for (int j = 0; j < cnt; j++) out[i0 + j] = uint8_t(v[j] == 1);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_rle_bool(DevBatch b, const Tile* tiles) {
+  __shared__ TileLds L;
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const int64_t t0 = int64_t(t.k) * kHybridTile;
+  int64_t t1 = t0 + kHybridTile;
+  if (t1 > S.val_limit) t1 = S.val_limit;
+  if (t0 >= t1) return;
+  const DevChunk C = b.chunks[P.chunk];
+  BoolSink sink{C.values + S.value_base};
+  expand_hybrid(b.payload + P.image_off, S.val_e, 1, b.ckpts[P.ck_val + t.k], t0, t1, L, sink);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_copy: PLAIN fixed-width values (int32/int64/float/double/INT96/FLBA): little-endian copy of
+// notNull * size bytes (type_int32.go:21-31 ...), 16-byte vector loads and stores.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_copy(DevBatch b, const Tile* tiles) {
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const int64_t total = int64_t(S.val_limit) * P.value_size;
+  const int64_t c0 = int64_t(t.k) * kCopyTileBytes;
+  int64_t c1 = c0 + kCopyTileBytes;
+  if (c1 > total) c1 = total;
+  if (c0 >= c1) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const uint8_t* src = b.payload + P.image_off + S.val_s;
+  uint8_t* dst = C.values + S.value_base * P.value_size;
+  int64_t o = c0 + 16 * int64_t(threadIdx.x);
+  for (; o + 16 * 3 * kBlock + 16 <= c1; o += 16 * 4 * kBlock) {  // 4 independent 16-B loads in flight
+    uint4 a, bb, c, d;
+    __builtin_memcpy(&a, src + o, 16);
+    __builtin_memcpy(&bb, src + o + 16 * kBlock, 16);
+    __builtin_memcpy(&c, src + o + 32 * kBlock, 16);
+    __builtin_memcpy(&d, src + o + 48 * kBlock, 16);
+    __builtin_memcpy(dst + o, &a, 16);
+    __builtin_memcpy(dst + o + 16 * kBlock, &bb, 16);
+    __builtin_memcpy(dst + o + 32 * kBlock, &c, 16);
+    __builtin_memcpy(dst + o + 48 * kBlock, &d, 16);
+  }
+  for (; o < c1; o += 16 * kBlock) {
+    if (o + 16 <= c1) {
+      uint4 a;
+      __builtin_memcpy(&a, src + o, 16);
+      __builtin_memcpy(dst + o, &a, 16);
+    } else {
+      for (int64_t k = o; k < c1; k++) dst[k] = src[k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_bool_plain: booleanPlainDecoder (type_boolean.go:43-69), LSB-first bits -> 0/1 bytes.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
+
+__global__ __launch_bounds__(256) void k_bool_plain(DevBatch b, const Tile* tiles) {
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const int64_t lim = S.val_limit;
+  const int64_t v0 = int64_t(t.k) * kBoolTile + int64_t(threadIdx.x) * 128;
+  if (v0 >= lim) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const uint8_t* src = b.payload + P.image_off + S.val_s + (v0 >> 3);
+  uint8_t* dst = C.values + S.value_base + v0;
+  uint8_t in[16];
+  __builtin_memcpy(in, src, 16);
+  if (v0 + 128 <= lim) {
+    for (int q = 0; q < 8; q++) {
+      uint4 o;
+      o.x = nibble_bytes(in[2 * q] & 15);
+      o.y = nibble_bytes(in[2 * q] >> 4);
+      o.z = nibble_bytes(in[2 * q + 1] & 15);
+      o.w = nibble_bytes(in[2 * q + 1] >> 4);
+      __builtin_memcpy(dst + 16 * q, &o, 16);
+    }
+  } else {
+    for (int64_t j = 0; v0 + j < lim; j++) dst[j] = (in[j >> 3] >> (j & 7)) & 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_prologue(const DevBatch& b, hipStream_t s) {
+  if (b.num_pages <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prologue, dim3((b.num_pages + 3) / 4), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(const DevBatch& b, hipStream_t s) {
+  if (b.num_chunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scan, dim3(b.num_chunks), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_levels(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_levels, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_bool_plain(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bool_plain, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_dict(const DevBatch& b, const Tile* tiles, int32_t n, int32_t value_size, bool lds, size_t lds_bytes,
+                       hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const size_t shm = lds ? (lds_bytes > 16 ? lds_bytes : 16) : 0;
+  if (value_size == 4) {
+    if (lds) hipLaunchKernelGGL((k_dict<4, true>), dim3(n), dim3(256), shm, s, b, tiles);
+    else hipLaunchKernelGGL((k_dict<4, false>), dim3(n), dim3(256), 0, s, b, tiles);
+  } else if (value_size == 8) {
+    if (lds) hipLaunchKernelGGL((k_dict<8, true>), dim3(n), dim3(256), shm, s, b, tiles);
+    else hipLaunchKernelGGL((k_dict<8, false>), dim3(n), dim3(256), 0, s, b, tiles);
+  } else {
+    if (lds) hipLaunchKernelGGL((k_dict<0, true>), dim3(n), dim3(256), shm, s, b, tiles);
+    else hipLaunchKernelGGL((k_dict<0, false>), dim3(n), dim3(256), 0, s, b, tiles);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rle_bool(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rle_bool, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+}  // namespace pqhip

@@ -523,6 +523,7 @@ int pqg_write(const pqg_schema_element* schema, int32_t num_schema, const pqg_co
   std::atomic<int64_t> next{0};
   int nt = opt->num_threads > 0 ? opt->num_threads : int(std::thread::hardware_concurrency());
   if (nt < 1) nt = 1;
+  if (nt > 16) nt = 16;  // the GPU box's CPU share
   if (nt > nchunks) nt = int(std::max<int64_t>(1, nchunks));
   auto work = [&]() {
     for (;;) {

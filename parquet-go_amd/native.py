@@ -1,0 +1,357 @@
+"""ctypes declaration of the C-ABI in include/pqhip.h (libpqhip.so) and thin RAII wrappers.
+
+Every symbol bound here is declared in include/pqhip.h; tests/test_abi.py checks the library
+exports all of them.  There is no CPU fallback: constructing a Context without a HIP device
+raises, and the decode always runs through the HIP kernels.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+i32, i64, u32, f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double
+vp, cp = ctypes.c_void_p, ctypes.c_char_p
+
+# status codes (pqh_status)
+STATUS = {
+    0: "OK", 1: "EOF", 2: "UNEXPECTED_EOF", 3: "VARINT_OVERFLOW", 4: "INT32_RANGE", 5: "EMPTY_BP_RUN",
+    6: "EMPTY_RLE_RUN", 7: "RLE_VALUE_TOO_LARGE", 8: "READER_NOT_INITIALIZED", 9: "DICT_BIT_WIDTH",
+    10: "DICT_INDEX", 11: "DELTA_BLOCK_SIZE", 12: "DELTA_MINIBLOCKS", 13: "DELTA_VALUE_COUNT",
+    14: "DELTA_BIT_WIDTH", 15: "DELTA_STREAM", 16: "NEGATIVE_LENGTH", 17: "NEGATIVE_DLBA_LENGTH",
+    18: "DBA_PREFIX", 19: "DBA_COUNT", 20: "INT96_SHORT", 21: "UNSUPPORTED", 22: "PAGE_HEADER",
+    23: "DECOMPRESS", 24: "CRC", 25: "THRIFT", 26: "IO", 27: "ARG", 28: "HIP", 29: "NOMEM", 30: "SCHEMA",
+    31: "DICT_PAGE", 32: "NO_DEVICE", 33: "NOT_IMPLEMENTED",
+}
+OK = 0
+NOT_IMPLEMENTED = 33
+CTX_PROFILE = 1
+PAYLOAD_PAD = 256
+
+
+class Column(ctypes.Structure):
+    _fields_ = [("physical_type", i32), ("type_length", i32), ("max_def", i32), ("max_rep", i32)]
+
+
+class Page(ctypes.Structure):
+    _fields_ = [("image_offset", i64), ("image_len", i32), ("page_type", i32), ("num_values", i32),
+                ("encoding", i32), ("def_levels_byte_length", i32), ("rep_levels_byte_length", i32),
+                ("chunk", i32), ("reserved", i32)]
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [("column", Column), ("first_page", i32), ("num_pages", i32), ("host_status", i32),
+                ("reserved", i32)]
+
+
+class ChunkOut(ctypes.Structure):
+    _fields_ = [("num_values", i64), ("num_non_null", i64), ("value_size", i32), ("status", i32),
+                ("error_page", i32), ("error_phase", i32), ("error_index", i64), ("values", vp),
+                ("offsets", vp), ("bytes", vp), ("num_bytes", i64), ("def_levels", vp), ("rep_levels", vp)]
+
+
+class PageResult(ctypes.Structure):
+    _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_non_null", i32), ("reserved", i32),
+                ("value_offset", i64), ("level_offset", i64)]
+
+
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", i32), ("work_items", i32), ("total_ms", f64),
+                ("bytes_read", f64), ("bytes_written", f64)]
+
+
+# (name, restype, argtypes) for every function of include/pqhip.h
+PROTOTYPES = [
+    ("pqh_abi_version", ctypes.c_int, []),
+    ("pqh_device_count", ctypes.c_int, [ctypes.POINTER(i32)]),
+    ("pqh_ctx_create", ctypes.c_int, [i32, u32, ctypes.POINTER(vp)]),
+    ("pqh_ctx_destroy", None, [vp]),
+    ("pqh_last_error", cp, [vp]),
+    ("pqh_ctx_stream", vp, [vp]),
+    ("pqh_malloc", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
+    ("pqh_free", ctypes.c_int, [vp, vp]),
+    ("pqh_host_alloc", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
+    ("pqh_host_free", ctypes.c_int, [vp, vp]),
+    ("pqh_memcpy_h2d", ctypes.c_int, [vp, vp, vp, ctypes.c_size_t]),
+    ("pqh_memcpy_d2h", ctypes.c_int, [vp, vp, vp, ctypes.c_size_t]),
+    ("pqh_sync", ctypes.c_int, [vp]),
+    ("pqh_batch_create", ctypes.c_int, [vp, ctypes.POINTER(Chunk), i32, ctypes.POINTER(Page), i32, vp, i64,
+                                        ctypes.POINTER(vp)]),
+    ("pqh_batch_run", ctypes.c_int, [vp]),
+    ("pqh_batch_sync", ctypes.c_int, [vp]),
+    ("pqh_batch_chunk_out", ctypes.c_int, [vp, i32, ctypes.POINTER(ChunkOut)]),
+    ("pqh_batch_page_results", ctypes.c_int, [vp, ctypes.POINTER(PageResult), i32]),
+    ("pqh_batch_kernel_stats", ctypes.c_int, [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]),
+    ("pqh_batch_reset_stats", ctypes.c_int, [vp]),
+    ("pqh_batch_traffic", ctypes.c_int, [vp, ctypes.POINTER(f64), ctypes.POINTER(f64)]),
+    ("pqh_batch_destroy", None, [vp]),
+    ("pqh_file_open", ctypes.c_int, [cp, ctypes.POINTER(vp)]),
+    ("pqh_file_open_memory", ctypes.c_int, [vp, i64, ctypes.POINTER(vp)]),
+    ("pqh_file_close", None, [vp]),
+    ("pqh_file_error", cp, [vp]),
+    ("pqh_file_num_row_groups", i32, [vp]),
+    ("pqh_file_num_rows", i64, [vp]),
+    ("pqh_file_row_group_num_rows", i64, [vp, i32]),
+    ("pqh_file_num_columns", i32, [vp]),
+    ("pqh_file_column", ctypes.c_int, [vp, i32, ctypes.POINTER(Column), ctypes.c_char_p, i32]),
+    ("pqh_file_load", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]),
+    ("pqh_host_batch_num_chunks", i32, [vp]),
+    ("pqh_host_batch_num_pages", i32, [vp]),
+    ("pqh_host_batch_chunks", ctypes.POINTER(Chunk), [vp]),
+    ("pqh_host_batch_pages", ctypes.POINTER(Page), [vp]),
+    ("pqh_host_batch_payload", ctypes.POINTER(ctypes.c_uint8), [vp]),
+    ("pqh_host_batch_payload_bytes", i64, [vp]),
+    ("pqh_host_batch_decompress_seconds", f64, [vp]),
+    ("pqh_host_batch_free", None, [vp]),
+    ("pqh_batch_create_from_host", ctypes.c_int, [vp, vp, ctypes.POINTER(vp)]),
+]
+
+
+def bind(L):
+    for name, res, args in PROTOTYPES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+class PqhError(RuntimeError):
+    def __init__(self, status, msg=""):
+        self.status = status
+        super().__init__(f"{STATUS.get(status, status)}: {msg}")
+
+
+def _check(rc, msg=""):
+    if rc != OK:
+        raise PqhError(rc, msg)
+
+
+def device_count():
+    n = i32()
+    _lib.hip().pqh_device_count(ctypes.byref(n))
+    return n.value
+
+
+class Context:
+    """One HIP device + stream (pqh_ctx)."""
+
+    def __init__(self, device=0, profile=False):
+        L = _lib.hip()
+        self.L = L
+        h = vp()
+        rc = L.pqh_ctx_create(device, CTX_PROFILE if profile else 0, ctypes.byref(h))
+        if rc != OK:
+            raise PqhError(rc, (L.pqh_last_error(None) or b"").decode())
+        self.h = h
+        self.device = device
+
+    def error(self):
+        return (self.L.pqh_last_error(self.h) or b"").decode()
+
+    def check(self, rc):
+        _check(rc, self.error())
+
+    def sync(self):
+        self.check(self.L.pqh_sync(self.h))
+
+    def malloc(self, n):
+        p = vp()
+        self.check(self.L.pqh_malloc(self.h, ctypes.byref(p), n))
+        return p.value
+
+    def free(self, p):
+        if p:
+            self.L.pqh_free(self.h, p)
+
+    def h2d(self, dst, src_ptr, n):
+        self.check(self.L.pqh_memcpy_h2d(self.h, dst, src_ptr, n))
+
+    def d2h_array(self, src, n, dtype=np.uint8):
+        out = np.empty(n, dtype=dtype)
+        nbytes = out.nbytes
+        if nbytes:
+            self.check(self.L.pqh_memcpy_d2h(self.h, out.ctypes.data, src, nbytes))
+            self.sync()
+        return out
+
+    def close(self):
+        if self.h:
+            self.L.pqh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostBatch:
+    """Result of the host page walker (pqh_file_load)."""
+
+    def __init__(self, L, h):
+        self.L = L
+        self.h = h
+
+    @property
+    def num_chunks(self):
+        return self.L.pqh_host_batch_num_chunks(self.h)
+
+    @property
+    def num_pages(self):
+        return self.L.pqh_host_batch_num_pages(self.h)
+
+    def chunks(self):
+        p = self.L.pqh_host_batch_chunks(self.h)
+        return [p[i] for i in range(self.num_chunks)]
+
+    def pages(self):
+        p = self.L.pqh_host_batch_pages(self.h)
+        return [p[i] for i in range(self.num_pages)]
+
+    def payload(self):
+        n = self.L.pqh_host_batch_payload_bytes(self.h)
+        return np.ctypeslib.as_array(self.L.pqh_host_batch_payload(self.h), shape=(n + PAYLOAD_PAD,))
+
+    @property
+    def payload_bytes(self):
+        return self.L.pqh_host_batch_payload_bytes(self.h)
+
+    @property
+    def decompress_seconds(self):
+        return self.L.pqh_host_batch_decompress_seconds(self.h)
+
+    def close(self):
+        if self.h:
+            self.L.pqh_host_batch_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class File:
+    """Footer + page walker (pqh_file_*): no GPU needed."""
+
+    def __init__(self, source):
+        L = _lib.hip()
+        self.L = L
+        h = vp()
+        if isinstance(source, (bytes, bytearray, memoryview)):
+            self._buf = np.frombuffer(bytes(source), dtype=np.uint8)
+            rc = L.pqh_file_open_memory(self._buf.ctypes.data, len(self._buf), ctypes.byref(h))
+        else:
+            rc = L.pqh_file_open(str(source).encode(), ctypes.byref(h))
+        self.h = h
+        if rc != OK:
+            msg = (L.pqh_file_error(h) or b"").decode() if h else ""
+            self.close()
+            raise PqhError(rc, msg)
+
+    @property
+    def num_row_groups(self):
+        return self.L.pqh_file_num_row_groups(self.h)
+
+    @property
+    def num_rows(self):
+        return self.L.pqh_file_num_rows(self.h)
+
+    def row_group_num_rows(self, rg):
+        return self.L.pqh_file_row_group_num_rows(self.h, rg)
+
+    def columns(self):
+        out = []
+        buf = ctypes.create_string_buffer(1024)
+        for i in range(self.L.pqh_file_num_columns(self.h)):
+            c = Column()
+            _check(self.L.pqh_file_column(self.h, i, ctypes.byref(c), buf, 1024))
+            out.append((buf.value.decode(), c.physical_type, c.type_length, c.max_def, c.max_rep))
+        return out
+
+    def load(self, rg_begin, rg_end, columns, validate_crc=False):
+        cols = (i32 * len(columns))(*columns)
+        h = vp()
+        rc = self.L.pqh_file_load(self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc), ctypes.byref(h))
+        if rc != OK:
+            raise PqhError(rc, (self.L.pqh_file_error(self.h) or b"").decode())
+        return HostBatch(self.L, h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.pqh_file_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    """A planned device decode of a set of chunks (pqh_batch)."""
+
+    def __init__(self, ctx, h, owned=None):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.h = h
+        self._owned = owned  # device payload owned by the caller wrapper
+
+    @classmethod
+    def from_host(cls, ctx, hb):
+        h = vp()
+        ctx.check(ctx.L.pqh_batch_create_from_host(ctx.h, hb.h, ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_tables(cls, ctx, chunks, pages, d_payload, payload_bytes):
+        ch = (Chunk * len(chunks))(*chunks)
+        pg = (Page * len(pages))(*pages)
+        h = vp()
+        ctx.check(ctx.L.pqh_batch_create(ctx.h, ch, len(chunks), pg, len(pages), d_payload, payload_bytes,
+                                         ctypes.byref(h)))
+        return cls(ctx, h)
+
+    def run(self):
+        self.ctx.check(self.L.pqh_batch_run(self.h))
+
+    def sync(self):
+        self.ctx.check(self.L.pqh_batch_sync(self.h))
+
+    def chunk_out(self, i):
+        o = ChunkOut()
+        self.ctx.check(self.L.pqh_batch_chunk_out(self.h, i, ctypes.byref(o)))
+        return o
+
+    def page_results(self, n):
+        arr = (PageResult * max(n, 1))()
+        self.ctx.check(self.L.pqh_batch_page_results(self.h, arr, n))
+        return [arr[i] for i in range(n)]
+
+    def kernel_stats(self):
+        arr = (KernelStat * 32)()
+        n = i32()
+        self.ctx.check(self.L.pqh_batch_kernel_stats(self.h, arr, 32, ctypes.byref(n)))
+        return [arr[i] for i in range(n.value)]
+
+    def reset_stats(self):
+        self.L.pqh_batch_reset_stats(self.h)
+
+    def traffic(self):
+        r, w = f64(), f64()
+        self.ctx.check(self.L.pqh_batch_traffic(self.h, ctypes.byref(r), ctypes.byref(w)))
+        return r.value, w.value
+
+    def close(self):
+        if self.h:
+            self.L.pqh_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,161 @@
+"""Host-side mirror of the reference reader interface on top of the C-ABI.
+
+Mirrors github.com/fraugster/parquet-go's FileReader (file_reader.go:32-351) for the decode path:
+  NewFileReader(source, *columns)   -> FileReader   (NewFileReaderWithOptions + WithColumns)
+  FileReader.RowGroupCount()                          (file_reader.go:242-245)
+  FileReader.NumRows()                                (file_reader.go:247-250)
+  FileReader.SeekToRowGroup(i) / SkipRowGroup()       (file_reader.go:187-198, 275-277)
+  FileReader.PreLoad()                                (file_reader.go:280-288): the row group's
+      chunks are walked on the host (thrift + codecs) and decoded on the GPU in ONE batch
+  FileReader.ReadColumns()          -> {path: ColumnData}: columnar results of readValues for
+      every page of the chunk (values, dLevel, rLevel) — the "throughput path" of SURVEY.md §8(b)
+Errors follow the reference: any page error fails the read of that chunk and raises DecodeError
+carrying the status, phase, index and page of the FIRST error in decode order.
+"""
+import numpy as np
+
+from . import native
+
+BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
+_DTYPE = {INT32: np.int32, INT64: np.int64, FLOAT: np.float32, DOUBLE: np.float64, BOOLEAN: np.uint8}
+
+
+class DecodeError(RuntimeError):
+    def __init__(self, path, status, phase=0, index=0, page=-1):
+        self.path, self.status, self.phase, self.index, self.page = path, status, phase, index, page
+        super().__init__(f"{path}: {native.STATUS.get(status, status)} (phase {phase}, index {index}, page {page})")
+
+
+class ColumnData:
+    """One decoded column chunk (dense not-null values + level bytes), host copy."""
+
+    def __init__(self, path, column, out, page_results, ctx):
+        self.path = path
+        self.physical_type, self.type_length, self.max_def, self.max_rep = column
+        self.status = out.status
+        self.error_page, self.error_phase, self.error_index = out.error_page, out.error_phase, out.error_index
+        self.num_values = out.num_values
+        self.num_non_null = out.num_non_null
+        self.value_size = out.value_size
+        self.pages = page_results
+        self.values = None
+        self.def_levels = None
+        self.rep_levels = None
+        self.offsets = None
+        self.data = None
+        if out.status != native.OK:
+            return
+        if out.value_size > 0:
+            raw = ctx.d2h_array(out.values, out.num_non_null * out.value_size)
+            if self.physical_type in _DTYPE:
+                self.values = raw.view(_DTYPE[self.physical_type])
+            else:
+                self.values = raw.reshape(-1, out.value_size) if out.value_size else raw
+        elif out.offsets:
+            self.offsets = ctx.d2h_array(out.offsets, out.num_non_null + 1, np.int64)
+            self.data = ctx.d2h_array(out.bytes, out.num_bytes)
+        if out.def_levels:
+            self.def_levels = ctx.d2h_array(out.def_levels, out.num_values)
+        if out.rep_levels:
+            self.rep_levels = ctx.d2h_array(out.rep_levels, out.num_values)
+
+    def raise_for_status(self):
+        if self.status != native.OK:
+            raise DecodeError(self.path, self.status, self.error_phase, self.error_index, self.error_page)
+        return self
+
+    def to_pylist(self):
+        """Values as Python objects in reference order (bytes for byte arrays / FLBA / INT96)."""
+        if self.values is not None:
+            if self.values.ndim == 2:
+                return [bytes(r) for r in self.values]
+            if self.physical_type == BOOLEAN:
+                return [bool(v) for v in self.values]
+            return self.values.tolist()
+        if self.offsets is None:
+            return []
+        d = self.data.tobytes()
+        return [d[self.offsets[i]:self.offsets[i + 1]] for i in range(len(self.offsets) - 1)]
+
+
+def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, return_batch=False):
+    """Walk (host) and decode (GPU) the chunks of `columns` in row groups [rg_begin, rg_end).
+
+    Returns a list of ColumnData in (row group, column) order."""
+    hb = file.load(rg_begin, rg_end, columns, validate_crc)
+    batch = native.Batch.from_host(ctx, hb)
+    batch.run()
+    batch.sync()
+    cols = file.columns()
+    res = batch.page_results(hb.num_pages)
+    out = []
+    chunks = hb.chunks()
+    for i, ch in enumerate(chunks):
+        path, pt, tl, md, mr = cols[columns[i % len(columns)]]
+        pr = [res[p] for p in range(ch.first_page, ch.first_page + ch.num_pages)]
+        o = batch.chunk_out(i)
+        if ch.host_status != native.OK and o.status == native.OK:
+            o.status = ch.host_status
+        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx))
+    if return_batch:
+        return out, batch, hb
+    batch.close()
+    hb.close()
+    return out
+
+
+class FileReader:
+    def __init__(self, source, *columns, device=0, validate_crc=False, ctx=None):
+        self.file = native.File(source)
+        self.ctx = ctx or native.Context(device)
+        self.validate_crc = validate_crc
+        allc = self.file.columns()
+        self._paths = [c[0] for c in allc]
+        if columns:
+            sel = []
+            for c in columns:
+                if isinstance(c, int):
+                    sel.append(c)
+                else:
+                    sel.extend(i for i, p in enumerate(self._paths) if p == c or p.startswith(c + "."))
+            self.selected = sorted(set(sel))
+        else:
+            self.selected = list(range(len(allc)))
+        self.row_group = 0
+        self._loaded = None
+
+    @classmethod
+    def NewFileReader(cls, source, *columns, **kw):
+        return cls(source, *columns, **kw)
+
+    def RowGroupCount(self):
+        return self.file.num_row_groups
+
+    def NumRows(self):
+        return self.file.num_rows
+
+    def Columns(self):
+        return [self._paths[i] for i in self.selected]
+
+    def SeekToRowGroup(self, rg):
+        if rg < 0 or rg >= self.RowGroupCount():
+            raise IndexError("row group out of range")
+        self.row_group = rg
+        self._loaded = None
+
+    def SkipRowGroup(self):
+        self.row_group += 1
+        self._loaded = None
+
+    def PreLoad(self):
+        if self._loaded is None:
+            self._loaded = decode_chunks(self.ctx, self.file, self.row_group, self.row_group + 1, self.selected,
+                                         self.validate_crc)
+        return self
+
+    def ReadColumns(self):
+        self.PreLoad()
+        return {c.path: c.raise_for_status() for c in self._loaded}
+
+    def close(self):
+        self.file.close()

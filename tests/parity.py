@@ -1,0 +1,81 @@
+"""Chunk-level comparison of the product (C-ABI / HIP) against the CPU oracle."""
+import numpy as np
+
+from oracle import oracle as O
+
+
+class Expected:
+    def __init__(self):
+        self.status = 0
+        self.phase = 0
+        self.index = 0
+        self.page = -1
+        self.host_error = False
+        self.values = b""
+        self.offsets = None
+        self.data = b""
+        self.def_levels = None
+        self.rep_levels = None
+        self.nn = 0
+        self.n = 0
+
+
+def oracle_chunk(fr, rg, ci):
+    """readChunk + readValues for every page (oracle)."""
+    e = Expected()
+    ch = fr.read_chunk(rg, ci)
+    if ch.status:
+        e.status = ch.status
+        e.host_error = True
+        return e
+    col = ch.column
+    res = O.decode_chunk(ch)
+    vals, defs, reps, offs, data = [], [], [], [], []
+    base = 0
+    for i, r in enumerate(res):
+        if r.status and e.status == 0:
+            e.status, e.phase, e.index, e.page = r.status, r.phase, r.index, i
+        e.n += r.num_values
+        e.nn += r.nn
+        if r.def_levels is not None:
+            defs.append(r.def_levels)
+        elif col.max_def > 0:
+            defs.append(np.zeros(0, np.uint8))
+        if r.rep_levels is not None:
+            reps.append(r.rep_levels)
+        if r.offsets is not None:
+            offs.append(r.offsets[1:] + base)
+            base += len(r.values)
+            data.append(r.values)
+        else:
+            vals.append(r.values)
+    e.values = b"".join(vals)
+    e.data = b"".join(data)
+    if offs:
+        e.offsets = np.concatenate([np.zeros(1, np.int64)] + offs)
+    e.def_levels = np.concatenate(defs) if defs else None
+    e.rep_levels = np.concatenate(reps) if reps else None
+    return e
+
+
+def assert_chunk(gpu, exp, where=""):
+    """Bit-exact comparison of one decoded chunk; error status must agree."""
+    if exp.status:
+        assert gpu.status != 0, f"{where}: oracle fails with {exp.status} but the GPU decoded the chunk"
+        if not exp.host_error:
+            assert (gpu.status, gpu.error_phase, gpu.error_index) == (exp.status, exp.phase, exp.index), \
+                f"{where}: first error differs gpu={(gpu.status, gpu.error_phase, gpu.error_index)} " \
+                f"oracle={(exp.status, exp.phase, exp.index)}"
+        return
+    assert gpu.status == 0, f"{where}: GPU status {gpu.status} phase {gpu.error_phase} idx {gpu.error_index}"
+    assert gpu.num_non_null == exp.nn, where
+    if gpu.values is not None:
+        got = gpu.values.view(np.uint8).tobytes()
+        assert got == exp.values, f"{where}: values differ (len {len(got)} vs {len(exp.values)})"
+    else:
+        assert np.array_equal(gpu.offsets, exp.offsets), f"{where}: offsets differ"
+        assert gpu.data.tobytes() == exp.data, f"{where}: byte data differs"
+    if exp.def_levels is not None:
+        assert np.array_equal(gpu.def_levels, exp.def_levels), f"{where}: def levels differ"
+    if exp.rep_levels is not None:
+        assert np.array_equal(gpu.rep_levels, exp.rep_levels), f"{where}: rep levels differ"
