@@ -919,10 +919,12 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
   hybrid_t rdec, ddec; /* hybridDecoder(bits.Len16(max)) or constDecoder(0) when max == 0 */
   hybrid_new(&rdec, rw);
   hybrid_new(&ddec, dw);
+  /* phase-0 (page load) sub-steps, in the reference's order: 0 decoder selection
+   * (getValuesDecoder), 1 rDecoder.initSize, 2 dDecoder.initSize, 3 valuesDecoder.init */
   vdec_t v;
   int st = vdec_select(col, pg->encoding, &v);
   if (st) {
-    set_err(out, st, PQH_PHASE_LOAD, 2);
+    set_err(out, st, PQH_PHASE_LOAD, 0);
     return out->status;
   }
   rd_t r;
@@ -937,7 +939,7 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
       if (h->w == 0) continue; /* constDecoder / zero width: initSize reads nothing */
       uint8_t sz[4];
       if ((st = rd_read_full(&r, sz, 4))) {
-        set_err(out, st, PQH_PHASE_LOAD, k);
+        set_err(out, st, PQH_PHASE_LOAD, 1 + k);
         vdec_free(&v);
         return out->status;
       }
@@ -962,7 +964,7 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
     vals_len = img_len - rl - dl;
   }
   if ((st = vdec_init(&v, vals_base, vals_len))) {
-    set_err(out, st, PQH_PHASE_LOAD, 2);
+    set_err(out, st, PQH_PHASE_LOAD, 3);
     vdec_free(&v);
     return out->status;
   }

@@ -54,6 +54,7 @@ struct KernelRun {
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_levels", "k_copy", "k_bool_plain",
                               "k_dict",     "k_rle_bool"};
 constexpr int kNumKernels = 7;
+constexpr int kSideStreams = 4;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -148,13 +149,18 @@ struct pqh_batch {
   std::vector<double> k_read, k_written;  // per kernel kind algorithmic bytes of one run
   std::vector<hipEvent_t> event_pool;
   size_t event_next = 0;
+  std::vector<hipStream_t> side;  // side streams for the independent expand kernels
+  hipEvent_t fork = nullptr;
+  std::vector<hipEvent_t> join;
 };
 
 namespace {
 
 void free_batch(pqh_batch* b) {
-  for (auto& r : b->pending) (void)r;
   for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
+  for (hipStream_t st : b->side) hipStreamDestroy(st);
+  for (hipEvent_t e : b->join) hipEventDestroy(e);
+  if (b->fork) hipEventDestroy(b->fork);
   for (void* p : b->allocations) hipFree(p);
   if (b->owned_payload) hipFree(b->owned_payload);
 }
@@ -461,6 +467,21 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     delete b;
     return set_err(ctx, PQH_ERR_HIP, std::string("batch upload: ") + hipGetErrorString(e));
   }
+  b->side.assign(kSideStreams, nullptr);
+  b->join.assign(kSideStreams, nullptr);
+  for (int i = 0; i < kSideStreams; i++) {
+    if (hipStreamCreateWithFlags(&b->side[size_t(i)], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&b->join[size_t(i)], hipEventDisableTiming) != hipSuccess) {
+      free_batch(b);
+      delete b;
+      return set_err(ctx, PQH_ERR_HIP, "side stream creation failed");
+    }
+  }
+  if (hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) {
+    free_batch(b);
+    delete b;
+    return set_err(ctx, PQH_ERR_HIP, "event creation failed");
+  }
   b->stats.resize(kNumKernels);
   for (int k = 0; k < kNumKernels; k++) {
     memset(&b->stats[size_t(k)], 0, sizeof(pqh_kernel_stat));
@@ -479,38 +500,48 @@ int pqh_batch_run(pqh_batch* b) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size())};
   b->synced = false;
-  b->event_next = 0;
-  b->pending.clear();
-  auto timed = [&](int kind, int32_t items, auto&& fn) -> hipError_t {
+  auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
       e0 = next_event(b);
       e1 = next_event(b);
-      hipEventRecord(e0, s);
+      hipEventRecord(e0, st);
     }
-    hipError_t e = fn();
+    hipError_t e = fn(st);
     if (prof) {
-      hipEventRecord(e1, s);
+      hipEventRecord(e1, st);
       b->pending.push_back(KernelRun{kind, e0, e1, items});
     }
     return e;
   };
   hipError_t e;
-  e = timed(0, int32_t(b->pages.size()), [&] { return launch_prologue(d, s); });
-  if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), [&] { return launch_scan(d, s); });
+  e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
+  if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  // The expand kernels are independent of each other: fork them onto side streams so that their
+  // tails overlap, then join back into the context stream.
+  if (e == hipSuccess) e = hipEventRecord(b->fork, s);
+  int used = 0;
   for (auto& g : b->groups) {
     if (e != hipSuccess) break;
     if (g.tiles.empty()) continue;
     const Tile* t = b->d_tiles + g.offset;
     const int32_t n = int32_t(g.tiles.size());
+    hipStream_t st = b->side[size_t(used % kSideStreams)];
+    if (used < kSideStreams) e = hipStreamWaitEvent(st, b->fork, 0);
+    used++;
+    if (e != hipSuccess) break;
     switch (g.kernel) {
-      case 2: e = timed(2, n, [&] { return launch_levels(d, t, n, s); }); break;
-      case 3: e = timed(3, n, [&] { return launch_copy(d, t, n, s); }); break;
-      case 4: e = timed(4, n, [&] { return launch_bool_plain(d, t, n, s); }); break;
-      case 5: e = timed(5, n, [&] { return launch_dict(d, t, n, g.value_size, g.lds, g.shm, s); }); break;
-      case 6: e = timed(6, n, [&] { return launch_rle_bool(d, t, n, s); }); break;
+      case 2: e = timed(2, n, st, [&](hipStream_t x) { return launch_levels(d, t, n, x); }); break;
+      case 3: e = timed(3, n, st, [&](hipStream_t x) { return launch_copy(d, t, n, x); }); break;
+      case 4: e = timed(4, n, st, [&](hipStream_t x) { return launch_bool_plain(d, t, n, x); }); break;
+      case 5: e = timed(5, n, st, [&](hipStream_t x) { return launch_dict(d, t, n, g.value_size, g.lds, g.shm, x); }); break;
+      case 6: e = timed(6, n, st, [&](hipStream_t x) { return launch_rle_bool(d, t, n, x); }); break;
       default: break;
     }
+  }
+  for (int i = 0; i < used && i < kSideStreams && e == hipSuccess; i++) {
+    e = hipEventRecord(b->join[size_t(i)], b->side[size_t(i)]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, b->join[size_t(i)], 0);
   }
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   return PQH_OK;
@@ -535,6 +566,7 @@ int pqh_batch_sync(pqh_batch* b) {
     }
   }
   b->pending.clear();
+  b->event_next = 0;
   // algorithmic bytes of one run: page bytes read once, dictionaries once per
   // chunk, decoded bytes written; attributed to the kernel that moves them.
   double wr = 0;

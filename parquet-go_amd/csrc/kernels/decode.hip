@@ -162,7 +162,24 @@ __device__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, 
       const int64_t lim = (valid_end < N ? valid_end : N) - produced;
       if (!bp) {
         if (lane == 0 && data == match) cnt_lane += lim;
+      } else if (w == 1) {
+        // one bit per value: popcount 128 values per lane-load (16-byte loads, many in flight)
+        int64_t ones = 0;
+#pragma unroll 4
+        for (int64_t c = lane; c * 128 < lim; c += 64) {
+          const uint8_t* p = img + data + c * 16;
+          const uint64_t a = ld64_masked(p, end), b = ld64_masked(p + 8, end);
+          const int64_t nb = lim - c * 128;  // valid bits in this chunk
+          const uint64_t ma = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
+          const uint64_t mb = nb >= 128 ? ~0ull : nb <= 64 ? 0ull : ((1ull << (nb - 64)) - 1);
+          const int64_t valid = nb < 128 ? nb : 128;
+          const int64_t pc = __popcll(a & ma) + __popcll(b & mb);
+          ones += pc;
+          if (match == 0) cnt_lane += valid - pc;
+        }
+        if (match == 1) cnt_lane += ones;
       } else {
+#pragma unroll 4
         for (int64_t g = lane; g * 8 < lim; g += 64) {
           const uint64_t q = ld64_masked(img + data + g * w, end);
           const uint64_t q2 = w > 8 ? ld64_masked(img + data + g * w + 8, end) : 0;
