@@ -407,7 +407,7 @@ class FileReader:
     """The oracle's NewFileReader: footer + schema + page walker over a bytes object."""
 
     def __init__(self, data):
-        self.data = bytes(data)
+        self.data = data.tobytes() if hasattr(data, "tobytes") else bytes(data)
         if len(self.data) < 12 or self.data[:4] != b"PAR1" or self.data[-4:] != b"PAR1":
             raise ValueError("not a parquet file")
         flen = struct.unpack_from("<I", self.data, len(self.data) - 8)[0]

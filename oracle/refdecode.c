@@ -724,10 +724,16 @@ static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals,
           continue;
         }
         if (st) break; /* n == 0: EOF */
-        /* short read: the value is dropped; the reference only fails on the NEXT Read, i.e. it
-         * returns success with a nil slot when this is the last value.  The oracle (and the
-         * product) report that case as PQH_ERR_INT96_SHORT: a nil slot has no columnar form. */
-        st = PQH_ERR_INT96_SHORT;
+        /* short read: the value is dropped and the reader is at its end, so the NEXT iteration's
+         * Read returns io.EOF.  On the last value the reference returns success with a nil slot;
+         * the oracle (and the product) report that case as PQH_ERR_INT96_SHORT: a nil slot has no
+         * columnar form (documented divergence). */
+        if (i == nn - 1) {
+          st = PQH_ERR_INT96_SHORT;
+        } else {
+          st = PQH_ERR_EOF;
+          i++;
+        }
         break;
       }
       break;

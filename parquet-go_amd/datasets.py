@@ -16,7 +16,7 @@ def c1(rows=10_000_000, seed=1):
     dictionary = rng.integers(-2**31, 2**31 - 1, 4096).astype(np.int32)
     idx = np.random.default_rng(seed + 1).integers(0, 4096, rows)
     vals = dictionary[idx]
-    return W.flat([("v", W.Column(W.INT32, vals), W.REQUIRED)], rows, v2=False)
+    return W.flat([("v", W.Column(W.INT32, vals), W.REQUIRED)], rows, v2=False, as_array=True)
 
 
 def c2_columns(rows, seed=10):
@@ -42,14 +42,14 @@ def c2_columns(rows, seed=10):
 
 def c2(rows=100_000_000, row_groups=16, seed=10):
     per = -(-rows // row_groups)
-    return W.flat(c2_columns(rows, seed), per, v2=True)
+    return W.flat(c2_columns(rows, seed), per, v2=True, as_array=True)
 
 
 def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
     rng = np.random.default_rng(seed)
     ts = np.cumsum(1_000_000 + rng.integers(0, 4096, rows), dtype=np.int64) + 1_700_000_000_000_000_000
     return W.flat([("ts", W.Column(W.INT64, ts, encoding=W.DELTA_BINARY_PACKED, use_dict=False), W.REQUIRED)],
-                  rows_per_group, v2=False)
+                  rows_per_group, v2=False, as_array=True)
 
 
 WORKLOADS = {

@@ -240,7 +240,10 @@ class File:
         L = _lib.hip()
         self.L = L
         h = vp()
-        if isinstance(source, (bytes, bytearray, memoryview)):
+        if isinstance(source, np.ndarray):
+            self._buf = np.ascontiguousarray(source, dtype=np.uint8)
+            rc = L.pqh_file_open_memory(self._buf.ctypes.data, len(self._buf), ctypes.byref(h))
+        elif isinstance(source, (bytes, bytearray, memoryview)):
             self._buf = np.frombuffer(bytes(source), dtype=np.uint8)
             rc = L.pqh_file_open_memory(self._buf.ctypes.data, len(self._buf), ctypes.byref(h))
         else:

@@ -88,8 +88,10 @@ class Column:
         return c
 
 
-def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0):
-    """Write a file to bytes.  schema: list of element(...) tuples, root first, DFS order."""
+def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0,
+          as_array=False):
+    """Write a file to bytes (or a uint8 numpy array with as_array=True, for multi-GB files).
+    schema: list of element(...) tuples, root first, DFS order."""
     L = _lib.gen()
     names = [s[0].encode() for s in schema]
     els = (SchemaElement * len(schema))()
@@ -108,7 +110,9 @@ def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=
     if rc != 0:
         raise ValueError("pqg_write: " + err.value.decode())
     try:
-        return ctypes.string_at(out, out_len.value)
+        arr = np.empty(out_len.value, dtype=np.uint8)
+        ctypes.memmove(arr.ctypes.data, out, out_len.value)
+        return arr if as_array else arr.tobytes()
     finally:
         L.pqg_free(out)
 
