@@ -51,10 +51,8 @@ struct KernelRun {
   int32_t items;
 };
 
-const char* kKernelNames[] = {"k_prologue", "k_scan", "k_levels", "k_copy", "k_bool_plain",
-                              "k_dict",     "k_rle_bool"};
-constexpr int kNumKernels = 7;
-constexpr int kSideStreams = 4;
+const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global"};
+constexpr int kNumKernels = 4;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -115,22 +113,15 @@ int32_t resolve_kind(int32_t type, int32_t type_length, int32_t enc, int32_t* vs
 
 }  // namespace pqhip
 
-struct TileGroup {
-  int kernel;             // index into kKernelNames
-  int32_t value_size = 0; // dict groups
-  bool lds = false;
-  size_t shm = 0;
-  std::vector<Tile> tiles;
-  size_t offset = 0;      // into the device tile buffer
-};
-
 struct pqh_batch {
   pqh_ctx* ctx = nullptr;
   std::vector<pqh_chunk> chunks;
   std::vector<pqh_page> pages;
   std::vector<DevPage> hpages;
   std::vector<DevChunk> hchunks;
-  std::vector<TileGroup> groups;
+  std::vector<Tile> expand_tiles;   // k_expand work list (kinds interleaved)
+  std::vector<Tile> global_tiles;   // k_dict_global work list
+  size_t expand_lds = 0;            // dynamic LDS of k_expand: largest staged dictionary
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
   int64_t payload_bytes = 0;
@@ -149,18 +140,12 @@ struct pqh_batch {
   std::vector<double> k_read, k_written;  // per kernel kind algorithmic bytes of one run
   std::vector<hipEvent_t> event_pool;
   size_t event_next = 0;
-  std::vector<hipStream_t> side;  // side streams for the independent expand kernels
-  hipEvent_t fork = nullptr;
-  std::vector<hipEvent_t> join;
 };
 
 namespace {
 
 void free_batch(pqh_batch* b) {
   for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
-  for (hipStream_t st : b->side) hipStreamDestroy(st);
-  for (hipEvent_t e : b->join) hipEventDestroy(e);
-  if (b->fork) hipEventDestroy(b->fork);
   for (void* p : b->allocations) hipFree(p);
   if (b->owned_payload) hipFree(b->owned_payload);
 }
@@ -273,9 +258,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
 
   // ---- per-page planning ----
   int64_t ck_cursor = 0;
-  TileGroup levels{2}, copy{3}, bools{4}, rle{6};
-  std::map<std::pair<int, int>, TileGroup> dicts;  // (value size, lds) -> tiles
-  std::map<std::pair<int, int>, size_t> dict_shm;
+  std::vector<std::vector<Tile>> by_kind(6);
   for (int32_t c = 0; c < num_chunks; c++) {
     const pqh_chunk& C = chunks[c];
     DevChunk& D = b->hchunks[size_t(c)];
@@ -374,34 +357,31 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       }
       if (P.host_err != kNoError) continue;
       if (C.column.max_rep > 0 || C.column.max_def > 0)
-        for (int32_t k = 0; k < nt; k++) levels.tiles.push_back(Tile{p, k});
+        for (int32_t k = 0; k < nt; k += kLevelSpan)
+          by_kind[TK_LEVELS].push_back(Tile{p, k, TK_LEVELS, int32_t(std::min<int64_t>(kLevelSpan, nt - k))});
       switch (kind) {
         case K_PLAIN_FIXED:
         case K_PLAIN_INT96: {
           const int64_t ct = ceil_div(n * pvs, kCopyTileBytes);
-          for (int32_t k = 0; k < ct; k++) copy.tiles.push_back(Tile{p, k});
+          for (int32_t k = 0; k < ct; k++) by_kind[TK_COPY].push_back(Tile{p, k, TK_COPY, 1});
           break;
         }
         case K_PLAIN_BOOL: {
           const int64_t bt = ceil_div(n, kBoolTile);
-          for (int32_t k = 0; k < bt; k++) bools.tiles.push_back(Tile{p, k});
+          for (int32_t k = 0; k < bt; k++) by_kind[TK_BOOL].push_back(Tile{p, k, TK_BOOL, 1});
           break;
         }
         case K_RLE_BOOL:
-          for (int32_t k = 0; k < nt; k++) rle.tiles.push_back(Tile{p, k});
+          for (int32_t k = 0; k < nt; k += kDictSpan)
+            by_kind[TK_RLE_BOOL].push_back(Tile{p, k, TK_RLE_BOOL, int32_t(std::min<int64_t>(kDictSpan, nt - k))});
           break;
         case K_DICT: {
           int64_t dict_bytes = 0;
           if (D.dict_page >= 0) dict_bytes = int64_t(std::max(0, pages[D.dict_page].num_values)) * pvs;
-          const bool lds = dict_bytes <= kDictLdsMax;
-          const int vclass = pvs == 4 ? 4 : pvs == 8 ? 8 : 0;
-          auto key = std::make_pair(vclass, int(lds));
-          TileGroup& g = dicts[key];
-          g.kernel = 5;
-          g.value_size = vclass;
-          g.lds = lds;
-          if (lds) g.shm = std::max<size_t>(g.shm, size_t((dict_bytes + 15) & ~int64_t(15)));
-          for (int32_t k = 0; k < nt; k++) g.tiles.push_back(Tile{p, k});
+          const int tk = dict_bytes <= kDictLdsMax ? TK_DICT : TK_DICT_GLOBAL;
+          if (tk == TK_DICT) b->expand_lds = std::max<size_t>(b->expand_lds, size_t((dict_bytes + 15) & ~int64_t(15)));
+          for (int32_t k = 0; k < nt; k += kDictSpan)
+            by_kind[tk].push_back(Tile{p, k, tk, int32_t(std::min<int64_t>(kDictSpan, nt - k))});
           break;
         }
         default:
@@ -410,19 +390,22 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
     b->chunk_n[size_t(c)] = level_base;
   }
-  b->groups.push_back(levels);
-  b->groups.push_back(copy);
-  b->groups.push_back(bools);
-  for (auto& kv : dicts) b->groups.push_back(kv.second);
-  b->groups.push_back(rle);
+  // Interleave the kinds proportionally along the dispatch order (k_expand's grid), so that every
+  // CU sees a mix of byte-copy and bit-unpack tiles instead of one long phase per kind.
+  {
+    std::vector<std::pair<double, Tile>> keyed;
+    for (int kd = 0; kd < 5; kd++) {
+      const auto& v = by_kind[size_t(kd)];
+      for (size_t i = 0; i < v.size(); i++) keyed.push_back({(double(i) + 0.5) / double(v.size()), v[i]});
+    }
+    std::stable_sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& c) { return a.first < c.first; });
+    for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
+    b->global_tiles = by_kind[TK_DICT_GLOBAL];
+  }
 
   // ---- device allocations ----
   int rc;
-  size_t ntiles = 0;
-  for (auto& g : b->groups) {
-    g.offset = ntiles;
-    ntiles += g.tiles.size();
-  }
+  const size_t ntiles = b->expand_tiles.size() + b->global_tiles.size();
   if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_pages), sizeof(DevPage) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_states), sizeof(PageState) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ckpts), sizeof(Ckpt) * size_t(ck_cursor))) ||
@@ -452,9 +435,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     delete b;
     return rc;
   }
-  std::vector<Tile> all;
-  all.reserve(ntiles);
-  for (auto& g : b->groups) all.insert(all.end(), g.tiles.begin(), g.tiles.end());
+  std::vector<Tile> all(b->expand_tiles);
+  all.insert(all.end(), b->global_tiles.begin(), b->global_tiles.end());
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
   if (num_pages) e = hipMemcpyAsync(b->d_pages, b->hpages.data(), sizeof(DevPage) * size_t(num_pages), hipMemcpyHostToDevice, s);
@@ -466,21 +448,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     free_batch(b);
     delete b;
     return set_err(ctx, PQH_ERR_HIP, std::string("batch upload: ") + hipGetErrorString(e));
-  }
-  b->side.assign(kSideStreams, nullptr);
-  b->join.assign(kSideStreams, nullptr);
-  for (int i = 0; i < kSideStreams; i++) {
-    if (hipStreamCreateWithFlags(&b->side[size_t(i)], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&b->join[size_t(i)], hipEventDisableTiming) != hipSuccess) {
-      free_batch(b);
-      delete b;
-      return set_err(ctx, PQH_ERR_HIP, "side stream creation failed");
-    }
-  }
-  if (hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) != hipSuccess) {
-    free_batch(b);
-    delete b;
-    return set_err(ctx, PQH_ERR_HIP, "event creation failed");
   }
   b->stats.resize(kNumKernels);
   for (int k = 0; k < kNumKernels; k++) {
@@ -517,32 +484,11 @@ int pqh_batch_run(pqh_batch* b) {
   hipError_t e;
   e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
-  // The expand kernels are independent of each other: fork them onto side streams so that their
-  // tails overlap, then join back into the context stream.
-  if (e == hipSuccess) e = hipEventRecord(b->fork, s);
-  int used = 0;
-  for (auto& g : b->groups) {
-    if (e != hipSuccess) break;
-    if (g.tiles.empty()) continue;
-    const Tile* t = b->d_tiles + g.offset;
-    const int32_t n = int32_t(g.tiles.size());
-    hipStream_t st = b->side[size_t(used % kSideStreams)];
-    if (used < kSideStreams) e = hipStreamWaitEvent(st, b->fork, 0);
-    used++;
-    if (e != hipSuccess) break;
-    switch (g.kernel) {
-      case 2: e = timed(2, n, st, [&](hipStream_t x) { return launch_levels(d, t, n, x); }); break;
-      case 3: e = timed(3, n, st, [&](hipStream_t x) { return launch_copy(d, t, n, x); }); break;
-      case 4: e = timed(4, n, st, [&](hipStream_t x) { return launch_bool_plain(d, t, n, x); }); break;
-      case 5: e = timed(5, n, st, [&](hipStream_t x) { return launch_dict(d, t, n, g.value_size, g.lds, g.shm, x); }); break;
-      case 6: e = timed(6, n, st, [&](hipStream_t x) { return launch_rle_bool(d, t, n, x); }); break;
-      default: break;
-    }
-  }
-  for (int i = 0; i < used && i < kSideStreams && e == hipSuccess; i++) {
-    e = hipEventRecord(b->join[size_t(i)], b->side[size_t(i)]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, b->join[size_t(i)], 0);
-  }
+  const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
+  if (e == hipSuccess && ne)
+    e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
+  if (e == hipSuccess && ng)
+    e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   return PQH_OK;
 }
@@ -581,30 +527,34 @@ int pqh_batch_sync(pqh_batch* b) {
     const double levels = (C.max_def > 0 ? n : 0) + (C.max_rep > 0 ? n : 0);
     const double vals = double(S.nn) * P.value_size;
     wr += levels + vals;
+    // everything after the prologue is moved by k_expand (or k_dict_global for large dictionaries)
+    const int kx = (P.kind == K_DICT && P.dict_page >= 0 &&
+                    int64_t(std::max(0, b->pages[size_t(P.dict_page)].num_values)) * P.value_size > kDictLdsMax)
+                       ? 3 : 2;
     if (levels > 0) {
-      b->k_written[2] += levels;
       double lb = 0;
       if (S.rep_s >= 0) lb += S.rep_e - S.rep_s;
       if (S.def_s >= 0) lb += S.def_e - S.def_s;
       b->k_read[2] += lb;
+      b->k_written[2] += levels;
     }
     switch (P.kind) {
       case K_PLAIN_FIXED:
       case K_PLAIN_INT96:
-        b->k_read[3] += vals;
-        b->k_written[3] += vals;
+        b->k_read[2] += vals;
+        b->k_written[2] += vals;
         break;
       case K_PLAIN_BOOL:
-        b->k_read[4] += (S.nn + 7) / 8;
-        b->k_written[4] += S.nn;
+        b->k_read[2] += (S.nn + 7) / 8;
+        b->k_written[2] += S.nn;
         break;
       case K_DICT:
-        b->k_read[5] += S.val_e - S.val_s;
-        b->k_written[5] += vals;
+        b->k_read[kx] += S.val_e - S.val_s;
+        b->k_written[kx] += vals;
         break;
       case K_RLE_BOOL:
-        b->k_read[6] += S.val_e - S.val_s;
-        b->k_written[6] += S.nn;
+        b->k_read[2] += S.val_e - S.val_s;
+        b->k_written[2] += S.nn;
         break;
       default:
         break;
@@ -612,7 +562,10 @@ int pqh_batch_sync(pqh_batch* b) {
   }
   for (size_t c = 0; c < b->hchunks.size(); c++) {  // dictionaries once per chunk
     const DevChunk& C = b->hchunks[c];
-    if (C.dict_page >= 0) b->k_read[5] += b->pages[size_t(C.dict_page)].image_len;
+    if (C.dict_page < 0) continue;
+    const pqh_page& Q = b->pages[size_t(C.dict_page)];
+    b->k_read[int64_t(std::max(0, Q.num_values)) * b->hpages[size_t(C.dict_page)].value_size > kDictLdsMax ? 3 : 2] +=
+        Q.image_len;
   }
   b->bytes_written = wr;
   for (int k = 0; k < kNumKernels; k++) {

@@ -97,9 +97,18 @@ struct Ckpt {
   int32_t next_hdr;   // byte offset of the next run header (clamped); bit 31 = bit-packed run
 };
 
+enum TileKind : int32_t { TK_LEVELS = 0, TK_COPY = 1, TK_BOOL = 2, TK_DICT = 3, TK_RLE_BOOL = 4, TK_DICT_GLOBAL = 5 };
+
+// Work item of k_expand.  Hybrid-driven kinds cover [k, k+span) checkpoint intervals of
+// kHybridTile values; TK_COPY covers kCopyTileBytes bytes; TK_BOOL covers kBoolTile values.
 struct Tile {
   int32_t page;
-  int32_t k;  // tile index inside the page
+  int32_t k;
+  int32_t kind;
+  int32_t span;
 };
+
+constexpr int kLevelSpan = 4;  // 32768 level slots per tile
+constexpr int kDictSpan = 2;   // 16384 values per tile
 
 }  // namespace pqhip

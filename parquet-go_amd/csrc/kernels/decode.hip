@@ -27,13 +27,13 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
 }
 
 // 8 bytes at p; bytes at or past `end` read as zero (the reference zero-fills a short bit-packed
-// group read: hybrid_decoder.go:132-140).
+// group read: hybrid_decoder.go:132-140).  `end` never exceeds the payload, which carries
+// PQH_PAYLOAD_PAD readable bytes, so one 8-byte load at p < end stays inside the allocation.
 __device__ __forceinline__ uint64_t ld64_masked(const uint8_t* p, const uint8_t* end) {
-  if (p + 8 <= end) return ld64u(p);
-  uint64_t v = 0;
-  for (int k = 0; k < 8; k++)
-    if (p + k < end) v |= uint64_t(p[k]) << (8 * k);
-  return v;
+  const int64_t n = end - p;
+  if (n <= 0) return 0;
+  const uint64_t v = ld64u(p);
+  return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
 }
 
 __device__ __forceinline__ int bits_len32(uint32_t v) { return v ? 32 - __clz(int(v)) : 0; }
@@ -82,7 +82,7 @@ struct WalkOut {
   int64_t fail_index;
 };
 
-__device__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, int64_t N, int phase, Ckpt* ck,
+__device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, int64_t N, int phase, Ckpt* ck,
                                int match, int lane) {
   WalkOut o{kNoError, 0, N};
   if (N <= 0) return o;
@@ -179,7 +179,6 @@ __device__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, 
         }
         if (match == 1) cnt_lane += ones;
       } else {
-#pragma unroll 4
         for (int64_t g = lane; g * 8 < lim; g += 64) {
           const uint64_t q = ld64_masked(img + data + g * w, end);
           const uint64_t q2 = w > 8 ? ld64_masked(img + data + g * w + 8, end) : 0;
@@ -211,7 +210,8 @@ __device__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, 
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
   const int lane = threadIdx.x & 63;
-  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // one page per wave: make the page index provably wave-uniform so that its records live in SGPRs
+  const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
   if (p >= b.num_pages) return;
   const DevPage P = b.pages[p];
   const DevChunk C = b.chunks[P.chunk];
@@ -428,9 +428,14 @@ __global__ __launch_bounds__(256) void k_scan(DevBatch b) {
   }
 }
 
+
 // ------------------------------------------------------------------------------------------------
 // Tile expansion of a hybrid stream from a checkpoint.  Thread 0 re-walks the (already validated)
-// run headers of the tile into an LDS run list; every thread then expands 8 consecutive values.
+// run headers of the tile into an LDS run list.  A tile inside ONE bit-packed run (every
+// reference-writer stream: hybrid_encoder.go:55-70) takes the width-templated fast path: each
+// thread owns 8 groups of 8 values, strided by the workgroup, with all their loads in flight;
+// a tile inside one RLE run is a fill; anything else (pyarrow-style mixed runs) takes the general
+// per-group path.
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxRuns = 256;
 
@@ -446,9 +451,9 @@ struct TileLds {
   int32_t pad;
 };
 
-// Build the run list for values [from, t1) starting at run {rs, rl, data, bp} with the next
-// header at `pos`.  Returns via LDS; executed by one thread.
-__device__ void build_runs(const uint8_t* img, int w, int64_t t1, int64_t rs, int64_t rl, int32_t data, int32_t bp,
+// Build the run list for values up to t1 starting at run {rs, rl, data, bp} whose successor's
+// header is at `pos`.  One thread.
+__device__ __noinline__ void build_runs(const uint8_t* img, int w, int64_t t1, int64_t rs, int64_t rl, int32_t data, int32_t bp,
                            int64_t pos, TileLds& L) {
   int n = 0;
   int64_t cur_end = rs + rl;
@@ -492,7 +497,7 @@ __device__ __forceinline__ int find_run(const TileLds& L, int64_t i) {
   return lo;
 }
 
-// Decode up to 8 values [i0, i0+cnt) into v[].
+// General path: up to 8 values [i0, i0+cnt) from the LDS run list.
 __device__ __forceinline__ void decode8(const uint8_t* img, const uint8_t* end, int w, const TileLds& L, int64_t i0,
                                         int cnt, uint32_t v[8]) {
   int r = find_run(L, i0);
@@ -503,19 +508,6 @@ __device__ __forceinline__ void decode8(const uint8_t* img, const uint8_t* end, 
       return;
     }
     const int64_t rel = i0 - R.start;
-    if ((rel & 7) == 0 && w <= 16) {  // whole aligned group: one or two 8-byte loads
-      const uint8_t* p = img + R.data + (rel >> 3) * w;
-      const uint64_t q = ld64_masked(p, end);
-      const uint64_t q2 = w > 8 ? ld64_masked(p + 8, end) : 0;
-      const uint32_t m = mask_w(w);
-      for (int j = 0; j < 8; j++) {
-        const int bit = j * w;
-        if (bit + w <= 64) v[j] = uint32_t(q >> bit) & m;
-        else if (bit >= 64) v[j] = uint32_t(q2 >> (bit - 64)) & m;
-        else v[j] = uint32_t((q >> bit) | (q2 << (64 - bit))) & m;
-      }
-      return;
-    }
     for (int j = 0; j < 8; j++) v[j] = bp_value(img, end, R.data, rel + j, w);
     return;
   }
@@ -526,58 +518,118 @@ __device__ __forceinline__ void decode8(const uint8_t* img, const uint8_t* end, 
   }
 }
 
-// Expand values [t0, t1) of a stream whose tile checkpoint is `c`; calls sink(i0, v, cnt) for
-// every group of up to 8 values.  Must be called by the whole workgroup.
+// Fast path for a segment inside ONE bit-packed run: the segment's packed bytes are staged in LDS
+// with coalesced, aligned 16-byte loads (all in flight), bytes past the stream end zeroed; each
+// value is then two LDS dwords + alignbit, for any width 1..32 at run time.
+constexpr int kStageBytes = 16384;
+
 template <class Sink>
-__device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& c, int64_t t0, int64_t t1,
-                              TileLds& L, Sink& sink) {
+__device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, int64_t rs, int64_t t0, int64_t t1,
+                          uint32_t* stage, Sink& sink) {
+  const uint32_t m = mask_w(w);
   const uint8_t* end = img + e;
-  int64_t from = t0;
-  int64_t rs = c.run_start, rl = c.run_len, pos = c.next_hdr & 0x7fffffff;
-  int32_t data = c.data, bp = (c.next_hdr >> 31) & 1;
-  if (w == 0) {  // all zeros
-    for (int64_t i0 = t0 + 8 * int64_t(threadIdx.x); i0 < t1; i0 += 8 * kBlock) {
-      uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      const int cnt = int(t1 - i0 < 8 ? t1 - i0 : 8);
-      sink(i0, v, cnt);
+  int64_t chunk = (int64_t(kStageBytes - 32) * 8 / w) & ~int64_t(8 * kBlock - 1);
+  if (chunk < 8 * kBlock) chunk = 8 * kBlock;
+  for (int64_t c0 = t0; c0 < t1; c0 += chunk) {
+    const int64_t c1 = c0 + chunk < t1 ? c0 + chunk : t1;
+    const uint8_t* p0 = img + data + ((c0 - rs) >> 3) * w;        // group-aligned start
+    const uint8_t* p1 = img + data + ((c1 - rs + 7) >> 3) * w;    // group-rounded end
+    const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p0) & ~uintptr_t(15));
+    const int64_t nvec = (p1 - a0 + 15) >> 4;
+    const uint32_t lead_bits = uint32_t(p0 - a0) * 8;
+    __syncthreads();  // previous chunk fully consumed
+    for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
+      const uint8_t* src = a0 + k * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (src < end) {
+        x = *reinterpret_cast<const uint4*>(src);
+        const int64_t valid = end - src;
+        if (valid < 16) {  // zero the bytes past the stream end
+          uint32_t* w4 = reinterpret_cast<uint32_t*>(&x);
+          for (int q = 0; q < 4; q++) {
+            const int64_t vb = valid - 4 * q;
+            w4[q] = vb >= 4 ? w4[q] : vb <= 0 ? 0u : (w4[q] & ((1u << (8 * vb)) - 1u));
+          }
+        }
+      }
+      reinterpret_cast<uint4*>(stage)[k] = x;
     }
-    return;
-  }
-  while (from < t1) {
-    if (threadIdx.x == 0) build_runs(img, w, t1, rs, rl, data, bp, pos, L);
+    if (threadIdx.x == 0) stage[nvec * 4] = 0;  // the word after the last one (alignbit reads k+1)
     __syncthreads();
-    const int64_t seg_end = L.seg_end;
-    for (int64_t i0 = from + 8 * int64_t(threadIdx.x); i0 < seg_end; i0 += 8 * kBlock) {
+    for (int64_t i0 = c0 + 8 * int64_t(threadIdx.x); i0 < c1; i0 += 8 * kBlock) {
       uint32_t v[8];
-      const int cnt = int(seg_end - i0 < 8 ? seg_end - i0 : 8);
-      decode8(img, end, w, L, i0, cnt, v);
-      sink(i0, v, cnt);
-    }
-    // continue after the last listed run
-    const RunL last = L.runs[L.nruns - 1];
-    from = seg_end;
-    rs = last.start;
-    rl = int64_t(seg_end) - last.start;
-    data = last.data;
-    bp = last.bp;
-    pos = L.next_pos;
-    __syncthreads();
-    if (from < t1) {
-      // the last run may continue past seg_end only if it was clipped by t1, which ends the loop;
-      // otherwise the next run starts exactly at seg_end: restart from the header at next_pos with
-      // an empty pseudo-run.
-      rs = from;
-      rl = 0;
+      const uint32_t bit0 = lead_bits + uint32_t(i0 - c0) * uint32_t(w);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t bit = bit0 + uint32_t(j * w);
+        const uint32_t lo = stage[bit >> 5], hi = stage[(bit >> 5) + 1];
+        v[j] = __builtin_amdgcn_alignbit(hi, lo, bit & 31) & m;
+      }
+      sink(i0, v, int(c1 - i0 < 8 ? c1 - i0 : 8));
     }
   }
 }
 
+// Expand values [t0, t1) of a hybrid stream whose tile checkpoint is `c`; calls sink(i0, v, cnt)
+// for every group of up to 8 values.  Must be called by the whole workgroup.
+template <class Sink>
+__device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& c, int64_t t0, int64_t t1,
+                              TileLds& L, uint32_t* stage, Sink& sink) {
+  const uint8_t* end = img + e;
+  if (w == 0) {  // all zeros
+    for (int64_t i0 = t0 + 8 * int64_t(threadIdx.x); i0 < t1; i0 += 8 * kBlock) {
+      uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      sink(i0, v, int(t1 - i0 < 8 ? t1 - i0 : 8));
+    }
+    return;
+  }
+  int64_t from = t0;
+  int64_t rs = c.run_start, rl = c.run_len, pos = c.next_hdr & 0x7fffffff;
+  int32_t data = c.data, bp = (c.next_hdr >> 31) & 1;
+  while (from < t1) {
+    if (threadIdx.x == 0) build_runs(img, w, t1, rs, rl, data, bp, pos, L);
+    __syncthreads();
+    const int64_t seg_end = L.seg_end;
+    const RunL r0 = L.runs[0];
+    bool done = false;
+    if (L.nruns == 1 && r0.end >= seg_end) {  // the whole segment lies in one run
+      if (r0.bp) {
+        if (((from - r0.start) & 7) == 0 && w <= 32) {
+          bp_staged(img, e, w, r0.data, r0.start, from, seg_end, stage, sink);
+          done = true;
+        }
+      } else {
+        uint32_t v[8];
+        for (int j = 0; j < 8; j++) v[j] = uint32_t(r0.data);
+        for (int64_t i0 = from + 8 * int64_t(threadIdx.x); i0 < seg_end; i0 += 8 * kBlock)
+          sink(i0, v, int(seg_end - i0 < 8 ? seg_end - i0 : 8));
+        done = true;
+      }
+    }
+    if (!done) {
+      for (int64_t i0 = from + 8 * int64_t(threadIdx.x); i0 < seg_end; i0 += 8 * kBlock) {
+        uint32_t v[8];
+        const int cnt = int(seg_end - i0 < 8 ? seg_end - i0 : 8);
+        decode8(img, end, w, L, i0, cnt, v);
+        sink(i0, v, cnt);
+      }
+    }
+    from = seg_end;
+    pos = L.next_pos;
+    __syncthreads();
+    // the next segment starts exactly at a run header: an empty pseudo-run at `from`
+    rs = from;
+    rl = 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
-// k_levels: definition / repetition level bytes (decodePackedArray into uint8 slots).
+// Sinks: what a decoded group of up to 8 values turns into.
 // ------------------------------------------------------------------------------------------------
+// decodePackedArray into one byte per level slot.
 struct LevelSink {
   uint8_t* out;
-  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+  __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
     if (cnt == 8) {
       uint64_t x = 0;
       for (int j = 0; j < 8; j++) x |= uint64_t(v[j] & 0xff) << (8 * j);
@@ -588,41 +640,29 @@ struct LevelSink {
   }
 };
 
-__global__ __launch_bounds__(256) void k_levels(DevBatch b, const Tile* tiles) {
-  __shared__ TileLds L;
-  const Tile t = tiles[blockIdx.x];
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
-  if (page_failed_before_values(S)) return;
-  const DevChunk C = b.chunks[P.chunk];
-  const uint8_t* img = b.payload + P.image_off;
-  const int64_t n = P.num_values;
-  const int64_t t0 = int64_t(t.k) * kHybridTile;
-  const int64_t t1 = t0 + kHybridTile < n ? t0 + kHybridTile : n;
-  if (t0 >= n) return;
-  if (C.max_rep > 0) {
-    LevelSink sink{C.rep_levels + P.level_base};
-    expand_hybrid(img, S.rep_e, bits_len32(uint32_t(C.max_rep)), b.ckpts[P.ck_rep + t.k], t0, t1, L, sink);
-    __syncthreads();
+// booleanRLEDecoder.decodeValues (type_boolean.go:109-120): value == 1.
+struct BoolSink {
+  uint8_t* out;
+  __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+    if (cnt == 8) {
+      uint64_t x = 0;
+      for (int j = 0; j < 8; j++) x |= uint64_t(v[j] == 1) << (8 * j);
+      __builtin_memcpy(out + i0, &x, 8);
+    } else {
+      for (int j = 0; j < cnt; j++) out[i0 + j] = uint8_t(v[j] == 1);
+    }
   }
-  if (C.max_def > 0) {
-    LevelSink sink{C.def_levels + P.level_base};
-    expand_hybrid(img, S.def_e, bits_len32(uint32_t(C.max_def)), b.ckpts[P.ck_def + t.k], t0, t1, L, sink);
-  }
-}
+};
 
-// ------------------------------------------------------------------------------------------------
-// k_dict: dictDecoder.decodeValues (type_dict.go:40-60): bounds-checked gather of dictionary
-// entries; the dictionary is staged in LDS when it fits (kDictLdsMax).
-// ------------------------------------------------------------------------------------------------
+// dictDecoder.decodeValues (type_dict.go:40-60): bounds-checked gather of dictionary entries.
 template <int VS>
 struct DictSink {
-  const uint8_t* dict;  // LDS or global
+  const uint8_t* dict;  // LDS (fused kernel) or global (large dictionaries)
   uint8_t* out;         // chunk values + value_base * vs
   uint32_t K;
   int vs;               // runtime size when VS == 0
   int64_t* first_bad;   // per-thread min failing index
-  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+  __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
     bool ok = true;
     for (int j = 0; j < cnt; j++)
       if (v[j] >= K) {
@@ -642,14 +682,14 @@ struct DictSink {
       }
     } else if constexpr (VS == 8) {
       const uint64_t* d = reinterpret_cast<const uint64_t*>(dict);
-      for (int j = 0; j < cnt; j += 2) {
-        if (ok && j + 1 < cnt) {
+      if (ok && cnt == 8) {
+        for (int j = 0; j < 8; j += 2) {
           uint64_t pr[2] = {d[v[j]], d[v[j + 1]]};
           __builtin_memcpy(out + (i0 + j) * 8, pr, 16);
-        } else {
-          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 8, &d[v[j]], 8);
-          if (j + 1 < cnt && v[j + 1] < K) __builtin_memcpy(out + (i0 + j + 1) * 8, &d[v[j + 1]], 8);
         }
+      } else {
+        for (int j = 0; j < cnt; j++)
+          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 8, &d[v[j]], 8);
       }
     } else {
       for (int j = 0; j < cnt; j++) {
@@ -668,16 +708,38 @@ struct DictSink {
   }
 };
 
-template <int VS, bool LDS>
-__global__ __launch_bounds__(256) void k_dict(DevBatch b, const Tile* tiles) {
-  __shared__ TileLds L;
-  extern __shared__ __attribute__((aligned(16))) uint8_t dict_lds[];
-  const Tile t = tiles[blockIdx.x];
+// ------------------------------------------------------------------------------------------------
+// Tile bodies.  Every body reads its page/state/chunk records itself (all depend on t.page only).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const uint8_t* img = b.payload + P.image_off;
+  const int64_t n = P.num_values;
+  const int64_t t0 = int64_t(t.k) * kHybridTile;
+  int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
+  if (t1 > n) t1 = n;
+  if (t0 >= t1) return;
+  for (int s = 0; s < 2; s++) {  // repetition levels first, then definition levels
+    const int maxl = s == 0 ? C.max_rep : C.max_def;
+    if (maxl <= 0) continue;
+    LevelSink sink{(s == 0 ? C.rep_levels : C.def_levels) + P.level_base};
+    const Ckpt c = b.ckpts[(s == 0 ? P.ck_rep : P.ck_def) + t.k];
+    expand_hybrid(img, s == 0 ? S.rep_e : S.def_e, bits_len32(uint32_t(maxl)), c, t0, t1, L, stage, sink);
+    __syncthreads();
+  }
+}
+
+template <bool LDS>
+__device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage,
+                                          uint8_t* dict_lds) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
   if (page_failed_before_values(S)) return;
   const int64_t t0 = int64_t(t.k) * kHybridTile;
-  int64_t t1 = t0 + kHybridTile;
+  int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
   if (t1 > S.val_limit) t1 = S.val_limit;
   if (t0 >= t1) return;
   const DevChunk C = b.chunks[P.chunk];
@@ -691,7 +753,7 @@ __global__ __launch_bounds__(256) void k_dict(DevBatch b, const Tile* tiles) {
       dict = b.payload + b.pages[P.dict_page].image_off;
     }
   }
-  if constexpr (LDS) {
+  if constexpr (LDS) {  // stage the dictionary page's values in LDS (kDictLdsMax bytes at most)
     const int64_t bytes = int64_t(K) * vs;
     const int64_t words = (bytes + 3) >> 2;
     for (int64_t i = threadIdx.x; i < words; i += kBlock) {
@@ -706,49 +768,38 @@ __global__ __launch_bounds__(256) void k_dict(DevBatch b, const Tile* tiles) {
   }
   const uint8_t* img = b.payload + P.image_off;
   int64_t first_bad = INT64_MAX;
-  DictSink<VS> sink{dict, C.values + S.value_base * vs, K, vs, &first_bad};
-  expand_hybrid(img, S.val_e, S.width, b.ckpts[P.ck_val + t.k], t0, t1, L, sink);
+  uint8_t* out = C.values + S.value_base * vs;
+  const Ckpt c = b.ckpts[P.ck_val + t.k];
+  if (vs == 4) {
+    DictSink<4> sink{dict, out, K, vs, &first_bad};
+    expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
+  } else if (vs == 8) {
+    DictSink<8> sink{dict, out, K, vs, &first_bad};
+    expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
+  } else {
+    DictSink<0> sink{dict, out, K, vs, &first_bad};
+    expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
+  }
   if (first_bad != INT64_MAX)
     atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, PQH_ERR_DICT_INDEX));
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_rle_bool: booleanRLEDecoder.decodeValues (type_boolean.go:109-120): value == 1.
-// ------------------------------------------------------------------------------------------------
-struct BoolSink {
-  uint8_t* out;
-  __device__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
-    if (cnt == 8) {
-      uint64_t x = 0;
-      for (int j = 0; j < 8; j++) x |= uint64_t(v[j] == 1) << (8 * j);
-      __builtin_memcpy(out + i0, &x, 8);
-    } else {
-      for (int j = 0; j < cnt; j++) out[i0 + j] = uint8_t(v[j] == 1);
-    }
-  }
-};
-
-__global__ __launch_bounds__(256) void k_rle_bool(DevBatch b, const Tile* tiles) {
-  __shared__ TileLds L;
-  const Tile t = tiles[blockIdx.x];
+__device__ __forceinline__ void tile_rle_bool(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
   if (page_failed_before_values(S)) return;
   const int64_t t0 = int64_t(t.k) * kHybridTile;
-  int64_t t1 = t0 + kHybridTile;
+  int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
   if (t1 > S.val_limit) t1 = S.val_limit;
   if (t0 >= t1) return;
   const DevChunk C = b.chunks[P.chunk];
   BoolSink sink{C.values + S.value_base};
-  expand_hybrid(b.payload + P.image_off, S.val_e, 1, b.ckpts[P.ck_val + t.k], t0, t1, L, sink);
+  expand_hybrid(b.payload + P.image_off, S.val_e, 1, b.ckpts[P.ck_val + t.k], t0, t1, L, stage, sink);
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_copy: PLAIN fixed-width values (int32/int64/float/double/INT96/FLBA): little-endian copy of
-// notNull * size bytes (type_int32.go:21-31 ...), 16-byte vector loads and stores.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_copy(DevBatch b, const Tile* tiles) {
-  const Tile t = tiles[blockIdx.x];
+// PLAIN fixed-width values (int32/int64/float/double/INT96/FLBA): little-endian copy of
+// notNull * size bytes (type_int32.go:21-31 ...), 16-byte vector loads and stores, 4 in flight.
+__device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
   if (page_failed_before_values(S)) return;
@@ -761,7 +812,7 @@ __global__ __launch_bounds__(256) void k_copy(DevBatch b, const Tile* tiles) {
   const uint8_t* src = b.payload + P.image_off + S.val_s;
   uint8_t* dst = C.values + S.value_base * P.value_size;
   int64_t o = c0 + 16 * int64_t(threadIdx.x);
-  for (; o + 16 * 3 * kBlock + 16 <= c1; o += 16 * 4 * kBlock) {  // 4 independent 16-B loads in flight
+  for (; o + 16 * 3 * kBlock + 16 <= c1; o += 16 * 4 * kBlock) {
     uint4 a, bb, c, d;
     __builtin_memcpy(&a, src + o, 16);
     __builtin_memcpy(&bb, src + o + 16 * kBlock, 16);
@@ -783,36 +834,63 @@ __global__ __launch_bounds__(256) void k_copy(DevBatch b, const Tile* tiles) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_bool_plain: booleanPlainDecoder (type_boolean.go:43-69), LSB-first bits -> 0/1 bytes.
-// ------------------------------------------------------------------------------------------------
+// booleanPlainDecoder (type_boolean.go:43-69): LSB-first bits -> 0/1 bytes.
 __device__ __forceinline__ uint32_t nibble_bytes(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
 
-__global__ __launch_bounds__(256) void k_bool_plain(DevBatch b, const Tile* tiles) {
-  const Tile t = tiles[blockIdx.x];
+__device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
   if (page_failed_before_values(S)) return;
   const int64_t lim = S.val_limit;
-  const int64_t v0 = int64_t(t.k) * kBoolTile + int64_t(threadIdx.x) * 128;
-  if (v0 >= lim) return;
   const DevChunk C = b.chunks[P.chunk];
-  const uint8_t* src = b.payload + P.image_off + S.val_s + (v0 >> 3);
-  uint8_t* dst = C.values + S.value_base + v0;
-  uint8_t in[16];
-  __builtin_memcpy(in, src, 16);
-  if (v0 + 128 <= lim) {
-    for (int q = 0; q < 8; q++) {
-      uint4 o;
-      o.x = nibble_bytes(in[2 * q] & 15);
-      o.y = nibble_bytes(in[2 * q] >> 4);
-      o.z = nibble_bytes(in[2 * q + 1] & 15);
-      o.w = nibble_bytes(in[2 * q + 1] >> 4);
-      __builtin_memcpy(dst + 16 * q, &o, 16);
+  for (int q = 0; q < 2; q++) {
+    const int64_t v0 = int64_t(t.k) * kBoolTile + int64_t(q) * (kBoolTile / 2) + int64_t(threadIdx.x) * 64;
+    if (v0 >= lim) return;
+    const uint8_t* src = b.payload + P.image_off + S.val_s + (v0 >> 3);
+    uint8_t* dst = C.values + S.value_base + v0;
+    uint8_t in[8];
+    __builtin_memcpy(in, src, 8);
+    if (v0 + 64 <= lim) {
+      for (int k = 0; k < 4; k++) {
+        uint4 o;
+        o.x = nibble_bytes(in[2 * k] & 15);
+        o.y = nibble_bytes(in[2 * k] >> 4);
+        o.z = nibble_bytes(in[2 * k + 1] & 15);
+        o.w = nibble_bytes(in[2 * k + 1] >> 4);
+        __builtin_memcpy(dst + 16 * k, &o, 16);
+      }
+    } else {
+      for (int64_t j = 0; v0 + j < lim; j++) dst[j] = (in[j >> 3] >> (j & 7)) & 1;
     }
-  } else {
-    for (int64_t j = 0; v0 + j < lim; j++) dst[j] = (in[j >> 3] >> (j & 7)) & 1;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_expand: ONE launch for every data-parallel tile of the batch (levels, PLAIN copies, booleans,
+// dictionary gathers with the dictionary in LDS, RLE booleans).  Tile kinds are interleaved by the
+// planner so every CU sees a mix of byte-copy and bit-unpack work.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
+  __shared__ TileLds L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // [stage kStageBytes+16][dictionary]
+  uint32_t* stage = reinterpret_cast<uint32_t*>(lds);
+  uint8_t* dict_lds = lds + kStageBytes + 16;
+  const Tile t = tiles[blockIdx.x];
+  switch (t.kind) {
+    case TK_LEVELS: tile_levels(b, t, L, stage); break;
+    case TK_COPY: tile_copy(b, t); break;
+    case TK_BOOL: tile_bool_plain(b, t); break;
+    case TK_DICT: tile_dict<true>(b, t, L, stage, dict_lds); break;
+    case TK_RLE_BOOL: tile_rle_bool(b, t, L, stage); break;
+    default: break;
+  }
+}
+
+// Dictionaries larger than kDictLdsMax: gathered from global memory (L2 / Infinity Cache).
+__global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* tiles) {
+  __shared__ TileLds L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  tile_dict<false>(b, tiles[blockIdx.x], L, reinterpret_cast<uint32_t*>(lds), nullptr);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -830,44 +908,15 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_levels(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_levels, dim3(n), dim3(256), 0, s, b, tiles);
+  hipLaunchKernelGGL(k_expand, dim3(n), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles);
   return hipGetLastError();
 }
 
-hipError_t launch_copy(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_copy, dim3(n), dim3(256), 0, s, b, tiles);
-  return hipGetLastError();
-}
-
-hipError_t launch_bool_plain(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bool_plain, dim3(n), dim3(256), 0, s, b, tiles);
-  return hipGetLastError();
-}
-
-hipError_t launch_dict(const DevBatch& b, const Tile* tiles, int32_t n, int32_t value_size, bool lds, size_t lds_bytes,
-                       hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  const size_t shm = lds ? (lds_bytes > 16 ? lds_bytes : 16) : 0;
-  if (value_size == 4) {
-    if (lds) hipLaunchKernelGGL((k_dict<4, true>), dim3(n), dim3(256), shm, s, b, tiles);
-    else hipLaunchKernelGGL((k_dict<4, false>), dim3(n), dim3(256), 0, s, b, tiles);
-  } else if (value_size == 8) {
-    if (lds) hipLaunchKernelGGL((k_dict<8, true>), dim3(n), dim3(256), shm, s, b, tiles);
-    else hipLaunchKernelGGL((k_dict<8, false>), dim3(n), dim3(256), 0, s, b, tiles);
-  } else {
-    if (lds) hipLaunchKernelGGL((k_dict<0, true>), dim3(n), dim3(256), shm, s, b, tiles);
-    else hipLaunchKernelGGL((k_dict<0, false>), dim3(n), dim3(256), 0, s, b, tiles);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_rle_bool(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rle_bool, dim3(n), dim3(256), 0, s, b, tiles);
+  hipLaunchKernelGGL(k_dict_global, dim3(n), dim3(256), size_t(kStageBytes + 16), s, b, tiles);
   return hipGetLastError();
 }
 

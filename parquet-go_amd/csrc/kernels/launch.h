@@ -19,12 +19,10 @@ struct DevBatch {
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
-hipError_t launch_levels(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
-hipError_t launch_copy(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
-hipError_t launch_bool_plain(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
-// Hybrid-driven values: dictionary gathers (value_size 4, 8 or generic) and RLE booleans.
-hipError_t launch_dict(const DevBatch& b, const Tile* tiles, int32_t n, int32_t value_size, bool lds,
-                       size_t lds_bytes, hipStream_t s);
-hipError_t launch_rle_bool(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
+// LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
+hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
+// Dictionaries too large for LDS.
+hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 
 }  // namespace pqhip
