@@ -60,6 +60,30 @@ def cpu_baseline(data, seconds):
                       f"(C restatement of the reference Go decoders), single thread, {spent:.1f} s"}
 
 
+def pmc_traffic(kernel, workload, rows):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the same
+    workload (profiles/*/pmc_summary.json, written by scripts/pmc_summary.py from FETCH_SIZE x2 +
+    WRITE_SIZE passes of this bench).  bench.py cannot collect PMC counters itself."""
+    prof = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(prof):
+        return None, None
+    for tag in sorted(os.listdir(prof), reverse=True):
+        p = os.path.join(prof, tag, "pmc_summary.json")
+        if not os.path.exists(p):
+            continue
+        try:
+            s = json.load(open(p))
+        except Exception:
+            continue
+        lines = s.get("bench_lines") or []
+        if not lines or lines[0]["config"]["workload"] != workload or lines[0]["config"]["rows_per_gpu"] != rows:
+            continue
+        k = s["kernels"].get(kernel) or {}
+        if k.get("hbm_traffic_bytes_per_launch"):
+            return k["hbm_traffic_bytes_per_launch"], f"profiles/{tag}/pmc_summary.json"
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,9 +188,12 @@ def main():
     if dom is not None:
         avg_ms = dom.total_ms / dom.launches
         ach = (dom.bytes_read + dom.bytes_written) / (avg_ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic(dom.name.decode(), desc, f.num_rows)
         roof = {"bound": "hbm", "kernel": dom.name.decode(), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written}
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_source": src,
+                "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
+                "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
     all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)
     if rank == 0:
         cpu = None
