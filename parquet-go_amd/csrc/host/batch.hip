@@ -51,8 +51,9 @@ struct KernelRun {
   int32_t items;
 };
 
-const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global"};
-constexpr int kNumKernels = 4;
+const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
+                              "k_delta_walk", "k_delta_sum", "k_delta_scan"};
+constexpr int kNumKernels = 7;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -121,6 +122,8 @@ struct pqh_batch {
   std::vector<DevChunk> hchunks;
   std::vector<Tile> expand_tiles;   // k_expand work list (kinds interleaved)
   std::vector<Tile> global_tiles;   // k_dict_global work list
+  std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
+  std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   size_t expand_lds = 0;            // dynamic LDS of k_expand: largest staged dictionary
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
@@ -130,6 +133,11 @@ struct pqh_batch {
   PageState* d_states = nullptr;
   Ckpt* d_ckpts = nullptr;
   Tile* d_tiles = nullptr;
+  Tile* d_dtiles = nullptr;
+  int32_t* d_delta_pages = nullptr;
+  DeltaState* d_dstates = nullptr;
+  DeltaBlock* d_dblocks = nullptr;
+  uint64_t* d_dsums = nullptr;
   std::vector<void*> allocations;
   std::vector<PageState> states;   // host copy after sync
   std::vector<int64_t> chunk_n;    // level slots per chunk
@@ -257,8 +265,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   b->k_written.assign(kNumKernels, 0);
 
   // ---- per-page planning ----
-  int64_t ck_cursor = 0;
-  std::vector<std::vector<Tile>> by_kind(6);
+  int64_t ck_cursor = 0, dblk_cursor = 0, dtile_cursor = 0;
+  std::vector<std::vector<Tile>> by_kind(8);
   for (int32_t c = 0; c < num_chunks; c++) {
     const pqh_chunk& C = chunks[c];
     DevChunk& D = b->hchunks[size_t(c)];
@@ -294,6 +302,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       P.chunk = c;
       P.dict_page = -1;
       P.ck_rep = P.ck_def = P.ck_val = -1;
+      P.dblk_base = -1;
       P.host_err = chunk_err;
       if (Q.image_offset < 0 || Q.image_len < 0 || Q.image_offset + Q.image_len > payload_bytes) {
         delete b;
@@ -332,12 +341,24 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       if (kind == K_UNSUPPORTED) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
       const bool device_ready = kind == K_PLAIN_FIXED || kind == K_PLAIN_INT96 || kind == K_PLAIN_BOOL ||
                                 kind == K_RLE_BOOL || kind == K_FLBA_NEGATIVE || kind == K_UNSUPPORTED ||
-                                (kind == K_DICT && pvs > 0);
+                                kind == K_DELTA32 || kind == K_DELTA64 || (kind == K_DICT && pvs > 0);
       if (!device_ready) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
       const int64_t n = Q.num_values > 0 ? Q.num_values : 0;
       P.level_base = level_base;
       level_base += n;
       b->bytes_read += Q.image_len;
+      if ((kind == K_DELTA32 || kind == K_DELTA64) && P.host_err == kNoError) {
+        // the values decoder is initialised (and may fail) even for pages without values
+        P.dblk_base = int32_t(dblk_cursor);
+        P.dblk_cap = int32_t(ceil_div(n, kDeltaBlockMin) + 1);
+        dblk_cursor += P.dblk_cap;
+        P.dtile_base = int32_t(dtile_cursor);
+        P.dtile_n = int32_t(ceil_div(n, kDeltaTile));
+        dtile_cursor += P.dtile_n;
+        b->delta_pages.push_back(p);
+        for (int32_t k = 0; k < P.dtile_n; k++) by_kind[TK_DELTA].push_back(Tile{p, k, TK_DELTA, 1});
+        by_kind[TK_DELTA_SERIAL].push_back(Tile{p, 0, TK_DELTA_SERIAL, 1});
+      }
       if (n == 0) continue;
       const int64_t nt = ceil_div(n, kHybridTile);
       if (C.column.max_rep > 0) {
@@ -394,13 +415,16 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   // CU sees a mix of byte-copy and bit-unpack tiles instead of one long phase per kind.
   {
     std::vector<std::pair<double, Tile>> keyed;
-    for (int kd = 0; kd < 5; kd++) {
+    for (int kd : {int(TK_LEVELS), int(TK_COPY), int(TK_BOOL), int(TK_DICT), int(TK_RLE_BOOL), int(TK_DELTA)}) {
       const auto& v = by_kind[size_t(kd)];
       for (size_t i = 0; i < v.size(); i++) keyed.push_back({(double(i) + 0.5) / double(v.size()), v[i]});
     }
     std::stable_sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& c) { return a.first < c.first; });
     for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
+    // serial delta pages (rare geometries) first: they are the longest work items
+    b->expand_tiles.insert(b->expand_tiles.begin(), by_kind[TK_DELTA_SERIAL].begin(), by_kind[TK_DELTA_SERIAL].end());
     b->global_tiles = by_kind[TK_DICT_GLOBAL];
+    b->delta_tiles = by_kind[TK_DELTA];
   }
 
   // ---- device allocations ----
@@ -409,7 +433,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_pages), sizeof(DevPage) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_states), sizeof(PageState) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ckpts), sizeof(Ckpt) * size_t(ck_cursor))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_tiles), sizeof(Tile) * ntiles))) {
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_tiles), sizeof(Tile) * ntiles)) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dtiles), sizeof(Tile) * b->delta_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_delta_pages), sizeof(int32_t) * b->delta_pages.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * size_t(num_pages))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dblocks), sizeof(DeltaBlock) * size_t(dblk_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor)))) {
     free_batch(b);
     delete b;
     return rc;
@@ -443,6 +472,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   if (e == hipSuccess && num_chunks)
     e = hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * size_t(num_chunks), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && ntiles) e = hipMemcpyAsync(b->d_tiles, all.data(), sizeof(Tile) * ntiles, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->delta_tiles.empty())
+    e = hipMemcpyAsync(b->d_dtiles, b->delta_tiles.data(), sizeof(Tile) * b->delta_tiles.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->delta_pages.empty())
+    e = hipMemcpyAsync(b->d_delta_pages, b->delta_pages.data(), sizeof(int32_t) * b->delta_pages.size(),
+                       hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     free_batch(b);
@@ -465,7 +499,7 @@ int pqh_batch_run(pqh_batch* b) {
   const bool prof = (ctx->flags & PQH_CTX_PROFILE) != 0;
   hipStream_t s = ctx->stream;
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
-             int32_t(b->chunks.size())};
+             int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums};
   b->synced = false;
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -482,8 +516,15 @@ int pqh_batch_run(pqh_batch* b) {
     return e;
   };
   hipError_t e;
+  const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
+  if (e == hipSuccess && ndp)
+    e = timed(4, ndp, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ndp, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  if (e == hipSuccess && ndt)
+    e = timed(5, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
+  if (e == hipSuccess && ndp)
+    e = timed(6, ndp, s, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
   if (e == hipSuccess && ne)
     e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
@@ -555,6 +596,12 @@ int pqh_batch_sync(pqh_batch* b) {
       case K_RLE_BOOL:
         b->k_read[2] += S.val_e - S.val_s;
         b->k_written[2] += S.nn;
+        break;
+      case K_DELTA32:
+      case K_DELTA64:  // the walk reads block headers; sums and expand each read the packed deltas
+        b->k_read[2] += S.val_e - S.val_s;
+        b->k_written[2] += vals;
+        b->k_read[5] += S.val_e - S.val_s;
         break;
       default:
         break;

@@ -59,6 +59,10 @@ struct DevPage {
   int32_t ck_rep, ck_def, ck_val;  // checkpoint table offsets (entries), -1 if none
   int32_t ck_rep_n, ck_def_n, ck_val_n;
   uint64_t host_err;     // error key found by the host planner (header-level), kNoError if none
+  int32_t dblk_base;     // DELTA_BINARY_PACKED: first DeltaBlock record, -1 if not a delta page
+  int32_t dblk_cap;      // records available (pages of blockSize >= 128)
+  int32_t dtile_base;    // first per-tile delta sum
+  int32_t dtile_n;       // delta tiles of the page (kDeltaTile values each)
 };
 
 struct DevChunk {
@@ -89,6 +93,32 @@ struct PageState {
   int64_t byte_base;       // byte arrays: first byte
 };
 
+// DELTA_BINARY_PACKED (deltabp_decoder.go): per page, written by k_delta_walk.
+enum DeltaMode : int32_t { DM_NONE = 0, DM_FAST = 1, DM_SERIAL = 2 };
+
+struct DeltaState {
+  int32_t mode;           // DeltaMode
+  int32_t block_size;
+  int32_t mb_count;
+  int32_t mbvc;           // values per miniblock
+  int32_t nblocks;        // records written
+  int32_t limit;          // values decodable before the first error (<= notNull)
+  uint64_t first;         // first value (bits; int32 pages sign-extended)
+  int64_t end_pos;        // reader position (image offset) after the walk
+};
+
+// One block: header already parsed; data of miniblock m starts at data_off + sum_{j<m} mbvc/8*w_j.
+struct DeltaBlock {
+  uint64_t min_delta;
+  int32_t data_off;       // image offset of the first miniblock's data
+  int32_t first_pos;      // position (value index) of the block's first delta
+  uint64_t widths;        // miniblock bit widths, 8 bits each (mb_count <= 8 on the fast path)
+  uint64_t pad;
+};
+
+constexpr int kDeltaTile = 8192;     // values per delta tile (block size must divide 2048)
+constexpr int kDeltaBlockMin = 128;  // record capacity assumes blocks of >= 128 values
+
 // Run checkpoint at a tile boundary: the run that contains the tile's first value.
 struct Ckpt {
   int32_t run_start;  // value index where the run starts
@@ -97,7 +127,16 @@ struct Ckpt {
   int32_t next_hdr;   // byte offset of the next run header (clamped); bit 31 = bit-packed run
 };
 
-enum TileKind : int32_t { TK_LEVELS = 0, TK_COPY = 1, TK_BOOL = 2, TK_DICT = 3, TK_RLE_BOOL = 4, TK_DICT_GLOBAL = 5 };
+enum TileKind : int32_t {
+  TK_LEVELS = 0,
+  TK_COPY = 1,
+  TK_BOOL = 2,
+  TK_DICT = 3,
+  TK_RLE_BOOL = 4,
+  TK_DICT_GLOBAL = 5,
+  TK_DELTA = 6,         // kDeltaTile values of a DM_FAST delta page
+  TK_DELTA_SERIAL = 7   // a whole DM_SERIAL delta page (exact sequential decoder)
+};
 
 // Work item of k_expand.  Hybrid-driven kinds cover [k, k+span) checkpoint intervals of
 // kHybridTile values; TK_COPY covers kCopyTileBytes bytes; TK_BOOL covers kBoolTile values.

@@ -373,6 +373,9 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
               }
               break;
             }
+            case K_DELTA32:
+            case K_DELTA64:  // init + block walk in k_delta_walk (atomicMin into the same key)
+              break;
             case K_FLBA_NEGATIVE:
               err = err_key(3, 0, PQH_ERR_NEGATIVE_LENGTH);
               limit = 0;
@@ -870,6 +873,8 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 // dictionary gathers with the dictionary in LDS, RLE booleans).  Tile kinds are interleaved by the
 // planner so every CU sees a mix of byte-copy and bit-unpack work.
 // ------------------------------------------------------------------------------------------------
+#include "delta_impl.h"
+
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // [stage kStageBytes+16][dictionary]
@@ -882,6 +887,12 @@ __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
     case TK_BOOL: tile_bool_plain(b, t); break;
     case TK_DICT: tile_dict<true>(b, t, L, stage, dict_lds); break;
     case TK_RLE_BOOL: tile_rle_bool(b, t, L, stage); break;
+    case TK_DELTA: {
+      __shared__ DeltaLds DL;
+      tile_delta(b, t, stage, DL);
+      break;
+    }
+    case TK_DELTA_SERIAL: delta_serial(b, t); break;
     default: break;
   }
 }
@@ -911,6 +922,24 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s) {
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_expand, dim3(n), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_walk, dim3((n + 3) / 4), dim3(256), 0, s, b, delta_pages, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_sum, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_scan, dim3((n + 255) / 256), dim3(256), 0, s, b, delta_pages, n);
   return hipGetLastError();
 }
 

@@ -1,0 +1,541 @@
+// delta_impl.h — DELTA_BINARY_PACKED on the device (included by decode.hip).
+//
+// Reference: deltaBitPackDecoder32/64 (deltabp_decoder.go:13-333).  The stream is a chain of
+// blocks whose byte length depends on their own header (varint minDelta + miniblock widths), so
+// it is walked sequentially, once per page, by one wave64 reading the page through an LDS window
+// (k_delta_walk).  The walk replays next()'s exact read pattern — eager block + first miniblock
+// header at init, the one-delta read-ahead, the padding skip at position+8 >= valuesCount with its
+// currentMiniBlock index quirk (:149-164) — and records, per block, minDelta, widths and the data
+// offset.  Decoding is then data parallel: per-tile delta sums (k_delta_sum) -> per-page exclusive
+// scan seeded with the first value (k_delta_scan) -> per tile: unpack from LDS, block-wide scan,
+// store (TK_DELTA in k_expand).  Streams outside the fast-path geometry (miniblock count > 8,
+// miniblock values not a multiple of 8, block size not dividing 2048) are decoded by an exact
+// sequential restatement (TK_DELTA_SERIAL).
+#pragma once
+
+constexpr int kWin = 8192;  // LDS window per wave for the block walk
+
+struct Win {
+  const uint8_t* img;
+  int64_t e;     // end of the stream (image offset)
+  uint8_t* buf;  // LDS, kWin bytes
+  int64_t lo, hi;
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Refill the window so that it starts at (16-byte aligned) pos.  Bytes at or past `e` are never
+// interpreted (every read checks pos < e); the 16-byte loads stay inside the payload pad.
+__device__ __forceinline__ void win_load(Win& w, int64_t pos, int lane) {
+  const int64_t lo = pos - int64_t((reinterpret_cast<uintptr_t>(w.img) + uintptr_t(pos)) & 15);
+  wave_lds_sync();
+  for (int k = lane; k < kWin / 16; k += 64) {
+    const int64_t o = lo + 16 * int64_t(k);
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (o < w.e) x = *reinterpret_cast<const uint4*>(w.img + o);
+    reinterpret_cast<uint4*>(w.buf)[k] = x;
+  }
+  wave_lds_sync();
+  w.lo = lo;
+  w.hi = lo + kWin;
+}
+
+__device__ __forceinline__ void win_ensure(Win& w, int64_t pos, int need, int lane) {
+  if (pos < w.lo || pos + need > w.hi) win_load(w, pos, lane);
+}
+
+// binary.ReadUvarint through the window.
+__device__ int win_uvarint(Win& w, int64_t& pos, uint64_t& v, int lane) {
+  win_ensure(w, pos, 10, lane);
+  uint64_t x = 0;
+  int s = 0;
+  for (int i = 0; i < 10; i++) {
+    if (pos >= w.e) return i ? PQH_ERR_UNEXPECTED_EOF : PQH_ERR_EOF;
+    const uint32_t c = w.buf[pos - w.lo];
+    pos++;
+    if (c < 0x80) {
+      if (i == 9 && c > 1) return PQH_ERR_VARINT_OVERFLOW;
+      v = x | (uint64_t(c) << s);
+      return PQH_OK;
+    }
+    x |= uint64_t(c & 0x7f) << s;
+    s += 7;
+  }
+  return PQH_ERR_VARINT_OVERFLOW;
+}
+
+// readUVariant32 (helpers.go:151-167)
+__device__ __forceinline__ int win_uvar32(Win& w, int64_t& pos, int32_t& out, int lane) {
+  uint64_t v;
+  int st = win_uvarint(w, pos, v, lane);
+  if (st) return st;
+  if (v > 0x7fffffffull) return PQH_ERR_INT32_RANGE;
+  out = int32_t(v);
+  return PQH_OK;
+}
+
+// readVariant32 / readVariant64 (helpers.go:169-208) as uint64 bits
+__device__ __forceinline__ int win_varint(Win& w, int64_t& pos, bool is64, uint64_t& out, int lane) {
+  uint64_t u;
+  int st = win_uvarint(w, pos, u, lane);
+  if (st) return st;
+  const int64_t x = int64_t(u >> 1) ^ -int64_t(u & 1);
+  if (!is64 && (x > 2147483647ll || x < -2147483648ll)) return PQH_ERR_INT32_RANGE;
+  out = uint64_t(x);
+  return PQH_OK;
+}
+
+// readMiniBlockHeader (:88-111 / :247-270): minDelta + mb_count width bytes (mb_count <= 8).
+__device__ __forceinline__ int win_miniblock_header(Win& w, int64_t& pos, bool is64, int mbc, uint64_t& min_delta,
+                                                    uint64_t& widths, int lane) {
+  int st = win_varint(w, pos, is64, min_delta, lane);
+  if (st) return st;
+  const int64_t avail = w.e - pos;
+  if (avail <= 0) return PQH_ERR_EOF;
+  if (avail < mbc) return PQH_ERR_UNEXPECTED_EOF;
+  win_ensure(w, pos, 8, lane);
+  widths = 0;
+  for (int i = 0; i < mbc; i++) {
+    const uint32_t wb = w.buf[pos - w.lo + i];
+    if (wb > (is64 ? 64u : 32u)) return PQH_ERR_DELTA_BIT_WIDTH;
+    widths |= uint64_t(wb) << (8 * i);
+  }
+  pos += mbc;
+  return PQH_OK;
+}
+
+__device__ __forceinline__ int mb_width(uint64_t widths, int m) { return int((widths >> (8 * m)) & 0xff); }
+
+// The block walk of one page (whole wave, uniform).  Returns the first error key.
+__device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaBlock* recs, int32_t cap,
+                               DeltaState& D, int lane) {
+  D.mode = DM_NONE;
+  D.nblocks = 0;
+  D.limit = 0;
+  D.first = 0;
+  D.end_pos = vs;
+  int64_t pos = vs;
+  int st;
+  // ---- init (page load, phase 0 step 3): readBlockHeader + readMiniBlockHeader ----
+  int32_t bs, mbc, vc;
+  if ((st = win_uvar32(w, pos, bs, lane))) return err_key(0, 3, st);
+  if ((st = win_uvar32(w, pos, mbc, lane))) return err_key(0, 3, st);
+  if (mbc <= 0 || bs % mbc != 0) return err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  const int32_t mbvc = bs / mbc;
+  if (mbvc == 0) return err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  if ((st = win_uvar32(w, pos, vc, lane))) return err_key(0, 3, st);
+  uint64_t first;
+  if ((st = win_varint(w, pos, is64, first, lane))) return err_key(0, 3, st);
+  D.block_size = bs;
+  D.mb_count = mbc;
+  D.mbvc = mbvc;
+  D.first = first;
+  const bool fast = mbc <= 8 && (mbvc & 7) == 0 && bs >= kDeltaBlockMin && (2048 % bs) == 0;
+  if (!fast) {
+    D.mode = DM_SERIAL;  // exact sequential decoder (TK_DELTA_SERIAL) redoes the page
+    return kNoError;
+  }
+  uint64_t md, widths;
+  if ((st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) return err_key(0, 3, st);
+  D.mode = DM_FAST;
+  // ---- readValues: positions [0, nn) (phase 3) ----
+  const int64_t L = nn < vc ? nn : vc;                                 // reachable positions
+  const int64_t pstar = vc <= 8 ? 0 : ((int64_t(vc) - 8 + 7) / 8) * 8;  // padding-skip group
+  const int64_t gbytes = mbvc / 8;
+  uint64_t err = kNoError;
+  int64_t limit = nn;
+  bool padded = false;
+  for (int64_t b = 0; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
+    const int64_t p0 = b * bs;
+    if (b > 0 && (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
+      err = err_key(3, p0, st);
+      limit = p0;
+      break;
+    }
+    if (D.nblocks >= cap) {
+      D.mode = DM_SERIAL;
+      return kNoError;
+    }
+    if (lane == 0) recs[D.nblocks] = DeltaBlock{md, int32_t(pos), int32_t(p0), widths, 0};
+    D.nblocks++;
+    for (int m = 0; m < mbc; m++) {
+      const int64_t pm = p0 + int64_t(m) * mbvc;
+      if (pm >= L) break;
+      const int wm = mb_width(widths, m);
+      const int64_t pend = pm + mbvc < L ? pm + mbvc : L;
+      const bool has_pad = pstar >= pm && pstar < pend;
+      const int64_t ng = has_pad ? (pstar - pm) / 8 + 1 : (pend - pm + 7) / 8;  // group reads
+      if (wm > 0) {  // io.ReadFull(w bytes) per group: the first group past the end fails
+        const int64_t avail = w.e - pos > 0 ? w.e - pos : 0;
+        const int64_t gf = avail / wm;
+        if (gf < ng) {
+          err = err_key(3, pm + 8 * gf, avail - gf * wm <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+          limit = pm + 8 * gf;
+          break;
+        }
+      }
+      pos += ng * wm;
+      if (has_pad) {  // skip the rest of this miniblock, then (sic) widths[currentMiniBlock] per miniblock left
+        const int64_t l = gbytes * wm - ng * wm;
+        pos = pos + l < w.e ? pos + l : (pos > w.e ? pos : w.e);
+        if (m + 1 < mbc) {
+          const int w2 = mb_width(widths, m + 1);
+          for (int i = m + 1; i < mbc; i++)
+            if (w2 != 0) pos = pos + gbytes * w2 < w.e ? pos + gbytes * w2 : (pos > w.e ? pos : w.e);
+        }
+        padded = true;
+        break;
+      }
+    }
+  }
+  if (err == kNoError && nn > vc) {  // next() at position >= valuesCount -> io.EOF
+    err = err_key(3, vc, PQH_ERR_EOF);
+    limit = vc;
+  }
+  D.limit = int32_t(limit);
+  D.end_pos = pos;
+  return err;
+}
+
+// One wave per delta page.
+__global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* delta_pages, int32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kWin];
+  const int lane = threadIdx.x & 63;
+  const int wv = int(threadIdx.x >> 6);
+  const int idx = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+  if (idx >= n) return;
+  const int p = delta_pages[idx];
+  const DevPage P = b.pages[p];
+  const PageState S = b.states[p];
+  DeltaState D;
+  D.mode = DM_NONE;
+  D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = 0;
+  D.first = 0;
+  D.end_pos = 0;
+  uint64_t err = kNoError;
+  // A page whose earlier load steps failed never initialises its values decoder.
+  const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
+  if (P.host_err == kNoError && load_ok) {
+    Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
+    win_load(w, S.val_s, lane);
+    const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+    err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn,
+                     b.dblocks + P.dblk_base, P.dblk_cap, D, lane);
+  }
+  if (lane == 0) {
+    b.dstates[p] = D;
+    if (err != kNoError) atomicMin(&b.states[p].err, (unsigned long long)err);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile work: deltas of values [c0, c1) staged in LDS block by block.
+// ------------------------------------------------------------------------------------------------
+struct DeltaLds {
+  int32_t mboff[16][8];  // byte offset of each miniblock's data relative to the stage start
+  uint8_t mbw[16][8];
+  uint64_t md[16];
+  uint64_t wsum[4];
+  int32_t lead;          // bytes between the 16-aligned stage start and the first data byte
+  int32_t pad;
+};
+
+__device__ __forceinline__ uint64_t extract64(const uint32_t* stage, uint32_t bit, int w) {
+  if (w == 0) return 0;
+  const uint32_t k = bit >> 5, s = bit & 31;
+  const uint64_t lo = uint64_t(stage[k]) | (uint64_t(stage[k + 1]) << 32);
+  uint64_t v = s ? ((lo >> s) | (uint64_t(stage[k + 2]) << (64 - s))) : lo;
+  return w >= 64 ? v : (v & ((1ull << w) - 1));
+}
+
+// Inclusive block-wide scan of one uint64 per thread; returns the exclusive prefix, *total set.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* wsum, uint64_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t incl = x;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0;
+  for (int k = 0; k < wv; k++) before += wsum[k];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return before + incl - x;
+}
+
+// Process values [v0, v1) of a DM_FAST delta page: sum (store == false) or store values.
+// Returns the sum of (delta + minDelta) over positions [v0, v1).  Sub-chunks of 256*VPT positions
+// are staged in LDS from the byte holding the first position's bits (at most 8 KiB of deltas plus
+// the headers of <= 16 blocks); VPT consecutive positions per thread always share one miniblock.
+template <bool IS64>
+__device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaState& D, int64_t v0, int64_t v1,
+                               uint64_t base, bool store, uint8_t* out, uint32_t* stage, DeltaLds& DL) {
+  constexpr int VPT = IS64 ? 4 : 8;
+  constexpr int SUB = kBlock * VPT;
+  const uint8_t* img = b.payload + P.image_off;
+  const DeltaBlock* recs = b.dblocks + P.dblk_base;
+  const int bs = D.block_size, mbvc = D.mbvc, mbc = D.mb_count;
+  uint64_t carry = base, total_all = 0;
+  for (int64_t c0 = v0; c0 < v1; c0 += SUB) {
+    const int64_t c1 = c0 + SUB < v1 ? c0 + SUB : v1;
+    const int bb0 = int(c0 / bs), nb = int((c1 - 1) / bs) - bb0 + 1;
+    __syncthreads();
+    if (threadIdx.x < nb) {  // per-block miniblock data offsets (image offsets)
+      const DeltaBlock r = recs[bb0 + threadIdx.x];
+      int32_t off = r.data_off;
+      for (int m = 0; m < 8; m++) {
+        const int wm = m < mbc ? mb_width(r.widths, m) : 0;
+        DL.mboff[threadIdx.x][m] = off;
+        DL.mbw[threadIdx.x][m] = uint8_t(wm);
+        off += (mbvc / 8) * wm;
+      }
+      DL.md[threadIdx.x] = r.min_delta;
+    }
+    __syncthreads();
+    // exact byte range holding the bits of positions [c0, c1)
+    const int m0 = int((c0 % bs) / mbvc), j0 = int((c0 % bs) % mbvc);
+    const int64_t q = c1 - 1;
+    const int bl = int(q / bs) - bb0, m1 = int((q % bs) / mbvc), j1 = int((q % bs) % mbvc);
+    const int64_t start = DL.mboff[0][m0] + (int64_t(j0) * DL.mbw[0][m0]) / 8;
+    const int64_t end = DL.mboff[bl][m1] + (int64_t(j1 + 1) * DL.mbw[bl][m1] + 7) / 8;
+    const int64_t a0 = start - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(start)) & 15);
+    const int64_t nvec = end > a0 ? (end - a0 + 15) >> 4 : 0;
+    const int64_t e = P.image_len;  // never past the page image (+pad)
+    for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
+      const int64_t o = a0 + k * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
+      reinterpret_cast<uint4*>(stage)[k] = x;
+    }
+    if (threadIdx.x == 0) {
+      stage[nvec * 4] = 0;
+      stage[nvec * 4 + 1] = 0;
+    }
+    __syncthreads();
+    const int64_t p = c0 + VPT * int64_t(threadIdx.x);
+    uint64_t d[VPT];
+    uint64_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < VPT; j++) d[j] = 0;
+    if (p < c1) {
+      const int blk = int(p / bs) - bb0;
+      const int m = int((p % bs) / mbvc);
+      const int wm = DL.mbw[blk][m];
+      const uint32_t bit0 = uint32_t(DL.mboff[blk][m] - a0) * 8 + uint32_t((p % bs) % mbvc) * uint32_t(wm);
+      const uint64_t md = DL.md[blk];
+#pragma unroll
+      for (int j = 0; j < VPT; j++) {
+        const uint64_t x = p + j < c1 ? extract64(stage, bit0 + uint32_t(j * wm), wm) + md : 0;
+        d[j] = x;
+        tsum += x;
+      }
+    }
+    uint64_t tot;
+    const uint64_t excl = block_exclusive_scan(tsum, DL.wsum, &tot);
+    if (store && p < c1) {
+      uint64_t v = carry + excl;
+      using T = typename std::conditional<IS64, uint64_t, uint32_t>::type;
+      T vals[VPT];
+#pragma unroll
+      for (int j = 0; j < VPT; j++) {
+        vals[j] = T(v);
+        v += d[j];
+      }
+      T* o = reinterpret_cast<T*>(out) + p;
+      if (p + VPT <= c1) {
+        __builtin_memcpy(o, vals, sizeof(vals));
+      } else {
+#pragma unroll
+        for (int j = 0; j < VPT; j++)
+          if (p + j < c1) o[j] = vals[j];
+      }
+    }
+    carry += tot;
+    total_all += tot;
+  }
+  return total_all;
+}
+
+// k_delta_sum: per tile sum of (delta + minDelta) over its positions.
+__global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles) {
+  __shared__ __attribute__((aligned(16))) uint32_t stage[(kStageBytes + 32) / 4];
+  __shared__ DeltaLds DL;
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  const DeltaState D = b.dstates[t.page];
+  if (D.mode != DM_FAST) return;
+  const int64_t v0 = int64_t(t.k) * kDeltaTile;
+  int64_t v1 = v0 + kDeltaTile;
+  const int64_t have = int64_t(D.nblocks) * D.block_size;
+  if (v1 > have) v1 = have;
+  if (v1 > D.limit) v1 = D.limit;
+  uint64_t s = 0;
+  if (v0 < v1)
+    s = P.kind == K_DELTA64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, stage, DL)
+                            : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, stage, DL);
+  if (threadIdx.x == 0) b.dsums[P.dtile_base + t.k] = s;
+}
+
+// k_delta_scan: one thread per delta page; tile bases = first + exclusive scan of tile sums.
+__global__ __launch_bounds__(256) void k_delta_scan(DevBatch b, const int32_t* delta_pages, int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int p = delta_pages[i];
+  const DevPage P = b.pages[p];
+  uint64_t run = b.dstates[p].first;
+  for (int k = 0; k < P.dtile_n; k++) {
+    const uint64_t s = b.dsums[P.dtile_base + k];
+    b.dsums[P.dtile_base + k] = run;
+    run += s;
+  }
+}
+
+// TK_DELTA: values [k*kDeltaTile, ...) of a DM_FAST page.
+__device__ __forceinline__ void tile_delta(const DevBatch& b, const Tile& t, uint32_t* stage, DeltaLds& DL) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const DeltaState D = b.dstates[t.page];
+  if (D.mode != DM_FAST) return;
+  const int64_t v0 = int64_t(t.k) * kDeltaTile;
+  int64_t v1 = v0 + kDeltaTile;
+  if (v1 > D.limit) v1 = D.limit;
+  if (v0 >= v1) return;
+  const DevChunk C = b.chunks[P.chunk];
+  uint8_t* out = C.values + S.value_base * P.value_size;
+  // value[i] needs deltas p < i: the last value of the page needs no delta of its own, and
+  // positions past the last recorded block are never reached (the walk stops there).
+  const uint64_t base = b.dsums[P.dtile_base + t.k];
+  if (P.kind == K_DELTA64) delta_tile<true>(b, P, D, v0, v1, base, true, out, stage, DL);
+  else delta_tile<false>(b, P, D, v0, v1, base, true, out, stage, DL);
+}
+
+// TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.next for streams outside
+// the fast-path geometry.  One thread; the rest of the workgroup idles (rare layouts only).
+__device__ void delta_serial(const DevBatch& b, const Tile& t) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  const DeltaState D0 = b.dstates[t.page];
+  if (D0.mode != DM_SERIAL || threadIdx.x != 0) return;
+  const uint8_t* img = b.payload + P.image_off;
+  const int64_t e = S.val_e;
+  const bool is64 = P.kind == K_DELTA64;
+  const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+  const int64_t nn = before_values ? 0 : S.nn;
+  const DevChunk C = b.chunks[P.chunk];
+  uint8_t* out = C.values + S.value_base * P.value_size;
+  int64_t pos = S.val_s;
+  auto uvar = [&](uint64_t& v) { return read_uvarint(img, pos, e, v); };
+  auto uvar32 = [&](int32_t& o) {
+    uint64_t v;
+    int st = uvar(v);
+    if (st) return st;
+    if (v > 0x7fffffffull) return int(PQH_ERR_INT32_RANGE);
+    o = int32_t(v);
+    return int(PQH_OK);
+  };
+  auto var = [&](uint64_t& o) {
+    uint64_t u;
+    int st = uvar(u);
+    if (st) return st;
+    const int64_t x = int64_t(u >> 1) ^ -int64_t(u & 1);
+    if (!is64 && (x > 2147483647ll || x < -2147483648ll)) return int(PQH_ERR_INT32_RANGE);
+    o = uint64_t(x);
+    return int(PQH_OK);
+  };
+  auto read_full_skip = [&](int64_t nbytes) {  // io.ReadFull, errors ignored
+    if (nbytes <= 0) return;
+    pos = pos + nbytes < e ? pos + nbytes : (pos > e ? pos : e);
+  };
+  uint64_t err = kNoError;
+  int32_t bs = 0, mbc = 0, vc = 0, mbvc = 0;
+  uint64_t prev = 0, md = 0;
+  int64_t widths_pos = 0;  // widths live in the image at widths_pos (mbc bytes)
+  int st;
+  // ---- init ----
+  if ((st = uvar32(bs)) || (st = uvar32(mbc))) err = err_key(0, 3, st);
+  if (err == kNoError && (mbc <= 0 || bs % mbc != 0)) err = err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  if (err == kNoError) {
+    mbvc = bs / mbc;
+    if (mbvc == 0) err = err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  }
+  if (err == kNoError && (st = uvar32(vc))) err = err_key(0, 3, st);
+  if (err == kNoError && (st = var(prev))) err = err_key(0, 3, st);
+  auto mini_header = [&]() -> int {
+    int s2 = var(md);
+    if (s2) return s2;
+    const int64_t avail = e - pos;
+    if (avail <= 0) return PQH_ERR_EOF;
+    if (avail < mbc) {
+      pos = e;
+      return PQH_ERR_UNEXPECTED_EOF;
+    }
+    widths_pos = pos;
+    for (int32_t i = 0; i < mbc; i++)
+      if (img[pos + i] > (is64 ? 64 : 32)) return PQH_ERR_DELTA_BIT_WIDTH;
+    pos += mbc;
+    return PQH_OK;
+  };
+  if (err == kNoError && (st = mini_header())) err = err_key(0, 3, st);
+  // ---- next() x nn ----
+  int32_t cur_mb = 0, cur_w = 0, mb_pos = 0;
+  int64_t gpos = 0;  // byte offset of the current group of 8 deltas
+  for (int64_t position = 0; err == kNoError && position < nn; position++) {
+    if (position >= vc) {
+      err = err_key(3, position, PQH_ERR_EOF);
+      break;
+    }
+    if (position % 8 == 0) {
+      if (position % mbvc == 0) {
+        if (cur_mb >= mbc) {
+          if ((st = mini_header())) {
+            err = err_key(3, position, st);
+            break;
+          }
+          cur_mb = 0;
+        }
+        cur_w = img[widths_pos + cur_mb];
+        mb_pos = 0;
+        cur_mb++;
+      }
+      const int32_t w = cur_w;
+      if (w > 0) {
+        const int64_t avail = e - pos;
+        if (avail < w) {
+          err = err_key(3, position, avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+          break;
+        }
+      }
+      gpos = pos;
+      pos += w;
+      mb_pos += w;
+      if (position + 8 >= vc) {
+        const int64_t l = int64_t(mbvc / 8) * w - mb_pos;
+        if (l < 0) {
+          err = err_key(3, position, PQH_ERR_DELTA_STREAM);
+          break;
+        }
+        read_full_skip(l);
+        for (int32_t i = cur_mb; i < mbc; i++) {
+          const int32_t w2 = img[widths_pos + cur_mb];
+          if (w2 != 0) read_full_skip(int64_t(mbvc / 8) * w2);
+        }
+      }
+    }
+    if (is64) reinterpret_cast<uint64_t*>(out)[position] = prev;
+    else reinterpret_cast<uint32_t*>(out)[position] = uint32_t(prev);
+    uint64_t delta = 0;  // unpack8 (LSB first) of this position's w bits
+    for (int k2 = 0; k2 < cur_w; k2++) {
+      const int64_t bit = int64_t(position % 8) * cur_w + k2;
+      delta |= uint64_t((img[gpos + (bit >> 3)] >> (bit & 7)) & 1) << k2;
+    }
+    prev += delta + md;
+  }
+  if (err != kNoError) atomicMin(&b.states[t.page].err, (unsigned long long)err);
+}

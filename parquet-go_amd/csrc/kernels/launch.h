@@ -15,6 +15,9 @@ struct DevBatch {
   Ckpt* ckpts;
   int32_t num_pages;
   int32_t num_chunks;
+  DeltaState* dstates;   // per page (delta pages only are written)
+  DeltaBlock* dblocks;
+  uint64_t* dsums;       // per delta tile: sum, then (after k_delta_scan) the tile's base value
 };
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
@@ -22,6 +25,10 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
+// DELTA_BINARY_PACKED: block walk (one wave per delta page), per-tile sums, per-page scan.
+hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
+hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.
 hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 

@@ -136,7 +136,14 @@ def _fuzz(pq, ctx, data, seed, per_page=3):
                 if ptype == O.DATA_PAGE_V2 and rl + dl > len(img2):
                     continue  # the host walker rejects such headers before the device sees them
                 cases.append((col, dict_img, (ptype, nv, enc, dl, rl, img2)))
-    # build one batch: every case is its own chunk (dictionary page first when present)
+    return _run_cases(pq, ctx, cases)
+
+
+def _run_cases(pq, ctx, cases):
+    """Decode `cases` = [(column, dictionary (num_values, encoding, image) or None, data page)] in ONE
+    batch (every case its own chunk) and compare each against the oracle's decode_page."""
+    N = pq.native
+    # every case is its own chunk (dictionary page first when present)
     blobs, chunks, pages = [], [], []
     off = 0
 
@@ -208,3 +215,85 @@ def test_fuzz_pyarrow_pages(pq, ctx, seed):
 def test_fuzz_nested_pages(pq, ctx):
     compared, errors = _fuzz(pq, ctx, fixtures.nested_list_map(n=1500), 6)
     assert compared > 5
+
+
+# ---------------------------------------------------------------------------------------------
+# DELTA_BINARY_PACKED: every block geometry the reference decoder accepts
+# ---------------------------------------------------------------------------------------------
+DELTA_GEOMETRIES = [(128, 4), (128, 1), (256, 8), (512, 4), (1024, 8), (2048, 4), (2048, 1),  # device fast path
+                    (64, 2), (128, 16), (96, 3), (24, 3), (12, 3), (4096, 4), (32, 1)]     # serial decoder
+
+
+def _delta_cases(rng, sizes, kinds, mutate):
+    import delta_streams as DS
+    W = fixtures.W
+    cases = []
+    for bs, mbc in DELTA_GEOMETRIES:
+        for bits in (32, 64):
+            col = (W.INT32 if bits == 32 else W.INT64, 0, 0, 0)
+            for n in sizes:
+                kind = kinds[int(rng.integers(0, len(kinds)))]
+                finish = "omit" if rng.random() < 0.5 else "full"
+                vals = DS.random_values(rng, n, bits, kind)
+                img = DS.encode(vals, bits, bs, mbc, finish)
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img)))
+                if not mutate:
+                    continue
+                # page claims more values than the stream holds; header count below the page's
+                cases.append((col, None, (O.DATA_PAGE, n + int(rng.integers(1, 20)), W.DELTA_BINARY_PACKED, 0, 0, img)))
+                img2 = DS.encode(vals, bits, bs, mbc, finish, total=max(0, n - int(rng.integers(1, 10))))
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img2)))
+                # truncated anywhere, or a corrupted byte
+                cut = int(rng.integers(0, len(img) + 1))
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img[:cut])))
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, _mutate(rng, img))))
+    return cases
+
+
+def test_delta_geometries(pq, ctx):
+    rng = np.random.default_rng(31)
+    cases = _delta_cases(rng, [1, 2, 8, 9, 33, 129, 257, 1000, 2049, 4097], ["const", "mono", "small", "full", "mixed"],
+                         mutate=True)
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors > 50
+
+
+def test_delta_multi_tile_pages(pq, ctx):
+    """Pages spanning several 8192-value delta tiles (tile sums + page scan)."""
+    rng = np.random.default_rng(32)
+    cases = _delta_cases(rng, [8193, 30001], ["small", "mixed", "full"], mutate=False)
+    compared, _ = _run_cases(pq, ctx, cases)
+    assert compared == len(cases)
+
+
+def test_delta_optional_v2(pq, ctx):
+    """DELTA values behind definition levels (notNull < num_values) on V2 pages."""
+    import delta_streams as DS
+    W = fixtures.W
+    rng = np.random.default_rng(33)
+    cases = []
+    for bits in (32, 64):
+        for n in (1, 100, 129, 5000, 20000):
+            mask = rng.random(n) < 0.7
+            dl = W.hybrid_encode(1, mask.astype(np.int32))
+            nn = int(mask.sum())
+            img = DS.encode(DS.random_values(rng, nn, bits, "mixed"), bits, 128, 4, "omit") if nn else DS.encode([], bits)
+            col = (W.INT32 if bits == 32 else W.INT64, 0, 1, 0)
+            cases.append((col, None, (O.DATA_PAGE_V2, n, W.DELTA_BINARY_PACKED, len(dl), 0, dl + img)))
+    compared, _ = _run_cases(pq, ctx, cases)
+    assert compared == len(cases)
+
+
+def test_delta_writer_pages(pq, ctx):
+    """Reference-writer delta columns (128/4 blocks) in files: required, optional, large pages."""
+    W = fixtures.W
+    rng = np.random.default_rng(34)
+    n = 300000
+    cols = [("a", W.Column(W.INT64, np.cumsum(rng.integers(-5, 100, n)), encoding=W.DELTA_BINARY_PACKED), W.REQUIRED),
+            ("b", W.Column(W.INT32, rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype(np.int32),
+                           encoding=W.DELTA_BINARY_PACKED), W.REQUIRED),
+            ("c", W.optional(W.INT64, rng.integers(0, 2**40, n), rng.random(n) < 0.2, encoding=W.DELTA_BINARY_PACKED,
+                             use_dict=False), W.OPTIONAL)]
+    for v2 in (False, True):
+        checked, _ = _run_file(pq, ctx, W.flat(cols, n // 2, v2=v2), allow_not_implemented=False)
+        assert checked == 6
