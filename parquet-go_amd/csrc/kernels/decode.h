@@ -63,6 +63,10 @@ struct DevPage {
   int32_t dblk_cap;      // records available (pages of blockSize >= 128)
   int32_t dtile_base;    // first per-tile delta sum
   int32_t dtile_n;       // delta tiles of the page (kDeltaTile values each)
+  int32_t aux_base;      // byte-array dictionary page: first entry of its dcum table
+  int32_t batile_base;   // byte-array data page: first kBaTile tile sum (chunk-contiguous)
+  int32_t batile_n;
+  int32_t pad;
 };
 
 struct DevChunk {
@@ -77,6 +81,9 @@ struct DevChunk {
   uint8_t* rep_levels;
   int64_t values_cap;    // values capacity (elements)
   int64_t bytes_cap;
+  int32_t* aux;          // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH) or dictionary key
+  int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
+  int32_t batile_n;
 };
 
 // Written by the prologue (one wave per page) and the scan kernel.
@@ -135,8 +142,11 @@ enum TileKind : int32_t {
   TK_RLE_BOOL = 4,
   TK_DICT_GLOBAL = 5,
   TK_DELTA = 6,         // kDeltaTile values of a DM_FAST delta page
-  TK_DELTA_SERIAL = 7   // a whole DM_SERIAL delta page (exact sequential decoder)
+  TK_DELTA_SERIAL = 7,  // a whole DM_SERIAL delta page (exact sequential decoder)
+  TK_BA = 8             // kBaTile values of a byte-array data page (k_ba_sum / k_ba_expand)
 };
+
+constexpr int kBaTile = 2048;  // byte-array values per tile (one 256 x 8 block scan)
 
 // Work item of k_expand.  Hybrid-driven kinds cover [k, k+span) checkpoint intervals of
 // kHybridTile values; TK_COPY covers kCopyTileBytes bytes; TK_BOOL covers kBoolTile values.

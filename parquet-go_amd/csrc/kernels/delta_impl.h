@@ -111,8 +111,10 @@ __device__ __forceinline__ int win_miniblock_header(Win& w, int64_t& pos, bool i
 __device__ __forceinline__ int mb_width(uint64_t widths, int m) { return int((widths >> (8 * m)) & 0xff); }
 
 // The block walk of one page (whole wave, uniform).  Returns the first error key.
+// init_all: byteArrayDeltaLengthDecoder.init (type_bytearray.go:104-116) decodes ALL valuesCount
+// lengths at page load: every error is a load error (phase 0, step 3) and nn is ignored.
 __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaBlock* recs, int32_t cap,
-                               DeltaState& D, int lane) {
+                               DeltaState& D, int lane, bool init_all) {
   D.mode = DM_NONE;
   D.nblocks = 0;
   D.limit = 0;
@@ -143,6 +145,7 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   if ((st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) return err_key(0, 3, st);
   D.mode = DM_FAST;
   // ---- readValues: positions [0, nn) (phase 3) ----
+  if (init_all) nn = vc;
   const int64_t L = nn < vc ? nn : vc;                                 // reachable positions
   const int64_t pstar = vc <= 8 ? 0 : ((int64_t(vc) - 8 + 7) / 8) * 8;  // padding-skip group
   const int64_t gbytes = mbvc / 8;
@@ -152,7 +155,7 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   for (int64_t b = 0; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
     const int64_t p0 = b * bs;
     if (b > 0 && (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
-      err = err_key(3, p0, st);
+      err = init_all ? err_key(0, 3, st) : err_key(3, p0, st);
       limit = p0;
       break;
     }
@@ -173,7 +176,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
         const int64_t avail = w.e - pos > 0 ? w.e - pos : 0;
         const int64_t gf = avail / wm;
         if (gf < ng) {
-          err = err_key(3, pm + 8 * gf, avail - gf * wm <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+          const int code = avail - gf * wm <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
+          err = init_all ? err_key(0, 3, code) : err_key(3, pm + 8 * gf, code);
           limit = pm + 8 * gf;
           break;
         }
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
     win_load(w, S.val_s, lane);
     const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
     err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn,
-                     b.dblocks + P.dblk_base, P.dblk_cap, D, lane);
+                     b.dblocks + P.dblk_base, P.dblk_cap, D, lane, P.kind == K_DLBA);
   }
   if (lane == 0) {
     b.dstates[p] = D;
@@ -408,7 +412,10 @@ __device__ __forceinline__ void tile_delta(const DevBatch& b, const Tile& t, uin
   if (v1 > D.limit) v1 = D.limit;
   if (v0 >= v1) return;
   const DevChunk C = b.chunks[P.chunk];
-  uint8_t* out = C.values + S.value_base * P.value_size;
+  const bool dlba = P.kind == K_DLBA;  // lengths of a DELTA_LENGTH_BYTE_ARRAY page -> aux (int32)
+  if (dlba && v1 > S.nn) v1 = S.nn;
+  if (v0 >= v1) return;
+  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(C.aux + S.value_base) : C.values + S.value_base * P.value_size;
   // value[i] needs deltas p < i: the last value of the page needs no delta of its own, and
   // positions past the last recorded block are never reached (the walk stops there).
   const uint64_t base = b.dsums[P.dtile_base + t.k];
@@ -418,6 +425,8 @@ __device__ __forceinline__ void tile_delta(const DevBatch& b, const Tile& t, uin
 
 // TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.next for streams outside
 // the fast-path geometry.  One thread; the rest of the workgroup idles (rare layouts only).
+// DELTA_LENGTH_BYTE_ARRAY pages decode all valuesCount lengths at init (errors are load errors),
+// keep the first notNull of them and record where the string bytes start.
 __device__ void delta_serial(const DevBatch& b, const Tile& t) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
@@ -427,9 +436,11 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
   const int64_t e = S.val_e;
   const bool is64 = P.kind == K_DELTA64;
   const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
-  const int64_t nn = before_values ? 0 : S.nn;
+  const bool dlba = P.kind == K_DLBA;
+  const int64_t nvals = before_values ? 0 : S.nn;  // values the page keeps
+  int64_t nn = nvals;
   const DevChunk C = b.chunks[P.chunk];
-  uint8_t* out = C.values + S.value_base * P.value_size;
+  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(C.aux + S.value_base) : C.values + S.value_base * P.value_size;
   int64_t pos = S.val_s;
   auto uvar = [&](uint64_t& v) { return read_uvarint(img, pos, e, v); };
   auto uvar32 = [&](int32_t& o) {
@@ -484,6 +495,8 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
   };
   if (err == kNoError && (st = mini_header())) err = err_key(0, 3, st);
   // ---- next() x nn ----
+  if (dlba) nn = vc;
+  auto verr = [&](int64_t position, int code) { return dlba ? err_key(0, 3, code) : err_key(3, position, code); };
   int32_t cur_mb = 0, cur_w = 0, mb_pos = 0;
   int64_t gpos = 0;  // byte offset of the current group of 8 deltas
   for (int64_t position = 0; err == kNoError && position < nn; position++) {
@@ -495,7 +508,7 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
       if (position % mbvc == 0) {
         if (cur_mb >= mbc) {
           if ((st = mini_header())) {
-            err = err_key(3, position, st);
+            err = verr(position, st);
             break;
           }
           cur_mb = 0;
@@ -508,7 +521,7 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
       if (w > 0) {
         const int64_t avail = e - pos;
         if (avail < w) {
-          err = err_key(3, position, avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
+          err = verr(position, avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
           break;
         }
       }
@@ -518,7 +531,7 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
       if (position + 8 >= vc) {
         const int64_t l = int64_t(mbvc / 8) * w - mb_pos;
         if (l < 0) {
-          err = err_key(3, position, PQH_ERR_DELTA_STREAM);
+          err = verr(position, PQH_ERR_DELTA_STREAM);
           break;
         }
         read_full_skip(l);
@@ -529,13 +542,17 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
       }
     }
     if (is64) reinterpret_cast<uint64_t*>(out)[position] = prev;
-    else reinterpret_cast<uint32_t*>(out)[position] = uint32_t(prev);
+    else if (position < nvals) reinterpret_cast<uint32_t*>(out)[position] = uint32_t(prev);
     uint64_t delta = 0;  // unpack8 (LSB first) of this position's w bits
     for (int k2 = 0; k2 < cur_w; k2++) {
       const int64_t bit = int64_t(position % 8) * cur_w + k2;
       delta |= uint64_t((img[gpos + (bit >> 3)] >> (bit & 7)) & 1) << k2;
     }
     prev += delta + md;
+  }
+  if (dlba) {
+    b.dstates[t.page].end_pos = pos;
+    b.dstates[t.page].limit = err == kNoError ? vc : 0;
   }
   if (err != kNoError) atomicMin(&b.states[t.page].err, (unsigned long long)err);
 }

@@ -18,6 +18,9 @@ struct DevBatch {
   DeltaState* dstates;   // per page (delta pages only are written)
   DeltaBlock* dblocks;
   uint64_t* dsums;       // per delta tile: sum, then (after k_delta_scan) the tile's base value
+  int32_t* dcum;         // byte-array dictionary pages: cumulative entry bytes (num_values + 1 each)
+  int64_t* basums;       // per byte-array tile: byte sum, then (after k_ba_scan) the tile's first offset
+  int64_t* chunk_bytes;  // per chunk: total string bytes (k_ba_scan)
 };
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
@@ -29,6 +32,12 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
 hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
+// Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
+// per-chunk offset scan, offsets + byte copy.
+hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s);
+hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, hipStream_t s);
+hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.
 hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 
