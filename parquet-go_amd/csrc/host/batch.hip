@@ -52,8 +52,9 @@ struct KernelRun {
 };
 
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
-                              "k_delta_walk", "k_delta_sum", "k_delta_scan"};
-constexpr int kNumKernels = 7;
+                              "k_delta_walk", "k_delta_sum", "k_delta_scan",
+                              "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand"};
+constexpr int kNumKernels = 11;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -124,6 +125,10 @@ struct pqh_batch {
   std::vector<Tile> global_tiles;   // k_dict_global work list
   std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
+  std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
+  std::vector<int32_t> ba_pages;    // k_ba_walk work list (PLAIN byte-array data + dictionary pages)
+  std::vector<int32_t> ba_chunks;   // k_ba_scan work list
+  std::vector<int64_t> chunk_bytes; // host copy after sync
   size_t expand_lds = 0;            // dynamic LDS of k_expand: largest staged dictionary
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
@@ -138,6 +143,12 @@ struct pqh_batch {
   DeltaState* d_dstates = nullptr;
   DeltaBlock* d_dblocks = nullptr;
   uint64_t* d_dsums = nullptr;
+  Tile* d_batiles = nullptr;
+  int32_t* d_ba_pages = nullptr;
+  int32_t* d_ba_chunks = nullptr;
+  int32_t* d_dcum = nullptr;
+  int64_t* d_basums = nullptr;
+  int64_t* d_chunk_bytes = nullptr;
   std::vector<void*> allocations;
   std::vector<PageState> states;   // host copy after sync
   std::vector<int64_t> chunk_n;    // level slots per chunk
@@ -265,7 +276,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   b->k_written.assign(kNumKernels, 0);
 
   // ---- per-page planning ----
-  int64_t ck_cursor = 0, dblk_cursor = 0, dtile_cursor = 0;
+  int64_t ck_cursor = 0, dblk_cursor = 0, dtile_cursor = 0, dcum_cursor = 0;
+  std::vector<int64_t> bytes_est(size_t(num_chunks), 0);
   std::vector<std::vector<Tile>> by_kind(8);
   for (int32_t c = 0; c < num_chunks; c++) {
     const pqh_chunk& C = chunks[c];
@@ -286,6 +298,10 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       return set_err(ctx, PQH_ERR_ARG, "chunk page range out of bounds");
     }
     const uint64_t chunk_err = C.host_status != PQH_OK ? err_key(0, 0, C.host_status) : kNoError;
+    const bool ba_chunk = C.column.physical_type == PQH_BYTE_ARRAY ||
+                          (C.column.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && C.column.type_length == 0);
+    D.batile_base = int32_t(b->ba_tiles.size());
+    if (ba_chunk) b->ba_chunks.push_back(c);
     int64_t level_base = 0;
     for (int32_t i = 0; i < C.num_pages; i++) {
       const int32_t p = C.first_page + i;
@@ -320,8 +336,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
           P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
         else if (C.column.physical_type == PQH_BOOLEAN)
           P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
-        else if (dvs == 0)
-          P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
+        if (kind == K_PLAIN_BA && P.host_err == kNoError) {  // byte-array dictionary: PLAIN chain walk
+          P.aux_base = int32_t(dcum_cursor);
+          dcum_cursor += int64_t(std::max(0, Q.num_values)) + 1;
+          b->ba_pages.push_back(p);
+        }
         if (i == 0) D.dict_page = p;
         b->bytes_read += Q.image_len;
         continue;
@@ -341,13 +360,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       if (kind == K_UNSUPPORTED) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
       const bool device_ready = kind == K_PLAIN_FIXED || kind == K_PLAIN_INT96 || kind == K_PLAIN_BOOL ||
                                 kind == K_RLE_BOOL || kind == K_FLBA_NEGATIVE || kind == K_UNSUPPORTED ||
-                                kind == K_DELTA32 || kind == K_DELTA64 || (kind == K_DICT && pvs > 0);
+                                kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DICT || kind == K_PLAIN_BA ||
+                                kind == K_DLBA;
       if (!device_ready) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
       const int64_t n = Q.num_values > 0 ? Q.num_values : 0;
       P.level_base = level_base;
       level_base += n;
       b->bytes_read += Q.image_len;
-      if ((kind == K_DELTA32 || kind == K_DELTA64) && P.host_err == kNoError) {
+      if ((kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DLBA) && P.host_err == kNoError) {
         // the values decoder is initialised (and may fail) even for pages without values
         P.dblk_base = int32_t(dblk_cursor);
         P.dblk_cap = int32_t(ceil_div(n, kDeltaBlockMin) + 1);
@@ -358,6 +378,23 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         b->delta_pages.push_back(p);
         for (int32_t k = 0; k < P.dtile_n; k++) by_kind[TK_DELTA].push_back(Tile{p, k, TK_DELTA, 1});
         by_kind[TK_DELTA_SERIAL].push_back(Tile{p, 0, TK_DELTA_SERIAL, 1});
+      }
+      const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT);
+      if (ba_page && P.host_err == kNoError && n > 0) {
+        P.batile_base = int32_t(b->ba_tiles.size());
+        P.batile_n = int32_t(ceil_div(n, kBaTile));
+        for (int32_t k = 0; k < P.batile_n; k++) b->ba_tiles.push_back(Tile{p, k, TK_BA, 1});
+        if (kind == K_PLAIN_BA) b->ba_pages.push_back(p);
+        // output bytes: at most the page (PLAIN / DELTA_LENGTH); dictionary gathers are estimated
+        // from the dictionary page's mean entry and re-sized after the first run if short
+        int64_t est = Q.image_len;
+        if (kind == K_DICT && D.dict_page >= 0) {
+          const pqh_page& DQ = pages[D.dict_page];
+          const int64_t nv = std::max(1, DQ.num_values);
+          const int64_t mean = std::max<int64_t>(0, DQ.image_len - 4 * nv) / nv;
+          est = n * std::min<int64_t>(std::max<int64_t>(DQ.image_len, 0), 2 * mean + 16);
+        }
+        bytes_est[size_t(c)] += est;
       }
       if (n == 0) continue;
       const int64_t nt = ceil_div(n, kHybridTile);
@@ -410,6 +447,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       }
     }
     b->chunk_n[size_t(c)] = level_base;
+    D.batile_n = int32_t(b->ba_tiles.size()) - D.batile_base;
   }
   // Interleave the kinds proportionally along the dispatch order (k_expand's grid), so that every
   // CU sees a mix of byte-copy and bit-unpack tiles instead of one long phase per kind.
@@ -438,7 +476,13 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_delta_pages), sizeof(int32_t) * b->delta_pages.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dblocks), sizeof(DeltaBlock) * size_t(dblk_cursor))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor)))) {
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_batiles), sizeof(Tile) * b->ba_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
     return rc;
@@ -448,8 +492,18 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     const int64_t n = b->chunk_n[size_t(c)];
     D.values_cap = n;
     void* p = nullptr;
-    if ((rc = dalloc(b, &p, size_t(n) * size_t(std::max(D.value_size, 1)) + 64))) break;
+    const bool ba_chunk = D.physical_type == PQH_BYTE_ARRAY || (D.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && D.type_length == 0);
+    if ((rc = dalloc(b, &p, ba_chunk ? 64 : size_t(n) * size_t(std::max(D.value_size, 1)) + 64))) break;
     D.values = static_cast<uint8_t*>(p);
+    if (ba_chunk) {
+      if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int64_t)))) break;
+      D.offsets = static_cast<int64_t*>(p);
+      if ((rc = dalloc(b, &p, size_t(n) * sizeof(int32_t) + 64))) break;
+      D.aux = static_cast<int32_t*>(p);
+      D.bytes_cap = bytes_est[size_t(c)];
+      if ((rc = dalloc(b, &p, size_t(D.bytes_cap) + 64))) break;
+      D.bytes = static_cast<uint8_t*>(p);
+    }
     if (D.max_def > 0) {
       if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
       D.def_levels = static_cast<uint8_t*>(p);
@@ -477,6 +531,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   if (e == hipSuccess && !b->delta_pages.empty())
     e = hipMemcpyAsync(b->d_delta_pages, b->delta_pages.data(), sizeof(int32_t) * b->delta_pages.size(),
                        hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_tiles.empty())
+    e = hipMemcpyAsync(b->d_batiles, b->ba_tiles.data(), sizeof(Tile) * b->ba_tiles.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_pages.empty())
+    e = hipMemcpyAsync(b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_chunks.empty())
+    e = hipMemcpyAsync(b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size(),
+                       hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     free_batch(b);
@@ -499,7 +561,8 @@ int pqh_batch_run(pqh_batch* b) {
   const bool prof = (ctx->flags & PQH_CTX_PROFILE) != 0;
   hipStream_t s = ctx->stream;
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
-             int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums};
+             int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
+             b->d_chunk_bytes};
   b->synced = false;
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -521,6 +584,9 @@ int pqh_batch_run(pqh_batch* b) {
   if (e == hipSuccess && ndp)
     e = timed(4, ndp, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ndp, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
+  if (e == hipSuccess && nbp)
+    e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
   if (e == hipSuccess && ndt)
     e = timed(5, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
   if (e == hipSuccess && ndp)
@@ -530,6 +596,13 @@ int pqh_batch_run(pqh_batch* b) {
     e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
   if (e == hipSuccess && ng)
     e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
+  if (e == hipSuccess && nbt) {
+    e = timed(8, nbt, s, [&](hipStream_t st) { return launch_ba_sum(d, b->d_batiles, nbt, st); });
+    if (e == hipSuccess)
+      e = timed(9, nbc, s, [&](hipStream_t st) { return launch_ba_scan(d, b->d_ba_chunks, nbc, b->d_batiles, st); });
+    if (e == hipSuccess)
+      e = timed(10, nbt, s, [&](hipStream_t st) { return launch_ba_expand(d, b->d_batiles, nbt, st); });
+  }
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   return PQH_OK;
 }
@@ -542,7 +615,40 @@ int pqh_batch_sync(pqh_batch* b) {
   if (!b->pages.empty())
     HIP_TRY(ctx, hipMemcpyAsync(b->states.data(), b->d_states, sizeof(PageState) * b->pages.size(),
                                 hipMemcpyDeviceToHost, ctx->stream));
+  b->chunk_bytes.assign(b->chunks.size(), 0);
+  if (!b->ba_chunks.empty())
+    HIP_TRY(ctx, hipMemcpyAsync(b->chunk_bytes.data(), b->d_chunk_bytes, sizeof(int64_t) * b->chunks.size(),
+                                hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  // Byte-array outputs sized from an estimate (dictionary gathers): grow the chunks that came out
+  // short (and decoded without error), then decode again.  Contents are deterministic, so this
+  // happens at most once per batch.
+  bool regrow = false;
+  for (int32_t c : b->ba_chunks) {
+    DevChunk& D = b->hchunks[size_t(c)];
+    if (b->chunk_bytes[size_t(c)] <= D.bytes_cap) continue;
+    bool ok = true;
+    for (int32_t i = 0; i < D.num_pages && ok; i++) ok = b->states[size_t(D.first_page + i)].err == kNoError;
+    if (!ok) continue;
+    void* np = nullptr;
+    const int64_t cap = b->chunk_bytes[size_t(c)];
+    HIP_TRY(ctx, hipMalloc(&np, size_t(cap) + 64));
+    for (auto& a : b->allocations)
+      if (a == D.bytes) {
+        hipFree(a);
+        a = np;
+      }
+    D.bytes = static_cast<uint8_t*>(np);
+    D.bytes_cap = cap;
+    regrow = true;
+  }
+  if (regrow) {
+    HIP_TRY(ctx, hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * b->hchunks.size(),
+                                hipMemcpyHostToDevice, ctx->stream));
+    int rc = pqh_batch_run(b);
+    if (rc != PQH_OK) return rc;
+    return pqh_batch_sync(b);
+  }
   for (auto& r : b->pending) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess) {
@@ -603,6 +709,10 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[2] += vals;
         b->k_read[5] += S.val_e - S.val_s;
         break;
+      case K_PLAIN_BA:  // walked by k_ba_walk, bytes moved by k_ba_expand
+      case K_DLBA:
+        b->k_read[10] += S.val_e - S.val_s;
+        break;
       default:
         break;
     }
@@ -613,6 +723,15 @@ int pqh_batch_sync(pqh_batch* b) {
     const pqh_page& Q = b->pages[size_t(C.dict_page)];
     b->k_read[int64_t(std::max(0, Q.num_values)) * b->hpages[size_t(C.dict_page)].value_size > kDictLdsMax ? 3 : 2] +=
         Q.image_len;
+  }
+  for (int32_t c : b->ba_chunks) {  // offsets (8 B per value + 1) and string bytes, written by k_ba_expand
+    const DevChunk& C = b->hchunks[size_t(c)];
+    int64_t nn = 0;
+    for (int32_t i = 0; i < C.num_pages; i++)
+      if (b->hpages[size_t(C.first_page + i)].page_type != PQH_DICTIONARY_PAGE) nn += b->states[size_t(C.first_page + i)].nn;
+    const double w = double(nn + 1) * 8 + double(b->chunk_bytes[size_t(c)]);
+    wr += w;
+    b->k_written[10] += w;
   }
   b->bytes_written = wr;
   for (int k = 0; k < kNumKernels; k++) {
@@ -648,9 +767,10 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   memset(out, 0, sizeof(*out));
   out->num_values = b->chunk_n[size_t(chunk)];
   out->value_size = D.value_size;
-  out->values = D.values;
+  out->values = D.value_size > 0 ? D.values : nullptr;
   out->offsets = D.offsets;
   out->bytes = D.bytes;
+  out->num_bytes = D.offsets ? b->chunk_bytes[size_t(chunk)] : 0;
   out->def_levels = D.def_levels;
   out->rep_levels = D.rep_levels;
   out->status = PQH_OK;

@@ -244,9 +244,10 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
       } else {
         S.dict_n = int32_t(n);
       }
-    } else {
-      err = err_key(0, 0, PQH_ERR_UNSUPPORTED);  // byte-array dictionaries: k_ba_chain (next round)
+    } else if (P.kind == K_FLBA_NEGATIVE) {  // byteArrayPlainDecoder{length < 0}: first value fails
+      if (n > 0) err = err_key(0, 0, PQH_ERR_NEGATIVE_LENGTH);
     }
+    // byte-array dictionaries (K_PLAIN_BA): the PLAIN chain is walked by k_ba_walk
   } else if (err == kNoError) {
     const int64_t n = P.num_values;
     const int rw = bits_len32(uint32_t(C.max_rep)), dw = bits_len32(uint32_t(C.max_def));
@@ -375,6 +376,8 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
             }
             case K_DELTA32:
             case K_DELTA64:  // init + block walk in k_delta_walk (atomicMin into the same key)
+            case K_DLBA:     // lengths: k_delta_walk; bytes: k_ba_expand
+            case K_PLAIN_BA: // the [u32 len][bytes] chain: k_ba_walk
               break;
             case K_FLBA_NEGATIVE:
               err = err_key(3, 0, PQH_ERR_NEGATIVE_LENGTH);
@@ -711,6 +714,26 @@ struct DictSink {
   }
 };
 
+// Byte-array dictionary pages: the index stream becomes per-value keys (aux); lengths and bytes are
+// resolved against the dictionary's cumulative-bytes table by k_ba_sum / k_ba_expand.
+struct KeySink {
+  int32_t* out;  // chunk aux + value_base
+  uint32_t K;
+  int64_t* first_bad;
+  __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+    for (int j = 0; j < cnt; j++)
+      if (v[j] >= K && i0 + j < *first_bad) *first_bad = i0 + j;
+    if (cnt == 8) {
+      uint4 a = make_uint4(v[0], v[1], v[2], v[3]);
+      uint4 c = make_uint4(v[4], v[5], v[6], v[7]);
+      __builtin_memcpy(out + i0, &a, 16);
+      __builtin_memcpy(out + i0 + 4, &c, 16);
+    } else {
+      for (int j = 0; j < cnt; j++) out[i0 + j] = int32_t(v[j]);
+    }
+  }
+};
+
 // ------------------------------------------------------------------------------------------------
 // Tile bodies.  Every body reads its page/state/chunk records itself (all depend on t.page only).
 // ------------------------------------------------------------------------------------------------
@@ -773,7 +796,10 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
   int64_t first_bad = INT64_MAX;
   uint8_t* out = C.values + S.value_base * vs;
   const Ckpt c = b.ckpts[P.ck_val + t.k];
-  if (vs == 4) {
+  if (vs == 0) {
+    KeySink sink{C.aux + S.value_base, K, &first_bad};
+    expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
+  } else if (vs == 4) {
     DictSink<4> sink{dict, out, K, vs, &first_bad};
     expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
   } else if (vs == 8) {
@@ -874,6 +900,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 // planner so every CU sees a mix of byte-copy and bit-unpack work.
 // ------------------------------------------------------------------------------------------------
 #include "delta_impl.h"
+#include "bytearray_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
@@ -940,6 +967,30 @@ hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hip
 hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_delta_scan, dim3((n + 255) / 256), dim3(256), 0, s, b, delta_pages, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_walk, dim3((n + 3) / 4), dim3(256), 0, s, b, ba_pages, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_sum, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_scan, dim3(n), dim3(256), 0, s, b, ba_chunks, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_expand, dim3(n), dim3(256), 0, s, b, tiles);
   return hipGetLastError();
 }
 

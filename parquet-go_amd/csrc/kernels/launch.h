@@ -36,7 +36,7 @@ hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int3
 // per-chunk offset scan, offsets + byte copy.
 hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s);
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
-hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, hipStream_t s);
+hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.
 hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);

@@ -297,3 +297,79 @@ def test_delta_writer_pages(pq, ctx):
     for v2 in (False, True):
         checked, _ = _run_file(pq, ctx, W.flat(cols, n // 2, v2=v2), allow_not_implemented=False)
         assert checked == 6
+
+
+# ---------------------------------------------------------------------------------------------
+# Byte arrays (byte-array dictionaries of a6/a11)
+# ---------------------------------------------------------------------------------------------
+def _plain_chain(strs):
+    return b"".join(len(x).to_bytes(4, "little") + x for x in strs)
+
+
+def _ba_cases(rng):
+    import delta_streams as DS
+    W = fixtures.W
+    col = (W.BYTE_ARRAY, 0, 0, 0)
+    cases = []
+    for n in (0, 1, 7, 100, 129, 2049, 5000):
+        strs = [rng.bytes(int(rng.integers(0, 40))) for _ in range(n)]
+        plain = _plain_chain(strs)
+        dlba = DS.encode([len(x) for x in strs], 32, 128, 4, "omit") + b"".join(strs)
+        for enc, img in ((W.PLAIN, plain), (W.DELTA_LENGTH_BYTE_ARRAY, dlba)):
+            cases.append((col, None, (O.DATA_PAGE, n, enc, 0, 0, img)))
+            cases.append((col, None, (O.DATA_PAGE, n, enc, 0, 0, img[: int(rng.integers(0, len(img) + 1))])))
+            cases.append((col, None, (O.DATA_PAGE, n + 3, enc, 0, 0, img)))
+            cases.append((col, None, (O.DATA_PAGE, n, enc, 0, 0, _mutate(rng, img))))
+        if n > 2:
+            k = int(rng.integers(0, n))
+            bad = list(strs)
+            neg = _plain_chain(bad[:k]) + b"\xff\xff\xff\xff" + _plain_chain(bad[k:])
+            cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, neg)))
+            lens = [len(x) for x in strs]
+            lens[k] = -int(rng.integers(1, 5))
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_LENGTH_BYTE_ARRAY, 0, 0,
+                                      DS.encode(lens, 32, 128, 4, "omit") + b"".join(strs))))
+            lens = [len(x) for x in strs]
+            lens[k] += 1000  # bytes run past the page
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_LENGTH_BYTE_ARRAY, 0, 0,
+                                      DS.encode(lens, 32, 128, 4, "omit") + b"".join(strs))))
+    # byte-array dictionaries: PLAIN chain dictionary page + hybrid index pages
+    for K in (1, 37, 3000):
+        dstrs = [rng.bytes(int(rng.integers(0, 30))) for _ in range(K)]
+        dimg = _plain_chain(dstrs)
+        w = max(1, int(K - 1).bit_length())
+        for n in (1, 500, 20000):
+            idx = rng.integers(0, K, n).astype(np.int32)
+            img = bytes([w]) + W.hybrid_encode(w, idx)
+            cases.append((col, (K, W.PLAIN, dimg), (O.DATA_PAGE, n, W.RLE_DICTIONARY, 0, 0, img)))
+            idx2 = idx.copy()
+            idx2[int(rng.integers(0, n))] = min(K + 3, (1 << w) - 1)  # out of range (when representable)
+            img2 = bytes([w]) + W.hybrid_encode(w, idx2)
+            cases.append((col, (K, W.PLAIN, dimg), (O.DATA_PAGE, n, W.RLE_DICTIONARY, 0, 0, img2)))
+        cases.append((col, (K + 2, W.PLAIN, dimg), (O.DATA_PAGE, 10, W.RLE_DICTIONARY, 0, 0,
+                                                      bytes([w]) + W.hybrid_encode(w, np.zeros(10, np.int32)))))
+        cases.append((col, (K, W.PLAIN, dimg[: len(dimg) // 2]), (O.DATA_PAGE, 10, W.RLE_DICTIONARY, 0, 0,
+                                                                   bytes([w]) + W.hybrid_encode(w, np.zeros(10, np.int32)))))
+    return cases
+
+
+def test_byte_array_pages(pq, ctx):
+    cases = _ba_cases(np.random.default_rng(41))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors > 20
+
+
+def test_byte_array_files(pq, ctx):
+    """Reference-writer string columns: PLAIN, DELTA_LENGTH, dictionary (+ nulls), V1/V2, codecs."""
+    W = fixtures.W
+    rng = np.random.default_rng(42)
+    n = 60000
+    s = [rng.bytes(int(rng.integers(8, 41))) for _ in range(n)]
+    mask = rng.random(n) < 0.1
+    cols = [("p", W.Column(W.BYTE_ARRAY, s, use_dict=False), W.REQUIRED),
+            ("l", W.Column(W.BYTE_ARRAY, s, encoding=W.DELTA_LENGTH_BYTE_ARRAY, use_dict=False), W.REQUIRED),
+            ("d", W.Column(W.BYTE_ARRAY, [s[k % 4000] for k in range(n)]), W.REQUIRED),
+            ("o", W.optional(W.BYTE_ARRAY, [s[k % 300] for k in range(n)], mask), W.OPTIONAL)]
+    for v2, codec in ((False, 0), (True, 1), (True, 2)):
+        checked, _ = _run_file(pq, ctx, W.flat(cols, 25000, v2=v2, codec=codec), allow_not_implemented=False)
+        assert checked == 3 * 4
