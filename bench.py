@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -115,7 +115,7 @@ def main():
     kw = {}
     if args.rows:
         kw["rows"] = args.rows
-    seed_kw = {"c1": 1, "c2": 10, "c3": 20}[args.workload] + 1000 * rank
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c5": 40}[args.workload] + 1000 * rank
     t0 = time.perf_counter()
     data = builder(seed=seed_kw, **kw)
     gen_s = time.perf_counter() - t0
@@ -212,7 +212,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32/int64/f32/f64/bool/flba16 (bit-exact integer/byte decode)" if args.workload == "c2"
-            else "int32" if args.workload == "c1" else "int64",
+            else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload == "c5"
+            else "int64",
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
             "config": {"workload": desc, "rows_per_gpu": f.num_rows, "row_groups_per_gpu": f.num_row_groups,
                        "pages_per_gpu": hb.num_pages, "parallelism": f"row-group sharded x{world}, no collective",

@@ -172,7 +172,7 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
       const int64_t pend = pm + mbvc < L ? pm + mbvc : L;
       const bool has_pad = pstar >= pm && pstar < pend;
       const int64_t ng = has_pad ? (pstar - pm) / 8 + 1 : (pend - pm + 7) / 8;  // group reads
-      if (wm > 0) {  // io.ReadFull(w bytes) per group: the first group past the end fails
+      if (wm > 0 && pos + ng * wm > w.e) {  // io.ReadFull(w bytes) per group: the first group past the end fails
         const int64_t avail = w.e - pos > 0 ? w.e - pos : 0;
         const int64_t gf = avail / wm;
         if (gf < ng) {
@@ -288,7 +288,7 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
   uint64_t carry = base, total_all = 0;
   for (int64_t c0 = v0; c0 < v1; c0 += SUB) {
     const int64_t c1 = c0 + SUB < v1 ? c0 + SUB : v1;
-    const int bb0 = int(c0 / bs), nb = int((c1 - 1) / bs) - bb0 + 1;
+    const int bb0 = int(int32_t(c0) / bs), nb = int(int32_t(c1 - 1) / bs) - bb0 + 1;
     __syncthreads();
     if (threadIdx.x < nb) {  // per-block miniblock data offsets (image offsets)
       const DeltaBlock r = recs[bb0 + threadIdx.x];
@@ -303,9 +303,10 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
     }
     __syncthreads();
     // exact byte range holding the bits of positions [c0, c1)
-    const int m0 = int((c0 % bs) / mbvc), j0 = int((c0 % bs) % mbvc);
+    const int32_t r0 = int32_t(c0) % bs, r1 = int32_t(c1 - 1) % bs;
+    const int m0 = r0 / mbvc, j0 = r0 % mbvc;
     const int64_t q = c1 - 1;
-    const int bl = int(q / bs) - bb0, m1 = int((q % bs) / mbvc), j1 = int((q % bs) % mbvc);
+    const int bl = int(int32_t(q) / bs) - bb0, m1 = r1 / mbvc, j1 = r1 % mbvc;
     const int64_t start = DL.mboff[0][m0] + (int64_t(j0) * DL.mbw[0][m0]) / 8;
     const int64_t end = DL.mboff[bl][m1] + (int64_t(j1 + 1) * DL.mbw[bl][m1] + 7) / 8;
     const int64_t a0 = start - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(start)) & 15);
@@ -328,10 +329,11 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
 #pragma unroll
     for (int j = 0; j < VPT; j++) d[j] = 0;
     if (p < c1) {
-      const int blk = int(p / bs) - bb0;
-      const int m = int((p % bs) / mbvc);
+      const int32_t rp = int32_t(p) % bs;
+      const int blk = int(int32_t(p) / bs) - bb0;
+      const int m = rp / mbvc;
       const int wm = DL.mbw[blk][m];
-      const uint32_t bit0 = uint32_t(DL.mboff[blk][m] - a0) * 8 + uint32_t((p % bs) % mbvc) * uint32_t(wm);
+      const uint32_t bit0 = uint32_t(DL.mboff[blk][m] - a0) * 8 + uint32_t(rp % mbvc) * uint32_t(wm);
       const uint64_t md = DL.md[blk];
 #pragma unroll
       for (int j = 0; j < VPT; j++) {

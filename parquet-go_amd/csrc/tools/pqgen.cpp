@@ -232,14 +232,25 @@ void encode_chunk(const Ctx& ctx, const Leaf& L, const pqg_column_data& c, int64
   bool use_dict = c.use_dict && L.type != BOOLEAN;
   std::vector<int32_t> idx;  // per value of the chunk
   std::vector<std::string_view> dict;
+  // dict_page_limit > 0 (not the reference writer): the dictionary stops growing at
+  // the first value that would push its PLAIN page past the limit (or past 32767 entries); that value
+  // and every later one go to pages of the column's own encoding (mid-chunk fallback).
+  int64_t fallback_v = v1;
   if (use_dict) {
     std::unordered_map<std::string_view, int32_t> m;
     m.reserve(1 << 15);
     idx.resize(size_t(v1 - v0));
+    int64_t dict_bytes = 0;
     for (int64_t i = v0; i < v1 && use_dict; i++) {
       std::string_view v = value_at(L, c, i);
       auto it = m.find(v);
       if (it == m.end()) {
+        const int64_t sz = L.type == BYTE_ARRAY ? 4 + int64_t(v.size()) : int64_t(v.size());
+        if (c.dict_page_limit > 0 && (dict_bytes + sz > c.dict_page_limit || dict.size() >= 32767)) {
+          fallback_v = i;
+          break;
+        }
+        dict_bytes += sz;
         int32_t k = int32_t(dict.size());
         m.emplace(v, k);
         dict.push_back(v);
@@ -254,7 +265,8 @@ void encode_chunk(const Ctx& ctx, const Leaf& L, const pqg_column_data& c, int64
       dict.clear();
     }
   }
-  const int enc = use_dict ? E_RLE_DICT : c.encoding;
+  const int dict_enc = use_dict ? E_RLE_DICT : c.encoding;
+  int enc = dict_enc;
   out.enc = c.encoding;
   out.has_dict = use_dict;
 
@@ -322,7 +334,7 @@ void encode_chunk(const Ctx& ctx, const Leaf& L, const pqg_column_data& c, int64
         est_vals += sz;
         if (c.use_dict && L.type != BOOLEAN && uniq_count <= 32767) {
           bool fresh;
-          if (use_dict) {
+          if (use_dict && v < fallback_v) {
             int32_t id = idx[size_t(v - v0)];
             fresh = !seen[size_t(id)];
             seen[size_t(id)] = 1;
@@ -341,7 +353,17 @@ void encode_chunk(const Ctx& ctx, const Leaf& L, const pqg_column_data& c, int64
       int64_t cnt = s - ps;
       int64_t lvl = ((cnt - 1) / 8) * (rw + dw);
       int64_t est = (c.use_dict && L.type != BOOLEAN) ? uniq_bytes + 4 * (v - pv) + lvl : est_vals + lvl;
-      if (est >= ctx.max_page) break;
+      if (pv < fallback_v && v >= fallback_v) break;  // dictionary pages end where the fallback starts
+      if (est >= ctx.max_page) {
+        // Generator choice (not the reference writer): a DELTA-family page of n values with
+        // (n-1) % 128 == 0 cannot be read back by the reference decoder (read-ahead quirk,
+        // SURVEY.md A.3), so such a page takes one more record when one is left.
+        const bool delta_page = !(use_dict && pv < fallback_v) &&
+                                (c.encoding == E_DELTA_BP || c.encoding == E_DLBA || c.encoding == E_DBA);
+        const int64_t nv = v - pv;
+        if (delta_page && nv > 0 && (nv - 1) % 128 == 0 && s < s1) continue;
+        break;
+      }
     }
     // encode the page [ps, s) with values [pv, v)
     int32_t nslots = int32_t(s - ps), nvals = int32_t(v - pv);
@@ -356,7 +378,9 @@ void encode_chunk(const Ctx& ctx, const Leaf& L, const pqg_column_data& c, int64
       if (v2) hybrid_encode(dw, tmp.data(), nslots, ld);
       else hybrid_encode_sized(dw, tmp.data(), nslots, ld);
     }
-    if (use_dict) {  // dictEncoder.Close (type_dict.go:113-127)
+    const bool page_dict = use_dict && pv < fallback_v;
+    enc = page_dict ? dict_enc : c.encoding;
+    if (page_dict) {  // dictEncoder.Close (type_dict.go:113-127)
       int w = bits_len(dict.size());
       vals.push_back(uint8_t(w));
       tmp.assign(idx.begin() + (pv - v0), idx.begin() + (v - v0));

@@ -40,6 +40,8 @@ typedef struct pqg_column_data {
   const uint8_t* def_levels;  /* num_slots bytes, NULL when max_def == 0 */
   const uint8_t* rep_levels;  /* num_slots bytes, NULL when max_rep == 0 */
   int64_t num_slots;          /* level slots in the whole file */
+  int64_t dict_page_limit;    /* 0: reference writer; > 0: mid-chunk fallback once the dictionary page
+                                 would exceed this many bytes */
 } pqg_column_data;
 
 typedef struct pqg_options {

@@ -5,6 +5,9 @@ reference writer's layout by libpqgen.  Used by bench.py and the tests; nothing 
   C2  configs[1]: 6 flat columns (int32 dict K=1000, int64 PLAIN, float dict K=256, optional double
                   PLAIN 1% nulls, boolean PLAIN, FLBA(16) PLAIN), V2 pages, 16 row groups
   C3  configs[2]: INT64 timestamps DELTA_BINARY_PACKED 128/4, row groups of 7,812,500 rows
+  C5  configs[4]: required BYTE_ARRAY strings, length U[8,40], ~half unique; each chunk starts with
+                  RLE_DICTIONARY pages (dictionary page <= 1 MiB) and falls back to
+                  DELTA_LENGTH_BYTE_ARRAY; SNAPPY
 """
 import numpy as np
 
@@ -52,9 +55,41 @@ def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
                   rows_per_group, v2=False, as_array=True)
 
 
+def c5_strings(rows, seed=40, chunk=4_000_000):
+    """(data, offsets) of `rows` strings drawn from a pool of rows/2 random lowercase strings of
+    length U[8,40] (about 43% of the rows distinct)."""
+    rng = np.random.default_rng(seed)
+    pool_n = max(1, rows // 2)
+    plen = rng.integers(8, 41, pool_n).astype(np.int64)
+    poff = np.zeros(pool_n + 1, np.int64)
+    np.cumsum(plen, out=poff[1:])
+    pool = rng.integers(97, 123, int(poff[-1]), dtype=np.uint8)
+    idx = rng.integers(0, pool_n, rows)
+    lens = plen[idx]
+    offsets = np.zeros(rows + 1, np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.empty(int(offsets[-1]) + 1, np.uint8)
+    for a in range(0, rows, chunk):  # gather pool bytes chunk by chunk (bounded index arrays)
+        b = min(rows, a + chunk)
+        ln = lens[a:b]
+        starts = np.repeat(poff[idx[a:b]] - offsets[a:b], ln)
+        pos = np.arange(offsets[a], offsets[b], dtype=np.int64)
+        data[offsets[a]:offsets[b]] = pool[pos + starts]
+    return data, offsets
+
+
+def c5(rows=50_000_000, row_groups=8, seed=40, codec=W.SNAPPY):
+    per = -(-rows // row_groups)
+    col = W.Column(W.BYTE_ARRAY, c5_strings(rows, seed), encoding=W.DELTA_LENGTH_BYTE_ARRAY,
+                   dict_page_limit=1 << 20)
+    return W.flat([("s", col, W.REQUIRED)], per, v2=False, codec=codec, as_array=True)
+
+
 WORKLOADS = {
     "c1": ("C1: 10M rows, required INT32 dictionary K=4096 (width 13), UNCOMPRESSED, data page V1", c1),
     "c2": ("C2: 100M rows x 6 columns (int32 dict / int64 PLAIN / float dict / optional double PLAIN "
            "1% null / boolean PLAIN / FLBA(16) PLAIN), data page V2, 16 row groups", c2),
     "c3": ("C3: INT64 timestamps DELTA_BINARY_PACKED 128/4, 7,812,500-row row groups", c3),
+    "c5": ("C5: required BYTE_ARRAY strings U[8,40] ~half unique, RLE_DICTIONARY (dict page <= 1 MiB) "
+           "then DELTA_LENGTH_BYTE_ARRAY fallback, SNAPPY, 8 row groups", c5),
 }

@@ -26,7 +26,8 @@ class SchemaElement(ctypes.Structure):
 class ColumnData(ctypes.Structure):
     _fields_ = [("encoding", ctypes.c_int32), ("use_dict", ctypes.c_int32),
                 ("values", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("num_values", ctypes.c_int64),
-                ("def_levels", ctypes.c_void_p), ("rep_levels", ctypes.c_void_p), ("num_slots", ctypes.c_int64)]
+                ("def_levels", ctypes.c_void_p), ("rep_levels", ctypes.c_void_p), ("num_slots", ctypes.c_int64),
+                ("dict_page_limit", ctypes.c_int64)]
 
 
 class Options(ctypes.Structure):
@@ -42,8 +43,9 @@ class Column:
     """Leaf data: not-null values in order plus optional def/rep levels for every slot."""
 
     def __init__(self, ptype, values, def_levels=None, rep_levels=None, encoding=PLAIN, use_dict=True,
-                 type_length=0):
+                 type_length=0, dict_page_limit=0):
         self.ptype = ptype
+        self.dict_page_limit = dict_page_limit
         self.encoding = encoding
         self.use_dict = bool(use_dict) and ptype != BOOLEAN
         self.type_length = type_length
@@ -85,6 +87,7 @@ class Column:
         c.def_levels = self.def_levels.ctypes.data if self.def_levels is not None else None
         c.rep_levels = self.rep_levels.ctypes.data if self.rep_levels is not None else None
         c.num_slots = self.num_slots
+        c.dict_page_limit = self.dict_page_limit
         return c
 
 

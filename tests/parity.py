@@ -72,8 +72,9 @@ def assert_chunk(gpu, exp, where=""):
     if gpu.values is not None:
         got = gpu.values.view(np.uint8).tobytes()
         assert got == exp.values, f"{where}: values differ (len {len(got)} vs {len(exp.values)})"
-    else:
-        assert np.array_equal(gpu.offsets, exp.offsets), f"{where}: offsets differ"
+    else:  # byte arrays: a chunk without values still has offsets [0]
+        exp_offsets = exp.offsets if exp.offsets is not None else np.zeros(1, np.int64)
+        assert np.array_equal(gpu.offsets, exp_offsets), f"{where}: offsets differ"
         assert gpu.data.tobytes() == exp.data, f"{where}: byte data differs"
     if exp.def_levels is not None:
         assert np.array_equal(gpu.def_levels, exp.def_levels), f"{where}: def levels differ"

@@ -373,3 +373,12 @@ def test_byte_array_files(pq, ctx):
     for v2, codec in ((False, 0), (True, 1), (True, 2)):
         checked, _ = _run_file(pq, ctx, W.flat(cols, 25000, v2=v2, codec=codec), allow_not_implemented=False)
         assert checked == 3 * 4
+
+
+def test_c5_dictionary_fallback(pq, ctx):
+    """C5 layout: RLE_DICTIONARY pages (dictionary page <= 1 MiB) then DELTA_LENGTH fallback, SNAPPY."""
+    from parquet_go_amd import datasets
+
+    data = datasets.c5(rows=600_000, row_groups=2)
+    checked, _ = _run_file(pq, ctx, data, allow_not_implemented=False)
+    assert checked == 2
