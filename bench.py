@@ -158,15 +158,8 @@ def main():
         batch.run()
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([bytes_written], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        total_written = float(tot.item())
-    else:
-        total_written = bytes_written
+    # whole job: max step time over ranks, sum of decoded bytes (shard.py; RCCL for N > 1)
+    elapsed, total_written = pkg.shard.reduce_step(elapsed, bytes_written, device=f"cuda:{local}" if world > 1 else None)
     batch.sync()
     stats = batch.kernel_stats()
     ms_per_step = elapsed / args.steps * 1e3

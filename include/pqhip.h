@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 1
+#define PQH_ABI_VERSION 2
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -137,7 +137,12 @@ typedef struct pqh_column {
   int32_t type_length;   /* FIXED_LEN_BYTE_ARRAY length (SchemaElement.type_length) */
   int32_t max_def;       /* Column.MaxDefinitionLevel() (schema.go:904-914) */
   int32_t max_rep;       /* Column.MaxRepetitionLevel() */
+  int32_t rep_def[8];    /* definition level of the k-th REPEATED node on the path (k < max_rep), from
+                            readColumnSchema/readGroupSchema (schema.go:893-990); used by the nesting
+                            outputs (pqh_batch_nesting), which need max_rep <= PQH_MAX_NEST */
 } pqh_column;
+
+#define PQH_MAX_NEST 8
 
 /* One page as the reference page walker sees it (parquet.PageHeader fields + the decompressed
  * page image).  For DATA_PAGE and DICTIONARY_PAGE the image is the decompressed block; for
@@ -181,6 +186,29 @@ typedef struct pqh_chunk_out {
   uint8_t* def_levels;   /* one byte per level slot, NULL when max_def == 0 (device) */
   uint8_t* rep_levels;   /* one byte per level slot, NULL when max_rep == 0 (device) */
 } pqh_chunk_out;
+
+/* Nesting of a repeated column, the columnar form of the reference's record
+ * assembly (ColumnStore.get data_store.go:262-309, Column.getNextData/getData schema.go:216-312).
+ * Level k (1..max_rep) has one list per enclosing instance (rows at level 1, elements of level k-1
+ * below); offsets[i]..offsets[i+1] are the list's elements; validity[i] = 1 when the list is present
+ * (its parent object exists; it may be empty).  Leaf slots are the elements of the innermost level;
+ * leaf_validity = 1 when the value is non-null (d == max_def), i.e. the leaf's dense values are the
+ * leaf slots with validity 1, in order. */
+typedef struct pqh_nest_level {
+  int32_t def_level;     /* definition level of this level's REPEATED node */
+  int32_t reserved;
+  int64_t num_lists;
+  int32_t* offsets;      /* device, num_lists + 1 */
+  uint8_t* validity;     /* device, num_lists */
+} pqh_nest_level;
+
+typedef struct pqh_nest_out {
+  int32_t num_levels;    /* max_rep (0: not a repeated column; outputs empty) */
+  int32_t status;        /* PQH_OK, or the chunk's decode error (outputs undefined) */
+  int64_t num_leaf_slots;
+  uint8_t* leaf_validity;  /* device, num_leaf_slots */
+  pqh_nest_level levels[PQH_MAX_NEST];
+} pqh_nest_out;
 
 /* Per-page result (host copy). */
 typedef struct pqh_page_result {
@@ -234,6 +262,9 @@ int pqh_batch_run(pqh_batch* batch);
 /* Wait for the last run and copy back per-page results. */
 int pqh_batch_sync(pqh_batch* batch);
 int pqh_batch_chunk_out(const pqh_batch* batch, int32_t chunk, pqh_chunk_out* out);
+/* Nesting outputs of one chunk (after pqh_batch_sync).  Chunks with max_rep > PQH_MAX_NEST return
+ * PQH_ERR_NOT_IMPLEMENTED. */
+int pqh_batch_nesting(const pqh_batch* batch, int32_t chunk, pqh_nest_out* out);
 int pqh_batch_page_results(const pqh_batch* batch, pqh_page_result* out, int32_t num_pages);
 /* Kernel timing accumulated since the last reset (requires PQH_CTX_PROFILE). */
 int pqh_batch_kernel_stats(const pqh_batch* batch, pqh_kernel_stat* out, int32_t max_stats,

@@ -336,12 +336,13 @@ class CompactReader:
 # File reader restatement
 # ------------------------------------------------------------------------------------------------
 class Column:
-    def __init__(self, path, element, max_def, max_rep):
+    def __init__(self, path, element, max_def, max_rep, rep_def=()):
         self.path = path
         self.physical_type = element.get(1)
         self.type_length = element.get(2, 0)
         self.max_def = max_def
         self.max_rep = max_rep
+        self.rep_def = tuple(rep_def)  # definition level of each REPEATED node on the path, outermost first
 
     def desc(self):
         return (self.physical_type, self.type_length or 0, self.max_def, self.max_rep)
@@ -351,24 +352,25 @@ def read_schema(schema):
     """readSchema / readGroupSchema / readColumnSchema (schema.go:893-1015): leaves in DFS order."""
     leaves = []
 
-    def walk(idx, path, d, r, is_root):
+    def walk(idx, path, d, r, rd, is_root):
         s = schema[idx]
         rep = s.get(3)
         if not is_root and rep is not None and rep != 0:
             d += 1
         if not is_root and rep == 2:
             r += 1
+            rd = rd + [d]
         name = s.get(4, b"").decode()
         p = path + ([name] if not is_root else [])
         if s.get(1) is not None and not is_root:
-            leaves.append(Column(".".join(p), s, d, r))
+            leaves.append(Column(".".join(p), s, d, r, rd))
             return idx + 1
         idx += 1
         for _ in range(s.get(5, 0)):
-            idx = walk(idx, p, d, r, False)
+            idx = walk(idx, p, d, r, rd, False)
         return idx
 
-    walk(0, [], 0, 0, True)
+    walk(0, [], 0, 0, [], True)
     return leaves
 
 
@@ -524,3 +526,37 @@ def decode_chunk(ch):
         return []
     return [decode_page(ch.column.desc(), p.page_type, p.num_values, p.encoding, p.def_len, p.rep_len,
                         p.image, ch.dict_page) for p in ch.pages]
+
+
+# ---------------------------------------------------------------------------------------------
+# Nesting: levels -> per repetition level list offsets / validity + leaf validity
+# ---------------------------------------------------------------------------------------------
+def nest_levels(def_levels, rep_levels, max_def, rep_def):
+    """Columnar form of the reference's record assembly for one leaf column
+    (ColumnStore.get data_store.go:262-309: d < maxD is a null at depth d, a repeated value collects
+    while the next r >= maxR; Column.getNextData / getData schema.go:216-312: a group exists when a
+    child is defined at its depth, a repeated group collects while r >= its maxR).
+
+    rep_def[l-1] = definition level D_l of the l-th REPEATED node on the path.  For level l:
+      a list starts at slot i when r_i <= l-1 and (l == 1 or d_i >= D_{l-1}): one list per row at
+      level 1, one per element of the enclosing level otherwise;
+      an element of level l starts at slot i when r_i <= l and d_i >= D_l;
+      the list is present (possibly empty) when d >= D_l - 1 at its first slot.
+    Leaf slots are the elements of the innermost level (every slot when max_rep == 0); a leaf value
+    is non-null when d == max_def.
+    Returns ([(offsets int32[lists+1], validity u8[lists]) per level], leaf_validity u8)."""
+    d = np.asarray(def_levels, dtype=np.int32)
+    r = np.asarray(rep_levels, dtype=np.int32) if rep_levels is not None else np.zeros_like(d)
+    levels = []
+    for l in range(1, len(rep_def) + 1):
+        D = rep_def[l - 1]
+        start = (r <= l - 1) & ((d >= rep_def[l - 2]) if l >= 2 else True)
+        elem = (r <= l) & (d >= D)
+        before = np.concatenate([[0], np.cumsum(elem)])  # elements before each slot
+        idx = np.nonzero(start)[0]
+        offsets = np.concatenate([before[idx], [before[-1]]]).astype(np.int32)
+        validity = (d[idx] >= D - 1).astype(np.uint8)
+        levels.append((offsets, validity))
+    leaf = d >= rep_def[-1] if len(rep_def) else np.ones(len(d), bool)
+    leaf_valid = (d[leaf] == max_def).astype(np.uint8)
+    return levels, leaf_valid

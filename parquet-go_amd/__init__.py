@@ -14,6 +14,6 @@ __all__ = ["reader", "writer", "native"]
 def __getattr__(name):
     import importlib
 
-    if name in ("reader", "writer", "native", "datasets", "build"):
+    if name in ("reader", "writer", "native", "datasets", "build", "shard"):
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

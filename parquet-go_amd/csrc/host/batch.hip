@@ -53,8 +53,9 @@ struct KernelRun {
 
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
                               "k_delta_walk", "k_delta_sum", "k_delta_scan",
-                              "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand"};
-constexpr int kNumKernels = 11;
+                              "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
+                              "k_nest_count", "k_nest_scan", "k_nest_write"};
+constexpr int kNumKernels = 14;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -129,6 +130,10 @@ struct pqh_batch {
   std::vector<int32_t> ba_pages;    // k_ba_walk work list (PLAIN byte-array data + dictionary pages)
   std::vector<int32_t> ba_chunks;   // k_ba_scan work list
   std::vector<int64_t> chunk_bytes; // host copy after sync
+  std::vector<DevNest> nests;       // repeated chunks with nesting outputs
+  std::vector<int32_t> chunk_nest;  // chunk -> nests index, -1
+  std::vector<Tile> nest_tiles;     // k_nest_count / k_nest_write work list
+  std::vector<int64_t> nest_totals; // host copy after sync (kNestFlags per nest)
   size_t expand_lds = 0;            // dynamic LDS of k_expand: largest staged dictionary
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
@@ -149,6 +154,10 @@ struct pqh_batch {
   int32_t* d_dcum = nullptr;
   int64_t* d_basums = nullptr;
   int64_t* d_chunk_bytes = nullptr;
+  DevNest* d_nests = nullptr;
+  Tile* d_nest_tiles = nullptr;
+  int64_t* d_nsums = nullptr;
+  int64_t* d_ntotals = nullptr;
   std::vector<void*> allocations;
   std::vector<PageState> states;   // host copy after sync
   std::vector<int64_t> chunk_n;    // level slots per chunk
@@ -513,6 +522,44 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       D.rep_levels = static_cast<uint8_t*>(p);
     }
   }
+  // nesting outputs of repeated chunks (levels -> list offsets / presence / leaf validity)
+  b->chunk_nest.assign(size_t(num_chunks), -1);
+  for (int32_t c = 0; c < num_chunks && !rc; c++) {
+    const pqh_column& col = chunks[c].column;
+    const int64_t n = b->chunk_n[size_t(c)];
+    if (col.max_rep <= 0 || col.max_rep > kMaxNest || n <= 0) continue;
+    bool ok = true;  // repeated-node definition levels must rise strictly within [1, max_def]
+    for (int l = 0; l < col.max_rep; l++)
+      ok = ok && col.rep_def[l] >= 1 && col.rep_def[l] <= col.max_def && (l == 0 || col.rep_def[l] > col.rep_def[l - 1]);
+    if (!ok) continue;
+    DevNest N;
+    memset(&N, 0, sizeof(N));
+    N.chunk = c;
+    N.levels = col.max_rep;
+    N.max_def = col.max_def;
+    N.n = n;
+    N.tile_base = int32_t(b->nest_tiles.size());
+    N.tile_n = int32_t(ceil_div(n, kNestTile));
+    for (int l = 0; l < col.max_rep; l++) {
+      N.rep_def[l] = col.rep_def[l];
+      void* p = nullptr;
+      if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int32_t)))) break;
+      N.offsets[l] = static_cast<int32_t*>(p);
+      if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
+      N.validity[l] = static_cast<uint8_t*>(p);
+    }
+    void* p = nullptr;
+    if (rc || (rc = dalloc(b, &p, size_t(n) + 64))) break;
+    N.leaf_valid = static_cast<uint8_t*>(p);
+    b->chunk_nest[size_t(c)] = int32_t(b->nests.size());
+    for (int32_t k = 0; k < N.tile_n; k++) b->nest_tiles.push_back(Tile{int32_t(b->nests.size()), k, 0, 1});
+    b->nests.push_back(N);
+  }
+  if (!rc && !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nests), sizeof(DevNest) * b->nests.size())) &&
+      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nest_tiles), sizeof(Tile) * b->nest_tiles.size())) &&
+      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nsums), sizeof(int64_t) * kNestFlags * b->nest_tiles.size())))
+    rc = dalloc(b, reinterpret_cast<void**>(&b->d_ntotals), sizeof(int64_t) * kNestFlags * b->nests.size());
+  for (size_t i = 0; i < b->nests.size(); i++) b->nests[i].totals = b->d_ntotals + i * kNestFlags;
   if (rc || (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunks), sizeof(DevChunk) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
@@ -539,6 +586,10 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     e = hipMemcpyAsync(b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size(),
                        hipMemcpyHostToDevice, s);
   if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
+  if (e == hipSuccess && !b->nests.empty())
+    e = hipMemcpyAsync(b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->nest_tiles.empty())
+    e = hipMemcpyAsync(b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     free_batch(b);
@@ -562,7 +613,7 @@ int pqh_batch_run(pqh_batch* b) {
   hipStream_t s = ctx->stream;
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
-             b->d_chunk_bytes};
+             b->d_chunk_bytes, b->d_nests, b->d_nsums};
   b->synced = false;
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -603,6 +654,13 @@ int pqh_batch_run(pqh_batch* b) {
     if (e == hipSuccess)
       e = timed(10, nbt, s, [&](hipStream_t st) { return launch_ba_expand(d, b->d_batiles, nbt, st); });
   }
+  const int32_t nnt = int32_t(b->nest_tiles.size()), nns = int32_t(b->nests.size());
+  if (e == hipSuccess && nnt) {
+    e = timed(11, nnt, s, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
+    if (e == hipSuccess) e = timed(12, nns, s, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    if (e == hipSuccess)
+      e = timed(13, nnt, s, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+  }
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   return PQH_OK;
 }
@@ -618,6 +676,10 @@ int pqh_batch_sync(pqh_batch* b) {
   b->chunk_bytes.assign(b->chunks.size(), 0);
   if (!b->ba_chunks.empty())
     HIP_TRY(ctx, hipMemcpyAsync(b->chunk_bytes.data(), b->d_chunk_bytes, sizeof(int64_t) * b->chunks.size(),
+                                hipMemcpyDeviceToHost, ctx->stream));
+  b->nest_totals.assign(b->nests.size() * kNestFlags, 0);
+  if (!b->nests.empty())
+    HIP_TRY(ctx, hipMemcpyAsync(b->nest_totals.data(), b->d_ntotals, sizeof(int64_t) * b->nest_totals.size(),
                                 hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   // Byte-array outputs sized from an estimate (dictionary gathers): grow the chunks that came out
@@ -733,6 +795,16 @@ int pqh_batch_sync(pqh_batch* b) {
     wr += w;
     b->k_written[10] += w;
   }
+  for (size_t i = 0; i < b->nests.size(); i++) {  // list offsets (4 B) + presence (1 B) per list, leaf validity
+    const DevNest& N = b->nests[i];
+    double w = 0;
+    for (int l = 0; l < N.levels; l++) w += double(b->nest_totals[i * kNestFlags + size_t(l)] + 1) * 4 +
+                                          double(b->nest_totals[i * kNestFlags + size_t(l)]);
+    w += double(b->nest_totals[i * kNestFlags + size_t(N.levels)]);
+    wr += w;
+    b->k_written[13] += w;
+    b->k_read[13] += 2.0 * double(N.n);
+  }
   b->bytes_written = wr;
   for (int k = 0; k < kNumKernels; k++) {
     b->stats[size_t(k)].bytes_read = b->k_read[size_t(k)];
@@ -788,6 +860,40 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
     if (b->hpages[size_t(p)].page_type != PQH_DICTIONARY_PAGE) nn += S.nn;
   }
   out->num_non_null = nn;
+  return PQH_OK;
+}
+
+int pqh_batch_nesting(const pqh_batch* b, int32_t chunk, pqh_nest_out* out) {
+  if (!b || !out || chunk < 0 || size_t(chunk) >= b->chunks.size())
+    return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad chunk");
+  if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
+  memset(out, 0, sizeof(*out));
+  const pqh_column& col = b->chunks[size_t(chunk)].column;
+  if (col.max_rep == 0) return PQH_OK;
+  const int32_t ni = b->chunk_nest[size_t(chunk)];
+  if (ni < 0) {
+    if (b->chunk_n[size_t(chunk)] == 0) {  // no level slots: empty outputs
+      out->num_levels = col.max_rep;
+      return PQH_OK;
+    }
+    return set_err(b->ctx, PQH_ERR_NOT_IMPLEMENTED, "nesting needs max_rep <= 8 and the repeated nodes' definition levels");
+  }
+  const DevNest& N = b->nests[size_t(ni)];
+  const DevChunk& D = b->hchunks[size_t(chunk)];
+  for (int32_t i = 0; i < D.num_pages; i++) {
+    const PageState& S = b->states[size_t(D.first_page + i)];
+    if (S.err != kNoError && out->status == PQH_OK) out->status = int32_t(S.err & 0xff);
+  }
+  out->num_levels = N.levels;
+  const int64_t* tot = b->nest_totals.data() + size_t(ni) * kNestFlags;
+  for (int l = 0; l < N.levels; l++) {
+    out->levels[l].def_level = N.rep_def[l];
+    out->levels[l].num_lists = tot[l];
+    out->levels[l].offsets = N.offsets[l];
+    out->levels[l].validity = N.validity[l];
+  }
+  out->num_leaf_slots = tot[N.levels];
+  out->leaf_validity = N.leaf_valid;
   return PQH_OK;
 }
 

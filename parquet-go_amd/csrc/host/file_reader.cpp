@@ -149,6 +149,7 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
     int32_t remaining;
     int32_t d, r;
     std::string path;
+    std::vector<int32_t> rep_def;  // definition level of each REPEATED node above
   };
   std::vector<Frame> st;
   const SchemaEl& root = s[0];
@@ -156,7 +157,7 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
     f->err = "invalid schema root";
     return false;
   }
-  st.push_back({root.num_children, 0, 0, ""});
+  st.push_back({root.num_children, 0, 0, "", {}});
   for (size_t i = 1; i < s.size(); i++) {
     while (!st.empty() && st.back().remaining == 0) st.pop_back();
     if (st.empty()) {
@@ -172,15 +173,20 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
     }
     const std::string path = parent.path.empty() ? e.name : parent.path + "." + e.name;
     int32_t d = parent.d, r = parent.r;
+    std::vector<int32_t> rd = parent.rep_def;
     if (e.has_type) {
       if (!e.has_rep) {
         f->err = "field RepetitionType is nil";
         return false;
       }
       if (e.rep != 0) d++;
-      if (e.rep == 2) r++;
+      if (e.rep == 2) {
+        r++;
+        rd.push_back(d);
+      }
       ColumnMeta cm;
-      cm.col = pqh_column{e.type, e.type_length, d, r};
+      cm.col = pqh_column{e.type, e.type_length, d, r, {0, 0, 0, 0, 0, 0, 0, 0}};
+      for (size_t k = 0; k < rd.size() && k < PQH_MAX_NEST; k++) cm.col.rep_def[k] = rd[k];
       cm.path = path;
       f->columns.push_back(cm);
     } else {
@@ -189,8 +195,11 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
         return false;
       }
       if (e.has_rep && e.rep != 0) d++;
-      if (e.has_rep && e.rep == 2) r++;
-      st.push_back({e.num_children, d, r, path});
+      if (e.has_rep && e.rep == 2) {
+        r++;
+        rd.push_back(d);
+      }
+      st.push_back({e.num_children, d, r, path, rd});
     }
   }
   for (auto& fr : st)

@@ -148,6 +148,27 @@ enum TileKind : int32_t {
 
 constexpr int kBaTile = 2048;  // byte-array values per tile (one 256 x 8 block scan)
 
+// Nesting outputs of a repeated chunk (pqh_batch_nesting): list offsets / presence per repetition
+// level and leaf validity, from the chunk's decoded level bytes.
+constexpr int kMaxNest = 8;
+constexpr int kNestTile = 8192;  // level slots per tile (256 threads x 32)
+constexpr int kNestFlags = kMaxNest + 1;  // rows (r == 0) and element starts of levels 1..L
+
+struct DevNest {
+  int32_t chunk;
+  int32_t levels;        // max_rep (1..kMaxNest)
+  int32_t max_def;
+  int32_t tile_base;     // tiles [tile_base, tile_base + tile_n) of the k_nest_* work list
+  int32_t tile_n;
+  int32_t pad;
+  int64_t n;             // level slots of the chunk
+  int32_t rep_def[kMaxNest];
+  int32_t* offsets[kMaxNest];
+  uint8_t* validity[kMaxNest];
+  uint8_t* leaf_valid;
+  int64_t* totals;       // kNestFlags per chunk: rows, elements of each level (k_nest_scan)
+};
+
 // Work item of k_expand.  Hybrid-driven kinds cover [k, k+span) checkpoint intervals of
 // kHybridTile values; TK_COPY covers kCopyTileBytes bytes; TK_BOOL covers kBoolTile values.
 struct Tile {

@@ -901,6 +901,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 // ------------------------------------------------------------------------------------------------
 #include "delta_impl.h"
 #include "bytearray_impl.h"
+#include "nest_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
@@ -991,6 +992,24 @@ hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ba_expand, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_nest_count(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nest_count, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s) {
+  if (num_nests <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nest_scan, dim3(num_nests), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nest_write, dim3(n), dim3(256), 0, s, b, tiles);
   return hipGetLastError();
 }
 

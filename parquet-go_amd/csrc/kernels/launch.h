@@ -21,6 +21,8 @@ struct DevBatch {
   int32_t* dcum;         // byte-array dictionary pages: cumulative entry bytes (num_values + 1 each)
   int64_t* basums;       // per byte-array tile: byte sum, then (after k_ba_scan) the tile's first offset
   int64_t* chunk_bytes;  // per chunk: total string bytes (k_ba_scan)
+  const DevNest* nests;  // repeated chunks with nesting outputs
+  int64_t* nsums;        // per nest tile: kNestFlags counts, then (after k_nest_scan) bases
 };
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
@@ -38,6 +40,10 @@ hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n,
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// Nesting (levels -> list offsets / presence / leaf validity): counts, per-chunk scan, write.
+hipError_t launch_nest_count(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s);
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.
 hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 

@@ -5,6 +5,8 @@ reference writer's layout by libpqgen.  Used by bench.py and the tests; nothing 
   C2  configs[1]: 6 flat columns (int32 dict K=1000, int64 PLAIN, float dict K=256, optional double
                   PLAIN 1% nulls, boolean PLAIN, FLBA(16) PLAIN), V2 pages, 16 row groups
   C3  configs[2]: INT64 timestamps DELTA_BINARY_PACKED 128/4, row groups of 7,812,500 rows
+  C4  configs[3]: optional LIST<optional int64> + optional MAP<string, optional int32>, V1 or V2,
+                  UNCOMPRESSED (levels -> list offsets / validity)
   C5  configs[4]: required BYTE_ARRAY strings, length U[8,40], ~half unique; each chunk starts with
                   RLE_DICTIONARY pages (dictionary page <= 1 MiB) and falls back to
                   DELTA_LENGTH_BYTE_ARRAY; SNAPPY
@@ -55,6 +57,59 @@ def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
                   rows_per_group, v2=False, as_array=True)
 
 
+def _repeated_levels(rng, rows, mean, p_null, p_empty, p_null_elem, max_d):
+    """Levels of one repeated leaf under an optional group (max_d = 3 with an optional leaf):
+    per row a null group (d 0), an empty group (d 1) or Poisson(mean) >= 1 entries (d max_d, or
+    max_d - 1 for a null leaf); r = 0 at each row's first slot."""
+    u = rng.random(rows)
+    k = np.maximum(1, rng.poisson(mean, rows))
+    k[u < p_null + p_empty] = 1
+    starts = np.zeros(rows + 1, np.int64)
+    np.cumsum(k, out=starts[1:])
+    n = int(starts[-1])
+    rep = np.ones(n, np.uint8)
+    rep[starts[:-1]] = 0
+    d = np.full(n, max_d, np.uint8)
+    if p_null_elem > 0:
+        d[rng.random(n) < p_null_elem] = max_d - 1
+    d[starts[:-1][u < p_null]] = 0
+    d[starts[:-1][(u >= p_null) & (u < p_null + p_empty)]] = 1
+    return d, rep
+
+
+def c4(rows=20_000_000, row_groups=4, v2=False, seed=30):
+    rng = np.random.default_rng(seed)
+    ld, lr = _repeated_levels(rng, rows, 4.0, 0.05, 0.05, 0.05, 3)
+    lv = rng.integers(-2**40, 2**40, int((ld == 3).sum()))
+    rng = np.random.default_rng(seed + 1)
+    kd, kr = _repeated_levels(rng, rows, 3.0, 0.0, 0.05, 0.0, 2)
+    nk = int((kd == 2).sum())
+    klen = rng.integers(4, 13, nk).astype(np.int64)
+    koff = np.zeros(nk + 1, np.int64)
+    np.cumsum(klen, out=koff[1:])
+    kdata = np.concatenate([rng.integers(97, 123, int(koff[-1]), dtype=np.uint8), np.zeros(1, np.uint8)])
+    vd = kd.copy()
+    vd[vd == 2] = 3
+    vd[(vd == 3) & (rng.random(len(vd)) < 0.05)] = 2
+    vv = rng.integers(-2**31, 2**31 - 1, int((vd == 3).sum())).astype(np.int32)
+    schema = [
+        W.element("schema", repetition=-1, num_children=2),
+        W.element("l", repetition=W.OPTIONAL, num_children=1, converted_type=3),
+        W.element("list", repetition=W.REPEATED, num_children=1),
+        W.element("element", W.INT64, W.OPTIONAL),
+        W.element("m", repetition=W.OPTIONAL, num_children=1, converted_type=1),
+        W.element("key_value", repetition=W.REPEATED, num_children=2),
+        W.element("key", W.BYTE_ARRAY, W.REQUIRED, converted_type=0),
+        W.element("value", W.INT32, W.OPTIONAL),
+    ]
+    cols = [W.Column(W.INT64, lv, def_levels=ld, rep_levels=lr, use_dict=False),
+            W.Column(W.BYTE_ARRAY, (kdata, koff), def_levels=kd, rep_levels=kr, use_dict=False),
+            W.Column(W.INT32, vv, def_levels=vd, rep_levels=kr, use_dict=False)]
+    per = -(-rows // row_groups)
+    rg = [min(per, rows - i * per) for i in range(row_groups)]
+    return W.write(schema, cols, rg, v2=v2, as_array=True)
+
+
 def c5_strings(rows, seed=40, chunk=4_000_000):
     """(data, offsets) of `rows` strings drawn from a pool of rows/2 random lowercase strings of
     length U[8,40] (about 43% of the rows distinct)."""
@@ -90,6 +145,8 @@ WORKLOADS = {
     "c2": ("C2: 100M rows x 6 columns (int32 dict / int64 PLAIN / float dict / optional double PLAIN "
            "1% null / boolean PLAIN / FLBA(16) PLAIN), data page V2, 16 row groups", c2),
     "c3": ("C3: INT64 timestamps DELTA_BINARY_PACKED 128/4, 7,812,500-row row groups", c3),
+    "c4": ("C4: optional LIST<optional int64> + optional MAP<string, optional int32>, 20M rows, V1, "
+           "UNCOMPRESSED", c4),
     "c5": ("C5: required BYTE_ARRAY strings U[8,40] ~half unique, RLE_DICTIONARY (dict page <= 1 MiB) "
            "then DELTA_LENGTH_BYTE_ARRAY fallback, SNAPPY, 8 row groups", c5),
 }

@@ -30,7 +30,8 @@ PAYLOAD_PAD = 256
 
 
 class Column(ctypes.Structure):
-    _fields_ = [("physical_type", i32), ("type_length", i32), ("max_def", i32), ("max_rep", i32)]
+    _fields_ = [("physical_type", i32), ("type_length", i32), ("max_def", i32), ("max_rep", i32),
+                ("rep_def", i32 * 8)]
 
 
 class Page(ctypes.Structure):
@@ -50,6 +51,15 @@ class ChunkOut(ctypes.Structure):
                 ("offsets", vp), ("bytes", vp), ("num_bytes", i64), ("def_levels", vp), ("rep_levels", vp)]
 
 
+class NestLevel(ctypes.Structure):
+    _fields_ = [("def_level", i32), ("reserved", i32), ("num_lists", i64), ("offsets", vp), ("validity", vp)]
+
+
+class NestOut(ctypes.Structure):
+    _fields_ = [("num_levels", i32), ("status", i32), ("num_leaf_slots", i64), ("leaf_validity", vp),
+                ("levels", NestLevel * 8)]
+
+
 class PageResult(ctypes.Structure):
     _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_non_null", i32), ("reserved", i32),
                 ("value_offset", i64), ("level_offset", i64)]
@@ -61,6 +71,8 @@ class KernelStat(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
+ABI_VERSION = 2  # include/pqhip.h PQH_ABI_VERSION
+
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
     ("pqh_device_count", ctypes.c_int, [ctypes.POINTER(i32)]),
@@ -80,6 +92,7 @@ PROTOTYPES = [
     ("pqh_batch_run", ctypes.c_int, [vp]),
     ("pqh_batch_sync", ctypes.c_int, [vp]),
     ("pqh_batch_chunk_out", ctypes.c_int, [vp, i32, ctypes.POINTER(ChunkOut)]),
+    ("pqh_batch_nesting", ctypes.c_int, [vp, i32, ctypes.POINTER(NestOut)]),
     ("pqh_batch_page_results", ctypes.c_int, [vp, ctypes.POINTER(PageResult), i32]),
     ("pqh_batch_kernel_stats", ctypes.c_int, [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]),
     ("pqh_batch_reset_stats", ctypes.c_int, [vp]),
@@ -108,6 +121,8 @@ PROTOTYPES = [
 
 
 def bind(L):
+    if L.pqh_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libpqhip ABI {L.pqh_abi_version()} != {ABI_VERSION}: rebuild (python parquet-go_amd/build.py)")
     for name, res, args in PROTOTYPES:
         f = getattr(L, name)
         f.restype = res
@@ -327,6 +342,11 @@ class Batch:
     def chunk_out(self, i):
         o = ChunkOut()
         self.ctx.check(self.L.pqh_batch_chunk_out(self.h, i, ctypes.byref(o)))
+        return o
+
+    def nesting(self, i):
+        o = NestOut()
+        self.ctx.check(self.L.pqh_batch_nesting(self.h, i, ctypes.byref(o)))
         return o
 
     def page_results(self, n):

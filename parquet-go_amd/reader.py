@@ -29,7 +29,7 @@ class DecodeError(RuntimeError):
 class ColumnData:
     """One decoded column chunk (dense not-null values + level bytes), host copy."""
 
-    def __init__(self, path, column, out, page_results, ctx):
+    def __init__(self, path, column, out, page_results, ctx, nest=None):
         self.path = path
         self.physical_type, self.type_length, self.max_def, self.max_rep = column
         self.status = out.status
@@ -58,6 +58,17 @@ class ColumnData:
             self.def_levels = ctx.d2h_array(out.def_levels, out.num_values)
         if out.rep_levels:
             self.rep_levels = ctx.d2h_array(out.rep_levels, out.num_values)
+        self.nesting = None  # [(offsets int32, validity u8) per repetition level], leaf validity u8
+        if nest is not None and nest.num_levels and nest.status == native.OK:
+            levels = []
+            for k in range(nest.num_levels):
+                lv = nest.levels[k]
+                levels.append((ctx.d2h_array(lv.offsets, lv.num_lists + 1, np.int32) if lv.offsets else
+                               np.zeros(1, np.int32),
+                               ctx.d2h_array(lv.validity, lv.num_lists) if lv.validity else np.zeros(0, np.uint8)))
+            leaf = ctx.d2h_array(nest.leaf_validity, nest.num_leaf_slots) if nest.leaf_validity else \
+                np.zeros(0, np.uint8)
+            self.nesting = (levels, leaf)
 
     def raise_for_status(self):
         if self.status != native.OK:
@@ -96,7 +107,7 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
         o = batch.chunk_out(i)
         if ch.host_status != native.OK and o.status == native.OK:
             o.status = ch.host_status
-        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx))
+        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None))
     if return_batch:
         return out, batch, hb
     batch.close()

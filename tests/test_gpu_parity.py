@@ -382,3 +382,67 @@ def test_c5_dictionary_fallback(pq, ctx):
     data = datasets.c5(rows=600_000, row_groups=2)
     checked, _ = _run_file(pq, ctx, data, allow_not_implemented=False)
     assert checked == 2
+
+
+# ---------------------------------------------------------------------------------------------
+# Nesting: levels -> list offsets / presence per level + leaf validity
+# ---------------------------------------------------------------------------------------------
+def _check_nesting(pq, ctx, data):
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(ncols)))
+    fr = O.FileReader(data)
+    checked = 0
+    for k, col in enumerate(res):
+        rg, ci = divmod(k, ncols)
+        c = fr.columns[ci]
+        if c.max_rep == 0:
+            continue
+        e = oracle_chunk(fr, rg, ci)
+        assert e.status == 0 and col.status == 0, (rg, c.path)
+        want_levels, want_leaf = O.nest_levels(e.def_levels, e.rep_levels, c.max_def, c.rep_def)
+        got_levels, got_leaf = col.nesting
+        assert len(got_levels) == len(want_levels) == c.max_rep
+        for lvl, ((o, v), (wo, wv)) in enumerate(zip(got_levels, want_levels)):
+            np.testing.assert_array_equal(o, wo, err_msg=f"rg{rg} {c.path} level {lvl + 1} offsets")
+            np.testing.assert_array_equal(v, wv, err_msg=f"rg{rg} {c.path} level {lvl + 1} validity")
+        np.testing.assert_array_equal(got_leaf, want_leaf, err_msg=f"rg{rg} {c.path} leaf validity")
+        assert int(got_leaf.sum()) == col.num_non_null
+        checked += 1
+    return checked
+
+
+@pytest.mark.parametrize("v2", [False, True])
+def test_nesting_list_map(pq, ctx, v2):
+    assert _check_nesting(pq, ctx, fixtures.nested_list_map(n=6000, v2=v2)) == 6
+
+
+def test_nesting_c4_multi_tile(pq, ctx):
+    from parquet_go_amd import datasets
+
+    assert _check_nesting(pq, ctx, datasets.c4(rows=150_000, row_groups=2)) == 6
+
+
+def test_nesting_deep_lists(pq, ctx):
+    """list<list<int32>> and list<struct<list<string>>> from pyarrow (max_rep 2)."""
+    import io
+
+    import pyarrow as pa
+    import pyarrow.parquet as pqa
+
+    rng = np.random.default_rng(7)
+
+    def inner(p_null):
+        if rng.random() < 0.1:
+            return None
+        return [None if rng.random() < p_null else int(rng.integers(0, 1000)) for _ in range(rng.poisson(2))]
+
+    a = [None if rng.random() < 0.1 else [inner(0.1) for _ in range(rng.poisson(3))] for _ in range(20000)]
+    b = [None if rng.random() < 0.1 else [{"s": None if rng.random() < 0.2 else
+                                           [str(rng.integers(0, 99)) for _ in range(rng.poisson(1.5))]}
+                                          for _ in range(rng.poisson(2))] for _ in range(20000)]
+    t = pa.table({"a": pa.array(a, pa.list_(pa.list_(pa.int32()))),
+                  "b": pa.array(b, pa.list_(pa.struct([("s", pa.list_(pa.string()))])))})
+    buf = io.BytesIO()
+    pqa.write_table(t, buf, row_group_size=7000, data_page_size=8192, use_dictionary=False)
+    assert _check_nesting(pq, ctx, buf.getvalue()) == 6

@@ -1,0 +1,100 @@
+"""World-size-2 gloo run of the sharded decode path on CPU.
+
+Each rank takes its contiguous block of row groups (shard.row_group_block), decodes it (here with
+the CPU oracle: there is no GPU in this container; the GPU ranks run the same sharding in bench.py
+with RCCL), and the measurement reduction (max time, sum of bytes) runs over gloo.  Rank 0 checks
+that the union of the shards is the whole file, in order, bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, path, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_package
+        from oracle import oracle as O
+
+        shard = load_package().shard
+        data = np.fromfile(path, dtype=np.uint8)
+        fr = O.FileReader(data)
+        rg0, rg1 = shard.row_group_block(len(fr.row_groups), world, rank)
+        blobs, nbytes = [], 0
+        for rg in range(rg0, rg1):
+            for ci in range(len(fr.columns)):
+                for r in O.decode_chunk(fr.read_chunk(rg, ci)):
+                    assert r.status == 0
+                    blobs.append((rg, ci, bytes(r.values)))
+                    nbytes += len(r.values)
+        t, total = shard.reduce_step(0.5 + rank, nbytes)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, blobs)
+        if rank == 0:
+            q.put((t, total, [b for g in gathered for b in g]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_group_block():
+    from conftest import load_package
+
+    shard = load_package().shard
+    for n in (0, 1, 7, 16, 128):
+        for world in (1, 2, 3, 8):
+            blocks = [shard.row_group_block(n, world, r) for r in range(world)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+    assert shard.row_offsets([5, 7, 0, 3]) == [0, 5, 12, 12]
+
+
+def test_two_rank_gloo_shards(tmp_path):
+    import fixtures
+    from oracle import oracle as O
+
+    W = fixtures.W
+    rng = np.random.default_rng(3)
+    n = 9000
+    data = W.flat([("a", W.Column(W.INT64, rng.integers(0, 1 << 40, n), use_dict=False), W.REQUIRED),
+                   ("b", W.Column(W.INT32, rng.integers(0, 50, n).astype(np.int32)), W.REQUIRED)], 1000)
+    path = tmp_path / "f.parquet"
+    path.write_bytes(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    t, total, blobs = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fr = O.FileReader(np.frombuffer(data, dtype=np.uint8))
+    want = []
+    for rg in range(len(fr.row_groups)):
+        for ci in range(len(fr.columns)):
+            for r in O.decode_chunk(fr.read_chunk(rg, ci)):
+                want.append((rg, ci, bytes(r.values)))
+    assert blobs == want
+    assert t == 1.5 and total == sum(len(b[2]) for b in want)
