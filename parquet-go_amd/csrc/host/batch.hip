@@ -52,7 +52,7 @@ struct KernelRun {
 };
 
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
-                              "k_delta_walk", "k_delta_sum", "k_delta_scan",
+                              "k_delta_walk", "k_delta_expand", "k_reserved",
                               "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write"};
 constexpr int kNumKernels = 14;
@@ -148,6 +148,9 @@ struct pqh_batch {
   DeltaState* d_dstates = nullptr;
   DeltaBlock* d_dblocks = nullptr;
   uint64_t* d_dsums = nullptr;
+  uint32_t* d_dflag = nullptr;   // delta look-back: per delta tile flag (+ the ticket counter at the end)
+  uint64_t* d_dagg = nullptr;
+  uint64_t* d_dpre = nullptr;
   Tile* d_batiles = nullptr;
   int32_t* d_ba_pages = nullptr;
   int32_t* d_ba_chunks = nullptr;
@@ -462,7 +465,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   // CU sees a mix of byte-copy and bit-unpack tiles instead of one long phase per kind.
   {
     std::vector<std::pair<double, Tile>> keyed;
-    for (int kd : {int(TK_LEVELS), int(TK_COPY), int(TK_BOOL), int(TK_DICT), int(TK_RLE_BOOL), int(TK_DELTA)}) {
+    for (int kd : {int(TK_LEVELS), int(TK_COPY), int(TK_BOOL), int(TK_DICT), int(TK_RLE_BOOL)}) {
       const auto& v = by_kind[size_t(kd)];
       for (size_t i = 0; i < v.size(); i++) keyed.push_back({(double(i) + 0.5) / double(v.size()), v[i]});
     }
@@ -486,6 +489,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dblocks), sizeof(DeltaBlock) * size_t(dblk_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dflag), sizeof(uint32_t) * size_t(dtile_cursor + 1))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dagg), sizeof(uint64_t) * size_t(dtile_cursor))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dpre), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_batiles), sizeof(Tile) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
@@ -638,10 +644,13 @@ int pqh_batch_run(pqh_batch* b) {
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
   if (e == hipSuccess && nbp)
     e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
-  if (e == hipSuccess && ndt)
-    e = timed(5, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
-  if (e == hipSuccess && ndp)
-    e = timed(6, ndp, s, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
+  if (e == hipSuccess && ndt) {
+    e = hipMemsetAsync(b->d_dflag, 0, sizeof(uint32_t) * size_t(ndt + 1), s);
+    if (e == hipSuccess)
+      e = timed(5, ndt, s, [&](hipStream_t st) {
+        return launch_delta_expand(d, b->d_dtiles, ndt, b->d_dflag, b->d_dagg, b->d_dpre, b->d_dflag + ndt, st);
+      });
+  }
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
   if (e == hipSuccess && ne)
     e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
@@ -766,10 +775,9 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[2] += S.nn;
         break;
       case K_DELTA32:
-      case K_DELTA64:  // the walk reads block headers; sums and expand each read the packed deltas
-        b->k_read[2] += S.val_e - S.val_s;
-        b->k_written[2] += vals;
+      case K_DELTA64:  // the walk reads block headers; k_delta_expand reads the stream once from HBM
         b->k_read[5] += S.val_e - S.val_s;
+        b->k_written[5] += vals;
         break;
       case K_PLAIN_BA:  // walked by k_ba_walk, bytes moved by k_ba_expand
       case K_DLBA:

@@ -915,11 +915,6 @@ __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
     case TK_BOOL: tile_bool_plain(b, t); break;
     case TK_DICT: tile_dict<true>(b, t, L, stage, dict_lds); break;
     case TK_RLE_BOOL: tile_rle_bool(b, t, L, stage); break;
-    case TK_DELTA: {
-      __shared__ DeltaLds DL;
-      tile_delta(b, t, stage, DL);
-      break;
-    }
     case TK_DELTA_SERIAL: delta_serial(b, t); break;
     default: break;
   }
@@ -959,15 +954,10 @@ hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int3
   return hipGetLastError();
 }
 
-hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, uint32_t* flag, uint64_t* agg,
+                               uint64_t* pre, uint32_t* ticket, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_delta_sum, dim3(n), dim3(256), 0, s, b, tiles);
-  return hipGetLastError();
-}
-
-hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_delta_scan, dim3((n + 255) / 256), dim3(256), 0, s, b, delta_pages, n);
+  hipLaunchKernelGGL(k_delta_expand, dim3(n), dim3(256), 0, s, b, tiles, DeltaLookback{flag, agg, pre, ticket});
   return hipGetLastError();
 }
 

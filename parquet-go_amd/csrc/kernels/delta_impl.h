@@ -110,6 +110,55 @@ __device__ __forceinline__ int win_miniblock_header(Win& w, int64_t& pos, bool i
 
 __device__ __forceinline__ int mb_width(uint64_t widths, int m) { return int((widths >> (8 * m)) & 0xff); }
 
+// Bytes [pos, pos + 16) of the window as two little-endian words (window holds pos + 24).
+__device__ __forceinline__ void win_bytes16(const Win& w, int64_t pos, uint64_t& a, uint64_t& b) {
+  const int64_t off = pos - w.lo;
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(w.buf) + (off >> 3);
+  const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
+  const int sh = int(off & 7) * 8;
+  a = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+  b = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+}
+
+// Common case of readMiniBlockHeader: a varint of <= 8 bytes followed by the widths, all well inside
+// the stream, values in range.  One LDS round trip; anything else returns false and the exact
+// byte-by-byte reader produces the reference's error.
+__device__ __forceinline__ bool fast_block_header(Win& w, int64_t& pos, bool is64, int mbc, uint64_t& md,
+                                                  uint64_t& widths, int lane) {
+  if (w.e - pos < 24) return false;
+  win_ensure(w, pos, 24, lane);
+  uint64_t a, b;
+  win_bytes16(w, pos, a, b);
+  const uint64_t stop = ~a & 0x8080808080808080ull;
+  if (!stop) return false;
+  const int len = (__builtin_ctzll(stop) >> 3) + 1;
+  uint64_t u = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (i < len) u |= ((a >> (8 * i)) & 0x7f) << (7 * i);
+  const int64_t x = int64_t(u >> 1) ^ -int64_t(u & 1);
+  if (!is64 && (x > 2147483647ll || x < -2147483648ll)) return false;
+  const int sh = len * 8;
+  uint64_t wd = sh == 64 ? b : (a >> sh) | (b << (64 - sh));
+  if (mbc < 8) wd &= (1ull << (8 * mbc)) - 1;
+  const uint32_t lim = is64 ? 64u : 32u;
+  bool ok = true;
+#pragma unroll
+  for (int m = 0; m < 8; m++) ok = ok && ((wd >> (8 * m)) & 0xff) <= lim;
+  if (!ok) return false;
+  md = uint64_t(x);
+  widths = wd;
+  pos += len + mbc;
+  return true;
+}
+
+__device__ __forceinline__ int64_t block_data_bytes(uint64_t widths, int mbvc) {
+  int64_t sum = 0;
+#pragma unroll
+  for (int m = 0; m < 8; m++) sum += int64_t((widths >> (8 * m)) & 0xff);
+  return sum * (mbvc / 8);
+}
+
 // The block walk of one page (whole wave, uniform).  Returns the first error key.
 // init_all: byteArrayDeltaLengthDecoder.init (type_bytearray.go:104-116) decodes ALL valuesCount
 // lengths at page load: every error is a load error (phase 0, step 3) and nn is ignored.
@@ -154,7 +203,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   bool padded = false;
   for (int64_t b = 0; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
     const int64_t p0 = b * bs;
-    if (b > 0 && (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
+    if (b > 0 && !fast_block_header(w, pos, is64, mbc, md, widths, lane) &&
+        (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
       err = init_all ? err_key(0, 3, st) : err_key(3, p0, st);
       limit = p0;
       break;
@@ -165,6 +215,15 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
     }
     if (lane == 0) recs[D.nblocks] = DeltaBlock{md, int32_t(pos), int32_t(p0), widths, 0};
     D.nblocks++;
+    // a whole block before the padding group and the last reachable position, inside the stream:
+    // every group read succeeds
+    if (p0 + bs <= L && p0 + bs <= pstar) {
+      const int64_t nb = block_data_bytes(widths, mbvc);
+      if (pos + nb <= w.e) {
+        pos += nb;
+        continue;
+      }
+    }
     for (int m = 0; m < mbc; m++) {
       const int64_t pm = p0 + int64_t(m) * mbvc;
       if (pm >= L) break;
@@ -368,61 +427,74 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
   return total_all;
 }
 
-// k_delta_sum: per tile sum of (delta + minDelta) over its positions.
-__global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles) {
+// ------------------------------------------------------------------------------------------------
+// k_delta_expand: single pass over the packed deltas with a decoupled look-back across the tiles of
+// a page (Merrill & Garland's single-pass scan).  Tiles take tickets in start order, so a tile's
+// predecessor always started before it.  Per tile: unpack + sum (aggregate published), look back
+// for the exclusive prefix (inclusive prefix published), unpack again from L2 and store
+// value[i] = prefix + sum of the deltas before i.  Tile 0 of a page starts from the first value.
+// ------------------------------------------------------------------------------------------------
+struct DeltaLookback {
+  uint32_t* flag;  // per delta tile: 0 nothing yet, 1 aggregate, 2 inclusive prefix (reset per run)
+  uint64_t* agg;
+  uint64_t* pre;
+  uint32_t* ticket;
+};
+
+__device__ __forceinline__ void lb_publish(uint64_t* slot, uint32_t* flag, uint64_t v, uint32_t f) {
+  __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(flag, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles, DeltaLookback lb) {
   __shared__ __attribute__((aligned(16))) uint32_t stage[(kStageBytes + 32) / 4];
   __shared__ DeltaLds DL;
-  const Tile t = tiles[blockIdx.x];
-  const DevPage P = b.pages[t.page];
-  const DeltaState D = b.dstates[t.page];
-  if (D.mode != DM_FAST) return;
-  const int64_t v0 = int64_t(t.k) * kDeltaTile;
-  int64_t v1 = v0 + kDeltaTile;
-  const int64_t have = int64_t(D.nblocks) * D.block_size;
-  if (v1 > have) v1 = have;
-  if (v1 > D.limit) v1 = D.limit;
-  uint64_t s = 0;
-  if (v0 < v1)
-    s = P.kind == K_DELTA64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, stage, DL)
-                            : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, stage, DL);
-  if (threadIdx.x == 0) b.dsums[P.dtile_base + t.k] = s;
-}
-
-// k_delta_scan: one thread per delta page; tile bases = first + exclusive scan of tile sums.
-__global__ __launch_bounds__(256) void k_delta_scan(DevBatch b, const int32_t* delta_pages, int32_t n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int p = delta_pages[i];
-  const DevPage P = b.pages[p];
-  uint64_t run = b.dstates[p].first;
-  for (int k = 0; k < P.dtile_n; k++) {
-    const uint64_t s = b.dsums[P.dtile_base + k];
-    b.dsums[P.dtile_base + k] = run;
-    run += s;
-  }
-}
-
-// TK_DELTA: values [k*kDeltaTile, ...) of a DM_FAST page.
-__device__ __forceinline__ void tile_delta(const DevBatch& b, const Tile& t, uint32_t* stage, DeltaLds& DL) {
+  __shared__ int32_t s_ticket;
+  __shared__ uint64_t s_base;
+  if (threadIdx.x == 0) s_ticket = int32_t(atomicAdd(lb.ticket, 1u));
+  __syncthreads();
+  const Tile t = tiles[s_ticket];
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
-  if (page_failed_before_values(S)) return;
   const DeltaState D = b.dstates[t.page];
-  if (D.mode != DM_FAST) return;
+  // every tile of a page sees the same page verdict, so no tile waits on a tile that skipped
+  if (page_failed_before_values(S) || D.mode != DM_FAST) return;
+  const bool dlba = P.kind == K_DLBA;
   const int64_t v0 = int64_t(t.k) * kDeltaTile;
   int64_t v1 = v0 + kDeltaTile;
   if (v1 > D.limit) v1 = D.limit;
-  if (v0 >= v1) return;
-  const DevChunk C = b.chunks[P.chunk];
-  const bool dlba = P.kind == K_DLBA;  // lengths of a DELTA_LENGTH_BYTE_ARRAY page -> aux (int32)
   if (dlba && v1 > S.nn) v1 = S.nn;
-  if (v0 >= v1) return;
+  if (v0 >= v1) return;  // so is every later tile of the page
+  const bool is64 = P.kind == K_DELTA64;
+  const uint64_t agg = is64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, stage, DL)
+                            : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, stage, DL);
+  const int64_t me = int64_t(P.dtile_base) + t.k;
+  if (threadIdx.x == 0) {
+    uint64_t base;
+    if (t.k == 0) {
+      base = D.first;
+    } else {
+      lb_publish(lb.agg + me, lb.flag + me, agg, 1u);
+      base = 0;
+      for (int64_t j = me - 1;; j--) {
+        uint32_t f;
+        while ((f = __hip_atomic_load(lb.flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+          __builtin_amdgcn_s_sleep(1);
+        if (f == 2u) {
+          base += __hip_atomic_load(lb.pre + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        base += __hip_atomic_load(lb.agg + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    lb_publish(lb.pre + me, lb.flag + me, base + agg, 2u);
+    s_base = base;
+  }
+  __syncthreads();
+  const DevChunk C = b.chunks[P.chunk];
   uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(C.aux + S.value_base) : C.values + S.value_base * P.value_size;
-  // value[i] needs deltas p < i: the last value of the page needs no delta of its own, and
-  // positions past the last recorded block are never reached (the walk stops there).
-  const uint64_t base = b.dsums[P.dtile_base + t.k];
-  if (P.kind == K_DELTA64) delta_tile<true>(b, P, D, v0, v1, base, true, out, stage, DL);
-  else delta_tile<false>(b, P, D, v0, v1, base, true, out, stage, DL);
+  if (is64) delta_tile<true>(b, P, D, v0, v1, s_base, true, out, stage, DL);
+  else delta_tile<false>(b, P, D, v0, v1, s_base, true, out, stage, DL);
 }
 
 // TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.next for streams outside
