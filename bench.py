@@ -217,8 +217,12 @@ def main():
             "algo_gbps_all_kernels": round((bytes_read + bytes_written) / (all_ms * 1e-3) / 1e9, 1) if all_ms else None,
             "roofline": roof,
             "kernels": kernels,
-            "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 2),
+            "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 3),
                      "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
+            # end-to-end per GPU: host decompression excluded, pinned H2D of the
+            # decompressed pages + one decode; never `value`
+            "e2e": {"payload_bytes": hb.payload_bytes, "h2d_s": round(h2d_s, 4), "decode_s": round(ms_per_step / 1e3, 5),
+                    "gbps": round(bytes_written / (h2d_s + ms_per_step / 1e3) / 1e9, 2)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -4,7 +4,7 @@
 // decodeValues fills into []interface{} of []byte (type_bytearray.go).  Three producers of
 // per-value lengths feed one offsets/copy pipeline:
 //   PLAIN       byteArrayPlainDecoder.next (type_bytearray.go:24-45): a [u32 len][bytes] chain,
-//               walked by one wave per page (k_ba_walk) -> lengths in aux + the first error;
+//               resolved by one workgroup per page (k_ba_walk) -> lengths in aux + the first error;
 //   DELTA_LEN   byteArrayDeltaLengthDecoder (type_bytearray.go:98-140): the lengths are a
 //               DELTA_BINARY_PACKED stream decoded by the delta pipeline into aux (init decodes
 //               all valuesCount lengths: delta_walk init_all); the string bytes follow the stream;
@@ -16,74 +16,264 @@
 #pragma once
 
 // ------------------------------------------------------------------------------------------------
-// k_ba_walk: one wave64 per PLAIN byte-array page (data pages and byte-array dictionary pages).
-// The chain [u32 len][len bytes] is inherently sequential; the wave reads it through an LDS window
-// and records one length (data page) or one cumulative offset (dictionary page) per value,
-// flushed 64 at a time with one coalesced store.
+// k_ba_walk: one workgroup per PLAIN byte-array page (data pages and byte-array dictionary pages).
+// The chain [u32 len][len bytes] (byteArrayPlainDecoder.next, type_bytearray.go:24-45) is sequential
+// by definition; it is resolved in parallel and exactly, 64 KiB window by window:
+//   1. each thread owns a 256-byte segment and walks it from a SPECULATIVE start (the first offset
+//      whose length field describes a record inside the stream; segment 0 starts at the known
+//      entry), marking the record starts it visits in a 256-bit mask;
+//   2. the true entry of segment j is the exit of segment j-1.  Segment j is right when that entry
+//      is one of its marked starts (the chains merge) or lies past the segment (a long record);
+//      one parallel check confirms the common case, otherwise thread 0 sweeps the segments in
+//      order and re-walks the ones whose speculation was wrong;
+//   3. records are numbered with a block scan of the per-segment counts and emitted: lengths (data
+//      page -> aux) or cumulative offsets (dictionary page -> dcum); the first invalid record on the
+//      true chain (short length, negative length, short data) is the page's error.
 // ------------------------------------------------------------------------------------------------
+constexpr int kChainWin = 65536;
+constexpr int kChainSeg = kChainWin / kBlock;  // 256 bytes per thread
+constexpr int kChainWords = kChainSeg / 64;     // mask words per segment
+
+struct ChainLds {
+  uint32_t win[(kChainWin + 64) / 4];
+  uint64_t mask[kBlock][kChainWords];
+  int32_t exitv[kBlock];
+  uint8_t exitbad[kBlock];
+  int32_t first_bad;
+  int32_t stop;
+  uint64_t wsum[4];
+};
+
+// One record at page offset p (window-relative o): 0 and the next offset, or the error code.
+__device__ __forceinline__ int chain_step(const ChainLds& C, int64_t wb, int64_t e0, int64_t p, int64_t& next,
+                                          int32_t& len) {
+  const int64_t avail = e0 - p;
+  if (avail < 4) return avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;  // binary.Read(u32)
+  const int64_t o = p - wb;
+  const uint32_t w0 = C.win[o >> 2], w1 = C.win[(o >> 2) + 1];
+  len = int32_t(__builtin_amdgcn_alignbit(w1, w0, uint32_t(o & 3) * 8));
+  if (len < 0) return PQH_ERR_NEGATIVE_LENGTH;
+  if (len > 0 && avail - 4 < len) return avail - 4 <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;  // ReadFull
+  next = p + 4 + len;
+  return PQH_OK;
+}
+
+// Walk segment [s0, s0 + kChainSeg) from `start` (must lie in the segment): marks + exit.
+__device__ void chain_walk(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t start) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = s0 + kChainSeg;
+  uint64_t m[kChainWords];
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) m[k] = 0;
+  int64_t p = start;
+  uint8_t bad = 0;
+  while (p < s1) {
+    int64_t nx;
+    int32_t l;
+    const int st = chain_step(C, wb, e0, p, nx, l);
+    if (st) {
+      bad = uint8_t(st);
+      break;
+    }
+    const int q = int(p - s0);
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++)
+      if ((q >> 6) == k) m[k] |= 1ull << (q & 63);
+    p = nx;
+  }
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) C.mask[j][k] = m[k];
+  C.exitv[j] = int32_t(p);
+  C.exitbad[j] = bad;
+}
+
+__device__ __forceinline__ bool chain_has(const ChainLds& C, int j, int q) {
+  return (C.mask[j][q >> 6] >> (q & 63)) & 1;
+}
+
+// Is segment j's stored result right for its true entry (the previous segment's exit)?  By
+// induction from segment 0 (whose start is the known entry), when every segment passes, all
+// segments up to the first invalid exit are exact and that exit is the true end of the chain.
+__device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb, int64_t entry) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+  int64_t T = entry;
+  uint8_t pbad = 0;
+  if (j > 0) {
+    T = C.exitv[j - 1];
+    pbad = C.exitbad[j - 1];
+  }
+  bool empty = true;
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) empty = empty && C.mask[j][k] == 0;
+  if (pbad) return true;  // the chain ended before j (exactly, if j-1 is right): nothing here counts
+  if (T >= s0 + kChainSeg) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
+  return chain_has(C, j, int(T - s0));
+}
+
+// Make segment j right for its true entry.
+__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t entry) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+  int64_t T = entry;
+  uint8_t pbad = 0;
+  if (j > 0) {
+    T = C.exitv[j - 1];
+    pbad = C.exitbad[j - 1];
+  }
+  if (pbad || T >= s0 + kChainSeg) {
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+    C.exitv[j] = int32_t(T);
+    C.exitbad[j] = pbad;
+  } else if (!chain_has(C, j, int(T - s0))) {
+    chain_walk(C, j, wb, e0, T);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_pages, int32_t n) {
-  __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kWin];
-  const int lane = threadIdx.x & 63;
-  const int wv = int(threadIdx.x >> 6);
-  const int idx = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
-  if (idx >= n) return;
-  const int p = ba_pages[idx];
+  __shared__ ChainLds C;
+  const int j = threadIdx.x;
+  const int p = ba_pages[blockIdx.x];
   const DevPage P = b.pages[p];
   const PageState S = b.states[p];
   const bool dict = P.page_type == PQH_DICTIONARY_PAGE;
   if (S.err != kNoError && (dict || page_failed_before_values(S))) return;
-  int64_t count, s0, e0;
+  int64_t count, entry, e0;
   int32_t* out;
   if (dict) {  // dictPageReader.read: num_values PLAIN entries over the whole page
     count = P.num_values;
-    s0 = 0;
+    entry = 0;
     e0 = P.image_len;
     out = b.dcum + P.aux_base;
   } else {
     count = S.nn;
-    s0 = S.val_s;
+    entry = S.val_s;
     e0 = S.val_e;
     out = b.chunks[P.chunk].aux + S.value_base;
   }
-  Win w{b.payload + P.image_off, e0, win_all[wv], 0, 0};
-  win_load(w, s0, lane);
-  int64_t pos = s0, i = 0;
-  int32_t cum = 0, mine = 0;
+  const uint8_t* img = b.payload + P.image_off;
+  int64_t done = 0;      // records emitted so far
+  int64_t cum = 0;       // dictionary: bytes of the entries so far
   int code = PQH_OK;
-  for (; i < count; i++) {
-    const int64_t avail = e0 - pos;
-    if (avail < 4) {  // binary.Read of the u32 length
-      code = avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
+  while (done < count) {
+    if (entry >= e0) {  // no bytes left for the next length
+      code = PQH_ERR_EOF;
       break;
     }
-    win_ensure(w, pos, 4, lane);
-    const uint8_t* q = w.buf + (pos - w.lo);
-    const int32_t l = int32_t(uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) | (uint32_t(q[3]) << 24));
-    if (l < 0) {
-      code = PQH_ERR_NEGATIVE_LENGTH;
-      break;
+    // window [wb, wb + kChainWin) with wb 16-byte aligned (payload address) at or before entry
+    const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(entry)) & 15);
+    __syncthreads();
+    for (int k = j; k < (kChainWin + 64) / 16; k += kBlock) {
+      const int64_t o = wb + 16 * int64_t(k);
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (o < e0) x = *reinterpret_cast<const uint4*>(img + o);  // the 16 B past e0 stay in the pad
+      reinterpret_cast<uint4*>(C.win)[k] = x;
     }
-    const int64_t rem = avail - 4;
-    if (l > 0 && rem < l) {  // io.ReadFull(len bytes)
-      code = rem <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
-      break;
+    if (j == 0) C.stop = 0;
+    __syncthreads();
+    // 1. speculative walks
+    {
+      const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = s0 + kChainSeg;
+      int64_t start = -1;
+      if (j == 0) {
+        start = entry;
+      } else {
+        for (int64_t x = s0; x < s1 && x < e0; x++) {
+          int64_t nx;
+          int32_t l;
+          if (chain_step(C, wb, e0, x, nx, l) == PQH_OK) {
+            start = x;
+            break;
+          }
+        }
+      }
+      if (start >= 0) {
+        chain_walk(C, j, wb, e0, start);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+        C.exitv[j] = int32_t(s1);
+        C.exitbad[j] = 0;
+      }
     }
-    pos += 4 + int64_t(l);
-    const int32_t rec = dict ? cum : l;
-    cum += l;
-    if (lane == int(i & 63)) mine = rec;
-    if ((i & 63) == 63) out[i - 63 + lane] = mine;
-  }
-  const int64_t tail = i & 63;
-  if (lane < tail) out[i - tail + lane] = mine;
-  if (lane == 0) {
+    __syncthreads();
+    // 2. resolution: one parallel check, then an in-order sweep if anything was mis-speculated
+    if (!chain_good(C, j, wb, entry)) atomicOr(&C.stop, 1);
+    __syncthreads();
+    if (C.stop) {
+      if (j == 0)
+        for (int s = 0; s < kBlock; s++) chain_fix(C, s, wb, e0, entry);
+      __syncthreads();
+    }
+    // 3. number the records of the true chain, emit, find where the chain ends
+    if (j == 0) C.first_bad = kBlock;
+    __syncthreads();
+    if (C.exitbad[j]) atomicMin(&C.first_bad, j);  // segments before the chain's end are exact and valid
+    __syncthreads();
+    const int fb = C.first_bad;
+    const int64_t s0 = wb + int64_t(j) * kChainSeg;
+    const int64_t T = j == 0 ? entry : int64_t(C.exitv[j - 1]);
+    const bool live = j <= fb;
+    uint64_t m[kChainWords];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++) {
+      m[k] = live ? C.mask[j][k] : 0;
+      const int64_t lo = T - s0 - 64 * k;  // drop speculative starts before the true entry
+      if (lo > 0) m[k] = lo >= 64 ? 0 : m[k] & ~((1ull << lo) - 1);
+      cnt += __popcll(m[k]);
+    }
+    uint64_t tot;
+    const int64_t before = int64_t(block_exclusive_scan(uint64_t(cnt), C.wsum, &tot));
+    int64_t bytes = 0;
     if (dict) {
-      out[i] = cum;
-      if (code == PQH_OK) b.states[p].dict_n = int32_t(i);
-      else atomicMin(&b.states[p].err, (unsigned long long)err_key(0, i, code));
+#pragma unroll
+      for (int k = 0; k < kChainWords; k++) {
+        uint64_t x = m[k];
+        while (x) {
+          const int64_t o = s0 + __builtin_ctzll(x) + 64 * k - wb;
+          x &= x - 1;
+          bytes += int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
+        }
+      }
+    }
+    uint64_t btot = 0;
+    const int64_t bbefore = dict ? int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot)) : 0;
+    int64_t r = done + before, c = cum + bbefore;
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++) {
+      uint64_t x = m[k];
+      while (x) {
+        const int64_t o = s0 + __builtin_ctzll(x) + 64 * k - wb;
+        x &= x - 1;
+        const int32_t l = int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
+        if (r < count) {
+          out[r] = dict ? int32_t(c) : l;
+          if (dict && r == count - 1) out[count] = int32_t(c + l);
+        }
+        r++;
+        c += l;
+      }
+    }
+    done += int64_t(tot);  // segments after the chain's end hold no records
+    cum += int64_t(btot);
+    if (fb < kBlock) {
+      code = C.exitbad[fb];
+      break;
+    }
+    entry = C.exitv[kBlock - 1];
+  }
+  if (j == 0) {
+    if (done >= count) {  // all values read (records past `count` are never looked at)
+      if (dict) {
+        if (count == 0) out[0] = 0;
+        b.states[p].dict_n = int32_t(count);
+      } else {
+        b.states[p].val_limit = int32_t(count);
+      }
+    } else if (dict) {
+      atomicMin(&b.states[p].err, (unsigned long long)err_key(0, done, code));
     } else {
-      b.states[p].val_limit = int32_t(i);
-      if (code != PQH_OK) atomicMin(&b.states[p].err, (unsigned long long)err_key(3, i, code));
+      b.states[p].val_limit = int32_t(done);
+      atomicMin(&b.states[p].err, (unsigned long long)err_key(3, done, code));
     }
   }
 }

@@ -963,7 +963,7 @@ hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, 
 
 hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_walk, dim3((n + 3) / 4), dim3(256), 0, s, b, ba_pages, n);
+  hipLaunchKernelGGL(k_ba_walk, dim3(n), dim3(256), 0, s, b, ba_pages, n);
   return hipGetLastError();
 }
 

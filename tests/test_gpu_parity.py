@@ -446,3 +446,46 @@ def test_nesting_deep_lists(pq, ctx):
     buf = io.BytesIO()
     pqa.write_table(t, buf, row_group_size=7000, data_page_size=8192, use_dictionary=False)
     assert _check_nesting(pq, ctx, buf.getvalue()) == 6
+
+
+def test_plain_chain_layouts(pq, ctx):
+    """PLAIN byte-array chains that stress the parallel chain resolution: runs of empty strings
+    (every offset looks like a record start), zero bytes inside strings, strings longer than a
+    segment (256 B) and than a window (64 KiB), pages spanning many windows, and dictionary pages."""
+    W = fixtures.W
+    rng = np.random.default_rng(43)
+    col = (W.BYTE_ARRAY, 0, 0, 0)
+    cases = []
+
+    def strings(n, kind):
+        out = []
+        for _ in range(n):
+            u = rng.random()
+            if kind == "empty_runs":
+                out.append(b"" if u < 0.7 else bytes(int(rng.integers(0, 3))))
+            elif kind == "zeros":
+                out.append(bytes(rng.integers(0, 2, int(rng.integers(0, 12))).astype(np.uint8)))
+            elif kind == "long":
+                out.append(rng.bytes(int(rng.integers(200, 3000))) if u < 0.8 else b"")
+            elif kind == "huge":
+                out.append(rng.bytes(int(rng.integers(60000, 140000))) if u < 0.3 else rng.bytes(5))
+            else:
+                out.append(bytes(rng.integers(97, 123, int(rng.integers(8, 41))).astype(np.uint8)))
+        return out
+
+    for kind, n in (("empty_runs", 40000), ("zeros", 30000), ("long", 400), ("huge", 12), ("ascii", 60000)):
+        s = strings(n, kind)
+        img = _plain_chain(s)
+        cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, img)))
+        cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, img[: len(img) * 2 // 3])))
+        cases.append((col, None, (O.DATA_PAGE, max(1, n // 2), W.PLAIN, 0, 0, img)))  # stops early
+        k = int(rng.integers(0, n))
+        cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0,
+                                  _plain_chain(s[:k]) + b"\x00\x00\x00\x80" + _plain_chain(s[k:]))))
+        d = s[: min(n, 3000)]
+        idx = rng.integers(0, len(d), 5000).astype(np.int32)
+        w = max(1, int(len(d) - 1).bit_length())
+        cases.append((col, (len(d), W.PLAIN, _plain_chain(d)),
+                      (O.DATA_PAGE, 5000, W.RLE_DICTIONARY, 0, 0, bytes([w]) + W.hybrid_encode(w, idx))))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors >= 10
