@@ -408,6 +408,41 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
   if (t == 0) b.chunk_bytes[c] = carry;
 }
 
+// Cooperative copy of n bytes by the workgroup: 16-byte aligned stores, each fed by two aligned
+// 16-byte loads of the (arbitrarily aligned) source funnel-shifted into place.  Loads stay inside
+// the source's 16-byte-aligned cover (the payload keeps PQH_PAYLOAD_PAD bytes after the last page).
+__device__ __forceinline__ void block_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const int64_t head = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < n
+                           ? int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) : n;
+  if (int64_t(threadIdx.x) < head) dst[threadIdx.x] = src[threadIdx.x];
+  const int64_t units = (n - head) >> 4;
+  uint8_t* d = dst + head;
+  const uint8_t* sp = src + head;
+  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(sp) & 15);
+  const uint4* sa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(sp) & ~uintptr_t(15));
+  for (int64_t u = threadIdx.x; u < units; u += kBlock) {
+    const uint4 x = sa[u];
+    uint4 y;
+    if (sh == 0) {
+      y = x;
+    } else {
+      const uint4 z = sa[u + 1];
+      const uint32_t w[8] = {x.x, x.y, x.z, x.w, z.x, z.y, z.z, z.w};
+      const uint32_t k = sh >> 2, bs = (sh & 3) * 8;
+      uint32_t o4[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t lo = w[(k + q) & 7], hi = w[(k + q + 1) & 7];  // k + q + 1 <= 7
+        o4[q] = __builtin_amdgcn_alignbit(hi, lo, bs);
+      }
+      y = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    }
+    reinterpret_cast<uint4*>(d)[u] = y;
+  }
+  const int64_t done = head + units * 16;
+  if (int64_t(threadIdx.x) < n - done) dst[done + threadIdx.x] = src[done + threadIdx.x];
+}
+
 // Byte copy of one value (unaligned on both sides; values average tens of bytes).
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len) {
   int64_t k = 0;
@@ -485,9 +520,16 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     } else {  // PLAIN: value i's bytes follow its u32 length
       src = img + S.val_s + 4 * (i + 1) + rel;
     }
-    if (src && l > 0 && o + l <= C.bytes_cap) copy_bytes(C.bytes + o, src, l);
+    if (!is_dlba && src && l > 0 && o + l <= C.bytes_cap) copy_bytes(C.bytes + o, src, l);
     o += l;
     offs[i] = o;
   }
   if (first_bad != INT64_MAX) atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, bad_code));
+  if (is_dlba) {  // the tile's strings are contiguous in the page: one cooperative copy
+    const int64_t rel0 = base - S.byte_base;
+    int64_t len_all = int64_t(tot);
+    if (len_all > data_n - rel0) len_all = data_n - rel0;   // bytes past the page belong to the error
+    if (len_all > C.bytes_cap - base) len_all = C.bytes_cap - base;
+    if (len_all > 0) block_copy(C.bytes + base, img + data_s + rel0, len_all);
+  }
 }
