@@ -54,8 +54,9 @@ struct KernelRun {
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
                               "k_delta_walk", "k_delta_expand", "k_reserved",
                               "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
-                              "k_nest_count", "k_nest_scan", "k_nest_write"};
-constexpr int kNumKernels = 14;
+                              "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
+                              "k_dba_prefix"};
+constexpr int kNumKernels = 16;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -156,6 +157,8 @@ struct pqh_batch {
   int32_t* d_ba_chunks = nullptr;
   int32_t* d_dcum = nullptr;
   int64_t* d_basums = nullptr;
+  int64_t* d_basums2 = nullptr;
+  bool has_dba = false;
   int64_t* d_chunk_bytes = nullptr;
   DevNest* d_nests = nullptr;
   Tile* d_nest_tiles = nullptr;
@@ -373,25 +376,28 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       const bool device_ready = kind == K_PLAIN_FIXED || kind == K_PLAIN_INT96 || kind == K_PLAIN_BOOL ||
                                 kind == K_RLE_BOOL || kind == K_FLBA_NEGATIVE || kind == K_UNSUPPORTED ||
                                 kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DICT || kind == K_PLAIN_BA ||
-                                kind == K_DLBA;
+                                kind == K_DLBA || (kind == K_DBA && C.column.physical_type == PQH_BYTE_ARRAY);
       if (!device_ready) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
       const int64_t n = Q.num_values > 0 ? Q.num_values : 0;
       P.level_base = level_base;
       level_base += n;
       b->bytes_read += Q.image_len;
-      if ((kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DLBA) && P.host_err == kNoError) {
-        // the values decoder is initialised (and may fail) even for pages without values
+      if ((kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DLBA || kind == K_DBA) && P.host_err == kNoError) {
+        // the values decoder is initialised (and may fail) even for pages without values;
+        // DELTA_BYTE_ARRAY: two length streams (prefix, suffix), each with its records and tiles
+        const int streams = kind == K_DBA ? 2 : 1;
         P.dblk_base = int32_t(dblk_cursor);
-        P.dblk_cap = int32_t(ceil_div(n, kDeltaBlockMin) + 1);
+        P.dblk_cap = int32_t(streams * (ceil_div(n, kDeltaBlockMin) + 1));
         dblk_cursor += P.dblk_cap;
         P.dtile_base = int32_t(dtile_cursor);
         P.dtile_n = int32_t(ceil_div(n, kDeltaTile));
-        dtile_cursor += P.dtile_n;
+        dtile_cursor += int64_t(streams) * P.dtile_n;
         b->delta_pages.push_back(p);
-        for (int32_t k = 0; k < P.dtile_n; k++) by_kind[TK_DELTA].push_back(Tile{p, k, TK_DELTA, 1});
-        by_kind[TK_DELTA_SERIAL].push_back(Tile{p, 0, TK_DELTA_SERIAL, 1});
+        for (int st = 0; st < streams; st++)  // Tile.kind = stream (k_delta_expand)
+          for (int32_t k = 0; k < P.dtile_n; k++) by_kind[TK_DELTA].push_back(Tile{p, k, st, 1});
+        if (kind == K_DBA) b->has_dba = true;
       }
-      const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT);
+      const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT || kind == K_DBA);
       if (ba_page && P.host_err == kNoError && n > 0) {
         P.batile_base = int32_t(b->ba_tiles.size());
         P.batile_n = int32_t(ceil_div(n, kBaTile));
@@ -399,7 +405,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         if (kind == K_PLAIN_BA) b->ba_pages.push_back(p);
         // output bytes: at most the page (PLAIN / DELTA_LENGTH); dictionary gathers are estimated
         // from the dictionary page's mean entry and re-sized after the first run if short
-        int64_t est = Q.image_len;
+        int64_t est = kind == K_DBA ? 4 * int64_t(Q.image_len) : Q.image_len;  // prefixes repeat bytes
         if (kind == K_DICT && D.dict_page >= 0) {
           const pqh_page& DQ = pages[D.dict_page];
           const int64_t nv = std::max(1, DQ.num_values);
@@ -471,8 +477,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
     std::stable_sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& c) { return a.first < c.first; });
     for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
-    // serial delta pages (rare geometries) first: they are the longest work items
-    b->expand_tiles.insert(b->expand_tiles.begin(), by_kind[TK_DELTA_SERIAL].begin(), by_kind[TK_DELTA_SERIAL].end());
     b->global_tiles = by_kind[TK_DICT_GLOBAL];
     b->delta_tiles = by_kind[TK_DELTA];
   }
@@ -486,7 +490,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_tiles), sizeof(Tile) * ntiles)) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dtiles), sizeof(Tile) * b->delta_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_delta_pages), sizeof(int32_t) * b->delta_pages.size())) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * size_t(num_pages))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * 2 * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dblocks), sizeof(DeltaBlock) * size_t(dblk_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dflag), sizeof(uint32_t) * size_t(dtile_cursor + 1))) ||
@@ -497,6 +501,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums2), sizeof(int64_t) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
@@ -515,6 +520,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       D.offsets = static_cast<int64_t*>(p);
       if ((rc = dalloc(b, &p, size_t(n) * sizeof(int32_t) + 64))) break;
       D.aux = static_cast<int32_t*>(p);
+      bool dba = false;
+      for (int32_t i = 0; i < D.num_pages; i++) dba = dba || b->hpages[size_t(D.first_page + i)].kind == K_DBA;
+      if (dba) {
+        if ((rc = dalloc(b, &p, size_t(n) * sizeof(int32_t) + 64))) break;
+        D.aux2 = static_cast<int32_t*>(p);
+      }
       D.bytes_cap = bytes_est[size_t(c)];
       if ((rc = dalloc(b, &p, size_t(D.bytes_cap) + 64))) break;
       D.bytes = static_cast<uint8_t*>(p);
@@ -619,7 +630,7 @@ int pqh_batch_run(pqh_batch* b) {
   hipStream_t s = ctx->stream;
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
-             b->d_chunk_bytes, b->d_nests, b->d_nsums};
+             b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2};
   b->synced = false;
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -651,6 +662,8 @@ int pqh_batch_run(pqh_batch* b) {
         return launch_delta_expand(d, b->d_dtiles, ndt, b->d_dflag, b->d_dagg, b->d_dpre, b->d_dflag + ndt, st);
       });
   }
+  if (e == hipSuccess && ndp)  // pages outside the fast-path geometry (most launches exit at once)
+    e = timed(14, ndp, s, [&](hipStream_t st) { return launch_delta_serial(d, b->d_delta_pages, ndp, st); });
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
   if (e == hipSuccess && ne)
     e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
@@ -662,6 +675,8 @@ int pqh_batch_run(pqh_batch* b) {
       e = timed(9, nbc, s, [&](hipStream_t st) { return launch_ba_scan(d, b->d_ba_chunks, nbc, b->d_batiles, st); });
     if (e == hipSuccess)
       e = timed(10, nbt, s, [&](hipStream_t st) { return launch_ba_expand(d, b->d_batiles, nbt, st); });
+    if (e == hipSuccess && b->has_dba)
+      e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });
   }
   const int32_t nnt = int32_t(b->nest_tiles.size()), nns = int32_t(b->nests.size());
   if (e == hipSuccess && nnt) {
@@ -781,6 +796,7 @@ int pqh_batch_sync(pqh_batch* b) {
         break;
       case K_PLAIN_BA:  // walked by k_ba_walk, bytes moved by k_ba_expand
       case K_DLBA:
+      case K_DBA:
         b->k_read[10] += S.val_e - S.val_s;
         break;
       default:

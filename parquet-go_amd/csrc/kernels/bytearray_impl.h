@@ -285,11 +285,18 @@ __device__ __forceinline__ int64_t ba_limit(const DevBatch& b, int page, const D
     const int64_t ei = int64_t((S.err >> 8) & 0xffffffffffffull);
     if (ei < lim) lim = ei;
   }
-  if (P.kind == K_DLBA) {
-    const int64_t dl = b.dstates[page].limit;  // valuesCount of the lengths stream
+  if (P.kind == K_DLBA || P.kind == K_DBA) {  // valuesCount of the (suffix) lengths stream
+    const int64_t dl = b.dstates[P.kind == K_DBA ? b.num_pages + page : page].limit;
     if (dl < lim) lim = dl;
   }
   return lim;
+}
+
+// DELTA_BYTE_ARRAY value i: prefix length (clamped at 0: a negative one adds nothing, and a
+// negative total panics, both checked in k_ba_expand) + suffix length.
+__device__ __forceinline__ int64_t dba_len(const int32_t* plen, const int32_t* slen, int64_t i) {
+  const int32_t p = plen[i];
+  return int64_t(p > 0 ? p : 0) + slen[i];
 }
 
 // Byte-array dictionary of a page: entry count and cumulative-bytes table (nullptr if failed).
@@ -346,19 +353,24 @@ __global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles) {
     const bool is_dict = P.kind == K_DICT;
     const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
     const int32_t* aux = C.aux + S.value_base;
-    int64_t first_neg = INT64_MAX;
+    const bool dba = P.kind == K_DBA;
+    const int32_t* aux2 = dba ? C.aux2 + S.value_base : nullptr;
+    int64_t first_neg = INT64_MAX, s2 = 0;
     for (int64_t i = v0 + threadIdx.x; i < v1; i += kBlock) {
-      const int64_t l = ba_len(d, is_dict, aux[i]);
+      const int64_t l = ba_len(d, is_dict, aux[i]);  // DELTA_BYTE_ARRAY: the suffix length
       if (l < 0) {
         if (i < first_neg) first_neg = i;
       } else {
-        s += l;
+        s += dba ? dba_len(aux2, aux, i) : l;
+        s2 += l;
       }
     }
-    if (P.kind == K_DLBA) {
+    s2 = block_sum64(dba ? s2 : 0, wsum);
+    if (threadIdx.x == 0) b.basums2[P.batile_base + t.k] = s2;
+    if (P.kind == K_DLBA || dba) {
       if (first_neg != INT64_MAX)  // make([]byte, negative) panics (re-panicked, file_reader.go:179-181)
         atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_neg, PQH_ERR_NEGATIVE_DLBA_LENGTH));
-      const int64_t vc = b.dstates[t.page].limit;
+      const int64_t vc = b.dstates[dba ? b.num_pages + t.page : t.page].limit;
       if (t.k == 0 && threadIdx.x == 0 && S.nn > vc)  // lens exhausted: io.EOF (type_bytearray.go:118-121)
         atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
     }
@@ -372,20 +384,14 @@ __global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles) {
 // chunk are contiguous and in page order) -> each tile's first output offset, each page's first
 // byte (byte_base), the chunk's byte total.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_chunks, const Tile* tiles) {
-  __shared__ int64_t wsum[4];
-  __shared__ int64_t carry;
-  const int c = ba_chunks[blockIdx.x];
-  const DevChunk C = b.chunks[c];
+__device__ int64_t chunk_scan(int64_t* sums, int32_t n, const Tile* tiles, PageState* states, int64_t* wsum,
+                              int64_t& carry) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t == 0) {
-    carry = 0;
-    if (C.offsets) C.offsets[0] = 0;
-  }
+  if (t == 0) carry = 0;
   __syncthreads();
-  for (int base = 0; base < C.batile_n; base += kBlock) {
+  for (int base = 0; base < n; base += kBlock) {
     const int i = base + t;
-    const int64_t x = i < C.batile_n ? b.basums[C.batile_base + i] : 0;
+    const int64_t x = i < n ? sums[i] : 0;
     int64_t incl = x;
     for (int off = 1; off < 64; off <<= 1) {
       const int64_t y = __shfl_up(incl, off, 64);
@@ -395,17 +401,27 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
     __syncthreads();
     int64_t before = carry;
     for (int k = 0; k < wv; k++) before += wsum[k];
-    if (i < C.batile_n) {
+    if (i < n) {
       const int64_t start = before + incl - x;
-      b.basums[C.batile_base + i] = start;
-      const Tile tt = tiles[C.batile_base + i];
-      if (tt.k == 0) b.states[tt.page].byte_base = start;
+      sums[i] = start;
+      if (states && tiles[i].k == 0) states[tiles[i].page].byte_base = start;
     }
     __syncthreads();
     if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }
-  if (t == 0) b.chunk_bytes[c] = carry;
+  return carry;
+}
+
+__global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_chunks, const Tile* tiles) {
+  __shared__ int64_t wsum[4];
+  __shared__ int64_t carry;
+  const int c = ba_chunks[blockIdx.x];
+  const DevChunk C = b.chunks[c];
+  if (threadIdx.x == 0 && C.offsets) C.offsets[0] = 0;
+  const int64_t total = chunk_scan(b.basums + C.batile_base, C.batile_n, tiles + C.batile_base, b.states, wsum, carry);
+  if (C.aux2) chunk_scan(b.basums2 + C.batile_base, C.batile_n, tiles + C.batile_base, nullptr, wsum, carry);
+  if (threadIdx.x == 0) b.chunk_bytes[c] = total;
 }
 
 // Cooperative copy of n bytes by the workgroup: 16-byte aligned stores, each fed by two aligned
@@ -444,6 +460,106 @@ __device__ __forceinline__ void block_copy(uint8_t* dst, const uint8_t* src, int
 }
 
 // Byte copy of one value (unaligned on both sides; values average tens of bytes).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len);
+
+// DELTA_BYTE_ARRAY tile (byteArrayDeltaDecoder.decodeValues, type_bytearray.go:213-240): offsets
+// from prefix + suffix lengths, the per-value checks in the reference's order (suffix read short,
+// negative total, prefix longer than the previous value), and each suffix copied into place after
+// its prefix; the prefixes themselves are filled by k_dba_prefix once every suffix is written.
+__device__ void dba_expand(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S, const DevChunk& C,
+                           int64_t v0, int64_t v1, uint64_t* wsum) {
+  const int32_t* slen = C.aux + S.value_base;
+  const int32_t* plen = C.aux2 + S.value_base;
+  const int64_t i0 = v0 + 8 * int64_t(threadIdx.x);
+  int64_t L[8], sl[8], ssum = 0, lsum = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const bool in = i0 + j < v1;
+    sl[j] = in ? slen[i0 + j] : 0;
+    L[j] = in ? dba_len(plen, slen, i0 + j) : 0;
+    ssum += sl[j];
+    lsum += L[j];
+  }
+  uint64_t tot, stot;
+  const int64_t excl = int64_t(block_exclusive_scan(uint64_t(lsum), wsum, &tot));
+  const int64_t sexcl = int64_t(block_exclusive_scan(uint64_t(ssum), wsum, &stot));
+  const int64_t base = b.basums[P.batile_base + t.k];
+  const int64_t sbase = b.basums2[P.batile_base + t.k] - b.basums2[P.batile_base];  // page-relative suffix bytes
+  const DeltaState D1 = b.dstates[b.num_pages + t.page];
+  const uint8_t* data = b.payload + P.image_off + D1.end_pos;  // suffix bytes follow the two length streams
+  const int64_t data_n = S.val_e - D1.end_pos;
+  int64_t* offs = C.offsets + S.value_base + 1;
+  int64_t o = base + excl, sr = sbase + sexcl;
+  int64_t prev_len = i0 > 0 && i0 < v1 ? dba_len(plen, slen, i0 - 1) : 0;  // previousValue starts empty
+  int64_t first_bad = INT64_MAX;
+  int bad_code = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t i = i0 + j;
+    if (i >= v1) break;
+    const int32_t p = plen[i];
+    int code = PQH_OK;
+    if (sl[j] > 0 && data_n - sr < sl[j]) code = data_n - sr <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
+    else if (int64_t(p) + sl[j] < 0) code = PQH_ERR_NEGATIVE_DLBA_LENGTH;
+    else if (prev_len < p) code = PQH_ERR_DBA_PREFIX;
+    if (code != PQH_OK && i < first_bad) {
+      first_bad = i;
+      bad_code = code;
+    }
+    const int64_t pp = p > 0 ? p : 0;
+    if (code == PQH_OK && sl[j] > 0 && o + L[j] <= C.bytes_cap) copy_bytes(C.bytes + o + pp, data + sr, sl[j]);
+    o += L[j];
+    offs[i] = o;
+    sr += sl[j];
+    prev_len = L[j];
+  }
+  if (first_bad != INT64_MAX) atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, bad_code));
+}
+
+__global__ __launch_bounds__(256) void k_dba_expand(DevBatch b, const Tile* tiles) {
+  __shared__ uint64_t wsum[4];
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  if (P.kind != K_DBA) return;
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const int64_t lim = ba_limit(b, t.page, P, S);
+  const int64_t v0 = int64_t(t.k) * kBaTile;
+  const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
+  if (v0 >= v1) return;
+  dba_expand(b, t, P, S, C, v0, v1, wsum);
+}
+
+// k_dba_prefix: value i's first plen_i bytes equal the previous value's (type_bytearray.go:229-231),
+// hence, going back, the suffix bytes of the nearest earlier values whose prefix is shorter:
+// byte k of value i is byte k of value m, m = the last j <= i with max(plen_j, 0) <= k, and that
+// byte lies in m's suffix, already in place.  Every byte is copied straight from its source.
+__global__ __launch_bounds__(256) void k_dba_prefix(DevBatch b, const Tile* tiles) {
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  if (P.kind != K_DBA) return;
+  const PageState S = b.states[t.page];
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const int64_t lim = ba_limit(b, t.page, P, S);
+  const int64_t v0 = int64_t(t.k) * kBaTile;
+  const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
+  const int32_t* plen = C.aux2 + S.value_base;
+  const int64_t* off = C.offsets + S.value_base;  // off[i] = first byte of value i
+  for (int64_t i = v0 + threadIdx.x; i < v1; i += kBlock) {
+    int64_t hi = plen[i];
+    const int64_t oi = off[i];
+    if (hi <= 0 || oi + hi > C.bytes_cap) continue;
+    for (int64_t j = i - 1; j >= 0 && hi > 0; j--) {
+      const int64_t pj = plen[j] > 0 ? plen[j] : 0;
+      if (pj < hi) {  // bytes [pj, hi) of value j are its own suffix bytes
+        copy_bytes(C.bytes + oi + pj, C.bytes + off[j] + pj, hi - pj);
+        hi = pj;
+      }
+    }
+  }
+}
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len) {
   int64_t k = 0;
   for (; k + 8 <= len; k += 8) {
@@ -471,10 +587,11 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
   const int64_t v0 = int64_t(t.k) * kBaTile;
   const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
   if (v0 >= v1) return;
-  const bool is_dict = P.kind == K_DICT, is_dlba = P.kind == K_DLBA;
+  const bool is_dict = P.kind == K_DICT, is_dlba = P.kind == K_DLBA, is_dba = P.kind == K_DBA;
   const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
   const int32_t* aux = C.aux + S.value_base;
   const int64_t i0 = v0 + 8 * int64_t(threadIdx.x);
+  if (is_dba) return;  // k_dba_expand
   int64_t len[8];
   int32_t a[8];
   int64_t tsum = 0;

@@ -81,7 +81,8 @@ struct DevChunk {
   uint8_t* rep_levels;
   int64_t values_cap;    // values capacity (elements)
   int64_t bytes_cap;
-  int32_t* aux;          // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH) or dictionary key
+  int32_t* aux;          // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH / suffix) or dictionary key
+  int32_t* aux2;         // DELTA_BYTE_ARRAY: per value slot, prefix length
   int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
   int32_t batile_n;
 };
@@ -112,7 +113,11 @@ struct DeltaState {
   int32_t limit;          // values decodable before the first error (<= notNull)
   uint64_t first;         // first value (bits; int32 pages sign-extended)
   int64_t end_pos;        // reader position (image offset) after the walk
+  int32_t rec_base;       // first DeltaBlock of this stream within the page's records
+  int32_t pad;
 };
+// DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
+// DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).
 
 // One block: header already parsed; data of miniblock m starts at data_off + sum_{j<m} mbvc/8*w_j.
 struct DeltaBlock {

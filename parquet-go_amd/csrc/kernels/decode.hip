@@ -915,7 +915,6 @@ __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
     case TK_BOOL: tile_bool_plain(b, t); break;
     case TK_DICT: tile_dict<true>(b, t, L, stage, dict_lds); break;
     case TK_RLE_BOOL: tile_rle_bool(b, t, L, stage); break;
-    case TK_DELTA_SERIAL: delta_serial(b, t); break;
     default: break;
   }
 }
@@ -961,6 +960,12 @@ hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, 
   return hipGetLastError();
 }
 
+hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_serial, dim3(n), dim3(64), 0, s, b, delta_pages);
+  return hipGetLastError();
+}
+
 hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ba_walk, dim3(n), dim3(256), 0, s, b, ba_pages, n);
@@ -1000,6 +1005,13 @@ hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s)
 hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_nest_write, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_dba_prefix(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dba_expand, dim3(n), dim3(256), 0, s, b, tiles);
+  hipLaunchKernelGGL(k_dba_prefix, dim3(n), dim3(256), 0, s, b, tiles);
   return hipGetLastError();
 }
 

@@ -169,6 +169,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   D.limit = 0;
   D.first = 0;
   D.end_pos = vs;
+  D.rec_base = 0;
+  D.pad = 0;
   int64_t pos = vs;
   int st;
   // ---- init (page load, phase 0 step 3): readBlockHeader + readMiniBlockHeader ----
@@ -274,23 +276,40 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   const int p = delta_pages[idx];
   const DevPage P = b.pages[p];
   const PageState S = b.states[p];
-  DeltaState D;
-  D.mode = DM_NONE;
-  D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = 0;
+  DeltaState D, D1;
+  D.mode = D1.mode = DM_NONE;
+  D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.pad = 0;
   D.first = 0;
   D.end_pos = 0;
+  D1 = D;
   uint64_t err = kNoError;
+  const bool dba = P.kind == K_DBA;
   // A page whose earlier load steps failed never initialises its values decoder.
   const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
   if (P.host_err == kNoError && load_ok) {
     Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
     win_load(w, S.val_s, lane);
     const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
-    err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn,
-                     b.dblocks + P.dblk_base, P.dblk_cap, D, lane, P.kind == K_DLBA);
+    DeltaBlock* recs = b.dblocks + P.dblk_base;
+    err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn, recs, P.dblk_cap, D, lane,
+                     P.kind == K_DLBA || dba);
+    if (dba && err == kNoError) {
+      // byteArrayDeltaDecoder.init (type_bytearray.go:195-211): prefix lengths, then the
+      // DELTA_LENGTH suffix decoder on the rest; both decode every length at load
+      if (D.mode == DM_FAST) {
+        err = delta_walk(w, D.end_pos, false, 0, recs + D.nblocks, P.dblk_cap - D.nblocks, D1, lane, true);
+        D1.rec_base = D.nblocks;
+        if (err == kNoError && D1.mode == DM_FAST && D.limit != D1.limit)
+          err = err_key(0, 3, PQH_ERR_DBA_COUNT);
+        if (D1.mode == DM_SERIAL) D.mode = DM_SERIAL;  // the serial tile redoes both streams
+      } else {
+        D1.mode = DM_SERIAL;
+      }
+    }
   }
   if (lane == 0) {
     b.dstates[p] = D;
+    if (dba) b.dstates[b.num_pages + p] = D1;
     if (err != kNoError) atomicMin(&b.states[p].err, (unsigned long long)err);
   }
 }
@@ -342,7 +361,7 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
   constexpr int VPT = IS64 ? 4 : 8;
   constexpr int SUB = kBlock * VPT;
   const uint8_t* img = b.payload + P.image_off;
-  const DeltaBlock* recs = b.dblocks + P.dblk_base;
+  const DeltaBlock* recs = b.dblocks + P.dblk_base + D.rec_base;
   const int bs = D.block_size, mbvc = D.mbvc, mbc = D.mb_count;
   uint64_t carry = base, total_all = 0;
   for (int64_t c0 = v0; c0 < v1; c0 += SUB) {
@@ -456,10 +475,11 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   const Tile t = tiles[s_ticket];
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
-  const DeltaState D = b.dstates[t.page];
+  const int stream = t.kind;  // DELTA_BYTE_ARRAY: 0 prefix lengths, 1 suffix lengths
+  const DeltaState D = b.dstates[stream ? b.num_pages + t.page : t.page];
   // every tile of a page sees the same page verdict, so no tile waits on a tile that skipped
   if (page_failed_before_values(S) || D.mode != DM_FAST) return;
-  const bool dlba = P.kind == K_DLBA;
+  const bool dlba = P.kind == K_DLBA || P.kind == K_DBA;  // int32 lengths into aux / aux2
   const int64_t v0 = int64_t(t.k) * kDeltaTile;
   int64_t v1 = v0 + kDeltaTile;
   if (v1 > D.limit) v1 = D.limit;
@@ -468,7 +488,7 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   const bool is64 = P.kind == K_DELTA64;
   const uint64_t agg = is64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, stage, DL)
                             : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, stage, DL);
-  const int64_t me = int64_t(P.dtile_base) + t.k;
+  const int64_t me = int64_t(P.dtile_base) + int64_t(stream) * P.dtile_n + t.k;
   if (threadIdx.x == 0) {
     uint64_t base;
     if (t.k == 0) {
@@ -492,30 +512,18 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   }
   __syncthreads();
   const DevChunk C = b.chunks[P.chunk];
-  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(C.aux + S.value_base) : C.values + S.value_base * P.value_size;
+  int32_t* lens = P.kind == K_DBA && stream == 0 ? C.aux2 : C.aux;
+  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(lens + S.value_base) : C.values + S.value_base * P.value_size;
   if (is64) delta_tile<true>(b, P, D, v0, v1, s_base, true, out, stage, DL);
   else delta_tile<false>(b, P, D, v0, v1, s_base, true, out, stage, DL);
 }
 
-// TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.next for streams outside
-// the fast-path geometry.  One thread; the rest of the workgroup idles (rare layouts only).
-// DELTA_LENGTH_BYTE_ARRAY pages decode all valuesCount lengths at init (errors are load errors),
-// keep the first notNull of them and record where the string bytes start.
-__device__ void delta_serial(const DevBatch& b, const Tile& t) {
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
-  const DeltaState D0 = b.dstates[t.page];
-  if (D0.mode != DM_SERIAL || threadIdx.x != 0) return;
-  const uint8_t* img = b.payload + P.image_off;
-  const int64_t e = S.val_e;
-  const bool is64 = P.kind == K_DELTA64;
-  const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
-  const bool dlba = P.kind == K_DLBA;
-  const int64_t nvals = before_values ? 0 : S.nn;  // values the page keeps
-  int64_t nn = nvals;
-  const DevChunk C = b.chunks[P.chunk];
-  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(C.aux + S.value_base) : C.values + S.value_base * P.value_size;
-  int64_t pos = S.val_s;
+// TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.init + next for streams
+// outside the fast-path geometry.  One thread; the rest of the workgroup idles (rare layouts only).
+// init_all (DELTA_LENGTH / DELTA_BYTE_ARRAY lengths): all valuesCount values are decoded at load and
+// every error is a load error; the first `nvals` values are kept.  Returns the first error key.
+__device__ uint64_t serial_stream(const uint8_t* img, int64_t& pos, int64_t e, bool is64, uint8_t* out,
+                                  int64_t nvals, bool init_all, int32_t& vc_out) {
   auto uvar = [&](uint64_t& v) { return read_uvarint(img, pos, e, v); };
   auto uvar32 = [&](int32_t& o) {
     uint64_t v;
@@ -538,20 +546,18 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
     if (nbytes <= 0) return;
     pos = pos + nbytes < e ? pos + nbytes : (pos > e ? pos : e);
   };
-  uint64_t err = kNoError;
   int32_t bs = 0, mbc = 0, vc = 0, mbvc = 0;
   uint64_t prev = 0, md = 0;
   int64_t widths_pos = 0;  // widths live in the image at widths_pos (mbc bytes)
   int st;
-  // ---- init ----
-  if ((st = uvar32(bs)) || (st = uvar32(mbc))) err = err_key(0, 3, st);
-  if (err == kNoError && (mbc <= 0 || bs % mbc != 0)) err = err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
-  if (err == kNoError) {
-    mbvc = bs / mbc;
-    if (mbvc == 0) err = err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
-  }
-  if (err == kNoError && (st = uvar32(vc))) err = err_key(0, 3, st);
-  if (err == kNoError && (st = var(prev))) err = err_key(0, 3, st);
+  vc_out = 0;
+  // ---- init: readBlockHeader + readMiniBlockHeader (deltabp_decoder.go:37-111) ----
+  if ((st = uvar32(bs)) || (st = uvar32(mbc))) return err_key(0, 3, st);
+  if (mbc <= 0 || bs % mbc != 0) return err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  mbvc = bs / mbc;
+  if (mbvc == 0) return err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
+  if ((st = uvar32(vc))) return err_key(0, 3, st);
+  if ((st = var(prev))) return err_key(0, 3, st);
   auto mini_header = [&]() -> int {
     int s2 = var(md);
     if (s2) return s2;
@@ -567,24 +573,19 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
     pos += mbc;
     return PQH_OK;
   };
-  if (err == kNoError && (st = mini_header())) err = err_key(0, 3, st);
-  // ---- next() x nn ----
-  if (dlba) nn = vc;
-  auto verr = [&](int64_t position, int code) { return dlba ? err_key(0, 3, code) : err_key(3, position, code); };
+  if ((st = mini_header())) return err_key(0, 3, st);
+  vc_out = vc;
+  // ---- next() x nn (deltabp_decoder.go:113-170) ----
+  const int64_t nn = init_all ? vc : nvals;
+  auto verr = [&](int64_t position, int code) { return init_all ? err_key(0, 3, code) : err_key(3, position, code); };
   int32_t cur_mb = 0, cur_w = 0, mb_pos = 0;
   int64_t gpos = 0;  // byte offset of the current group of 8 deltas
-  for (int64_t position = 0; err == kNoError && position < nn; position++) {
-    if (position >= vc) {
-      err = err_key(3, position, PQH_ERR_EOF);
-      break;
-    }
+  for (int64_t position = 0; position < nn; position++) {
+    if (position >= vc) return err_key(3, position, PQH_ERR_EOF);
     if (position % 8 == 0) {
       if (position % mbvc == 0) {
         if (cur_mb >= mbc) {
-          if ((st = mini_header())) {
-            err = verr(position, st);
-            break;
-          }
+          if ((st = mini_header())) return verr(position, st);
           cur_mb = 0;
         }
         cur_w = img[widths_pos + cur_mb];
@@ -594,20 +595,14 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
       const int32_t w = cur_w;
       if (w > 0) {
         const int64_t avail = e - pos;
-        if (avail < w) {
-          err = verr(position, avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
-          break;
-        }
+        if (avail < w) return verr(position, avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
       }
       gpos = pos;
       pos += w;
       mb_pos += w;
       if (position + 8 >= vc) {
         const int64_t l = int64_t(mbvc / 8) * w - mb_pos;
-        if (l < 0) {
-          err = verr(position, PQH_ERR_DELTA_STREAM);
-          break;
-        }
+        if (l < 0) return verr(position, PQH_ERR_DELTA_STREAM);
         read_full_skip(l);
         for (int32_t i = cur_mb; i < mbc; i++) {
           const int32_t w2 = img[widths_pos + cur_mb];
@@ -615,8 +610,10 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
         }
       }
     }
-    if (is64) reinterpret_cast<uint64_t*>(out)[position] = prev;
-    else if (position < nvals) reinterpret_cast<uint32_t*>(out)[position] = uint32_t(prev);
+    if (position < nvals) {
+      if (is64) reinterpret_cast<uint64_t*>(out)[position] = prev;
+      else reinterpret_cast<uint32_t*>(out)[position] = uint32_t(prev);
+    }
     uint64_t delta = 0;  // unpack8 (LSB first) of this position's w bits
     for (int k2 = 0; k2 < cur_w; k2++) {
       const int64_t bit = int64_t(position % 8) * cur_w + k2;
@@ -624,9 +621,41 @@ __device__ void delta_serial(const DevBatch& b, const Tile& t) {
     }
     prev += delta + md;
   }
-  if (dlba) {
+  return kNoError;
+}
+
+// k_delta_serial: one wave per delta page; pages the walk marked DM_SERIAL are decoded by lane 0:
+// plain delta values, DELTA_LENGTH lengths, or both DELTA_BYTE_ARRAY length streams (then the
+// count check of type_bytearray.go:206-208).
+__global__ __launch_bounds__(64) void k_delta_serial(DevBatch b, const int32_t* delta_pages) {
+  const Tile t{delta_pages[blockIdx.x], 0, TK_DELTA_SERIAL, 1};
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  const DeltaState D0 = b.dstates[t.page];
+  if (D0.mode != DM_SERIAL || threadIdx.x != 0) return;
+  const uint8_t* img = b.payload + P.image_off;
+  const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+  const int64_t nvals = before_values ? 0 : S.nn;
+  const DevChunk C = b.chunks[P.chunk];
+  int64_t pos = S.val_s;
+  int32_t vc = 0;
+  uint64_t err;
+  if (P.kind == K_DLBA) {
+    err = serial_stream(img, pos, S.val_e, false, reinterpret_cast<uint8_t*>(C.aux + S.value_base), nvals, true, vc);
     b.dstates[t.page].end_pos = pos;
     b.dstates[t.page].limit = err == kNoError ? vc : 0;
+  } else if (P.kind == K_DBA) {
+    err = serial_stream(img, pos, S.val_e, false, reinterpret_cast<uint8_t*>(C.aux2 + S.value_base), nvals, true, vc);
+    int32_t vc1 = 0;
+    if (err == kNoError) {
+      err = serial_stream(img, pos, S.val_e, false, reinterpret_cast<uint8_t*>(C.aux + S.value_base), nvals, true, vc1);
+      if (err == kNoError && vc != vc1) err = err_key(0, 3, PQH_ERR_DBA_COUNT);
+    }
+    b.dstates[t.page].limit = err == kNoError ? vc : 0;
+    b.dstates[b.num_pages + t.page].end_pos = pos;
+    b.dstates[b.num_pages + t.page].limit = err == kNoError ? vc1 : 0;
+  } else {
+    err = serial_stream(img, pos, S.val_e, P.kind == K_DELTA64, C.values + S.value_base * P.value_size, nvals, false, vc);
   }
   if (err != kNoError) atomicMin(&b.states[t.page].err, (unsigned long long)err);
 }

@@ -23,6 +23,7 @@ struct DevBatch {
   int64_t* chunk_bytes;  // per chunk: total string bytes (k_ba_scan)
   const DevNest* nests;  // repeated chunks with nesting outputs
   int64_t* nsums;        // per nest tile: kNestFlags counts, then (after k_nest_scan) bases
+  int64_t* basums2;      // DELTA_BYTE_ARRAY: per tile suffix-byte sum, then its first suffix byte
 };
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
@@ -42,10 +43,14 @@ hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n,
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// DELTA_BYTE_ARRAY: every value's shared prefix copied from the suffixes of earlier values.
+hipError_t launch_dba_prefix(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Nesting (levels -> list offsets / presence / leaf validity): counts, per-chunk scan, write.
 hipError_t launch_nest_count(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s);
 hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// Delta pages outside the fast-path geometry (exact sequential decode, one wave per delta page).
+hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.
 hipError_t launch_dict_global(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 

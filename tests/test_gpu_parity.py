@@ -489,3 +489,55 @@ def test_plain_chain_layouts(pq, ctx):
                       (O.DATA_PAGE, 5000, W.RLE_DICTIONARY, 0, 0, bytes([w]) + W.hybrid_encode(w, idx))))
     compared, errors = _run_cases(pq, ctx, cases)
     assert compared == len(cases) and errors >= 10
+
+
+def _dba_page(strs, total=None, plens=None, slens=None, geom=(128, 4)):
+    """DELTA_BYTE_ARRAY image: prefix lengths, suffix lengths (DELTA_BINARY_PACKED), suffixes."""
+    import delta_streams as DS
+    pl, sl, data, prev = [], [], [], b""
+    for x in strs:
+        p = 0
+        while p < len(prev) and p < len(x) and prev[p] == x[p]:
+            p += 1
+        pl.append(p)
+        sl.append(len(x) - p)
+        data.append(x[p:])
+        prev = x
+    pl = plens if plens is not None else pl
+    sl = slens if slens is not None else sl
+    return (DS.encode(pl, 32, geom[0], geom[1], "omit", total=total) +
+            DS.encode(sl, 32, geom[0], geom[1], "omit") + b"".join(data))
+
+
+def test_delta_byte_array_pages(pq, ctx):
+    """DELTA_BYTE_ARRAY (type_bytearray.go:189-240): sorted and random strings, long shared
+    prefixes, every error of decodeValues in the reference's order, count mismatch at init."""
+    W = fixtures.W
+    rng = np.random.default_rng(44)
+    col = (W.BYTE_ARRAY, 0, 0, 0)
+    cases = []
+    for n in (1, 2, 9, 300, 4097, 20000):
+        base = [bytes(rng.integers(97, 100, int(rng.integers(0, 30))).astype(np.uint8)) for _ in range(n)]
+        for strs in (sorted(base), base, [b"common/prefix/" * 3 + x for x in sorted(base)]):
+            img = _dba_page(strs)
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, img)))
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, img[: int(rng.integers(0, len(img)))])))
+            cases.append((col, None, (O.DATA_PAGE, n + 2, W.DELTA_BYTE_ARRAY, 0, 0, img)))
+        if n > 3:
+            strs = sorted(base)
+            k = int(rng.integers(1, n))
+            pl = [0] * n
+            pl[k] = 1000  # longer than the previous value
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, plens=pl))))
+            sl = [len(x) for x in strs]
+            sl[k] = -3
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0,
+                                      _dba_page(strs, plens=[0] * n, slens=sl))))
+            pl = [0] * n
+            pl[k] = -50  # negative total
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0,
+                                      _dba_page(strs, plens=pl, slens=[len(x) for x in strs]))))
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, total=n + 1))))
+            cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, geom=(96, 3)))))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors > 15
