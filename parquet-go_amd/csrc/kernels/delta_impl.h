@@ -498,8 +498,14 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
       base = 0;
       for (int64_t j = me - 1;; j--) {
         uint32_t f;
-        while ((f = __hip_atomic_load(lb.flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+        uint32_t spins = 0;  // a predecessor always publishes; the bound only guards against a hang
+        while ((f = __hip_atomic_load(lb.flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
+               ++spins < (1u << 26))
           __builtin_amdgcn_s_sleep(1);
+        if (f == 0u) {
+          atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, v0, PQH_ERR_HIP));
+          break;
+        }
         if (f == 2u) {
           base += __hip_atomic_load(lb.pre + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
