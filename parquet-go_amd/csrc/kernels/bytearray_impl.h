@@ -18,8 +18,8 @@
 // ------------------------------------------------------------------------------------------------
 // k_ba_walk: one workgroup per PLAIN byte-array page (data pages and byte-array dictionary pages).
 // The chain [u32 len][len bytes] (byteArrayPlainDecoder.next, type_bytearray.go:24-45) is sequential
-// by definition; it is resolved in parallel and exactly, 64 KiB window by window:
-//   1. each thread owns a 256-byte segment and walks it from a SPECULATIVE start (the first offset
+// by definition; it is resolved in parallel and exactly, 63 KiB window by window:
+//   1. each thread owns a 252-byte segment and walks it from a SPECULATIVE start (the first offset
 //      whose length field describes a record inside the stream; segment 0 starts at the known
 //      entry), marking the record starts it visits in a 256-bit mask;
 //   2. the true entry of segment j is the exit of segment j-1.  Segment j is right when that entry
@@ -30,9 +30,11 @@
 //      page -> aux) or cumulative offsets (dictionary page -> dcum); the first invalid record on the
 //      true chain (short length, negative length, short data) is the page's error.
 // ------------------------------------------------------------------------------------------------
-constexpr int kChainWin = 65536;
-constexpr int kChainSeg = kChainWin / kBlock;  // 256 bytes per thread
-constexpr int kChainWords = kChainSeg / 64;     // mask words per segment
+// 252-byte segments: neighbouring lanes' segments start 63 dwords apart, so their LDS reads fall in
+// different banks (a power-of-two stride would put a whole wave on one bank)
+constexpr int kChainSeg = 252;
+constexpr int kChainWin = kChainSeg * kBlock;      // 64512 bytes per window
+constexpr int kChainWords = (kChainSeg + 63) / 64; // mask words per segment
 
 struct ChainLds {
   uint32_t win[(kChainWin + 64) / 4];

@@ -377,6 +377,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
             case K_DELTA32:
             case K_DELTA64:  // init + block walk in k_delta_walk (atomicMin into the same key)
             case K_DLBA:     // lengths: k_delta_walk; bytes: k_ba_expand
+            case K_DBA:      // prefix + suffix lengths: k_delta_walk; bytes: k_dba_expand / k_dba_prefix
             case K_PLAIN_BA: // the [u32 len][bytes] chain: k_ba_walk
               break;
             case K_FLBA_NEGATIVE:

@@ -110,11 +110,17 @@ __device__ __forceinline__ int win_miniblock_header(Win& w, int64_t& pos, bool i
 
 __device__ __forceinline__ int mb_width(uint64_t widths, int m) { return int((widths >> (8 * m)) & 0xff); }
 
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  return uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x))))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x >> 32))))) << 32);
+}
+
 // Bytes [pos, pos + 16) of the window as two little-endian words (window holds pos + 24).
 __device__ __forceinline__ void win_bytes16(const Win& w, int64_t pos, uint64_t& a, uint64_t& b) {
   const int64_t off = pos - w.lo;
   const uint64_t* q = reinterpret_cast<const uint64_t*>(w.buf) + (off >> 3);
-  const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
+  // the walk is wave-uniform: move the words to SGPRs so the header arithmetic runs on the SALU
+  const uint64_t x0 = rfl64(q[0]), x1 = rfl64(q[1]), x2 = rfl64(q[2]);
   const int sh = int(off & 7) * 8;
   a = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
   b = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
@@ -465,8 +471,78 @@ __device__ __forceinline__ void lb_publish(uint64_t* slot, uint32_t* flag, uint6
   __hip_atomic_store(flag, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Whole-tile staging (the common case: a tile's packed deltas fit kTileStage bytes): the block
+// table of the tile's <= 64 blocks and all of its bytes are loaded once; both phases read LDS only.
+// Values are assigned in rows of 256 consecutive positions (thread t owns position row*256 + t), so
+// every store is coalesced; each row is one block-wide scan.  Block and miniblock sizes are powers
+// of two on the fast path (the block size divides 2048, the miniblock count divides it).
+constexpr int kTileStage = 32768;
+constexpr int kTileBlocks = kDeltaTile / kDeltaBlockMin;  // 64
+
+struct TileStageLds {
+  uint32_t data[(kTileStage + 64) / 4];
+  int32_t mbbit[kTileBlocks][8];  // first bit of each miniblock's data in `data`
+  uint8_t mbw[kTileBlocks][8];
+  uint64_t md[kTileBlocks];
+  uint64_t wtot[2][4];
+  int32_t fits;
+  int32_t pad;
+};
+
+// Stage the tile; returns false (uniformly) when its bytes exceed kTileStage.
+__device__ bool stage_tile(const DevBatch& b, const DevPage& P, const DeltaState& D, int64_t v0, int64_t v1,
+                           TileStageLds& T) {
+  const uint8_t* img = b.payload + P.image_off;
+  const DeltaBlock* recs = b.dblocks + P.dblk_base + D.rec_base;
+  const int lbs = __builtin_ctz(uint32_t(D.block_size));
+  const int bb0 = int(v0 >> lbs), nb = int(((v1 - 1) >> lbs)) - bb0 + 1;
+  const int mbc = D.mb_count, gbytes = D.mbvc / 8;
+  __shared__ int64_t s_start, s_end;
+  if (threadIdx.x < nb) {
+    const DeltaBlock r = recs[bb0 + threadIdx.x];
+    int32_t off = r.data_off;
+    for (int m = 0; m < 8; m++) {
+      const int wm = m < mbc ? mb_width(r.widths, m) : 0;
+      T.mbbit[threadIdx.x][m] = off;  // byte offset for now
+      T.mbw[threadIdx.x][m] = uint8_t(wm);
+      off += gbytes * wm;
+    }
+    T.md[threadIdx.x] = r.min_delta;
+    if (threadIdx.x == 0) s_start = r.data_off;
+    if (threadIdx.x == nb - 1) s_end = off;
+  }
+  __syncthreads();
+  const int64_t start = s_start, end = s_end;
+  const int64_t a0 = start - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(start)) & 15);
+  const int64_t nvec = (end - a0 + 15) >> 4;
+  if (nvec * 16 > kTileStage) return false;
+  if (threadIdx.x < nb)
+    for (int m = 0; m < 8; m++) T.mbbit[threadIdx.x][m] = int32_t(T.mbbit[threadIdx.x][m] - a0) * 8;
+  const int64_t e = P.image_len;
+  for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
+    const int64_t o = a0 + k * 16;
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
+    reinterpret_cast<uint4*>(T.data)[k] = x;
+  }
+  if (threadIdx.x < 4) T.data[nvec * 4 + threadIdx.x] = 0;
+  __syncthreads();
+  return true;
+}
+
+// delta(p) + minDelta of the staged tile (p relative to the page).
+__device__ __forceinline__ uint64_t staged_delta(const TileStageLds& T, int64_t p, int bb0, int lbs, int lmb) {
+  const int32_t q = int32_t(p);
+  const int blk = (q >> lbs) - bb0;
+  const int r = q & ((1 << lbs) - 1);
+  const int m = r >> lmb;
+  const int wm = T.mbw[blk][m];
+  const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
+  return extract64(T.data, bit, wm) + T.md[blk];
+}
+
 __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles, DeltaLookback lb) {
-  __shared__ __attribute__((aligned(16))) uint32_t stage[(kStageBytes + 32) / 4];
+  __shared__ TileStageLds T;
   __shared__ DeltaLds DL;
   __shared__ int32_t s_ticket;
   __shared__ uint64_t s_base;
@@ -486,8 +562,23 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   if (dlba && v1 > S.nn) v1 = S.nn;
   if (v0 >= v1) return;  // so is every later tile of the page
   const bool is64 = P.kind == K_DELTA64;
-  const uint64_t agg = is64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, stage, DL)
-                            : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, stage, DL);
+  const int lbs = __builtin_ctz(uint32_t(D.block_size)), lmb = __builtin_ctz(uint32_t(D.mbvc));
+  const int bb0 = int(v0 >> lbs);
+  const bool fits = stage_tile(b, P, D, v0, v1, T);
+  // phase A: the tile's aggregate (sum of delta + minDelta over its positions)
+  uint64_t agg;
+  if (fits) {
+    uint64_t s = 0;
+    for (int64_t p = v0 + threadIdx.x; p < v1; p += kBlock) s += staged_delta(T, p, bb0, lbs, lmb);
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) T.wtot[0][threadIdx.x >> 6] = s;
+    __syncthreads();
+    agg = T.wtot[0][0] + T.wtot[0][1] + T.wtot[0][2] + T.wtot[0][3];
+    __syncthreads();
+  } else {
+    agg = is64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL)
+               : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL);
+  }
   const int64_t me = int64_t(P.dtile_base) + int64_t(stream) * P.dtile_n + t.k;
   if (threadIdx.x == 0) {
     uint64_t base;
@@ -520,8 +611,34 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   const DevChunk C = b.chunks[P.chunk];
   int32_t* lens = P.kind == K_DBA && stream == 0 ? C.aux2 : C.aux;
   uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(lens + S.value_base) : C.values + S.value_base * P.value_size;
-  if (is64) delta_tile<true>(b, P, D, v0, v1, s_base, true, out, stage, DL);
-  else delta_tile<false>(b, P, D, v0, v1, s_base, true, out, stage, DL);
+  if (!fits) {
+    if (is64) delta_tile<true>(b, P, D, v0, v1, s_base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+    else delta_tile<false>(b, P, D, v0, v1, s_base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+    return;
+  }
+  // phase B: rows of 256 positions, one block scan each (wave totals double-buffered by row parity)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t carry = s_base;
+  int row = 0;
+  for (int64_t r0 = v0; r0 < v1; r0 += kBlock, row ^= 1) {
+    const int64_t p = r0 + threadIdx.x;
+    const uint64_t d = p < v1 ? staged_delta(T, p, bb0, lbs, lmb) : 0;
+    uint64_t incl = d;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) T.wtot[row][wv] = incl;
+    __syncthreads();
+    uint64_t before = carry;
+    for (int k = 0; k < wv; k++) before += T.wtot[row][k];
+    const uint64_t v = before + incl - d;
+    if (p < v1) {
+      if (is64) reinterpret_cast<uint64_t*>(out)[p] = v;
+      else reinterpret_cast<uint32_t*>(out)[p] = uint32_t(v);
+    }
+    carry += T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3];
+  }
 }
 
 // TK_DELTA_SERIAL: exact sequential restatement of deltaBitPackDecoder.init + next for streams

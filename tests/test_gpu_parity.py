@@ -178,8 +178,10 @@ def _run_cases(pq, ctx, cases):
                 continue
             cd = pq.reader.ColumnData("fuzz", col, o, [], ctx)
             od = O.decode_dict_page(col, dict_img[0], dict_img[1], dict_img[2]) if dict_img else None
-            if od is not None and od.status:
+            if od is not None and od.status:  # the dictionary page itself fails
                 assert cd.status != 0
+                compared += 1
+                errors += 1
                 continue
             r = O.decode_page(col, ptype, nv, enc, dl, rl, img, od)
             from parity import Expected
