@@ -52,7 +52,7 @@ struct KernelRun {
 };
 
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
-                              "k_delta_walk", "k_delta_expand", "k_reserved",
+                              "k_delta_walk", "k_delta_expand", "k_delta_sum_scan",
                               "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix"};
@@ -656,11 +656,10 @@ int pqh_batch_run(pqh_batch* b) {
   if (e == hipSuccess && nbp)
     e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
   if (e == hipSuccess && ndt) {
-    e = hipMemsetAsync(b->d_dflag, 0, sizeof(uint32_t) * size_t(ndt + 1), s);
+    e = timed(6, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
     if (e == hipSuccess)
-      e = timed(5, ndt, s, [&](hipStream_t st) {
-        return launch_delta_expand(d, b->d_dtiles, ndt, b->d_dflag, b->d_dagg, b->d_dpre, b->d_dflag + ndt, st);
-      });
+      e = timed(6, ndp, s, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
+    if (e == hipSuccess) e = timed(5, ndt, s, [&](hipStream_t st) { return launch_delta_expand(d, b->d_dtiles, ndt, st); });
   }
   if (e == hipSuccess && ndp)  // pages outside the fast-path geometry (most launches exit at once)
     e = timed(14, ndp, s, [&](hipStream_t st) { return launch_delta_serial(d, b->d_delta_pages, ndp, st); });

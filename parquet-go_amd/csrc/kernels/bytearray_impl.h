@@ -178,10 +178,14 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
       if (j == 0) {
         start = entry;
       } else {
+        // the first offset whose record is valid and either ends inside the window after another
+        // valid record inside the segment or crosses into a later segment of the window; bytes of a
+        // length field read at an offset of 1-3 give lengths of ~2^8..2^24 that jump far away
         for (int64_t x = s0; x < s1 && x < e0; x++) {
-          int64_t nx;
+          int64_t nx, nx2;
           int32_t l;
-          if (chain_step(C, wb, e0, x, nx, l) == PQH_OK) {
+          if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) continue;
+          if (nx >= s1 ? nx <= wb + kChainWin : chain_step(C, wb, e0, nx, nx2, l) == PQH_OK) {
             start = x;
             break;
           }

@@ -954,10 +954,21 @@ hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int3
   return hipGetLastError();
 }
 
-hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, uint32_t* flag, uint64_t* agg,
-                               uint64_t* pre, uint32_t* ticket, hipStream_t s) {
+hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_delta_expand, dim3(n), dim3(256), 0, s, b, tiles, DeltaLookback{flag, agg, pre, ticket});
+  hipLaunchKernelGGL(k_delta_sum, dim3(n), dim3(256), 0, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_scan, dim3((n + 255) / 256), dim3(256), 0, s, b, delta_pages, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_expand, dim3(n), dim3(256), 0, s, b, tiles);
   return hipGetLastError();
 }
 

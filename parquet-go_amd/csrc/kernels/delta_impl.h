@@ -459,18 +459,6 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
 // for the exclusive prefix (inclusive prefix published), unpack again from L2 and store
 // value[i] = prefix + sum of the deltas before i.  Tile 0 of a page starts from the first value.
 // ------------------------------------------------------------------------------------------------
-struct DeltaLookback {
-  uint32_t* flag;  // per delta tile: 0 nothing yet, 1 aggregate, 2 inclusive prefix (reset per run)
-  uint64_t* agg;
-  uint64_t* pre;
-  uint32_t* ticket;
-};
-
-__device__ __forceinline__ void lb_publish(uint64_t* slot, uint32_t* flag, uint64_t v, uint32_t f) {
-  __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(flag, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Whole-tile staging (the common case: a tile's packed deltas fit kTileStage bytes): the block
 // table of the tile's <= 64 blocks and all of its bytes are loaded once; both phases read LDS only.
 // Values are assigned in rows of 256 consecutive positions (thread t owns position row*256 + t), so
@@ -541,88 +529,109 @@ __device__ __forceinline__ uint64_t staged_delta(const TileStageLds& T, int64_t 
   return extract64(T.data, bit, wm) + T.md[blk];
 }
 
-__global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles, DeltaLookback lb) {
+// Delta tiles: the page-level prefix of the deltas is a three-step scan with kernel boundaries as
+// the only synchronisation (a single-pass decoupled look-back would need agent-scope release /
+// acquire per tile, i.e. L2 write-back / invalidate across the XCDs):
+//   k_delta_sum    per tile: stage it, sum of (delta + minDelta) over its positions
+//   k_delta_scan   per page stream: exclusive scan of its tile sums seeded with the first value
+//   k_delta_expand per tile: stage it again, rows of 256 positions with block scans, coalesced stores
+struct DeltaTileCtx {
+  DevPage P;
+  PageState S;
+  DeltaState D;
+  int64_t v0, v1;
+  int64_t me;  // index of this (page, stream, tile) in dsums
+  int stream;
+  bool ok;
+};
+
+__device__ __forceinline__ DeltaTileCtx delta_tile_ctx(const DevBatch& b, const Tile& t) {
+  DeltaTileCtx c;
+  c.P = b.pages[t.page];
+  c.S = b.states[t.page];
+  c.stream = t.kind;  // DELTA_BYTE_ARRAY: 0 prefix lengths, 1 suffix lengths
+  c.D = b.dstates[c.stream ? b.num_pages + t.page : t.page];
+  c.v0 = int64_t(t.k) * kDeltaTile;
+  c.v1 = c.v0 + kDeltaTile;
+  if (c.v1 > c.D.limit) c.v1 = c.D.limit;
+  const bool lens = c.P.kind == K_DLBA || c.P.kind == K_DBA;
+  if (lens && c.v1 > c.S.nn) c.v1 = c.S.nn;
+  c.me = int64_t(c.P.dtile_base) + int64_t(c.stream) * c.P.dtile_n + t.k;
+  c.ok = !page_failed_before_values(c.S) && c.D.mode == DM_FAST && c.v0 < c.v1;
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles) {
   __shared__ TileStageLds T;
   __shared__ DeltaLds DL;
-  __shared__ int32_t s_ticket;
-  __shared__ uint64_t s_base;
-  if (threadIdx.x == 0) s_ticket = int32_t(atomicAdd(lb.ticket, 1u));
-  __syncthreads();
-  const Tile t = tiles[s_ticket];
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
-  const int stream = t.kind;  // DELTA_BYTE_ARRAY: 0 prefix lengths, 1 suffix lengths
-  const DeltaState D = b.dstates[stream ? b.num_pages + t.page : t.page];
-  // every tile of a page sees the same page verdict, so no tile waits on a tile that skipped
-  if (page_failed_before_values(S) || D.mode != DM_FAST) return;
-  const bool dlba = P.kind == K_DLBA || P.kind == K_DBA;  // int32 lengths into aux / aux2
-  const int64_t v0 = int64_t(t.k) * kDeltaTile;
-  int64_t v1 = v0 + kDeltaTile;
-  if (v1 > D.limit) v1 = D.limit;
-  if (dlba && v1 > S.nn) v1 = S.nn;
-  if (v0 >= v1) return;  // so is every later tile of the page
-  const bool is64 = P.kind == K_DELTA64;
-  const int lbs = __builtin_ctz(uint32_t(D.block_size)), lmb = __builtin_ctz(uint32_t(D.mbvc));
-  const int bb0 = int(v0 >> lbs);
-  const bool fits = stage_tile(b, P, D, v0, v1, T);
-  // phase A: the tile's aggregate (sum of delta + minDelta over its positions)
+  const Tile t = tiles[blockIdx.x];
+  const DeltaTileCtx c = delta_tile_ctx(b, t);
+  if (!c.ok) return;
+  const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
   uint64_t agg;
-  if (fits) {
+  if (stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
+    const int bb0 = int(c.v0 >> lbs);
     uint64_t s = 0;
-    for (int64_t p = v0 + threadIdx.x; p < v1; p += kBlock) s += staged_delta(T, p, bb0, lbs, lmb);
+    for (int64_t p = c.v0 + threadIdx.x; p < c.v1; p += kBlock) s += staged_delta(T, p, bb0, lbs, lmb);
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0) T.wtot[0][threadIdx.x >> 6] = s;
     __syncthreads();
     agg = T.wtot[0][0] + T.wtot[0][1] + T.wtot[0][2] + T.wtot[0][3];
-    __syncthreads();
   } else {
-    agg = is64 ? delta_tile<true>(b, P, D, v0, v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL)
-               : delta_tile<false>(b, P, D, v0, v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL);
+    agg = c.P.kind == K_DELTA64
+              ? delta_tile<true>(b, c.P, c.D, c.v0, c.v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL)
+              : delta_tile<false>(b, c.P, c.D, c.v0, c.v1, 0, false, nullptr, reinterpret_cast<uint32_t*>(T.data), DL);
   }
-  const int64_t me = int64_t(P.dtile_base) + int64_t(stream) * P.dtile_n + t.k;
-  if (threadIdx.x == 0) {
-    uint64_t base;
-    if (t.k == 0) {
-      base = D.first;
-    } else {
-      lb_publish(lb.agg + me, lb.flag + me, agg, 1u);
-      base = 0;
-      for (int64_t j = me - 1;; j--) {
-        uint32_t f;
-        uint32_t spins = 0;  // a predecessor always publishes; the bound only guards against a hang
-        while ((f = __hip_atomic_load(lb.flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
-               ++spins < (1u << 26))
-          __builtin_amdgcn_s_sleep(1);
-        if (f == 0u) {
-          atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, v0, PQH_ERR_HIP));
-          break;
-        }
-        if (f == 2u) {
-          base += __hip_atomic_load(lb.pre + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        base += __hip_atomic_load(lb.agg + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+  if (threadIdx.x == 0) b.dsums[c.me] = agg;
+}
+
+// One thread per delta page: both streams of a DELTA_BYTE_ARRAY page.
+__global__ __launch_bounds__(256) void k_delta_scan(DevBatch b, const int32_t* delta_pages, int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int p = delta_pages[i];
+  const DevPage P = b.pages[p];
+  const int streams = P.kind == K_DBA ? 2 : 1;
+  for (int st = 0; st < streams; st++) {
+    const DeltaState D = b.dstates[st ? b.num_pages + p : p];
+    if (D.mode != DM_FAST) continue;
+    uint64_t run = D.first;
+    const int64_t base = int64_t(P.dtile_base) + int64_t(st) * P.dtile_n;
+    const int64_t nt = (int64_t(D.limit) + kDeltaTile - 1) / kDeltaTile;  // tiles with positions
+    for (int64_t k = 0; k < nt && k < P.dtile_n; k++) {
+      const uint64_t s = b.dsums[base + k];
+      b.dsums[base + k] = run;
+      run += s;
     }
-    lb_publish(lb.pre + me, lb.flag + me, base + agg, 2u);
-    s_base = base;
   }
-  __syncthreads();
-  const DevChunk C = b.chunks[P.chunk];
-  int32_t* lens = P.kind == K_DBA && stream == 0 ? C.aux2 : C.aux;
-  uint8_t* out = dlba ? reinterpret_cast<uint8_t*>(lens + S.value_base) : C.values + S.value_base * P.value_size;
-  if (!fits) {
-    if (is64) delta_tile<true>(b, P, D, v0, v1, s_base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
-    else delta_tile<false>(b, P, D, v0, v1, s_base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+}
+
+__global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles) {
+  __shared__ TileStageLds T;
+  __shared__ DeltaLds DL;
+  const Tile t = tiles[blockIdx.x];
+  const DeltaTileCtx c = delta_tile_ctx(b, t);
+  if (!c.ok) return;
+  const DevChunk C = b.chunks[c.P.chunk];
+  const bool lens = c.P.kind == K_DLBA || c.P.kind == K_DBA;  // int32 lengths into aux / aux2
+  const bool is64 = c.P.kind == K_DELTA64;
+  int32_t* lp = c.P.kind == K_DBA && c.stream == 0 ? C.aux2 : C.aux;
+  uint8_t* out = lens ? reinterpret_cast<uint8_t*>(lp + c.S.value_base) : C.values + c.S.value_base * c.P.value_size;
+  const uint64_t base = b.dsums[c.me];
+  if (!stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
+    if (is64) delta_tile<true>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+    else delta_tile<false>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
     return;
   }
-  // phase B: rows of 256 positions, one block scan each (wave totals double-buffered by row parity)
+  const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
+  const int bb0 = int(c.v0 >> lbs);
+  // rows of 256 positions, one block scan each (wave totals double-buffered by row parity)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t carry = s_base;
+  uint64_t carry = base;
   int row = 0;
-  for (int64_t r0 = v0; r0 < v1; r0 += kBlock, row ^= 1) {
+  for (int64_t r0 = c.v0; r0 < c.v1; r0 += kBlock, row ^= 1) {
     const int64_t p = r0 + threadIdx.x;
-    const uint64_t d = p < v1 ? staged_delta(T, p, bb0, lbs, lmb) : 0;
+    const uint64_t d = p < c.v1 ? staged_delta(T, p, bb0, lbs, lmb) : 0;
     uint64_t incl = d;
     for (int off = 1; off < 64; off <<= 1) {
       const uint64_t y = __shfl_up(incl, off, 64);
@@ -633,7 +642,7 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
     uint64_t before = carry;
     for (int k = 0; k < wv; k++) before += T.wtot[row][k];
     const uint64_t v = before + incl - d;
-    if (p < v1) {
+    if (p < c.v1) {
       if (is64) reinterpret_cast<uint64_t*>(out)[p] = v;
       else reinterpret_cast<uint32_t*>(out)[p] = uint32_t(v);
     }

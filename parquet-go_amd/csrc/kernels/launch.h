@@ -33,10 +33,10 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
 // DELTA_BINARY_PACKED: block walk (one wave per delta page).
 hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
-// Single pass over the delta tiles with a decoupled look-back per page (flag/agg/pre: one entry per
-// delta tile, flags and the ticket zeroed before the launch).
-hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, uint32_t* flag, uint64_t* agg,
-                               uint64_t* pre, uint32_t* ticket, hipStream_t s);
+// Delta tiles: per-tile sums, per-page scan (seeded with the first value), expand.
+hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
+hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
 // per-chunk offset scan, offsets + byte copy.
 hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s);
