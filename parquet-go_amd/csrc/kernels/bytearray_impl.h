@@ -169,7 +169,6 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
       if (o < e0) x = *reinterpret_cast<const uint4*>(img + o);  // the 16 B past e0 stay in the pad
       reinterpret_cast<uint4*>(C.win)[k] = x;
     }
-    if (j == 0) C.stop = 0;
     __syncthreads();
     // 1. speculative walks
     {
@@ -178,14 +177,14 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
       if (j == 0) {
         start = entry;
       } else {
-        // the first offset whose record is valid and either ends inside the window after another
-        // valid record inside the segment or crosses into a later segment of the window; bytes of a
-        // length field read at an offset of 1-3 give lengths of ~2^8..2^24 that jump far away
+        // the first offset whose record is valid and is followed, inside the window, by another
+        // valid record: the bytes of a length field read at an offset of 1-3 give lengths of
+        // ~2^8..2^24 that land in the middle of string bytes (or outside the window)
         for (int64_t x = s0; x < s1 && x < e0; x++) {
           int64_t nx, nx2;
           int32_t l;
           if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) continue;
-          if (nx >= s1 ? nx <= wb + kChainWin : chain_step(C, wb, e0, nx, nx2, l) == PQH_OK) {
+          if (nx < wb + kChainWin && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l) == PQH_OK)) {
             start = x;
             break;
           }
@@ -201,12 +200,14 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
       }
     }
     __syncthreads();
-    // 2. resolution: one parallel check, then an in-order sweep if anything was mis-speculated
-    if (!chain_good(C, j, wb, entry)) atomicOr(&C.stop, 1);
+    // 2. resolution: one parallel check, then an in-order sweep from the first mis-speculated segment
+    if (j == 0) C.stop = kBlock;
     __syncthreads();
-    if (C.stop) {
+    if (!chain_good(C, j, wb, entry)) atomicMin(&C.stop, j);
+    __syncthreads();
+    if (C.stop < kBlock) {
       if (j == 0)
-        for (int s = 0; s < kBlock; s++) chain_fix(C, s, wb, e0, entry);
+        for (int s = C.stop; s < kBlock; s++) chain_fix(C, s, wb, e0, entry);
       __syncthreads();
     }
     // 3. number the records of the true chain, emit, find where the chain ends

@@ -561,6 +561,20 @@ __device__ __forceinline__ DeltaTileCtx delta_tile_ctx(const DevBatch& b, const 
   return c;
 }
 
+// delta + minDelta of the 4 positions p..p+3 (p % 4 == 0: one miniblock, miniblocks hold >= 8).
+__device__ __forceinline__ void staged_delta4(const TileStageLds& T, int64_t p, int bb0, int lbs, int lmb,
+                                              uint64_t d[4]) {
+  const int32_t q = int32_t(p);
+  const int blk = (q >> lbs) - bb0;
+  const int r = q & ((1 << lbs) - 1);
+  const int m = r >> lmb;
+  const int wm = T.mbw[blk][m];
+  const uint64_t md = T.md[blk];
+  const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
+#pragma unroll
+  for (int j = 0; j < 4; j++) d[j] = extract64(T.data, bit + uint32_t(j * wm), wm) + md;
+}
+
 __global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles) {
   __shared__ TileStageLds T;
   __shared__ DeltaLds DL;
@@ -572,7 +586,12 @@ __global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles
   if (stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
     const int bb0 = int(c.v0 >> lbs);
     uint64_t s = 0;
-    for (int64_t p = c.v0 + threadIdx.x; p < c.v1; p += kBlock) s += staged_delta(T, p, bb0, lbs, lmb);
+    for (int64_t p = c.v0 + 4 * int64_t(threadIdx.x); p < c.v1; p += 4 * kBlock) {
+      uint64_t d[4];
+      staged_delta4(T, p, bb0, lbs, lmb, d);
+#pragma unroll
+      for (int j = 0; j < 4; j++) s += p + j < c.v1 ? d[j] : 0;
+    }
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0) T.wtot[0][threadIdx.x >> 6] = s;
     __syncthreads();
@@ -625,26 +644,45 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
   }
   const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
   const int bb0 = int(c.v0 >> lbs);
-  // rows of 256 positions, one block scan each (wave totals double-buffered by row parity)
+  // rows of 1024 positions (4 consecutive per thread), one block scan each (wave totals
+  // double-buffered by row parity); each thread stores 16 / 32 contiguous bytes
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t carry = base;
   int row = 0;
-  for (int64_t r0 = c.v0; r0 < c.v1; r0 += kBlock, row ^= 1) {
-    const int64_t p = r0 + threadIdx.x;
-    const uint64_t d = p < c.v1 ? staged_delta(T, p, bb0, lbs, lmb) : 0;
-    uint64_t incl = d;
+  for (int64_t r0 = c.v0; r0 < c.v1; r0 += 4 * kBlock, row ^= 1) {
+    const int64_t p = r0 + 4 * int64_t(threadIdx.x);
+    uint64_t d[4] = {0, 0, 0, 0};
+    if (p < c.v1) staged_delta4(T, p, bb0, lbs, lmb, d);
+#pragma unroll
+    for (int j = 0; j < 4; j++) d[j] = p + j < c.v1 ? d[j] : 0;
+    const uint64_t tsum = d[0] + d[1] + d[2] + d[3];
+    uint64_t incl = tsum;
     for (int off = 1; off < 64; off <<= 1) {
       const uint64_t y = __shfl_up(incl, off, 64);
       if (lane >= off) incl += y;
     }
     if (lane == 63) T.wtot[row][wv] = incl;
     __syncthreads();
-    uint64_t before = carry;
-    for (int k = 0; k < wv; k++) before += T.wtot[row][k];
-    const uint64_t v = before + incl - d;
-    if (p < c.v1) {
-      if (is64) reinterpret_cast<uint64_t*>(out)[p] = v;
-      else reinterpret_cast<uint32_t*>(out)[p] = uint32_t(v);
+    uint64_t v = carry + incl - tsum;
+    for (int k = 0; k < wv; k++) v += T.wtot[row][k];
+    if (p + 4 <= c.v1) {
+      if (is64) {
+        const uint64_t o4[4] = {v, v + d[0], v + d[0] + d[1], v + d[0] + d[1] + d[2]};
+        __builtin_memcpy(reinterpret_cast<uint64_t*>(out) + p, o4, 32);
+      } else {
+        const uint32_t o4[4] = {uint32_t(v), uint32_t(v + d[0]), uint32_t(v + d[0] + d[1]),
+                                uint32_t(v + d[0] + d[1] + d[2])};
+        __builtin_memcpy(reinterpret_cast<uint32_t*>(out) + p, o4, 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (p + j < c.v1) {
+          if (is64) reinterpret_cast<uint64_t*>(out)[p + j] = v;
+          else reinterpret_cast<uint32_t*>(out)[p + j] = uint32_t(v);
+        }
+        v += d[j];
+      }
     }
     carry += T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3];
   }
