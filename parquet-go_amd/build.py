@@ -19,8 +19,8 @@ INCLUDE = os.path.join(ROOT, "include")
 HOST_SRCS = ["host/codec.cpp", "host/file_reader.cpp"]
 HIP_SRCS = ["kernels/decode.hip", "host/batch.hip"]
 GEN_SRCS = ["tools/pqgen.cpp", "host/codec.cpp"]
-HEADERS = ["host/codec.h", "host/thrift_compact.h", "host/file_reader.h", "kernels/decode.h",
-           "tools/pqgen.h", "host/internal.h"]
+HEADERS = sorted(os.path.relpath(os.path.join(d, f), CSRC) for d, _, fs in os.walk(CSRC) for f in fs
+                 if f.endswith(".h"))
 
 ARCH = os.environ.get("PQH_OFFLOAD_ARCH", "gfx950")
 
@@ -67,7 +67,8 @@ def build_hip(force=False):
         for s in HIP_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                  "-munsafe-fp-atomics", "-I", INCLUDE, "-c", os.path.join(CSRC, s), "-o", o])
+                  "-munsafe-fp-atomics", "-I", INCLUDE] + os.environ.get("PQH_HIPFLAGS", "").split()
+                 + ["-c", os.path.join(CSRC, s), "-o", o])
             objs.append(o)
         for s in HOST_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")

@@ -32,12 +32,19 @@ __device__ __forceinline__ void wave_lds_sync() {
 // interpreted (every read checks pos < e); the 16-byte loads stay inside the payload pad.
 __device__ __forceinline__ void win_load(Win& w, int64_t pos, int lane) {
   const int64_t lo = pos - int64_t((reinterpret_cast<uintptr_t>(w.img) + uintptr_t(pos)) & 15);
+  constexpr int kPer = kWin / 16 / 64;
+  uint4 x[kPer];
+  // all loads in flight before the first LDS write (addresses past the stream clamp to `lo`)
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int64_t o = lo + 16 * int64_t(lane + 64 * k);
+    x[k] = *reinterpret_cast<const uint4*>(w.img + (o < w.e ? o : lo));
+  }
   wave_lds_sync();
-  for (int k = lane; k < kWin / 16; k += 64) {
-    const int64_t o = lo + 16 * int64_t(k);
-    uint4 x = make_uint4(0, 0, 0, 0);
-    if (o < w.e) x = *reinterpret_cast<const uint4*>(w.img + o);
-    reinterpret_cast<uint4*>(w.buf)[k] = x;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int64_t o = lo + 16 * int64_t(lane + 64 * k);
+    reinterpret_cast<uint4*>(w.buf)[lane + 64 * k] = o < w.e ? x[k] : make_uint4(0, 0, 0, 0);
   }
   wave_lds_sync();
   w.lo = lo;
@@ -165,11 +172,358 @@ __device__ __forceinline__ int64_t block_data_bytes(uint64_t widths, int mbvc) {
   return sum * (mbvc / 8);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Speculative lane-parallel block chain.  Walking the chain one block at a time costs the wave a
+// dependent round trip plus ~150 wave-uniform instructions per block, for 1024 blocks per
+// reference-writer page.  Instead the 64 lanes each take one byte segment of the stream, find a
+// plausible header in it (two consecutive headers that parse), and walk their own chain through
+// L2 until they leave the segment.  The segments are then stitched in order: from the true header
+// that enters a segment, the chain is deterministic, so a lane's list is kept from that header on.
+// A segment whose walk never meets the true chain, or outgrows its list, ends the speculation
+// there and the exact sequential walk takes over from the last verified header.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSpecCap = kWin / (64 * 4);
+
+#ifdef PQH_DEBUG_SPEC
+__device__ long long g_dbg_all[64][16];
+#define DBG_CLK(v) const long long v = clock64()
+#else
+#define DBG_CLK(v)
+#endif
+
+// The common-case readMiniBlockHeader over 16 bytes (a = bytes 0-7, b = 8-15): varint minDelta of
+// <= 8 bytes, value in range, mbc width bytes <= the limit.  Returns the header length or 0.
+__device__ __forceinline__ int parse_hdr16(uint64_t a, uint64_t b, bool is64, int mbc, uint64_t& md, uint64_t& wd) {
+  const uint64_t stop = ~a & 0x8080808080808080ull;
+  if (!stop) return 0;
+  const int len = (__builtin_ctzll(stop) >> 3) + 1;
+  // the len 7-bit groups, packed (SWAR: 8x7 -> 4x14 -> 2x28 -> 56 bits)
+  const int sh = len * 8;
+  uint64_t u = (sh == 64 ? a : a & ((1ull << sh) - 1)) & 0x7f7f7f7f7f7f7f7full;
+  u = (u & 0x007f007f007f007full) | ((u & 0x7f007f007f007f00ull) >> 1);
+  u = (u & 0x00003fff00003fffull) | ((u & 0x3fff00003fff0000ull) >> 2);
+  u = (u & 0x000000000fffffffull) | ((u & 0x0fffffff00000000ull) >> 4);
+  const int64_t x = int64_t(u >> 1) ^ -int64_t(u & 1);
+  if (!is64 && (x > 2147483647ll || x < -2147483648ll)) return 0;
+  uint64_t w = sh == 64 ? b : (a >> sh) | (b << (64 - sh));
+  if (mbc < 8) w &= (1ull << (8 * mbc)) - 1;
+  // any byte > lim: high bit set, or low 7 bits + (127 - lim) carries into bit 7 (no cross-byte carry)
+  const uint64_t lim = is64 ? 64 : 32;
+  const uint64_t bad = (((w & 0x7f7f7f7f7f7f7f7full) + (0x7f - lim) * 0x0101010101010101ull) | w) &
+                       0x8080808080808080ull;
+  if (bad) return 0;
+  md = uint64_t(x);
+  wd = w;
+  return len + mbc;
+}
+
+__device__ __forceinline__ int64_t widths_sum(uint64_t w) {
+  const uint64_t m = 0x00ff00ff00ff00ffull;
+  uint64_t t = (w & m) + ((w >> 8) & m);  // 4 x 16-bit sums
+  t += t >> 16;
+  t += t >> 32;
+  return int64_t(t & 0xffff);
+}
+
+typedef const __attribute__((address_space(1))) uint64_t* gptr64;
+
+// The 16 bytes at image offset p (image 8-byte aligned) as two little-endian words.
+__device__ __forceinline__ void bytes16_global(const uint8_t* img, int64_t p, uint64_t& a, uint64_t& b) {
+  const gptr64 q = (gptr64)(img + (p & ~int64_t(7)));
+  const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
+  const uint32_t sh = uint32_t(p & 7) * 8;
+  a = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+  b = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+}
+
+// Per lane, through L2: the header at image offset p.  dat = its data, nxt = the next header; false
+// unless the common-case parse applies and the whole block lies inside the stream.
+__device__ __forceinline__ bool hdr_global(const uint8_t* img, int64_t p, int64_t e, bool is64, int mbc, int gbytes,
+                                           uint64_t& md, uint64_t& wd, int64_t& dat, int64_t& nxt) {
+  if (e - p < 24) return false;
+  uint64_t a, b;
+  bytes16_global(img, p, a, b);
+  const int hl = parse_hdr16(a, b, is64, mbc, md, wd);
+  if (!hl) return false;
+  dat = p + hl;
+  nxt = dat + widths_sum(wd) * gbytes;
+  return nxt <= e;
+}
+
+// A block record written by the speculative walk holds only its header position (pad == 1): the
+// consumer parses the header (already validated by the walk) when it loads the record.
+__device__ __forceinline__ DeltaBlock load_block(const DeltaBlock* recs, int64_t i, const uint8_t* img, bool is64,
+                                                 int mbc) {
+  DeltaBlock r = recs[i];
+  if (r.pad) {
+    uint64_t a, b, md = 0, wd = 0;
+    bytes16_global(img, r.data_off, a, b);
+    r.data_off += parse_hdr16(a, b, is64, mbc, md, wd);
+    r.min_delta = md;
+    r.widths = wd;
+    r.pad = 0;
+  }
+  return r;
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t x, int i) {
+  return int64_t(uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(x))), i))) |
+                 (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(x) >> 32)), i))) << 32));
+}
+
+// Per byte of x: MSB set where the byte is <= lim (lim < 128; no carries cross bytes).
+__device__ __forceinline__ uint64_t small_bytes(uint64_t x, uint64_t lim) {
+  return ~(((x & 0x7f7f7f7f7f7f7f7full) + (0x7f - lim) * 0x0101010101010101ull) | x) & 0x8080808080808080ull;
+}
+
+// Per lane: the first position in [s0, s1) whose header parses and whose successor parses too
+// (s1 if none).  32 positions per step: a byte-parallel filter keeps the positions p whose byte is
+// a varint terminator (< 0x80) followed by mbc bytes <= the width limit, and only those get a full
+// parse.  A header whose varint ends at byte p has the same widths and successor as the 1-byte
+// varint at p, so p stands for every start of that varint (the stitch resolves which is true).
+__device__ int64_t spec_sync(const uint8_t* img, int64_t s0, int64_t s1, int64_t e, bool is64, int mbc,
+                             int gbytes) {
+  const uint64_t lim = is64 ? 64 : 32;
+  for (int64_t base = s0 & ~int64_t(15); base < s1; base += 32) {
+    if (e - base < 64) {  // stream tail: position by position
+      for (int64_t p = base > s0 ? base : s0; p < s1; p++) {
+        uint64_t md, wd;
+        int64_t dat, n1, n2;
+        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1) &&
+            hdr_global(img, n1, e, is64, mbc, gbytes, md, wd, dat, n2))
+          return p;
+      }
+      return s1;
+    }
+    const gptr64 q = (gptr64)(img + base);
+    uint64_t x[5], S[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      x[j] = q[j];
+      S[j] = small_bytes(x[j], lim);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint64_t cand = ~x[j] & 0x8080808080808080ull;
+      for (int k = 1; k <= mbc; k++) cand &= k == 8 ? S[j + 1] : (S[j] >> (8 * k)) | (S[j + 1] << (64 - 8 * k));
+      const int64_t w0 = base + 8 * j;
+      if (s0 > w0) cand &= s0 - w0 >= 8 ? 0 : ~0ull << (8 * (s0 - w0));
+      if (s1 - w0 < 8) cand &= s1 <= w0 ? 0 : (1ull << (8 * (s1 - w0))) - 1;
+      while (cand) {
+        const int64_t p = w0 + (__builtin_ctzll(cand) >> 3);
+        cand &= cand - 1;
+        uint64_t md, wd;
+        int64_t dat, n1, n2;
+        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1) &&
+            hdr_global(img, n1, e, is64, mbc, gbytes, md, wd, dat, n2))
+          return p;
+      }
+    }
+  }
+  return s1;
+}
+
+// Headers of the whole blocks [1, kmax) starting at h1 (block 1's header): records written, returns
+// r = blocks recorded including block 0 (1 <= r <= kmax) and *hr = the header of block r.  Rounds:
+// the span of the blocks still missing is estimated from the bytes per block so far and split over
+// the lanes; every round advances at least through lane 0's segment unless the true chain reaches
+// a header the fast parse rejects (the exact walk takes over there).
+__device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, int mbc, int gbytes, int bs,
+                          int kmax, int64_t blk0_bytes, DeltaBlock* recs, int32_t* lst, int lane, int64_t& hr,
+                          bool dbg = false) {
+#ifdef PQH_DEBUG_SPEC
+  long long* g_dbg = g_dbg_all[(blockIdx.x * 4 + (threadIdx.x >> 6)) % 64];
+#endif
+  int64_t T = h1, bytes_done = blk0_bytes;
+  int nb = 1;
+#ifdef PQH_DEBUG_SPEC
+  int dbg_rounds = 0, dbg_follow = 0, dbg_miss = 0;
+#endif
+  DBG_CLK(c_start);
+#ifdef PQH_DEBUG_SPEC
+  long long c_sync = 0, c_walk = 0, c_stitch = 0, c_rec = 0;
+#endif
+  while (nb < kmax) {
+#ifdef PQH_DEBUG_SPEC
+    dbg_rounds++;
+#endif
+    const int64_t avg = bytes_done / nb > 0 ? bytes_done / nb : 1;
+    int64_t span = int64_t(kmax - nb) * avg;
+    span += span / 8 + 64;
+    if (span > e - T) span = e - T;
+    int64_t seg = (span + 63) / 64;
+    if (seg < 32) seg = 32;
+    const int64_t s0 = T + seg * lane, s1 = s0 + seg;
+    int cnt = 0;
+    bool dead = false;
+    int64_t p = s0, x2 = -1;
+    wave_lds_sync();  // the previous round's readers of the lists are done
+    if (s0 < e) {
+      uint64_t md, wd;
+      int64_t dat, n1;
+      DBG_CLK(ca);
+      if (lane > 0) p = spec_sync(img, s0, s1, e, is64, mbc, gbytes);
+      DBG_CLK(cb);
+#ifdef PQH_DEBUG_SPEC
+      c_sync += cb - ca;
+#endif
+      while (p < s1 && cnt < kSpecCap - 1) {
+        lst[cnt * 64 + lane] = int32_t(p);
+        cnt++;
+        if (!hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1)) {
+          dead = true;
+          break;
+        }
+        p = n1;
+      }
+      // one block past the segment: the exit header (list slot cnt, not counted) and its successor
+      if (!dead && p >= s1 && p < e) {
+        lst[cnt * 64 + lane] = int32_t(p);
+        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1)) x2 = n1;
+      }
+    }
+    const bool full = !dead && p < s1;
+    wave_lds_sync();
+    // ---- stitch.  In parallel: where the left neighbour's exit header (and its successor) sit in
+    // my list; the true chain runs through every lane linked to its left neighbour that way.
+    const int64_t T0 = T;
+    const int nb0 = nb;
+    const int nseg = int((e - T0 + seg - 1) / seg) < 64 ? int((e - T0 + seg - 1) / seg) : 64;
+    const bool exit_ok = s0 < e && !dead && !full && p < e;
+    const int64_t xl = __shfl_up(p, 1, 64), x2l = __shfl_up(x2, 1, 64);
+    const bool left_ok = __shfl_up(int(exit_ok), 1, 64) != 0 && xl >= s0 && xl < s1;
+    int jd = -1, j2 = -1;
+    if (lane > 0 && left_ok)
+      for (int k = 0; k < cnt; k++) {
+        const int32_t q = lst[k * 64 + lane];
+        if (jd < 0 && q == int32_t(xl)) jd = k;
+        if (j2 < 0 && x2l >= 0 && q == int32_t(x2l)) j2 = k;
+      }
+    const bool link = lane < nseg && (lane == 0 || (left_ok && (jd >= 0 || j2 >= 0)));
+    int j = lane == 0 ? 0 : (jd >= 0 ? jd : j2);
+    // lane i synchronised just before T (the previous block's last data bytes continuing into T's
+    // varint) or on T's varint terminator and joined the true chain one block later: its left
+    // neighbour parsed T as its exit header (list slot cnt) and records it
+    const bool extra = lane > 0 && link && jd < 0;
+    const uint64_t linkm = __ballot(link);
+    const int k_bad = linkm == ~0ull ? 64 : __builtin_ctzll(~linkm);
+    const uint64_t deadm = __ballot(dead && lane < nseg) & (k_bad >= 64 ? ~0ull : (1ull << k_bad) - 1);
+    const int last = deadm ? __builtin_ctzll(deadm) : k_bad - 1;
+    const bool valid = lane <= last;
+    const bool extra_r = __shfl_down(int(extra), 1, 64) != 0 && lane + 1 <= last && lane < 63;
+    const int n_all = valid ? cnt - j - (dead ? 1 : 0) + (extra_r ? 1 : 0) : 0;
+    int incl = n_all;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    const int base = nb + incl - n_all;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    int my_j = j, my_base = base;
+    int my_n = base + n_all > kmax ? (kmax - base > 0 ? kmax - base : 0) : n_all;
+    bool stop = false;
+    int i_next = last + 1;
+    if (nb + total >= kmax) {
+      // block kmax's header: the entry after the last kept one
+      const bool hit = valid && base <= kmax && kmax < base + n_all;
+      const uint64_t hm = __ballot(hit);
+      const int32_t q = hit ? lst[(j + (kmax - base)) * 64 + lane] : 0;
+      T = hm ? int64_t(__builtin_amdgcn_readlane(q, __builtin_ctzll(hm))) : readlane64(p, last);
+      nb = kmax;
+      stop = true;
+    } else {
+      nb += total;
+      if (deadm) {  // the true chain reached a header the fast parse rejects
+        const int32_t q = lst[(cnt > 0 ? cnt - 1 : 0) * 64 + lane];
+        T = int64_t(__builtin_amdgcn_readlane(q, last));
+        stop = true;
+      } else if (last >= 0) {
+        T = readlane64(p, last);
+      }
+    }
+    DBG_CLK(cc);
+    // the rare cases, one segment at a time (wave-uniform): a block longer than a segment, a lane
+    // whose walk joined the true chain late or never, a lane that outgrew its list
+    for (int i = i_next; i < nseg && nb < kmax && !stop; i++) {
+      const int64_t seg_end = T0 + seg * (i + 1);
+      if (T >= seg_end) continue;  // no true header in segment i
+      const int ci = __builtin_amdgcn_readlane(cnt, i);
+      const bool di = __builtin_amdgcn_readlane(int(dead), i) != 0;
+      const bool fi = __builtin_amdgcn_readlane(int(full), i) != 0;
+      const int64_t xi = readlane64(p, i);
+      uint64_t m = __ballot(lane < ci && lst[lane * 64 + i] == int32_t(T));
+      // follow the true chain a few blocks by hand until it meets lane i's walk
+      for (int t = 0; t < 3 && !m && nb < kmax && T < seg_end; t++) {
+        uint64_t md, wd;
+        int64_t dat, nx;
+        if (!hdr_global(img, T, e, is64, mbc, gbytes, md, wd, dat, nx)) {
+          stop = true;
+          break;
+        }
+        if (lane == 0) recs[nb] = DeltaBlock{md, int32_t(dat), int32_t(int64_t(nb) * bs), wd, 0};
+        nb++;
+        T = nx;
+#ifdef PQH_DEBUG_SPEC
+        dbg_follow++;
+#endif
+        m = __ballot(lane < ci && lst[lane * 64 + i] == int32_t(T));
+      }
+      if (stop || nb >= kmax) break;
+      if (T >= seg_end) continue;
+#ifdef PQH_DEBUG_SPEC
+      if (!m) dbg_miss++;
+#endif
+      if (!m) break;  // lane i's walk never met the true chain: next round from T
+      const int jj = __builtin_ctzll(m);
+      int n = ci - jj - (di ? 1 : 0);
+      if (nb + n > kmax) n = kmax - nb;
+      if (lane == i) {
+        my_j = jj;
+        my_n = n;
+        my_base = nb;
+      }
+      nb += n;
+      T = jj + n < ci ? int64_t(__builtin_amdgcn_readfirstlane(lst[(jj + n) * 64 + i])) : xi;
+      if (di) stop = true;
+      if (di || fi) break;
+    }
+    DBG_CLK(cd);
+    // records: header positions only (pad = 1), parsed by their consumers
+    for (int k = 0; k < my_n; k++) {
+      const int b = my_base + k;
+      recs[b] = DeltaBlock{0, lst[(my_j + k) * 64 + lane], int32_t(int64_t(b) * bs), 0, 1};
+    }
+#ifdef PQH_DEBUG_SPEC
+    {
+      DBG_CLK(ce);
+      c_stitch += cd - cc;
+      c_rec += ce - cd;
+      c_walk = cc - c_start;
+    }
+#endif
+    if (nb == nb0 || stop) break;
+    bytes_done += T - T0;
+  }
+  wave_lds_sync();
+#ifdef PQH_DEBUG_SPEC
+  {
+    long long mxs = c_sync;
+    for (int off = 32; off > 0; off >>= 1) mxs = max(mxs, (long long)__shfl_xor(mxs, off, 64));
+    if (dbg) {
+      g_dbg[0] = kmax; g_dbg[1] = nb; g_dbg[2] = dbg_rounds; g_dbg[3] = dbg_follow; g_dbg[4] = dbg_miss;
+      g_dbg[5] = mxs; g_dbg[6] = c_walk; g_dbg[7] = c_stitch; g_dbg[8] = c_rec;
+    }
+  }
+#endif
+  hr = T;
+  return nb;
+}
+
 // The block walk of one page (whole wave, uniform).  Returns the first error key.
 // init_all: byteArrayDeltaLengthDecoder.init (type_bytearray.go:104-116) decodes ALL valuesCount
 // lengths at page load: every error is a load error (phase 0, step 3) and nn is ignored.
 __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaBlock* recs, int32_t cap,
-                               DeltaState& D, int lane, bool init_all) {
+                               DeltaState& D, int lane, bool init_all, bool dbg = false) {
   D.mode = DM_NONE;
   D.nblocks = 0;
   D.limit = 0;
@@ -209,7 +563,24 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   uint64_t err = kNoError;
   int64_t limit = nn;
   bool padded = false;
-  for (int64_t b = 0; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
+  int64_t b_start = 0;
+  {
+    // whole blocks [0, kmax): before the padding group and the last reachable position
+    const int64_t lp = L < pstar ? L : pstar;
+    const int64_t kmax = lp / bs < cap ? lp / bs : cap;
+    const int64_t nb0 = block_data_bytes(widths, mbvc);
+    if (kmax >= 2 && pos + nb0 <= w.e) {
+      if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), 0, widths, 0};
+      int64_t hr;
+      const int r = spec_chain(w.img, pos + nb0, w.e, is64, mbc, mbvc / 8, bs, int(kmax), pos + nb0 - vs, recs,
+                               reinterpret_cast<int32_t*>(w.buf), lane, hr, dbg);
+      D.nblocks = r;
+      b_start = r;
+      pos = hr;
+      w.lo = w.hi = 0;  // the window held the lane lists
+    }
+  }
+  for (int64_t b = b_start; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
     const int64_t p0 = b * bs;
     if (b > 0 && !fast_block_header(w, pos, is64, mbc, md, widths, lane) &&
         (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
@@ -297,8 +668,20 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
     win_load(w, S.val_s, lane);
     const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
     DeltaBlock* recs = b.dblocks + P.dblk_base;
+    DBG_CLK(c0);
+#ifdef PQH_DEBUG_SPEC
+    const long long w0 = wall_clock64();
+#endif
     err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn, recs, P.dblk_cap, D, lane,
-                     P.kind == K_DLBA || dba);
+                     P.kind == K_DLBA || dba, idx % 997 == 0);
+#ifdef PQH_DEBUG_SPEC
+    DBG_CLK(c1);
+    if (lane == 0 && idx % 997 == 0) {
+      const long long* g = g_dbg_all[idx % 64];
+      printf("page %d walk total %lld | kmax %lld nb %lld rounds %lld follow %lld miss %lld | sync(max) %lld sync+walk %lld stitch %lld rec %lld | wall %lld\n",
+             p, c1 - c0, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], (long long)(wall_clock64() - w0));
+    }
+#endif
     if (dba && err == kNoError) {
       // byteArrayDeltaDecoder.init (type_bytearray.go:195-211): prefix lengths, then the
       // DELTA_LENGTH suffix decoder on the rest; both decode every length at load
@@ -375,7 +758,7 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
     const int bb0 = int(int32_t(c0) / bs), nb = int(int32_t(c1 - 1) / bs) - bb0 + 1;
     __syncthreads();
     if (threadIdx.x < nb) {  // per-block miniblock data offsets (image offsets)
-      const DeltaBlock r = recs[bb0 + threadIdx.x];
+      const DeltaBlock r = load_block(recs, bb0 + threadIdx.x, img, P.kind == K_DELTA64, mbc);
       int32_t off = r.data_off;
       for (int m = 0; m < 8; m++) {
         const int wm = m < mbc ? mb_width(r.widths, m) : 0;
@@ -487,7 +870,7 @@ __device__ bool stage_tile(const DevBatch& b, const DevPage& P, const DeltaState
   const int mbc = D.mb_count, gbytes = D.mbvc / 8;
   __shared__ int64_t s_start, s_end;
   if (threadIdx.x < nb) {
-    const DeltaBlock r = recs[bb0 + threadIdx.x];
+    const DeltaBlock r = load_block(recs, bb0 + threadIdx.x, img, P.kind == K_DELTA64, mbc);
     int32_t off = r.data_off;
     for (int m = 0; m < 8; m++) {
       const int wm = m < mbc ? mb_width(r.widths, m) : 0;

@@ -268,6 +268,50 @@ def test_delta_multi_tile_pages(pq, ctx):
     assert compared == len(cases)
 
 
+def _regimes(rng, n, bits):
+    """Runs of constant, narrow and full-width deltas: blocks of 5 bytes next to blocks of 1-2 KiB."""
+    lo, hi = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+    d = np.zeros(n, np.int64)
+    i = 0
+    while i < n:
+        span = int(rng.integers(1, 3000))
+        kind = int(rng.integers(0, 3))
+        if kind == 1:
+            d[i:i + span] = rng.integers(-8, 8, min(span, n - i))
+        elif kind == 2:
+            d[i:i + span] = rng.integers(lo, hi, min(span, n - i), dtype=np.int64, endpoint=True)
+        i += span
+    v = np.cumsum(d.astype(np.uint64)).astype(np.int64) if bits == 64 else np.cumsum(d).astype(np.int32)
+    return v
+
+
+def test_delta_chain_speculation(pq, ctx):
+    """Large reference-writer pages (128/4 blocks) whose block chains the walk finds with per-lane
+    speculative segment walks: constant deltas (5-byte blocks), full-width deltas (2 KiB blocks),
+    regime changes, timestamps; plus corrupted bytes and cuts anywhere in them (the stitched chain
+    must hand over to the exact walk at the first bad header)."""
+    W = fixtures.W
+    rng = np.random.default_rng(36)
+    cases = []
+    for bits in (32, 64):
+        col = (W.INT32 if bits == 32 else W.INT64, 0, 0, 0)
+        dt = np.int32 if bits == 32 else np.int64
+        for n in (131072, 50001):
+            series = [np.full(n, 7, dt),
+                      rng.integers(-(1 << (bits - 1)), (1 << (bits - 1)) - 1, n, dtype=np.int64).astype(dt),
+                      _regimes(rng, n, bits),
+                      (np.cumsum(1_000_000 + rng.integers(0, 4096, n)) % (1 << 31)).astype(dt)]
+            for vals in series:
+                img = W.delta_encode(vals, bits)
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img)))
+                for _ in range(2):
+                    cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, _mutate(rng, img))))
+                cut = int(rng.integers(len(img) // 4, len(img)))
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img[:cut])))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors > 0
+
+
 def test_delta_optional_v2(pq, ctx):
     """DELTA values behind definition levels (notNull < num_values) on V2 pages."""
     import delta_streams as DS
