@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -55,8 +56,11 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_delta_walk", "k_delta_expand", "k_delta_sum_scan",
                               "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
-                              "k_dba_prefix"};
-constexpr int kNumKernels = 16;
+                              "k_dba_prefix", "k_delta_spec", "k_delta_page"};
+constexpr int kNumKernels = 18;
+// Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
+// fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
+constexpr size_t kDeltaPageModeMin = 1024;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -126,6 +130,8 @@ struct pqh_batch {
   std::vector<Tile> expand_tiles;   // k_expand work list (kinds interleaved)
   std::vector<Tile> global_tiles;   // k_dict_global work list
   std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
+  std::vector<Tile> delta_streams;  // k_delta_page work list: (page, 0, stream) with values
+  bool delta_page_mode = false;
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
   std::vector<int32_t> ba_pages;    // k_ba_walk work list (PLAIN byte-array data + dictionary pages)
@@ -393,8 +399,10 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         P.dtile_n = int32_t(ceil_div(n, kDeltaTile));
         dtile_cursor += int64_t(streams) * P.dtile_n;
         b->delta_pages.push_back(p);
-        for (int st = 0; st < streams; st++)  // Tile.kind = stream (k_delta_expand)
+        for (int st = 0; st < streams; st++) {  // Tile.kind = stream (k_delta_expand)
           for (int32_t k = 0; k < P.dtile_n; k++) by_kind[TK_DELTA].push_back(Tile{p, k, st, 1});
+          if (P.dtile_n > 0) b->delta_streams.push_back(Tile{p, 0, st, 1});
+        }
         if (kind == K_DBA) b->has_dba = true;
       }
       const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT || kind == K_DBA);
@@ -479,6 +487,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
     b->global_tiles = by_kind[TK_DICT_GLOBAL];
     b->delta_tiles = by_kind[TK_DELTA];
+    b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
+    if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
+      b->delta_page_mode = f[0] == '1';
   }
 
   // ---- device allocations ----
@@ -590,8 +601,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   if (e == hipSuccess && num_chunks)
     e = hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * size_t(num_chunks), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && ntiles) e = hipMemcpyAsync(b->d_tiles, all.data(), sizeof(Tile) * ntiles, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->delta_tiles.empty())
-    e = hipMemcpyAsync(b->d_dtiles, b->delta_tiles.data(), sizeof(Tile) * b->delta_tiles.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->delta_tiles.empty()) {
+    // page mode: the (shorter) stream list takes the tile list's place
+    const std::vector<Tile>& dl = b->delta_page_mode ? b->delta_streams : b->delta_tiles;
+    e = hipMemcpyAsync(b->d_dtiles, dl.data(), sizeof(Tile) * dl.size(), hipMemcpyHostToDevice, s);
+  }
   if (e == hipSuccess && !b->delta_pages.empty())
     e = hipMemcpyAsync(b->d_delta_pages, b->delta_pages.data(), sizeof(int32_t) * b->delta_pages.size(),
                        hipMemcpyHostToDevice, s);
@@ -650,12 +664,17 @@ int pqh_batch_run(pqh_batch* b) {
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
   if (e == hipSuccess && ndp)
+    e = timed(16, ndp, s, [&](hipStream_t st) { return launch_delta_spec(d, b->d_delta_pages, ndp, st); });
+  if (e == hipSuccess && ndp)
     e = timed(4, ndp, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ndp, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
   if (e == hipSuccess && nbp)
     e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
-  if (e == hipSuccess && ndt) {
+  if (e == hipSuccess && ndt && b->delta_page_mode) {
+    const int32_t nds = int32_t(b->delta_streams.size());
+    e = timed(17, nds, s, [&](hipStream_t st) { return launch_delta_page(d, b->d_dtiles, nds, st); });
+  } else if (e == hipSuccess && ndt) {
     e = timed(6, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
     if (e == hipSuccess)
       e = timed(6, ndp, s, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
@@ -789,10 +808,12 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[2] += S.nn;
         break;
       case K_DELTA32:
-      case K_DELTA64:  // the walk reads block headers; k_delta_expand reads the stream once from HBM
-        b->k_read[5] += S.val_e - S.val_s;
-        b->k_written[5] += vals;
+      case K_DELTA64: {  // the walks read block headers; k_delta_expand / k_delta_page read the stream once
+        const int kd = b->delta_page_mode ? 17 : 5;
+        b->k_read[kd] += S.val_e - S.val_s;
+        b->k_written[kd] += vals;
         break;
+      }
       case K_PLAIN_BA:  // walked by k_ba_walk, bytes moved by k_ba_expand
       case K_DLBA:
       case K_DBA:

@@ -948,6 +948,18 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
   return hipGetLastError();
 }
 
+hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_page, dim3(n), dim3(256), 0, s, b, streams);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_spec(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_spec, dim3((n + 3) / 4), dim3(256), 0, s, b, delta_pages, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_delta_walk, dim3((n + 3) / 4), dim3(256), 0, s, b, delta_pages, n);

@@ -32,19 +32,21 @@ __device__ __forceinline__ void wave_lds_sync() {
 // interpreted (every read checks pos < e); the 16-byte loads stay inside the payload pad.
 __device__ __forceinline__ void win_load(Win& w, int64_t pos, int lane) {
   const int64_t lo = pos - int64_t((reinterpret_cast<uintptr_t>(w.img) + uintptr_t(pos)) & 15);
-  constexpr int kPer = kWin / 16 / 64;
-  uint4 x[kPer];
-  // all loads in flight before the first LDS write (addresses past the stream clamp to `lo`)
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const int64_t o = lo + 16 * int64_t(lane + 64 * k);
-    x[k] = *reinterpret_cast<const uint4*>(w.img + (o < w.e ? o : lo));
-  }
+  constexpr int kPer = kWin / 16 / 64, kHalf = kPer / 2;
   wave_lds_sync();
+  // loads in flight four at a time (addresses past the stream clamp to `lo`)
+  for (int h = 0; h < kPer; h += kHalf) {
+    uint4 x[kHalf];
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const int64_t o = lo + 16 * int64_t(lane + 64 * k);
-    reinterpret_cast<uint4*>(w.buf)[lane + 64 * k] = o < w.e ? x[k] : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kHalf; k++) {
+      const int64_t o = lo + 16 * int64_t(lane + 64 * (h + k));
+      x[k] = *reinterpret_cast<const uint4*>(w.img + (o < w.e ? o : lo));
+    }
+#pragma unroll
+    for (int k = 0; k < kHalf; k++) {
+      const int64_t o = lo + 16 * int64_t(lane + 64 * (h + k));
+      reinterpret_cast<uint4*>(w.buf)[lane + 64 * (h + k)] = o < w.e ? x[k] : make_uint4(0, 0, 0, 0);
+    }
   }
   wave_lds_sync();
   w.lo = lo;
@@ -184,12 +186,7 @@ __device__ __forceinline__ int64_t block_data_bytes(uint64_t widths, int mbvc) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kSpecCap = kWin / (64 * 4);
 
-#ifdef PQH_DEBUG_SPEC
-__device__ long long g_dbg_all[64][16];
-#define DBG_CLK(v) const long long v = clock64()
-#else
-#define DBG_CLK(v)
-#endif
+
 
 // The common-case readMiniBlockHeader over 16 bytes (a = bytes 0-7, b = 8-15): varint minDelta of
 // <= 8 bytes, value in range, mbc width bytes <= the limit.  Returns the header length or 0.
@@ -276,47 +273,42 @@ __device__ __forceinline__ uint64_t small_bytes(uint64_t x, uint64_t lim) {
   return ~(((x & 0x7f7f7f7f7f7f7f7full) + (0x7f - lim) * 0x0101010101010101ull) | x) & 0x8080808080808080ull;
 }
 
-// Per lane: the first position in [s0, s1) whose header parses and whose successor parses too
-// (s1 if none).  32 positions per step: a byte-parallel filter keeps the positions p whose byte is
-// a varint terminator (< 0x80) followed by mbc bytes <= the width limit, and only those get a full
-// parse.  A header whose varint ends at byte p has the same widths and successor as the 1-byte
-// varint at p, so p stands for every start of that varint (the stitch resolves which is true).
+// Per lane: the first position in [s0, s1) whose header parses (s1 if none).  32 positions per
+// step: a byte-parallel filter keeps the positions p whose byte is a varint terminator (< 0x80)
+// followed by mbc bytes <= the width limit, and only those get a full parse (L1-hot).  A header
+// whose varint ends at byte p has the same widths and successor as the 1-byte varint at p, so p
+// stands for every start of that varint (the stitch resolves which one is true).
 __device__ int64_t spec_sync(const uint8_t* img, int64_t s0, int64_t s1, int64_t e, bool is64, int mbc,
-                             int gbytes) {
+                                          int gbytes) {
   const uint64_t lim = is64 ? 64 : 32;
-  for (int64_t base = s0 & ~int64_t(15); base < s1; base += 32) {
-    if (e - base < 64) {  // stream tail: position by position
-      for (int64_t p = base > s0 ? base : s0; p < s1; p++) {
-        uint64_t md, wd;
-        int64_t dat, n1, n2;
-        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1) &&
-            hdr_global(img, n1, e, is64, mbc, gbytes, md, wd, dat, n2))
-          return p;
+  for (int64_t base = s0 & ~int64_t(7); base < s1; base += 32) {
+    uint64_t cand[4];
+    if (e - base < 64) {  // stream tail: every position
+      cand[0] = cand[1] = cand[2] = cand[3] = 0x8080808080808080ull;
+    } else {
+      const gptr64 q = (gptr64)(img + base);
+      uint64_t x0 = q[0], S0 = small_bytes(x0, lim);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint64_t x1 = q[j + 1], S1 = small_bytes(x1, lim);
+        uint64_t c = ~x0 & 0x8080808080808080ull;
+        for (int k = 1; k <= mbc; k++) c &= k == 8 ? S1 : (S0 >> (8 * k)) | (S1 << (64 - 8 * k));
+        cand[j] = c;
+        x0 = x1;
+        S0 = S1;
       }
-      return s1;
     }
-    const gptr64 q = (gptr64)(img + base);
-    uint64_t x[5], S[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-      x[j] = q[j];
-      S[j] = small_bytes(x[j], lim);
-    }
-#pragma unroll
     for (int j = 0; j < 4; j++) {
-      uint64_t cand = ~x[j] & 0x8080808080808080ull;
-      for (int k = 1; k <= mbc; k++) cand &= k == 8 ? S[j + 1] : (S[j] >> (8 * k)) | (S[j + 1] << (64 - 8 * k));
+      uint64_t c = cand[j];
       const int64_t w0 = base + 8 * j;
-      if (s0 > w0) cand &= s0 - w0 >= 8 ? 0 : ~0ull << (8 * (s0 - w0));
-      if (s1 - w0 < 8) cand &= s1 <= w0 ? 0 : (1ull << (8 * (s1 - w0))) - 1;
-      while (cand) {
-        const int64_t p = w0 + (__builtin_ctzll(cand) >> 3);
-        cand &= cand - 1;
+      if (s0 > w0) c &= s0 - w0 >= 8 ? 0 : ~0ull << (8 * (s0 - w0));
+      if (s1 - w0 < 8) c &= s1 <= w0 ? 0 : (1ull << (8 * (s1 - w0))) - 1;
+      while (c) {
+        const int64_t p = w0 + (__builtin_ctzll(c) >> 3);
+        c &= c - 1;
         uint64_t md, wd;
-        int64_t dat, n1, n2;
-        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1) &&
-            hdr_global(img, n1, e, is64, mbc, gbytes, md, wd, dat, n2))
-          return p;
+        int64_t dat, n1;
+        if (hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1)) return p;
       }
     }
   }
@@ -329,24 +321,10 @@ __device__ int64_t spec_sync(const uint8_t* img, int64_t s0, int64_t s1, int64_t
 // the lanes; every round advances at least through lane 0's segment unless the true chain reaches
 // a header the fast parse rejects (the exact walk takes over there).
 __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, int mbc, int gbytes, int bs,
-                          int kmax, int64_t blk0_bytes, DeltaBlock* recs, int32_t* lst, int lane, int64_t& hr,
-                          bool dbg = false) {
-#ifdef PQH_DEBUG_SPEC
-  long long* g_dbg = g_dbg_all[(blockIdx.x * 4 + (threadIdx.x >> 6)) % 64];
-#endif
+                          int kmax, int64_t blk0_bytes, DeltaBlock* recs, int32_t* lst, int lane, int64_t& hr) {
   int64_t T = h1, bytes_done = blk0_bytes;
   int nb = 1;
-#ifdef PQH_DEBUG_SPEC
-  int dbg_rounds = 0, dbg_follow = 0, dbg_miss = 0;
-#endif
-  DBG_CLK(c_start);
-#ifdef PQH_DEBUG_SPEC
-  long long c_sync = 0, c_walk = 0, c_stitch = 0, c_rec = 0;
-#endif
   while (nb < kmax) {
-#ifdef PQH_DEBUG_SPEC
-    dbg_rounds++;
-#endif
     const int64_t avg = bytes_done / nb > 0 ? bytes_done / nb : 1;
     int64_t span = int64_t(kmax - nb) * avg;
     span += span / 8 + 64;
@@ -361,16 +339,16 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
     if (s0 < e) {
       uint64_t md, wd;
       int64_t dat, n1;
-      DBG_CLK(ca);
       if (lane > 0) p = spec_sync(img, s0, s1, e, is64, mbc, gbytes);
-      DBG_CLK(cb);
-#ifdef PQH_DEBUG_SPEC
-      c_sync += cb - ca;
-#endif
       while (p < s1 && cnt < kSpecCap - 1) {
         lst[cnt * 64 + lane] = int32_t(p);
         cnt++;
         if (!hdr_global(img, p, e, is64, mbc, gbytes, md, wd, dat, n1)) {
+          if (cnt == 2 && lane > 0) {  // the synchronisation point's successor does not parse: scan on
+            cnt = 0;
+            p = spec_sync(img, int64_t(lst[lane]) + 1, s1, e, is64, mbc, gbytes);
+            continue;
+          }
           dead = true;
           break;
         }
@@ -441,7 +419,6 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
         T = readlane64(p, last);
       }
     }
-    DBG_CLK(cc);
     // the rare cases, one segment at a time (wave-uniform): a block longer than a segment, a lane
     // whose walk joined the true chain late or never, a lane that outgrew its list
     for (int i = i_next; i < nseg && nb < kmax && !stop; i++) {
@@ -463,16 +440,10 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
         if (lane == 0) recs[nb] = DeltaBlock{md, int32_t(dat), int32_t(int64_t(nb) * bs), wd, 0};
         nb++;
         T = nx;
-#ifdef PQH_DEBUG_SPEC
-        dbg_follow++;
-#endif
         m = __ballot(lane < ci && lst[lane * 64 + i] == int32_t(T));
       }
       if (stop || nb >= kmax) break;
       if (T >= seg_end) continue;
-#ifdef PQH_DEBUG_SPEC
-      if (!m) dbg_miss++;
-#endif
       if (!m) break;  // lane i's walk never met the true chain: next round from T
       const int jj = __builtin_ctzll(m);
       int n = ci - jj - (di ? 1 : 0);
@@ -487,54 +458,26 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
       if (di) stop = true;
       if (di || fi) break;
     }
-    DBG_CLK(cd);
     // records: header positions only (pad = 1), parsed by their consumers
     for (int k = 0; k < my_n; k++) {
       const int b = my_base + k;
       recs[b] = DeltaBlock{0, lst[(my_j + k) * 64 + lane], int32_t(int64_t(b) * bs), 0, 1};
     }
-#ifdef PQH_DEBUG_SPEC
-    {
-      DBG_CLK(ce);
-      c_stitch += cd - cc;
-      c_rec += ce - cd;
-      c_walk = cc - c_start;
-    }
-#endif
     if (nb == nb0 || stop) break;
     bytes_done += T - T0;
   }
   wave_lds_sync();
-#ifdef PQH_DEBUG_SPEC
-  {
-    long long mxs = c_sync;
-    for (int off = 32; off > 0; off >>= 1) mxs = max(mxs, (long long)__shfl_xor(mxs, off, 64));
-    if (dbg) {
-      g_dbg[0] = kmax; g_dbg[1] = nb; g_dbg[2] = dbg_rounds; g_dbg[3] = dbg_follow; g_dbg[4] = dbg_miss;
-      g_dbg[5] = mxs; g_dbg[6] = c_walk; g_dbg[7] = c_stitch; g_dbg[8] = c_rec;
-    }
-  }
-#endif
   hr = T;
   return nb;
 }
 
-// The block walk of one page (whole wave, uniform).  Returns the first error key.
-// init_all: byteArrayDeltaLengthDecoder.init (type_bytearray.go:104-116) decodes ALL valuesCount
-// lengths at page load: every error is a load error (phase 0, step 3) and nn is ignored.
-__device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaBlock* recs, int32_t cap,
-                               DeltaState& D, int lane, bool init_all, bool dbg = false) {
-  D.mode = DM_NONE;
-  D.nblocks = 0;
-  D.limit = 0;
-  D.first = 0;
-  D.end_pos = vs;
-  D.rec_base = 0;
-  D.pad = 0;
-  int64_t pos = vs;
+// deltaBitPackDecoder.init (page load, phase 0 step 3): readBlockHeader + the first
+// readMiniBlockHeader.  D.mode = DM_FAST (geometry of the data-parallel path; pos = block 0's data),
+// DM_SERIAL (other geometries: the exact sequential decoder redoes the page) or an error key.
+__device__ uint64_t delta_init(Win& w, int64_t& pos, bool is64, DeltaState& D, int32_t& vc, uint64_t& md,
+                               uint64_t& widths, int lane) {
   int st;
-  // ---- init (page load, phase 0 step 3): readBlockHeader + readMiniBlockHeader ----
-  int32_t bs, mbc, vc;
+  int32_t bs, mbc;
   if ((st = win_uvar32(w, pos, bs, lane))) return err_key(0, 3, st);
   if ((st = win_uvar32(w, pos, mbc, lane))) return err_key(0, 3, st);
   if (mbc <= 0 || bs % mbc != 0) return err_key(0, 3, PQH_ERR_DELTA_MINIBLOCKS);
@@ -549,12 +492,42 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   D.first = first;
   const bool fast = mbc <= 8 && (mbvc & 7) == 0 && bs >= kDeltaBlockMin && (2048 % bs) == 0;
   if (!fast) {
-    D.mode = DM_SERIAL;  // exact sequential decoder (TK_DELTA_SERIAL) redoes the page
+    D.mode = DM_SERIAL;
     return kNoError;
   }
-  uint64_t md, widths;
   if ((st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) return err_key(0, 3, st);
   D.mode = DM_FAST;
+  return kNoError;
+}
+
+// Whole blocks [0, kmax): every group read of blocks before the padding-skip group and the last
+// reachable position succeeds when the block lies inside the stream.
+__device__ __forceinline__ int64_t delta_whole_blocks(int64_t nn, int32_t vc, int32_t bs, int32_t cap) {
+  const int64_t L = nn < vc ? nn : vc;
+  const int64_t pstar = vc <= 8 ? 0 : ((int64_t(vc) - 8 + 7) / 8) * 8;
+  const int64_t lp = L < pstar ? L : pstar;
+  return lp / bs < cap ? lp / bs : cap;
+}
+
+// The block walk of one page (whole wave, uniform).  Returns the first error key.
+// init_all: byteArrayDeltaLengthDecoder.init (type_bytearray.go:104-116) decodes ALL valuesCount
+// lengths at page load: every error is a load error (phase 0, step 3) and nn is ignored.
+__device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaBlock* recs, int32_t cap,
+                               DeltaState& D, int lane, bool init_all, int spec_r = 0, int64_t spec_hr = 0) {
+  D.mode = DM_NONE;
+  D.nblocks = 0;
+  D.limit = 0;
+  D.first = 0;
+  D.end_pos = vs;
+  D.rec_base = 0;
+  D.pad = 0;
+  int64_t pos = vs;
+  int st;
+  int32_t vc;
+  uint64_t md, widths;
+  const uint64_t ik = delta_init(w, pos, is64, D, vc, md, widths, lane);
+  if (ik != kNoError || D.mode != DM_FAST) return ik;
+  const int32_t bs = D.block_size, mbc = D.mb_count, mbvc = D.mbvc;
   // ---- readValues: positions [0, nn) (phase 3) ----
   if (init_all) nn = vc;
   const int64_t L = nn < vc ? nn : vc;                                 // reachable positions
@@ -564,21 +537,12 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   int64_t limit = nn;
   bool padded = false;
   int64_t b_start = 0;
-  {
-    // whole blocks [0, kmax): before the padding group and the last reachable position
-    const int64_t lp = L < pstar ? L : pstar;
-    const int64_t kmax = lp / bs < cap ? lp / bs : cap;
-    const int64_t nb0 = block_data_bytes(widths, mbvc);
-    if (kmax >= 2 && pos + nb0 <= w.e) {
-      if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), 0, widths, 0};
-      int64_t hr;
-      const int r = spec_chain(w.img, pos + nb0, w.e, is64, mbc, mbvc / 8, bs, int(kmax), pos + nb0 - vs, recs,
-                               reinterpret_cast<int32_t*>(w.buf), lane, hr, dbg);
-      D.nblocks = r;
-      b_start = r;
-      pos = hr;
-      w.lo = w.hi = 0;  // the window held the lane lists
-    }
+  if (spec_r >= 2 && spec_r <= delta_whole_blocks(nn, vc, bs, cap)) {
+    // blocks [1, spec_r) recorded by k_delta_spec; resume at block spec_r's header
+    if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), 0, widths, 0};
+    D.nblocks = spec_r;
+    b_start = spec_r;
+    pos = spec_hr;
   }
   for (int64_t b = b_start; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
     const int64_t p0 = b * bs;
@@ -644,6 +608,47 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
 }
 
 // One wave per delta page.
+// k_delta_spec: one wave per delta page, before k_delta_walk.  The page's init (as delta_walk), then
+// the speculative chain of its whole blocks [1, kmax): records written, (blocks found, header of the
+// next block) left in dstates[p].nblocks / end_pos for the walk to resume from.  DELTA_BYTE_ARRAY
+// suffix streams start where the prefix stream ends and are walked by k_delta_walk alone.
+__global__ __launch_bounds__(256) void k_delta_spec(DevBatch b, const int32_t* delta_pages, int32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kWin];
+  const int lane = threadIdx.x & 63;
+  const int wv = int(threadIdx.x >> 6);
+  const int idx = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+  if (idx >= n) return;
+  const int p = delta_pages[idx];
+  const DevPage P = b.pages[p];
+  const PageState S = b.states[p];
+  int r = 0;
+  int64_t hr = 0;
+  const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
+  if (P.host_err == kNoError && load_ok) {
+    Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
+    win_load(w, S.val_s, lane);
+    const bool is64 = P.kind == K_DELTA64;
+    const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+    DeltaState D;
+    int32_t vc;
+    uint64_t md, widths;
+    int64_t pos = S.val_s;
+    if (delta_init(w, pos, is64, D, vc, md, widths, lane) == kNoError && D.mode == DM_FAST) {
+      const int64_t nn = P.kind == K_DLBA || P.kind == K_DBA ? vc : (before_values ? 0 : S.nn);
+      const int64_t kmax = delta_whole_blocks(nn, vc, D.block_size, P.dblk_cap);
+      const int64_t h1 = pos + block_data_bytes(widths, D.mbvc);
+      if (kmax >= 2 && h1 <= w.e)
+        r = spec_chain(w.img, h1, w.e, is64, D.mb_count, D.mbvc / 8, D.block_size, int(kmax), h1 - S.val_s,
+                       b.dblocks + P.dblk_base, reinterpret_cast<int32_t*>(w.buf), lane, hr);
+    }
+  }
+  if (lane == 0) {
+    b.dstates[p].nblocks = r;
+    b.dstates[p].end_pos = hr;
+  }
+}
+
+// One wave per delta page.
 __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* delta_pages, int32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kWin];
   const int lane = threadIdx.x & 63;
@@ -653,6 +658,8 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   const int p = delta_pages[idx];
   const DevPage P = b.pages[p];
   const PageState S = b.states[p];
+  const int spec_r = __builtin_amdgcn_readfirstlane(b.dstates[p].nblocks);
+  const int64_t spec_hr = rfl64(uint64_t(b.dstates[p].end_pos));
   DeltaState D, D1;
   D.mode = D1.mode = DM_NONE;
   D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.pad = 0;
@@ -668,20 +675,8 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
     win_load(w, S.val_s, lane);
     const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
     DeltaBlock* recs = b.dblocks + P.dblk_base;
-    DBG_CLK(c0);
-#ifdef PQH_DEBUG_SPEC
-    const long long w0 = wall_clock64();
-#endif
     err = delta_walk(w, S.val_s, P.kind == K_DELTA64, before_values ? 0 : S.nn, recs, P.dblk_cap, D, lane,
-                     P.kind == K_DLBA || dba, idx % 997 == 0);
-#ifdef PQH_DEBUG_SPEC
-    DBG_CLK(c1);
-    if (lane == 0 && idx % 997 == 0) {
-      const long long* g = g_dbg_all[idx % 64];
-      printf("page %d walk total %lld | kmax %lld nb %lld rounds %lld follow %lld miss %lld | sync(max) %lld sync+walk %lld stitch %lld rec %lld | wall %lld\n",
-             p, c1 - c0, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], (long long)(wall_clock64() - w0));
-    }
-#endif
+                     P.kind == K_DLBA || dba, spec_r, spec_hr);
     if (dba && err == kNoError) {
       // byteArrayDeltaDecoder.init (type_bytearray.go:195-211): prefix lengths, then the
       // DELTA_LENGTH suffix decoder on the rest; both decode every length at load
@@ -1008,29 +1003,14 @@ __global__ __launch_bounds__(256) void k_delta_scan(DevBatch b, const int32_t* d
   }
 }
 
-__global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles) {
-  __shared__ TileStageLds T;
-  __shared__ DeltaLds DL;
-  const Tile t = tiles[blockIdx.x];
-  const DeltaTileCtx c = delta_tile_ctx(b, t);
-  if (!c.ok) return;
-  const DevChunk C = b.chunks[c.P.chunk];
-  const bool lens = c.P.kind == K_DLBA || c.P.kind == K_DBA;  // int32 lengths into aux / aux2
-  const bool is64 = c.P.kind == K_DELTA64;
-  int32_t* lp = c.P.kind == K_DBA && c.stream == 0 ? C.aux2 : C.aux;
-  uint8_t* out = lens ? reinterpret_cast<uint8_t*>(lp + c.S.value_base) : C.values + c.S.value_base * c.P.value_size;
-  const uint64_t base = b.dsums[c.me];
-  if (!stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
-    if (is64) delta_tile<true>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
-    else delta_tile<false>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
-    return;
-  }
+// Rows of 1024 positions of a staged tile (4 consecutive per thread), one block scan each (wave
+// totals double-buffered by row parity); each thread stores 16 / 32 contiguous bytes.  Returns the
+// carry after the tile.
+__device__ __forceinline__ uint64_t expand_rows(TileStageLds& T, const DeltaTileCtx& c, uint8_t* out, bool is64,
+                                                uint64_t carry) {
   const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
   const int bb0 = int(c.v0 >> lbs);
-  // rows of 1024 positions (4 consecutive per thread), one block scan each (wave totals
-  // double-buffered by row parity); each thread stores 16 / 32 contiguous bytes
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t carry = base;
   int row = 0;
   for (int64_t r0 = c.v0; r0 < c.v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
@@ -1068,6 +1048,59 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
       }
     }
     carry += T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3];
+  }
+  return carry;
+}
+
+__device__ __forceinline__ uint8_t* delta_out(const DevBatch& b, const DeltaTileCtx& c) {
+  const DevChunk C = b.chunks[c.P.chunk];
+  const bool lens = c.P.kind == K_DLBA || c.P.kind == K_DBA;  // int32 lengths into aux / aux2
+  int32_t* lp = c.P.kind == K_DBA && c.stream == 0 ? C.aux2 : C.aux;
+  return lens ? reinterpret_cast<uint8_t*>(lp + c.S.value_base) : C.values + c.S.value_base * c.P.value_size;
+}
+
+__global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* tiles) {
+  __shared__ TileStageLds T;
+  __shared__ DeltaLds DL;
+  const Tile t = tiles[blockIdx.x];
+  const DeltaTileCtx c = delta_tile_ctx(b, t);
+  if (!c.ok) return;
+  const bool is64 = c.P.kind == K_DELTA64;
+  uint8_t* out = delta_out(b, c);
+  const uint64_t base = b.dsums[c.me];
+  if (!stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
+    if (is64) delta_tile<true>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+    else delta_tile<false>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+    return;
+  }
+  expand_rows(T, c, out, is64, base);
+}
+
+// k_delta_page: one workgroup per (page, stream) decodes the stream's tiles in order with a running
+// carry seeded by the first value: no tile sums, no page scan, the packed deltas are read once.
+// Used when a batch has enough delta streams to fill the GPU with one workgroup each.
+__global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* streams) {
+  __shared__ TileStageLds T;
+  __shared__ DeltaLds DL;
+  Tile t = streams[blockIdx.x];
+  DeltaTileCtx c = delta_tile_ctx(b, t);
+  if (!c.ok) return;
+  const bool is64 = c.P.kind == K_DELTA64;
+  uint8_t* out = delta_out(b, c);
+  uint64_t carry = c.D.first;
+  for (;;) {
+    __syncthreads();  // the previous tile's readers of T are done
+    if (stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
+      carry = expand_rows(T, c, out, is64, carry);
+    } else {
+      const uint64_t sum =
+          is64 ? delta_tile<true>(b, c.P, c.D, c.v0, c.v1, carry, true, out, reinterpret_cast<uint32_t*>(T.data), DL)
+               : delta_tile<false>(b, c.P, c.D, c.v0, c.v1, carry, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
+      carry += sum;
+    }
+    t.k++;
+    c = delta_tile_ctx(b, t);
+    if (!c.ok) break;
   }
 }
 

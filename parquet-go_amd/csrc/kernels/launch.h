@@ -31,12 +31,16 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
-// DELTA_BINARY_PACKED: block walk (one wave per delta page).
+// DELTA_BINARY_PACKED: speculative chain of the whole blocks, then the exact block walk (one wave
+// per delta page each).
+hipError_t launch_delta_spec(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 // Delta tiles: per-tile sums, per-page scan (seeded with the first value), expand.
 hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// Many delta streams: one workgroup per (page, stream), its tiles in order with a running carry.
+hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
 // per-chunk offset scan, offsets + byte copy.
 hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s);
