@@ -233,13 +233,24 @@ __device__ __forceinline__ void bytes16_global(const uint8_t* img, int64_t p, ui
   b = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
 }
 
+typedef uint4 uint4_a8 __attribute__((aligned(8)));
+
 // Per lane, through L2: the header at image offset p.  dat = its data, nxt = the next header; false
-// unless the common-case parse applies and the whole block lies inside the stream.
+// unless the common-case parse applies and the whole block lies inside the stream.  One 16-byte load
+// (8-byte aligned) covers headers of up to 9 - p % 8 bytes; longer ones load the next 8 bytes.
 __device__ __forceinline__ bool hdr_global(const uint8_t* img, int64_t p, int64_t e, bool is64, int mbc, int gbytes,
                                            uint64_t& md, uint64_t& wd, int64_t& dat, int64_t& nxt) {
   if (e - p < 24) return false;
-  uint64_t a, b;
-  bytes16_global(img, p, a, b);
+  const uint8_t* q = img + (p & ~int64_t(7));
+  const uint4 v = *reinterpret_cast<const uint4_a8*>(q);
+  const uint64_t x0 = uint64_t(v.x) | (uint64_t(v.y) << 32), x1 = uint64_t(v.z) | (uint64_t(v.w) << 32);
+  const uint32_t sh = uint32_t(p & 7) * 8;
+  const uint64_t a = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+  uint64_t b = sh ? x1 >> sh : x1;
+  // header bytes past q + 16: varint terminator at byte len - 1 of a, then mbc width bytes
+  const uint64_t stop = ~a & 0x8080808080808080ull;
+  const int len = stop ? (__builtin_ctzll(stop) >> 3) + 1 : 8;
+  if (sh && int(sh / 8) + len + mbc > 16) b |= ((gptr64)q)[2] << (64 - sh);
   const int hl = parse_hdr16(a, b, is64, mbc, md, wd);
   if (!hl) return false;
   dat = p + hl;
@@ -281,16 +292,21 @@ __device__ __forceinline__ uint64_t small_bytes(uint64_t x, uint64_t lim) {
 __device__ int64_t spec_sync(const uint8_t* img, int64_t s0, int64_t s1, int64_t e, bool is64, int mbc,
                                           int gbytes) {
   const uint64_t lim = is64 ? 64 : 32;
-  for (int64_t base = s0 & ~int64_t(7); base < s1; base += 32) {
+  const int64_t se = s1 < e - 24 ? s1 : e - 24;  // headers need 24 bytes before the stream end
+  for (int64_t base = s0 & ~int64_t(15); base < se; base += 32) {
     uint64_t cand[4];
-    if (e - base < 64) {  // stream tail: every position
-      cand[0] = cand[1] = cand[2] = cand[3] = 0x8080808080808080ull;
-    } else {
-      const gptr64 q = (gptr64)(img + base);
-      uint64_t x0 = q[0], S0 = small_bytes(x0, lim);
+    {
+      // bytes past the stream end are read from the following image or the payload pad (>= 256
+      // zero bytes after the last image) and never accepted: hdr_global wants 24 bytes before e
+      const uint4* q4 = reinterpret_cast<const uint4*>(img + base);
+      const uint4 c0 = q4[0], c1 = q4[1], c2 = q4[2];
+      const uint64_t x[5] = {uint64_t(c0.x) | (uint64_t(c0.y) << 32), uint64_t(c0.z) | (uint64_t(c0.w) << 32),
+                             uint64_t(c1.x) | (uint64_t(c1.y) << 32), uint64_t(c1.z) | (uint64_t(c1.w) << 32),
+                             uint64_t(c2.x) | (uint64_t(c2.y) << 32)};
+      uint64_t x0 = x[0], S0 = small_bytes(x0, lim);
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const uint64_t x1 = q[j + 1], S1 = small_bytes(x1, lim);
+        const uint64_t x1 = x[j + 1], S1 = small_bytes(x1, lim);
         uint64_t c = ~x0 & 0x8080808080808080ull;
         for (int k = 1; k <= mbc; k++) c &= k == 8 ? S1 : (S0 >> (8 * k)) | (S1 << (64 - 8 * k));
         cand[j] = c;
@@ -302,7 +318,7 @@ __device__ int64_t spec_sync(const uint8_t* img, int64_t s0, int64_t s1, int64_t
       uint64_t c = cand[j];
       const int64_t w0 = base + 8 * j;
       if (s0 > w0) c &= s0 - w0 >= 8 ? 0 : ~0ull << (8 * (s0 - w0));
-      if (s1 - w0 < 8) c &= s1 <= w0 ? 0 : (1ull << (8 * (s1 - w0))) - 1;
+      if (se - w0 < 8) c &= se <= w0 ? 0 : (1ull << (8 * (se - w0))) - 1;
       while (c) {
         const int64_t p = w0 + (__builtin_ctzll(c) >> 3);
         c &= c - 1;
@@ -851,6 +867,7 @@ struct TileStageLds {
   uint8_t mbw[kTileBlocks][8];
   uint64_t md[kTileBlocks];
   uint64_t wtot[2][4];
+  uint64_t wtot2[2][4];
   int32_t fits;
   int32_t pad;
 };
@@ -940,8 +957,8 @@ __device__ __forceinline__ DeltaTileCtx delta_tile_ctx(const DevBatch& b, const 
 }
 
 // delta + minDelta of the 4 positions p..p+3 (p % 4 == 0: one miniblock, miniblocks hold >= 8).
-__device__ __forceinline__ void staged_delta4(const TileStageLds& T, int64_t p, int bb0, int lbs, int lmb,
-                                              uint64_t d[4]) {
+template <class L>
+__device__ __forceinline__ void staged_delta4(const L& T, int64_t p, int bb0, int lbs, int lmb, uint64_t d[4]) {
   const int32_t q = int32_t(p);
   const int blk = (q >> lbs) - bb0;
   const int r = q & ((1 << lbs) - 1);
@@ -1003,47 +1020,110 @@ __global__ __launch_bounds__(256) void k_delta_scan(DevBatch b, const int32_t* d
   }
 }
 
-// Rows of 1024 positions of a staged tile (4 consecutive per thread), one block scan each (wave
-// totals double-buffered by row parity); each thread stores 16 / 32 contiguous bytes.  Returns the
-// carry after the tile.
-__device__ __forceinline__ uint64_t expand_rows(TileStageLds& T, const DeltaTileCtx& c, uint8_t* out, bool is64,
-                                                uint64_t carry) {
-  const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
-  const int bb0 = int(c.v0 >> lbs);
+// DPP move of both halves of a 64-bit value (lanes without a source read 0).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, int(uint32_t(x)), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(uint32_t(x >> 32)), CTRL, ROWS, 0xf, false);
+  return uint64_t(uint32_t(lo)) | (uint64_t(uint32_t(hi)) << 32);
+}
+
+// Inclusive wave64 scan (wrapping uint64): row_shr 1/2/4/8 inside each row of 16 lanes, then
+// row_bcast:15 / row_bcast:31 carry the row totals across (GFX9 DPP, no LDS round trips).
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+  x += dpp64<0x111, 0xf>(x);
+  x += dpp64<0x112, 0xf>(x);
+  x += dpp64<0x114, 0xf>(x);
+  x += dpp64<0x118, 0xf>(x);
+  x += dpp64<0x142, 0xa>(x);
+  x += dpp64<0x143, 0xc>(x);
+  return x;
+}
+
+// delta + minDelta of the 2 positions p, p+1 (p even: one miniblock).
+template <class L>
+__device__ __forceinline__ void staged_delta2(const L& T, int64_t p, int bb0, int lbs, int lmb, uint64_t d[2]) {
+  const int32_t q = int32_t(p);
+  const int blk = (q >> lbs) - bb0;
+  const int r = q & ((1 << lbs) - 1);
+  const int m = r >> lmb;
+  const int wm = T.mbw[blk][m];
+  const uint64_t md = T.md[blk];
+  const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
+  d[0] = extract64(T.data, bit, wm) + md;
+  d[1] = extract64(T.data, bit + uint32_t(wm), wm) + md;
+}
+
+// Rows of 1024 positions of a staged tile, one block scan each (wave totals double-buffered by row
+// parity).  Every store instruction writes 16 contiguous bytes per lane, 1 KiB per wave: int32
+// values 4 consecutive per thread; int64 values 2 consecutive per thread in each half row (two
+// independent scans).  Returns the carry after the tile.
+template <class L>
+__device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, int lbs, int lmb, uint8_t* out,
+                                                bool is64, uint64_t carry) {
+  const int bb0 = int(v0 >> lbs);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int row = 0;
-  for (int64_t r0 = c.v0; r0 < c.v1; r0 += 4 * kBlock, row ^= 1) {
+  if (is64) {
+    uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
+    for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
+      const int64_t pa = r0 + 2 * int64_t(threadIdx.x), pb = pa + 2 * kBlock;
+      uint64_t a[2] = {0, 0}, c[2] = {0, 0};
+      if (pa < v1) staged_delta2(T, pa, bb0, lbs, lmb, a);
+      if (pb < v1) staged_delta2(T, pb, bb0, lbs, lmb, c);
+      a[1] = pa + 1 < v1 ? a[1] : 0;
+      c[0] = pb < v1 ? c[0] : 0;
+      c[1] = pb + 1 < v1 ? c[1] : 0;
+      const uint64_t sa = a[0] + a[1], sb = c[0] + c[1];
+      const uint64_t ia = wave_incl_scan(sa), ib = wave_incl_scan(sb);
+      if (lane == 63) {
+        T.wtot[row][wv] = ia;
+        T.wtot2[row][wv] = ib;
+      }
+      __syncthreads();
+      const uint64_t ta = T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3];
+      uint64_t va = carry + ia - sa, vb = carry + ta + ib - sb;
+      for (int k = 0; k < wv; k++) {
+        va += T.wtot[row][k];
+        vb += T.wtot2[row][k];
+      }
+      if (pa + 2 <= v1) {
+        const uint64_t o2[2] = {va, va + a[0]};
+        __builtin_memcpy(o64 + pa, o2, 16);
+      } else if (pa < v1) {
+        o64[pa] = va;
+      }
+      if (pb + 2 <= v1) {
+        const uint64_t o2[2] = {vb, vb + c[0]};
+        __builtin_memcpy(o64 + pb, o2, 16);
+      } else if (pb < v1) {
+        o64[pb] = vb;
+      }
+      carry += ta + T.wtot2[row][0] + T.wtot2[row][1] + T.wtot2[row][2] + T.wtot2[row][3];
+    }
+    return carry;
+  }
+  uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+  for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
     uint64_t d[4] = {0, 0, 0, 0};
-    if (p < c.v1) staged_delta4(T, p, bb0, lbs, lmb, d);
+    if (p < v1) staged_delta4(T, p, bb0, lbs, lmb, d);
 #pragma unroll
-    for (int j = 0; j < 4; j++) d[j] = p + j < c.v1 ? d[j] : 0;
+    for (int j = 0; j < 4; j++) d[j] = p + j < v1 ? d[j] : 0;
     const uint64_t tsum = d[0] + d[1] + d[2] + d[3];
-    uint64_t incl = tsum;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint64_t y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
-    }
+    const uint64_t incl = wave_incl_scan(tsum);
     if (lane == 63) T.wtot[row][wv] = incl;
     __syncthreads();
     uint64_t v = carry + incl - tsum;
     for (int k = 0; k < wv; k++) v += T.wtot[row][k];
-    if (p + 4 <= c.v1) {
-      if (is64) {
-        const uint64_t o4[4] = {v, v + d[0], v + d[0] + d[1], v + d[0] + d[1] + d[2]};
-        __builtin_memcpy(reinterpret_cast<uint64_t*>(out) + p, o4, 32);
-      } else {
-        const uint32_t o4[4] = {uint32_t(v), uint32_t(v + d[0]), uint32_t(v + d[0] + d[1]),
-                                uint32_t(v + d[0] + d[1] + d[2])};
-        __builtin_memcpy(reinterpret_cast<uint32_t*>(out) + p, o4, 16);
-      }
+    if (p + 4 <= v1) {
+      const uint32_t o4[4] = {uint32_t(v), uint32_t(v + d[0]), uint32_t(v + d[0] + d[1]),
+                              uint32_t(v + d[0] + d[1] + d[2])};
+      __builtin_memcpy(o32 + p, o4, 16);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        if (p + j < c.v1) {
-          if (is64) reinterpret_cast<uint64_t*>(out)[p + j] = v;
-          else reinterpret_cast<uint32_t*>(out)[p + j] = uint32_t(v);
-        }
+        if (p + j < v1) o32[p + j] = uint32_t(v);
         v += d[j];
       }
     }
@@ -1051,6 +1131,9 @@ __device__ __forceinline__ uint64_t expand_rows(TileStageLds& T, const DeltaTile
   }
   return carry;
 }
+
+
+
 
 __device__ __forceinline__ uint8_t* delta_out(const DevBatch& b, const DeltaTileCtx& c) {
   const DevChunk C = b.chunks[c.P.chunk];
@@ -1073,34 +1156,93 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
     else delta_tile<false>(b, c.P, c.D, c.v0, c.v1, base, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
     return;
   }
-  expand_rows(T, c, out, is64, base);
+  expand_rows(T, c.v0, c.v1, __builtin_ctz(uint32_t(c.D.block_size)), __builtin_ctz(uint32_t(c.D.mbvc)), out, is64,
+              base);
 }
 
-// k_delta_page: one workgroup per (page, stream) decodes the stream's tiles in order with a running
+// k_delta_page: one workgroup per (page, stream) decodes the stream's blocks in order with a running
 // carry seeded by the first value: no tile sums, no page scan, the packed deltas are read once.
-// Used when a batch has enough delta streams to fill the GPU with one workgroup each.
+// Used when a batch has enough delta streams to fill the GPU with one workgroup each.  Tiles are cut
+// by bytes: as many blocks (<= 64) as fit a 16 KiB stage, so that several workgroups share a CU.
+constexpr int kPageStage = 16384 + 64;  // >= one block of 2048 64-bit deltas + alignment lead
+
+struct PageTileLds {
+  uint32_t data[kPageStage / 4 + 4];
+  int32_t mbbit[kTileBlocks][8];  // first bit of each miniblock's data in `data`
+  uint8_t mbw[kTileBlocks][8];
+  uint64_t md[kTileBlocks];
+  uint64_t wtot[2][4];
+  uint64_t wtot2[2][4];
+  int64_t a0;
+  int32_t nfit;
+  int32_t end;
+};
+
 __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* streams) {
-  __shared__ TileStageLds T;
-  __shared__ DeltaLds DL;
-  Tile t = streams[blockIdx.x];
-  DeltaTileCtx c = delta_tile_ctx(b, t);
+  __shared__ PageTileLds T;
+  const DeltaTileCtx c = delta_tile_ctx(b, streams[blockIdx.x]);
   if (!c.ok) return;
   const bool is64 = c.P.kind == K_DELTA64;
   uint8_t* out = delta_out(b, c);
+  int64_t vlim = c.D.limit;
+  if ((c.P.kind == K_DLBA || c.P.kind == K_DBA) && vlim > c.S.nn) vlim = c.S.nn;
+  const int lbs = __builtin_ctz(uint32_t(c.D.block_size)), lmb = __builtin_ctz(uint32_t(c.D.mbvc));
+  const int mbc = c.D.mb_count, gbytes = c.D.mbvc / 8;
+  const uint8_t* img = b.payload + c.P.image_off;
+  const DeltaBlock* recs = b.dblocks + c.P.dblk_base + c.D.rec_base;
+  const int64_t nblk = (vlim + c.D.block_size - 1) >> lbs;
+  const int64_t e = c.P.image_len;
+  const int tid = threadIdx.x;
   uint64_t carry = c.D.first;
-  for (;;) {
+  for (int64_t blk0 = 0; blk0 < nblk;) {
     __syncthreads();  // the previous tile's readers of T are done
-    if (stage_tile(b, c.P, c.D, c.v0, c.v1, T)) {
-      carry = expand_rows(T, c, out, is64, carry);
-    } else {
-      const uint64_t sum =
-          is64 ? delta_tile<true>(b, c.P, c.D, c.v0, c.v1, carry, true, out, reinterpret_cast<uint32_t*>(T.data), DL)
-               : delta_tile<false>(b, c.P, c.D, c.v0, c.v1, carry, true, out, reinterpret_cast<uint32_t*>(T.data), DL);
-      carry += sum;
+    // block table of the next <= 64 blocks; the blocks whose bytes fit the stage form the tile
+    if (tid < 64) {
+      const bool have = blk0 + tid < nblk;
+      int32_t start = 0, end = 0;
+      if (have) {
+        const DeltaBlock r = load_block(recs, blk0 + tid, img, is64, mbc);
+        int32_t off = r.data_off;
+        start = off;
+        for (int m = 0; m < 8; m++) {
+          const int wm = m < mbc ? mb_width(r.widths, m) : 0;
+          T.mbbit[tid][m] = off;  // byte offset for now
+          T.mbw[tid][m] = uint8_t(wm);
+          off += gbytes * wm;
+        }
+        T.md[tid] = r.min_delta;
+        end = off;
+      }
+      const int32_t s0 = __builtin_amdgcn_readfirstlane(start);
+      const int64_t a0 = s0 - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(s0)) & 15);
+      const uint64_t fit = __ballot(have && int64_t(end) - a0 <= kPageStage - 16);
+      const int nfit = fit == ~0ull ? 64 : __builtin_ctzll(~fit);  // >= 1: a block never exceeds the stage
+      const int32_t end_last = __builtin_amdgcn_readlane(end, nfit - 1);
+      if (tid == 0) {
+        T.nfit = nfit;
+        T.a0 = a0;
+        T.end = end_last;
+      }
     }
-    t.k++;
-    c = delta_tile_ctx(b, t);
-    if (!c.ok) break;
+    __syncthreads();
+    const int nfit = T.nfit;
+    const int64_t a0 = T.a0, end = T.end;  // the tile's bytes run to the end of its last block's data
+    if (tid < nfit)
+      for (int m = 0; m < 8; m++) T.mbbit[tid][m] = int32_t(T.mbbit[tid][m] - a0) * 8;
+    const int64_t nvec = (end - a0 + 15) >> 4;
+    for (int64_t k = tid; k < nvec; k += kBlock) {
+      const int64_t o = a0 + k * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
+      reinterpret_cast<uint4*>(T.data)[k] = x;
+    }
+    if (tid < 4) T.data[nvec * 4 + tid] = 0;
+    __syncthreads();
+    const int64_t v0 = blk0 << lbs;
+    int64_t v1 = (blk0 + nfit) << lbs;
+    if (v1 > vlim) v1 = vlim;
+    carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+    blk0 += nfit;
   }
 }
 
