@@ -119,11 +119,12 @@ struct DeltaState {
 // DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
 // DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).
 
-// One block: header already parsed; data of miniblock m starts at data_off + sum_{j<m} mbvc/8*w_j.
+// One block: data of miniblock m starts at data_off + sum_{j<m} mbvc/8*w_j.  Records of the
+// speculative walk (pad == 1) carry only hdr_off: their consumers parse the header.
 struct DeltaBlock {
   uint64_t min_delta;
   int32_t data_off;       // image offset of the first miniblock's data
-  int32_t first_pos;      // position (value index) of the block's first delta
+  int32_t hdr_off;        // image offset of the block's header (varint minDelta)
   uint64_t widths;        // miniblock bit widths, 8 bits each (mb_count <= 8 on the fast path)
   uint64_t pad;
 };

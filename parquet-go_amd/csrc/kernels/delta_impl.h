@@ -453,7 +453,7 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
           stop = true;
           break;
         }
-        if (lane == 0) recs[nb] = DeltaBlock{md, int32_t(dat), int32_t(int64_t(nb) * bs), wd, 0};
+        if (lane == 0) recs[nb] = DeltaBlock{md, int32_t(dat), int32_t(T), wd, 0};
         nb++;
         T = nx;
         m = __ballot(lane < ci && lst[lane * 64 + i] == int32_t(T));
@@ -477,7 +477,8 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
     // records: header positions only (pad = 1), parsed by their consumers
     for (int k = 0; k < my_n; k++) {
       const int b = my_base + k;
-      recs[b] = DeltaBlock{0, lst[(my_j + k) * 64 + lane], int32_t(int64_t(b) * bs), 0, 1};
+      const int32_t h = lst[(my_j + k) * 64 + lane];
+      recs[b] = DeltaBlock{0, h, h, 0, 1};
     }
     if (nb == nb0 || stop) break;
     bytes_done += T - T0;
@@ -491,7 +492,7 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
 // readMiniBlockHeader.  D.mode = DM_FAST (geometry of the data-parallel path; pos = block 0's data),
 // DM_SERIAL (other geometries: the exact sequential decoder redoes the page) or an error key.
 __device__ uint64_t delta_init(Win& w, int64_t& pos, bool is64, DeltaState& D, int32_t& vc, uint64_t& md,
-                               uint64_t& widths, int lane) {
+                               uint64_t& widths, int lane, int64_t* hdr0 = nullptr) {
   int st;
   int32_t bs, mbc;
   if ((st = win_uvar32(w, pos, bs, lane))) return err_key(0, 3, st);
@@ -511,6 +512,7 @@ __device__ uint64_t delta_init(Win& w, int64_t& pos, bool is64, DeltaState& D, i
     D.mode = DM_SERIAL;
     return kNoError;
   }
+  if (hdr0) *hdr0 = pos;
   if ((st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) return err_key(0, 3, st);
   D.mode = DM_FAST;
   return kNoError;
@@ -541,7 +543,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   int st;
   int32_t vc;
   uint64_t md, widths;
-  const uint64_t ik = delta_init(w, pos, is64, D, vc, md, widths, lane);
+  int64_t hpos = pos;  // header of the block being read
+  const uint64_t ik = delta_init(w, pos, is64, D, vc, md, widths, lane, &hpos);
   if (ik != kNoError || D.mode != DM_FAST) return ik;
   const int32_t bs = D.block_size, mbc = D.mb_count, mbvc = D.mbvc;
   // ---- readValues: positions [0, nn) (phase 3) ----
@@ -555,13 +558,14 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   int64_t b_start = 0;
   if (spec_r >= 2 && spec_r <= delta_whole_blocks(nn, vc, bs, cap)) {
     // blocks [1, spec_r) recorded by k_delta_spec; resume at block spec_r's header
-    if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), 0, widths, 0};
+    if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), int32_t(hpos), widths, 0};
     D.nblocks = spec_r;
     b_start = spec_r;
     pos = spec_hr;
   }
   for (int64_t b = b_start; int64_t(b) * bs < L && !padded && err == kNoError; b++) {
     const int64_t p0 = b * bs;
+    if (b > 0) hpos = pos;
     if (b > 0 && !fast_block_header(w, pos, is64, mbc, md, widths, lane) &&
         (st = win_miniblock_header(w, pos, is64, mbc, md, widths, lane))) {
       err = init_all ? err_key(0, 3, st) : err_key(3, p0, st);
@@ -572,7 +576,7 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
       D.mode = DM_SERIAL;
       return kNoError;
     }
-    if (lane == 0) recs[D.nblocks] = DeltaBlock{md, int32_t(pos), int32_t(p0), widths, 0};
+    if (lane == 0) recs[D.nblocks] = DeltaBlock{md, int32_t(pos), int32_t(hpos), widths, 0};
     D.nblocks++;
     // a whole block before the padding group and the last reachable position, inside the stream:
     // every group read succeeds
@@ -732,6 +736,18 @@ __device__ __forceinline__ uint64_t extract64(const uint32_t* stage, uint32_t bi
   const uint64_t lo = uint64_t(stage[k]) | (uint64_t(stage[k + 1]) << 32);
   uint64_t v = s ? ((lo >> s) | (uint64_t(stage[k + 2]) << (64 - s))) : lo;
   return w >= 64 ? v : (v & ((1ull << w) - 1));
+}
+
+// n values of width w <= 32 starting at `bit`: one funnel shift each (v_alignbit) from the two
+// dwords holding it; w == 0 gives zeros.
+template <int N>
+__device__ __forceinline__ void extract32n(const uint32_t* stage, uint32_t bit, int w, uint64_t md, uint64_t* d) {
+  const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const uint32_t bj = bit + uint32_t(j * w), k = bj >> 5;
+    d[j] = uint64_t(__builtin_amdgcn_alignbit(stage[k + 1], stage[k], bj & 31) & mask) + md;
+  }
 }
 
 // Inclusive block-wide scan of one uint64 per thread; returns the exclusive prefix, *total set.
@@ -966,8 +982,12 @@ __device__ __forceinline__ void staged_delta4(const L& T, int64_t p, int bb0, in
   const int wm = T.mbw[blk][m];
   const uint64_t md = T.md[blk];
   const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
+  if (wm <= 32) {
+    extract32n<4>(T.data, bit, wm, md, d);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 4; j++) d[j] = extract64(T.data, bit + uint32_t(j * wm), wm) + md;
+    for (int j = 0; j < 4; j++) d[j] = extract64(T.data, bit + uint32_t(j * wm), wm) + md;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_delta_sum(DevBatch b, const Tile* tiles) {
@@ -1040,6 +1060,8 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   return x;
 }
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 // delta + minDelta of the 2 positions p, p+1 (p even: one miniblock).
 template <class L>
 __device__ __forceinline__ void staged_delta2(const L& T, int64_t p, int bb0, int lbs, int lmb, uint64_t d[2]) {
@@ -1050,8 +1072,12 @@ __device__ __forceinline__ void staged_delta2(const L& T, int64_t p, int bb0, in
   const int wm = T.mbw[blk][m];
   const uint64_t md = T.md[blk];
   const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
-  d[0] = extract64(T.data, bit, wm) + md;
-  d[1] = extract64(T.data, bit + uint32_t(wm), wm) + md;
+  if (wm <= 32) {
+    extract32n<2>(T.data, bit, wm, md, d);
+  } else {
+    d[0] = extract64(T.data, bit, wm) + md;
+    d[1] = extract64(T.data, bit + uint32_t(wm), wm) + md;
+  }
 }
 
 // Rows of 1024 positions of a staged tile, one block scan each (wave totals double-buffered by row
@@ -1088,14 +1114,12 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
         vb += T.wtot2[row][k];
       }
       if (pa + 2 <= v1) {
-        const uint64_t o2[2] = {va, va + a[0]};
-        __builtin_memcpy(o64 + pa, o2, 16);
+        __builtin_nontemporal_store(u64x2{va, va + a[0]}, reinterpret_cast<u64x2*>(o64 + pa));
       } else if (pa < v1) {
         o64[pa] = va;
       }
       if (pb + 2 <= v1) {
-        const uint64_t o2[2] = {vb, vb + c[0]};
-        __builtin_memcpy(o64 + pb, o2, 16);
+        __builtin_nontemporal_store(u64x2{vb, vb + c[0]}, reinterpret_cast<u64x2*>(o64 + pb));
       } else if (pb < v1) {
         o64[pb] = vb;
       }
