@@ -56,8 +56,9 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_delta_walk", "k_delta_expand", "k_delta_sum_scan",
                               "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
-                              "k_dba_prefix", "k_delta_spec", "k_delta_page"};
-constexpr int kNumKernels = 18;
+                              "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
+                              "k_delta_fused"};
+constexpr int kNumKernels = 20;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 1024;
@@ -132,6 +133,8 @@ struct pqh_batch {
   std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
   std::vector<Tile> delta_streams;  // k_delta_page work list: (page, 0, stream) with values
   bool delta_page_mode = false;
+  int32_t delta_int_pages = 0;      // page mode: DELTA_BINARY_PACKED pages first in delta_pages
+  int32_t delta_int_streams = 0;    //            and their streams first in delta_streams
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
   std::vector<int32_t> ba_pages;    // k_ba_walk work list (PLAIN byte-array data + dictionary pages)
@@ -490,6 +493,21 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
+    if (b->delta_page_mode) {
+      // DELTA_BINARY_PACKED pages (chased + decoded by k_delta_fused after the value scan) before
+      // the length streams of byte-array pages (walked before the scan: all their errors are load
+      // errors that the scan must see)
+      auto is_int = [&](int32_t p) {
+        const int32_t k = b->hpages[size_t(p)].kind;
+        return k == K_DELTA32 || k == K_DELTA64;
+      };
+      std::stable_partition(b->delta_pages.begin(), b->delta_pages.end(), is_int);
+      std::stable_partition(b->delta_streams.begin(), b->delta_streams.end(),
+                            [&](const Tile& t) { return is_int(t.page); });
+      b->delta_int_pages = int32_t(std::count_if(b->delta_pages.begin(), b->delta_pages.end(), is_int));
+      b->delta_int_streams = int32_t(std::count_if(b->delta_streams.begin(), b->delta_streams.end(),
+                                                   [&](const Tile& t) { return is_int(t.page); }));
+    }
   }
 
   // ---- device allocations ----
@@ -663,11 +681,24 @@ int pqh_batch_run(pqh_batch* b) {
   hipError_t e;
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
-  if (e == hipSuccess && ndp)
-    e = timed(16, ndp, s, [&](hipStream_t st) { return launch_delta_spec(d, b->d_delta_pages, ndp, st); });
-  if (e == hipSuccess && ndp)
-    e = timed(4, ndp, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ndp, st); });
+  // page mode: DELTA_BINARY_PACKED pages [0, ni) get their init errors now and are chased, decoded
+  // and walked after the value scan; byte-array length streams [ni, ndp) as in tile mode
+  int32_t ni = b->delta_page_mode ? b->delta_int_pages : 0;
+  if (const char* f = getenv("PQH_DELTA_FUSED"))  // experiments: "0" = speculative walk + k_delta_page
+    if (f[0] == '0') ni = 0;
+  if (e == hipSuccess && ni)
+    e = timed(18, ni, s, [&](hipStream_t st) { return launch_delta_init(d, b->d_delta_pages, ni, st); });
+  if (e == hipSuccess && ndp > ni)
+    e = timed(16, ndp - ni, s, [&](hipStream_t st) { return launch_delta_spec(d, b->d_delta_pages + ni, ndp - ni, st); });
+  if (e == hipSuccess && ndp > ni)
+    e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  if (e == hipSuccess && ni) {
+    const int32_t nis = b->delta_int_streams;
+    e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, st); });
+    if (e == hipSuccess)
+      e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
+  }
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
   if (e == hipSuccess && nbp)
     e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
@@ -809,7 +840,7 @@ int pqh_batch_sync(pqh_batch* b) {
         break;
       case K_DELTA32:
       case K_DELTA64: {  // the walks read block headers; k_delta_expand / k_delta_page read the stream once
-        const int kd = b->delta_page_mode ? 17 : 5;
+        const int kd = b->delta_page_mode ? 19 : 5;
         b->k_read[kd] += S.val_e - S.val_s;
         b->k_written[kd] += vals;
         break;

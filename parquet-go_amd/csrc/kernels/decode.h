@@ -114,7 +114,8 @@ struct DeltaState {
   uint64_t first;         // first value (bits; int32 pages sign-extended)
   int64_t end_pos;        // reader position (image offset) after the walk
   int32_t rec_base;       // first DeltaBlock of this stream within the page's records
-  int32_t pad;
+  int32_t head_blocks;    // blocks [0, head_blocks) already decoded by k_delta_fused (no records)
+  uint64_t head_carry;    // value at position head_blocks * block_size (bits)
 };
 // DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
 // DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).

@@ -61,6 +61,28 @@ __device__ int read_uvarint(const uint8_t* img, int64_t& pos, int64_t end, uint6
   return PQH_ERR_VARINT_OVERFLOW;
 }
 
+// Workgroup copy of nvec 16-byte vectors from src + 16k into LDS dst[k]; vectors at or past
+// `limit` (an offset from src) read as zeros.  Four vectors per thread are in flight at a time
+// (loads unconditional from a clamped address, then selected), so a tile costs one round trip per
+// 16 KiB instead of one per 4 KiB.
+__device__ __forceinline__ void stage_copy(uint4* dst, const uint8_t* src, int64_t nvec, int64_t limit) {
+  for (int64_t base = 0; base < nvec; base += 4 * kBlock) {
+    uint4 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int64_t k = base + threadIdx.x + j * kBlock;
+      const bool ok = k < nvec && 16 * k < limit;
+      x[j] = *reinterpret_cast<const uint4*>(src + (ok ? 16 * k : 0));
+      if (!ok) x[j] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int64_t k = base + threadIdx.x + j * kBlock;
+      if (k < nvec) dst[k] = x[j];
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t mask_w(int w) { return w >= 32 ? 0xffffffffu : ((1u << w) - 1u); }
 
 // Value i of a bit-packed run whose first group starts at byte `data`.
@@ -951,6 +973,18 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
 hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_delta_page, dim3(n), dim3(256), 0, s, b, streams);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_init, dim3((n + 3) / 4), dim3(256), 0, s, b, delta_pages, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_fused, dim3(n), dim3(256), 0, s, b, streams);
   return hipGetLastError();
 }
 

@@ -387,12 +387,15 @@ __device__ int spec_chain(const uint8_t* img, int64_t h1, int64_t e, bool is64, 
     const int64_t xl = __shfl_up(p, 1, 64), x2l = __shfl_up(x2, 1, 64);
     const bool left_ok = __shfl_up(int(exit_ok), 1, 64) != 0 && xl >= s0 && xl < s1;
     int jd = -1, j2 = -1;
-    if (lane > 0 && left_ok)
+    if (lane > 0 && left_ok) {
       for (int k = 0; k < cnt; k++) {
         const int32_t q = lst[k * 64 + lane];
         if (jd < 0 && q == int32_t(xl)) jd = k;
         if (j2 < 0 && x2l >= 0 && q == int32_t(x2l)) j2 = k;
       }
+      // the left neighbour's exit is my segment's only true header: its successor is my exit
+      if (jd < 0 && j2 < 0 && exit_ok && x2l == p) j2 = cnt;
+    }
     const bool link = lane < nseg && (lane == 0 || (left_ok && (jd >= 0 || j2 >= 0)));
     int j = lane == 0 ? 0 : (jd >= 0 ? jd : j2);
     // lane i synchronised just before T (the previous block's last data bytes continuing into T's
@@ -538,7 +541,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   D.first = 0;
   D.end_pos = vs;
   D.rec_base = 0;
-  D.pad = 0;
+  D.head_blocks = 0;
+  D.head_carry = 0;
   int64_t pos = vs;
   int st;
   int32_t vc;
@@ -556,8 +560,9 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   int64_t limit = nn;
   bool padded = false;
   int64_t b_start = 0;
-  if (spec_r >= 2 && spec_r <= delta_whole_blocks(nn, vc, bs, cap)) {
-    // blocks [1, spec_r) recorded by k_delta_spec; resume at block spec_r's header
+  if (spec_r >= 1 && spec_r <= delta_whole_blocks(nn, vc, bs, cap)) {
+    // blocks [1, spec_r) recorded by k_delta_spec, or [0, spec_r) decoded by k_delta_fused; resume
+    // at block spec_r's header
     if (lane == 0) recs[0] = DeltaBlock{md, int32_t(pos), int32_t(hpos), widths, 0};
     D.nblocks = spec_r;
     b_start = spec_r;
@@ -665,6 +670,7 @@ __global__ __launch_bounds__(256) void k_delta_spec(DevBatch b, const int32_t* d
   if (lane == 0) {
     b.dstates[p].nblocks = r;
     b.dstates[p].end_pos = hr;
+    b.dstates[p].head_blocks = 0;
   }
 }
 
@@ -680,9 +686,12 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   const PageState S = b.states[p];
   const int spec_r = __builtin_amdgcn_readfirstlane(b.dstates[p].nblocks);
   const int64_t spec_hr = rfl64(uint64_t(b.dstates[p].end_pos));
+  const int head_in = __builtin_amdgcn_readfirstlane(b.dstates[p].head_blocks);
+  const uint64_t carry_in = rfl64(b.dstates[p].head_carry);
   DeltaState D, D1;
   D.mode = D1.mode = DM_NONE;
-  D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.pad = 0;
+  D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.head_blocks = 0;
+  D.head_carry = 0;
   D.first = 0;
   D.end_pos = 0;
   D1 = D;
@@ -710,6 +719,11 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
         D1.mode = DM_SERIAL;
       }
     }
+  }
+  // blocks decoded by k_delta_fused count only if the walk resumed right after them
+  if (head_in > 0 && D.mode == DM_FAST && D.nblocks >= head_in && spec_r == head_in) {
+    D.head_blocks = head_in;
+    D.head_carry = carry_in;
   }
   if (lane == 0) {
     b.dstates[p] = D;
@@ -806,12 +820,7 @@ __device__ uint64_t delta_tile(const DevBatch& b, const DevPage& P, const DeltaS
     const int64_t a0 = start - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(start)) & 15);
     const int64_t nvec = end > a0 ? (end - a0 + 15) >> 4 : 0;
     const int64_t e = P.image_len;  // never past the page image (+pad)
-    for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
-      const int64_t o = a0 + k * 16;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
-      reinterpret_cast<uint4*>(stage)[k] = x;
-    }
+    stage_copy(reinterpret_cast<uint4*>(stage), img + a0, nvec, e - a0);
     if (threadIdx.x == 0) {
       stage[nvec * 4] = 0;
       stage[nvec * 4 + 1] = 0;
@@ -918,12 +927,7 @@ __device__ bool stage_tile(const DevBatch& b, const DevPage& P, const DeltaState
   if (threadIdx.x < nb)
     for (int m = 0; m < 8; m++) T.mbbit[threadIdx.x][m] = int32_t(T.mbbit[threadIdx.x][m] - a0) * 8;
   const int64_t e = P.image_len;
-  for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
-    const int64_t o = a0 + k * 16;
-    uint4 x = make_uint4(0, 0, 0, 0);
-    if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
-    reinterpret_cast<uint4*>(T.data)[k] = x;
-  }
+  stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, nvec, e - a0);
   if (threadIdx.x < 4) T.data[nvec * 4 + threadIdx.x] = 0;
   __syncthreads();
   return true;
@@ -1217,8 +1221,9 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
   const int64_t nblk = (vlim + c.D.block_size - 1) >> lbs;
   const int64_t e = c.P.image_len;
   const int tid = threadIdx.x;
-  uint64_t carry = c.D.first;
-  for (int64_t blk0 = 0; blk0 < nblk;) {
+  // blocks [0, head_blocks) were decoded by k_delta_fused
+  uint64_t carry = c.D.head_blocks ? c.D.head_carry : c.D.first;
+  for (int64_t blk0 = c.D.head_blocks; blk0 < nblk;) {
     __syncthreads();  // the previous tile's readers of T are done
     // block table of the next <= 64 blocks; the blocks whose bytes fit the stage form the tile
     if (tid < 64) {
@@ -1254,12 +1259,7 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
     if (tid < nfit)
       for (int m = 0; m < 8; m++) T.mbbit[tid][m] = int32_t(T.mbbit[tid][m] - a0) * 8;
     const int64_t nvec = (end - a0 + 15) >> 4;
-    for (int64_t k = tid; k < nvec; k += kBlock) {
-      const int64_t o = a0 + k * 16;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (o < e) x = *reinterpret_cast<const uint4*>(img + o);
-      reinterpret_cast<uint4*>(T.data)[k] = x;
-    }
+    stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, nvec, e - a0);
     if (tid < 4) T.data[nvec * 4 + tid] = 0;
     __syncthreads();
     const int64_t v0 = blk0 << lbs;
@@ -1410,4 +1410,301 @@ __global__ __launch_bounds__(64) void k_delta_serial(DevBatch b, const int32_t* 
     err = serial_stream(img, pos, S.val_e, P.kind == K_DELTA64, C.values + S.value_base * P.value_size, nvals, false, vc);
   }
   if (err != kNoError) atomicMin(&b.states[t.page].err, (unsigned long long)err);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Lane-parallel chase of the block headers inside a staged window (k_delta_fused): the speculative
+// segment walk of spec_chain, with LDS instead of L2 as the byte source and at most 64 blocks (one
+// tile) per call.  Lane i takes the byte segment [loc0 + i*S, loc0 + (i+1)*S) with S the mean block
+// span (so about one header per lane), synchronises on its first plausible header, walks to the
+// segment's exit header and parses that one's successor; lanes are linked to their left neighbour
+// when its exit header (or the exit's successor) is in their list.  A block is usable when its data
+// ends inside the window (dlim) and the stream (eloc).
+// ------------------------------------------------------------------------------------------------
+constexpr int kChaseCap = 8;  // chain entries per lane
+
+// Per lane: the header at local offset loc of the staged window.  Returns its data end (-1 if the
+// common-case parse fails), *dat / *md / *wd.
+__device__ __forceinline__ int32_t lds_hdr(const uint32_t* data, int32_t loc, bool is64, int mbc, int gbytes,
+                                           int32_t& dat, uint64_t& md, uint64_t& wd) {
+  const uint64_t* w64 = reinterpret_cast<const uint64_t*>(data);
+  const int32_t q = loc >> 3;
+  const uint64_t x0 = w64[q], x1 = w64[q + 1], x2 = w64[q + 2];
+  const uint32_t sh = uint32_t(loc & 7) * 8;
+  const uint64_t lo = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+  const uint64_t hi = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+  const int hl = parse_hdr16(lo, hi, is64, mbc, md, wd);
+  if (!hl) return -1;
+  dat = loc + hl;
+  return dat + int32_t(widths_sum(wd)) * gbytes;
+}
+
+// Usable header at loc: parses, its block ends inside the window and the stream.
+__device__ __forceinline__ bool lds_block(const uint32_t* data, int32_t loc, int32_t eloc, int32_t plim,
+                                          int32_t dlim, bool is64, int mbc, int gbytes, int32_t& dend) {
+  if (loc >= plim || loc + 24 > eloc) return false;
+  int32_t dat;
+  uint64_t md, wd;
+  dend = lds_hdr(data, loc, is64, mbc, gbytes, dat, md, wd);
+  return dend >= 0 && dend <= dlim && dend <= eloc;
+}
+
+__device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int32_t est, int nmax, bool is64, int mbc,
+                          int gbytes, int16_t (*lst)[64], int32_t* blkbit, uint64_t* blkw, uint64_t* mdt, int lane,
+                          int& n_out, int32_t& next_out, bool& stop_out) {
+  const int32_t plim = kPageStage - 32, dlim = kPageStage - 16;
+  const uint64_t lim = is64 ? 64 : 32;
+  if (est <= 0) {  // first tile: the span of block 0
+    int32_t d0 = -1;
+    est = lds_block(data, loc0, eloc, plim, dlim, is64, mbc, gbytes, d0) ? d0 - loc0 : 64;
+  }
+  const int32_t S = est < 16 ? 16 : est;
+  const int32_t s0 = loc0 + S * lane, s1 = s0 + S;
+  int cnt = 0;
+  bool dead = false, bad = false;  // bad: the chain reached a header the exact walk must handle
+  int32_t p = s0, x2 = -1;
+  if (s0 < plim) {
+    if (lane > 0) {  // synchronise: first plausible header in [s0, s1)
+      p = s1;
+      for (int32_t base = s0 & ~7; base < s1 && base < plim && p == s1; base += 32) {
+        const uint64_t* w64 = reinterpret_cast<const uint64_t*>(data) + (base >> 3);
+        uint64_t x0 = w64[0], S0 = small_bytes(x0, lim);
+        for (int j = 0; j < 4 && p == s1; j++) {
+          const uint64_t x1 = w64[j + 1], S1 = small_bytes(x1, lim);
+          uint64_t c = ~x0 & 0x8080808080808080ull;
+          for (int k = 1; k <= mbc; k++) c &= k == 8 ? S1 : (S0 >> (8 * k)) | (S1 << (64 - 8 * k));
+          const int32_t w0 = base + 8 * j;
+          if (s0 > w0) c &= s0 - w0 >= 8 ? 0 : ~0ull << (8 * (s0 - w0));
+          if (s1 - w0 < 8) c &= s1 <= w0 ? 0 : (1ull << (8 * (s1 - w0))) - 1;
+          while (c) {
+            const int32_t q = w0 + (__builtin_ctzll(c) >> 3);
+            c &= c - 1;
+            int32_t d;
+            if (lds_block(data, q, eloc, plim, dlim, is64, mbc, gbytes, d)) {
+              p = q;
+              break;
+            }
+          }
+          x0 = x1;
+          S0 = S1;
+        }
+      }
+    }
+    while (p < s1 && cnt < kChaseCap) {
+      lst[cnt][lane] = int16_t(p);
+      cnt++;
+      int32_t d;
+      if (!lds_block(data, p, eloc, plim, dlim, is64, mbc, gbytes, d)) {
+        dead = true;
+        // the true chain stops here for good unless the block merely runs past the window
+        int32_t dat;
+        uint64_t md, wd;
+        const int32_t de = p < plim ? lds_hdr(data, p, is64, mbc, gbytes, dat, md, wd) : 0;
+        bad = p + 24 > eloc || (p < plim && (de < 0 || de > eloc));
+        break;
+      }
+      p = d;
+    }
+    if (!dead && p >= s1 && cnt < kChaseCap) {  // exit header (slot cnt, not counted) and its successor
+      lst[cnt][lane] = int16_t(p);
+      int32_t d;
+      if (lds_block(data, p, eloc, plim, dlim, is64, mbc, gbytes, d)) x2 = d;
+    }
+  }
+  const bool full = !dead && p < s1;
+  // ---- stitch (as spec_chain): link to the left neighbour through its exit header or its successor
+  const int32_t xl = __shfl_up(p, 1, 64), x2l = __shfl_up(x2, 1, 64);
+  const bool exit_ok = s0 < plim && !dead && !full && cnt < kChaseCap;
+  const bool left_ok = __shfl_up(int(exit_ok), 1, 64) != 0 && xl >= s0 && xl < s1;
+  int jd = -1, j2 = -1;
+  if (lane > 0 && left_ok) {
+    for (int k = 0; k < cnt; k++) {
+      const int32_t q = lst[k][lane];
+      if (jd < 0 && q == xl) jd = k;
+      if (j2 < 0 && x2l >= 0 && q == x2l) j2 = k;
+    }
+    // the left neighbour's exit is my segment's only true header: its successor is my exit
+    if (jd < 0 && j2 < 0 && exit_ok && x2l == p) j2 = cnt;
+  }
+  const bool active = s0 < plim;
+  const bool link = active && (lane == 0 || (left_ok && (jd >= 0 || j2 >= 0)));
+  const int j = lane == 0 ? 0 : (jd >= 0 ? jd : j2);
+  const bool extra = lane > 0 && link && jd < 0;  // the left neighbour records its exit header
+  const uint64_t linkm = __ballot(link);
+  const int k_bad = linkm == ~0ull ? 64 : __builtin_ctzll(~linkm);
+  const uint64_t deadm = __ballot(dead) & (k_bad >= 64 ? ~0ull : (1ull << k_bad) - 1);
+  const int last = deadm ? __builtin_ctzll(deadm) : k_bad - 1;  // >= 0: lane 0 always links
+  const bool valid = lane <= last;
+  const bool extra_r = __shfl_down(int(extra), 1, 64) != 0 && lane + 1 <= last && lane < 63;
+  const int n_all = valid ? cnt - j - (dead ? 1 : 0) + (extra_r ? 1 : 0) : 0;
+  int incl = n_all;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  const int base = incl - n_all;
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  const int my_n = base + n_all > nmax ? (nmax - base > 0 ? nmax - base : 0) : n_all;
+  for (int k = 0; k < my_n; k++) {  // tables of the kept blocks
+    const int32_t q = lst[j + k][lane];
+    int32_t dat;
+    uint64_t md, wd;
+    lds_hdr(data, q, is64, mbc, gbytes, dat, md, wd);
+    blkbit[base + k] = dat * 8;
+    blkw[base + k] = wd;
+    mdt[base + k] = md;
+  }
+  int32_t nxt;
+  bool stop = false;
+  if (total > nmax) {  // the header after the last kept block
+    const bool hit = valid && base <= nmax && nmax < base + n_all;
+    const uint64_t hm = __ballot(hit);
+    const int32_t q = hit ? lst[j + (nmax - base)][lane] : 0;
+    nxt = __builtin_amdgcn_readlane(q, __builtin_ctzll(hm));
+  } else if (deadm) {
+    nxt = __builtin_amdgcn_readlane(int32_t(lst[cnt > 0 ? cnt - 1 : 0][lane]), last);
+    stop = __builtin_amdgcn_readlane(int(bad), last) != 0;
+  } else {
+    nxt = __builtin_amdgcn_readlane(p, last);
+  }
+  n_out = total < nmax ? total : nmax;
+  next_out = nxt;
+  stop_out = stop;
+}
+
+// k_delta_fused (page mode): one workgroup per DELTA_BINARY_PACKED / DELTA_LENGTH stream (and the
+// prefix-length stream of DELTA_BYTE_ARRAY pages).  The stream is staged 16 KiB at a time from the
+// next block header; wave 0 chases the block headers in LDS (wave-uniform, scalar), and the whole
+// blocks [0, kmax) are decoded with a running carry: the packed deltas are read from HBM once and
+// no block records are written.  The chase stops at the first header the common-case parse rejects
+// or a block that runs past the stream; k_delta_walk resumes there with the exact semantics (and the
+// records of the remaining blocks) and k_delta_page decodes the rest.
+__global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* streams) {
+  __shared__ PageTileLds T;
+  __shared__ int32_t s_blkbit[kTileBlocks];
+  __shared__ uint64_t s_blkw[kTileBlocks];
+  __shared__ int64_t s_h;
+  __shared__ uint64_t s_first;
+  __shared__ int32_t s_geo[5];  // kmax (0 = nothing to do), block size, miniblocks, values per miniblock, vc
+  __shared__ int32_t s_n, s_stop;
+  __shared__ int16_t s_lst[kChaseCap][64];
+  const Tile t = streams[blockIdx.x];
+  if (t.kind != 0) return;  // DELTA_BYTE_ARRAY suffix lengths: k_delta_walk + k_delta_page
+  const int p = t.page;
+  const DevPage P = b.pages[p];
+  const PageState S = b.states[p];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint8_t* img = b.payload + P.image_off;
+  const bool is64 = P.kind == K_DELTA64;
+  const bool lens = P.kind == K_DLBA || P.kind == K_DBA;
+  const int64_t e = S.val_e;
+  if (tid < 64) {
+    int32_t kmax = 0;
+    const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
+    if (P.host_err == kNoError && load_ok) {
+      Win w{img, e, reinterpret_cast<uint8_t*>(T.data), 0, 0};
+      win_load(w, S.val_s, lane);
+      const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+      DeltaState D;
+      int32_t vc;
+      uint64_t md, widths;
+      int64_t pos = S.val_s, h0 = pos;
+      if (delta_init(w, pos, is64, D, vc, md, widths, lane, &h0) == kNoError && D.mode == DM_FAST) {
+        const int64_t nn = lens ? vc : (before_values ? 0 : S.nn);
+        kmax = int32_t(delta_whole_blocks(nn, vc, D.block_size, P.dblk_cap));
+        if (tid == 0) {
+          s_geo[1] = D.block_size;
+          s_geo[2] = D.mb_count;
+          s_geo[3] = D.mbvc;
+          s_first = D.first;
+          s_h = h0;
+        }
+      }
+    }
+    if (tid == 0) s_geo[0] = kmax;
+  }
+  __syncthreads();
+  const int kmax = s_geo[0];
+  int r = 0;
+  int64_t h = s_h;
+  uint64_t carry = s_first;
+  if (kmax > 0) {
+    const int bs = s_geo[1], mbc = s_geo[2], mbvc = s_geo[3], gbytes = mbvc / 8;
+    const int lbs = __builtin_ctz(uint32_t(bs)), lmb = __builtin_ctz(uint32_t(mbvc));
+    const DevChunk C = b.chunks[P.chunk];
+    int32_t* lp = P.kind == K_DBA ? C.aux2 : C.aux;
+    uint8_t* out = lens ? reinterpret_cast<uint8_t*>(lp + S.value_base) : C.values + S.value_base * P.value_size;
+    const int64_t vcap = lens ? int64_t(S.nn) : int64_t(kmax) << lbs;  // values to emit
+    const int64_t img_len = P.image_len;
+    int32_t est = 0;  // 0: the first tile measures block 0
+    for (;;) {
+      __syncthreads();  // the previous tile's readers of T are done
+      const int64_t a0 = h - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(h)) & 15);
+      stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, kPageStage / 16, img_len - a0);
+      __syncthreads();
+      if (tid < 64) {
+        int n;
+        int32_t nxt;
+        bool stop;
+        const int nmax = kmax - r < kTileBlocks ? kmax - r : kTileBlocks;
+        lds_chase(T.data, int32_t(h - a0), int32_t(e - a0), est, nmax, is64, mbc,
+                  gbytes, s_lst, s_blkbit, s_blkw, T.md, lane, n, nxt, stop);
+        if (tid == 0) {
+          s_n = n;
+          s_stop = stop;
+          s_h = a0 + nxt;
+        }
+      }
+      __syncthreads();
+      const int n = s_n;
+      if (n == 0) break;
+      for (int i = tid; i < n * 8; i += kBlock) {  // miniblock tables
+        const int blk = i >> 3, m = i & 7;
+        const uint64_t wd = s_blkw[blk];
+        const int wm = m < mbc ? int((wd >> (8 * m)) & 0xff) : 0;
+        const uint64_t below = m ? wd & ((1ull << (8 * m)) - 1) : 0;
+        T.mbbit[blk][m] = s_blkbit[blk] + int32_t(widths_sum(below)) * mbvc;
+        T.mbw[blk][m] = uint8_t(wm);
+      }
+      __syncthreads();
+      const int64_t v0 = int64_t(r) << lbs;
+      int64_t v1 = int64_t(r + n) << lbs;
+      if (v1 > vcap) v1 = vcap;
+      if (v0 < v1) carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+      est = int32_t((s_h - h) / n);  // mean block span so far: the next tile's lane segments
+      r += n;
+      h = s_h;
+      if (s_stop || r >= kmax || v1 >= vcap) break;
+    }
+  }
+  if (tid == 0) {
+    b.dstates[p].nblocks = r;
+    b.dstates[p].end_pos = h;
+    b.dstates[p].head_blocks = r;
+    b.dstates[p].head_carry = carry;
+  }
+}
+
+// k_delta_init (page mode, before k_scan): deltaBitPackDecoder.init of every DELTA_BINARY_PACKED
+// page, so that its load errors (phase 0) are known to the value-offset scan before k_delta_fused
+// decodes into the chunk outputs.  k_delta_walk repeats the init later and finds the same keys.
+__global__ __launch_bounds__(256) void k_delta_init(DevBatch b, const int32_t* delta_pages, int32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kWin];
+  const int lane = threadIdx.x & 63;
+  const int wv = int(threadIdx.x >> 6);
+  const int idx = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+  if (idx >= n) return;
+  const int p = delta_pages[idx];
+  const DevPage P = b.pages[p];
+  const PageState S = b.states[p];
+  const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
+  if (P.host_err != kNoError || !load_ok) return;
+  Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
+  win_load(w, S.val_s, lane);
+  DeltaState D;
+  int32_t vc;
+  uint64_t md, widths;
+  int64_t pos = S.val_s;
+  const uint64_t err = delta_init(w, pos, P.kind == K_DELTA64, D, vc, md, widths, lane);
+  if (lane == 0 && err != kNoError) atomicMin(&b.states[p].err, (unsigned long long)err);
 }

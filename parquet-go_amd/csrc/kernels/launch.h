@@ -39,6 +39,10 @@ hipError_t launch_delta_walk(const DevBatch& b, const int32_t* delta_pages, int3
 hipError_t launch_delta_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_delta_scan(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// Page mode (many delta streams): init errors of the DELTA_BINARY_PACKED pages before the value
+// scan; whole blocks chased and decoded in one workgroup per stream (before the exact walk).
+hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
+hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Many delta streams: one workgroup per (page, stream), its tiles in order with a running carry.
 hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
