@@ -434,34 +434,24 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
 // Cooperative copy of n bytes by the workgroup: 16-byte aligned stores, each fed by two aligned
 // 16-byte loads of the (arbitrarily aligned) source funnel-shifted into place.  Loads stay inside
 // the source's 16-byte-aligned cover (the payload keeps PQH_PAYLOAD_PAD bytes after the last page).
-__device__ __forceinline__ void block_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+__device__ __forceinline__ void block_copy(PQH_G uint8_t* dst, const PQH_G uint8_t* src, int64_t n) {
+  // destination 16-byte aligned after the head; the source side uses unaligned 16-byte loads
   const int64_t head = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < n
                            ? int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) : n;
   if (int64_t(threadIdx.x) < head) dst[threadIdx.x] = src[threadIdx.x];
   const int64_t units = (n - head) >> 4;
-  uint8_t* d = dst + head;
-  const uint8_t* sp = src + head;
-  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(sp) & 15);
-  const uint4* sa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(sp) & ~uintptr_t(15));
-  for (int64_t u = threadIdx.x; u < units; u += kBlock) {
-    const uint4 x = sa[u];
-    uint4 y;
-    if (sh == 0) {
-      y = x;
-    } else {
-      const uint4 z = sa[u + 1];
-      const uint32_t w[8] = {x.x, x.y, x.z, x.w, z.x, z.y, z.z, z.w};
-      const uint32_t k = sh >> 2, bs = (sh & 3) * 8;
-      uint32_t o4[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t lo = w[(k + q) & 7], hi = w[(k + q + 1) & 7];  // k + q + 1 <= 7
-        o4[q] = __builtin_amdgcn_alignbit(hi, lo, bs);
-      }
-      y = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-    }
-    reinterpret_cast<uint4*>(d)[u] = y;
+  typedef uint4 uint4_u __attribute__((aligned(1)));
+  const PQH_G uint4_u* sp = reinterpret_cast<const PQH_G uint4_u*>(src + head);
+  PQH_G uint4* d = reinterpret_cast<PQH_G uint4*>(dst + head);
+  int64_t u = threadIdx.x;
+  for (; u + 3 * kBlock < units; u += 4 * kBlock) {
+    const uint4 x0 = sp[u], x1 = sp[u + kBlock], x2 = sp[u + 2 * kBlock], x3 = sp[u + 3 * kBlock];
+    d[u] = x0;
+    d[u + kBlock] = x1;
+    d[u + 2 * kBlock] = x2;
+    d[u + 3 * kBlock] = x3;
   }
+  for (; u < units; u += kBlock) d[u] = sp[u];
   const int64_t done = head + units * 16;
   if (int64_t(threadIdx.x) < n - done) dst[done + threadIdx.x] = src[done + threadIdx.x];
 }
@@ -611,7 +601,7 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
   uint64_t tot;
   const int64_t excl = int64_t(block_exclusive_scan(uint64_t(tsum), wsum, &tot));
   const int64_t base = b.basums[P.batile_base + t.k];
-  const uint8_t* img = b.payload + P.image_off;
+  const PQH_G uint8_t* img = b.payload + P.image_off;
   int64_t data_s = 0, data_n = 0;
   if (is_dlba) {
     data_s = b.dstates[t.page].end_pos;

@@ -11,6 +11,14 @@
 #define PQH_HD
 #endif
 
+// Output buffers are HBM: in device code their pointers live in the global address space, so every
+// access compiles to global_load / global_store (a flat access would also count against LDS waits).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PQH_KERNELS_TU)
+#define PQH_G __attribute__((address_space(1)))
+#else
+#define PQH_G
+#endif
+
 namespace pqhip {
 
 // Value decoder kinds: getValuesDecoder (reference chunk_reader.go:106-159) resolved per page.
@@ -74,15 +82,15 @@ struct DevChunk {
   int32_t first_page, num_pages;
   int32_t value_size;    // output bytes per value, 0 = byte array
   int32_t dict_page;     // batch page index or -1
-  uint8_t* values;
-  int64_t* offsets;
-  uint8_t* bytes;
-  uint8_t* def_levels;
-  uint8_t* rep_levels;
+  PQH_G uint8_t* values;
+  PQH_G int64_t* offsets;
+  PQH_G uint8_t* bytes;
+  PQH_G uint8_t* def_levels;
+  PQH_G uint8_t* rep_levels;
   int64_t values_cap;    // values capacity (elements)
   int64_t bytes_cap;
-  int32_t* aux;          // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH / suffix) or dictionary key
-  int32_t* aux2;         // DELTA_BYTE_ARRAY: per value slot, prefix length
+  PQH_G int32_t* aux;    // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH / suffix) or dictionary key
+  PQH_G int32_t* aux2;   // DELTA_BYTE_ARRAY: per value slot, prefix length
   int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
   int32_t batile_n;
 };
@@ -170,9 +178,9 @@ struct DevNest {
   int32_t pad;
   int64_t n;             // level slots of the chunk
   int32_t rep_def[kMaxNest];
-  int32_t* offsets[kMaxNest];
-  uint8_t* validity[kMaxNest];
-  uint8_t* leaf_valid;
+  PQH_G int32_t* offsets[kMaxNest];
+  PQH_G uint8_t* validity[kMaxNest];
+  PQH_G uint8_t* leaf_valid;
   int64_t* totals;       // kNestFlags per chunk: rows, elements of each level (k_nest_scan)
 };
 

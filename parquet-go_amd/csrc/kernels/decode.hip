@@ -10,6 +10,7 @@
 //   3. expand       data-parallel tiles over HBM-resident page images: level bytes, dictionary
 //                   gathers (dictionary staged in LDS), PLAIN copies and boolean bit expansion.
 // All bandwidth kernels: 16-byte vector loads/stores, no MFMA.
+#define PQH_KERNELS_TU 1  // output pointers in the global address space (decode.h)
 #include <hip/hip_runtime.h>
 
 #include "launch.h"
@@ -861,8 +862,8 @@ __device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
   if (c1 > total) c1 = total;
   if (c0 >= c1) return;
   const DevChunk C = b.chunks[P.chunk];
-  const uint8_t* src = b.payload + P.image_off + S.val_s;
-  uint8_t* dst = C.values + S.value_base * P.value_size;
+  const PQH_G uint8_t* src = b.payload + P.image_off + S.val_s;
+  PQH_G uint8_t* dst = C.values + S.value_base * P.value_size;
   int64_t o = c0 + 16 * int64_t(threadIdx.x);
   for (; o + 16 * 3 * kBlock + 16 <= c1; o += 16 * 4 * kBlock) {
     uint4 a, bb, c, d;
@@ -898,8 +899,8 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
   for (int q = 0; q < 2; q++) {
     const int64_t v0 = int64_t(t.k) * kBoolTile + int64_t(q) * (kBoolTile / 2) + int64_t(threadIdx.x) * 64;
     if (v0 >= lim) return;
-    const uint8_t* src = b.payload + P.image_off + S.val_s + (v0 >> 3);
-    uint8_t* dst = C.values + S.value_base + v0;
+    const PQH_G uint8_t* src = b.payload + P.image_off + S.val_s + (v0 >> 3);
+    PQH_G uint8_t* dst = C.values + S.value_base + v0;
     uint8_t in[8];
     __builtin_memcpy(in, src, 8);
     if (v0 + 64 <= lim) {

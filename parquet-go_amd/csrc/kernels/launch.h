@@ -8,7 +8,7 @@
 namespace pqhip {
 
 struct DevBatch {
-  const uint8_t* payload;
+  const PQH_G uint8_t* payload;
   const DevPage* pages;
   const DevChunk* chunks;
   PageState* states;
