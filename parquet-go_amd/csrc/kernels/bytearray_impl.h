@@ -108,18 +108,13 @@ __device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb,
   for (int k = 0; k < kChainWords; k++) empty = empty && C.mask[j][k] == 0;
   if (pbad) return true;  // the chain ended before j (exactly, if j-1 is right): nothing here counts
   if (T >= s0 + kChainSeg) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
+  if (empty && C.exitbad[j] && C.exitv[j] == T) return true;  // the record at T itself is invalid
   return chain_has(C, j, int(T - s0));
 }
 
-// Make segment j right for its true entry.
-__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t entry) {
+// Make segment j right for the entry T (pbad: the chain already ended before it).
+__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t T, uint8_t pbad) {
   const int64_t s0 = wb + int64_t(j) * kChainSeg;
-  int64_t T = entry;
-  uint8_t pbad = 0;
-  if (j > 0) {
-    T = C.exitv[j - 1];
-    pbad = C.exitbad[j - 1];
-  }
   if (pbad || T >= s0 + kChainSeg) {
 #pragma unroll
     for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
@@ -163,12 +158,8 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
     // window [wb, wb + kChainWin) with wb 16-byte aligned (payload address) at or before entry
     const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(entry)) & 15);
     __syncthreads();
-    for (int k = j; k < (kChainWin + 64) / 16; k += kBlock) {
-      const int64_t o = wb + 16 * int64_t(k);
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (o < e0) x = *reinterpret_cast<const uint4*>(img + o);  // the 16 B past e0 stay in the pad
-      reinterpret_cast<uint4*>(C.win)[k] = x;
-    }
+    // the 16 B past e0 stay in the pad
+    stage_copy(reinterpret_cast<uint4*>(C.win), img + wb, (kChainWin + 64) / 16, e0 - wb);
     __syncthreads();
     // 1. speculative walks
     {
@@ -180,14 +171,27 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
         // the first offset whose record is valid and is followed, inside the window, by another
         // valid record: the bytes of a length field read at an offset of 1-3 give lengths of
         // ~2^8..2^24 that land in the middle of string bytes (or outside the window)
-        for (int64_t x = s0; x < s1 && x < e0; x++) {
+        // Among the plausible starts at x..x+3 the shortest record wins: the last byte of a string
+        // followed by a small length field reads as a plausible record ~256x longer than the true one
+        // that starts a byte later.
+        auto plausible = [&](int64_t x, int32_t& l) {
           int64_t nx, nx2;
+          int32_t l2;
+          if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
+          return nx < wb + kChainWin && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
+        };
+        for (int64_t x = s0; x < s1 && x < e0; x++) {
           int32_t l;
-          if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) continue;
-          if (nx < wb + kChainWin && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l) == PQH_OK)) {
-            start = x;
-            break;
+          if (!plausible(x, l)) continue;
+          start = x;
+          for (int d = 1; d <= 3 && x + d < s1; d++) {
+            int32_t l2;
+            if (plausible(x + d, l2) && l2 < l) {
+              start = x + d;
+              l = l2;
+            }
           }
+          break;
         }
       }
       if (start >= 0) {
@@ -200,14 +204,17 @@ __global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_p
       }
     }
     __syncthreads();
-    // 2. resolution: one parallel check, then an in-order sweep from the first mis-speculated segment
-    if (j == 0) C.stop = kBlock;
-    __syncthreads();
-    if (!chain_good(C, j, wb, entry)) atomicMin(&C.stop, j);
-    __syncthreads();
-    if (C.stop < kBlock) {
-      if (j == 0)
-        for (int s = C.stop; s < kBlock; s++) chain_fix(C, s, wb, e0, entry);
+    // 2. resolution: a parallel check of every segment against its predecessor's exit, then the
+    // first mismatch (whose predecessor is exact) re-walks from its true entry; repeat.
+    for (int round = 0;; round++) {
+      // the first segment whose walk misses its true entry has a final predecessor: re-walk it
+      if (j == 0) C.stop = kBlock;
+      __syncthreads();
+      if (!chain_good(C, j, wb, entry)) atomicMin(&C.stop, j);
+      __syncthreads();
+      const int sg = C.stop;
+      if (sg >= kBlock) break;
+      if (j == sg) chain_fix(C, sg, wb, e0, sg == 0 ? entry : int64_t(C.exitv[sg - 1]), sg == 0 ? 0 : C.exitbad[sg - 1]);
       __syncthreads();
     }
     // 3. number the records of the true chain, emit, find where the chain ends

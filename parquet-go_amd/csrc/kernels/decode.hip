@@ -66,14 +66,16 @@ __device__ int read_uvarint(const uint8_t* img, int64_t& pos, int64_t end, uint6
 // `limit` (an offset from src) read as zeros.  Four vectors per thread are in flight at a time
 // (loads unconditional from a clamped address, then selected), so a tile costs one round trip per
 // 16 KiB instead of one per 4 KiB.
-__device__ __forceinline__ void stage_copy(uint4* dst, const uint8_t* src, int64_t nvec, int64_t limit) {
+__device__ __forceinline__ void stage_copy(uint4* dst, const uint8_t* src_, int64_t nvec, int64_t limit) {
+  // the payload is HBM: global loads (the generic pointer would compile to flat loads)
+  const PQH_G uint8_t* src = (const PQH_G uint8_t*)(src_);
   for (int64_t base = 0; base < nvec; base += 4 * kBlock) {
     uint4 x[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int64_t k = base + threadIdx.x + j * kBlock;
       const bool ok = k < nvec && 16 * k < limit;
-      x[j] = *reinterpret_cast<const uint4*>(src + (ok ? 16 * k : 0));
+      x[j] = *reinterpret_cast<const PQH_G uint4*>(src + (ok ? 16 * k : 0));
       if (!ok) x[j] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll

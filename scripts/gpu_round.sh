@@ -12,7 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   return 0
 }
-step gpu_tests 900 python -m pytest tests -q -m gpu ${PYTEST_K:+-k "$PYTEST_K"}
+step gpu_tests 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 [ -n "$NO_SMOKE" ] || step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 for w in ${BENCH_WORKLOADS:-c3 c2}; do
   step bench_$w 400 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu
