@@ -570,21 +570,17 @@ __device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, in
     const int64_t nvec = (p1 - a0 + 15) >> 4;
     const uint32_t lead_bits = uint32_t(p0 - a0) * 8;
     __syncthreads();  // previous chunk fully consumed
-    for (int64_t k = threadIdx.x; k < nvec; k += kBlock) {
-      const uint8_t* src = a0 + k * 16;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (src < end) {
-        x = *reinterpret_cast<const uint4*>(src);
-        const int64_t valid = end - src;
-        if (valid < 16) {  // zero the bytes past the stream end
-          uint32_t* w4 = reinterpret_cast<uint32_t*>(&x);
-          for (int q = 0; q < 4; q++) {
-            const int64_t vb = valid - 4 * q;
-            w4[q] = vb >= 4 ? w4[q] : vb <= 0 ? 0u : (w4[q] & ((1u << (8 * vb)) - 1u));
-          }
-        }
+    stage_copy(reinterpret_cast<uint4*>(stage), a0, nvec, end - a0);
+    if (end > a0 && end - a0 < nvec * 16 && ((end - a0) & 15)) {
+      // the vector holding the stream end: zero the bytes past it (the reference's short group
+      // read is zero-filled)
+      const int64_t kv = (end - a0) >> 4;
+      __syncthreads();  // the copy of vector kv is done
+      if (threadIdx.x < 4) {
+        const int64_t vb = (end - a0) - 16 * kv - 4 * int64_t(threadIdx.x);
+        uint32_t& wq = stage[kv * 4 + threadIdx.x];
+        wq = vb >= 4 ? wq : vb <= 0 ? 0u : (wq & ((1u << (8 * vb)) - 1u));
       }
-      reinterpret_cast<uint4*>(stage)[k] = x;
     }
     if (threadIdx.x == 0) stage[nvec * 4] = 0;  // the word after the last one (alignbit reads k+1)
     __syncthreads();
@@ -867,6 +863,17 @@ __device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
   const PQH_G uint8_t* src = b.payload + P.image_off + S.val_s;
   PQH_G uint8_t* dst = C.values + S.value_base * P.value_size;
   int64_t o = c0 + 16 * int64_t(threadIdx.x);
+  // 8 x 16 B in flight per thread (32 KiB per workgroup); streaming (nontemporal) stores
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  for (; o + 16 * 7 * kBlock + 16 <= c1; o += 16 * 8 * kBlock) {
+    u32x4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = *reinterpret_cast<const PQH_G u32x4_u*>(src + o + 16 * k * kBlock);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      __builtin_nontemporal_store(x[k], reinterpret_cast<PQH_G u32x4_u*>(dst + o + 16 * k * kBlock));
+  }
   for (; o + 16 * 3 * kBlock + 16 <= c1; o += 16 * 4 * kBlock) {
     uint4 a, bb, c, d;
     __builtin_memcpy(&a, src + o, 16);
