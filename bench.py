@@ -2,12 +2,13 @@
 """Benchmark: decoded output GB/s of the HIP page decoder + HBM roofline fraction.
 
 A "step" is one full decode pass (every page of every chunk of the rank's row groups) over
-HBM-resident page images: k_prologue -> k_scan -> k_levels / k_copy / k_bool_plain / k_dict.
+HBM-resident page images: k_prologue -> (delta / byte-array walks) -> k_scan -> k_expand (levels,
+PLAIN copies, booleans, dictionaries) / k_delta_* / k_ba_* / k_nest_*.
 Default workload = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16 row
 groups per GPU.  Multi-GPU: one process per GPU (torchrun), row groups sharded (each rank decodes
 its own 16 row groups, different seed), no data-path collective -> "scaling": "weak".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3] [--rows R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c5] [--rows R]
 """
 import argparse
 import json
@@ -175,7 +176,9 @@ def main():
         kernels[s.name.decode()] = {"avg_ms": round(avg_ms, 4), "launches": s.launches, "work_items": s.work_items,
                                     "algo_bytes": algo,
                                     "gbps": round(algo / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
-        if dom is None or s.total_ms > dom.total_ms:
+        # the dominant kernel = the longest one that moves algorithmic bytes (walks that only read
+        # headers carry none)
+        if algo > 0 and (dom is None or s.total_ms > dom.total_ms):
             dom = s
     roof = None
     if dom is not None:

@@ -54,11 +54,11 @@ struct KernelRun {
 
 const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global",
                               "k_delta_walk", "k_delta_expand", "k_delta_sum_scan",
-                              "k_ba_walk",    "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
+                              "k_ba_wspec",   "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
-                              "k_delta_fused"};
-constexpr int kNumKernels = 20;
+                              "k_delta_fused", "k_ba_wstitch", "k_ba_wemit"};
+constexpr int kNumKernels = 22;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 1024;
@@ -137,7 +137,8 @@ struct pqh_batch {
   int32_t delta_int_streams = 0;    //            and their streams first in delta_streams
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
-  std::vector<int32_t> ba_pages;    // k_ba_walk work list (PLAIN byte-array data + dictionary pages)
+  std::vector<int32_t> ba_pages;    // PLAIN byte-array data + dictionary pages (chain walks)
+  std::vector<int2> ba_wins, ba_pwin;
   std::vector<int32_t> ba_chunks;   // k_ba_scan work list
   std::vector<int64_t> chunk_bytes; // host copy after sync
   std::vector<DevNest> nests;       // repeated chunks with nesting outputs
@@ -163,6 +164,10 @@ struct pqh_batch {
   uint64_t* d_dpre = nullptr;
   Tile* d_batiles = nullptr;
   int32_t* d_ba_pages = nullptr;
+  int2* d_ba_wins = nullptr;        // (page, window) of every PLAIN chain window
+  int2* d_ba_pwin = nullptr;        // per PLAIN page: (first window, windows)
+  BaWin* d_ba_res = nullptr;
+  uint64_t* d_ba_marks = nullptr;
   int32_t* d_ba_chunks = nullptr;
   int32_t* d_dcum = nullptr;
   int64_t* d_basums = nullptr;
@@ -490,6 +495,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
     b->global_tiles = by_kind[TK_DICT_GLOBAL];
     b->delta_tiles = by_kind[TK_DELTA];
+    for (int32_t p : b->ba_pages) {  // chain windows: enough to cover the whole page image
+      const int64_t len = std::max<int64_t>(b->hpages[size_t(p)].image_len, 1);
+      const int32_t nw = int32_t((len + kChainStride - 1) / kChainStride);
+      b->ba_pwin.push_back(make_int2(int32_t(b->ba_wins.size()), nw));
+      for (int32_t w = 0; w < nw; w++) b->ba_wins.push_back(make_int2(p, w));
+    }
     b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
@@ -527,6 +538,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dpre), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_batiles), sizeof(Tile) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wins), sizeof(int2) * b->ba_wins.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pwin), sizeof(int2) * b->ba_pwin.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_res), sizeof(BaWin) * b->ba_wins.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_marks),
+                   sizeof(uint64_t) * size_t(kBlock) * kChainWords * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
@@ -631,6 +647,10 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     e = hipMemcpyAsync(b->d_batiles, b->ba_tiles.data(), sizeof(Tile) * b->ba_tiles.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !b->ba_pages.empty())
     e = hipMemcpyAsync(b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_wins.empty())
+    e = hipMemcpyAsync(b->d_ba_wins, b->ba_wins.data(), sizeof(int2) * b->ba_wins.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_pwin.empty())
+    e = hipMemcpyAsync(b->d_ba_pwin, b->ba_pwin.data(), sizeof(int2) * b->ba_pwin.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !b->ba_chunks.empty())
     e = hipMemcpyAsync(b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size(),
                        hipMemcpyHostToDevice, s);
@@ -700,8 +720,16 @@ int pqh_batch_run(pqh_batch* b) {
       e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
   }
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
-  if (e == hipSuccess && nbp)
-    e = timed(7, nbp, s, [&](hipStream_t st) { return launch_ba_walk(d, b->d_ba_pages, nbp, st); });
+  if (e == hipSuccess && nbp) {
+    const int32_t nw = int32_t(b->ba_wins.size());
+    e = timed(7, nw, s, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_marks, st); });
+    if (e == hipSuccess)
+      e = timed(20, nbp, s, [&](hipStream_t st) {
+        return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_marks, st);
+      });
+    if (e == hipSuccess)
+      e = timed(21, nw, s, [&](hipStream_t st) { return launch_ba_wemit(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_marks, st); });
+  }
   if (e == hipSuccess && ndt && b->delta_page_mode) {
     const int32_t nds = int32_t(b->delta_streams.size());
     e = timed(17, nds, s, [&](hipStream_t st) { return launch_delta_page(d, b->d_dtiles, nds, st); });
@@ -845,7 +873,7 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[kd] += vals;
         break;
       }
-      case K_PLAIN_BA:  // walked by k_ba_walk, bytes moved by k_ba_expand
+      case K_PLAIN_BA:  // walked by k_ba_wspec / k_ba_wstitch / k_ba_wemit, bytes moved by k_ba_expand
       case K_DLBA:
       case K_DBA:
         b->k_read[10] += S.val_e - S.val_s;

@@ -16,25 +16,26 @@
 #pragma once
 
 // ------------------------------------------------------------------------------------------------
-// k_ba_walk: one workgroup per PLAIN byte-array page (data pages and byte-array dictionary pages).
-// The chain [u32 len][len bytes] (byteArrayPlainDecoder.next, type_bytearray.go:24-45) is sequential
-// by definition; it is resolved in parallel and exactly, 63 KiB window by window:
-//   1. each thread owns a 252-byte segment and walks it from a SPECULATIVE start (the first offset
-//      whose length field describes a record inside the stream; segment 0 starts at the known
-//      entry), marking the record starts it visits in a 256-bit mask;
-//   2. the true entry of segment j is the exit of segment j-1.  Segment j is right when that entry
-//      is one of its marked starts (the chains merge) or lies past the segment (a long record);
-//      one parallel check confirms the common case, otherwise thread 0 sweeps the segments in
-//      order and re-walks the ones whose speculation was wrong;
-//   3. records are numbered with a block scan of the per-segment counts and emitted: lengths (data
-//      page -> aux) or cumulative offsets (dictionary page -> dcum); the first invalid record on the
-//      true chain (short length, negative length, short data) is the page's error.
+// PLAIN byte-array chains (data pages and byte-array dictionary pages).  The chain [u32 len][len
+// bytes] (byteArrayPlainDecoder.next, type_bytearray.go:24-45) is sequential by definition; it is
+// resolved in parallel and exactly, over many workgroups per page:
+//   * a page's bytes are cut into windows: window w holds the records whose start lies in
+//     [B_w, B_w+1), B_w = entry + w * kChainStride;
+//   * k_ba_wspec (one workgroup per window): window w's entry (the first record start >= B_w) is
+//     guessed (window 0: the known entry), then resolved inside the window: each thread owns a
+//     252-byte segment and walks it from a speculative start (the shortest plausible record among
+//     four neighbouring offsets), the walks are checked in parallel against their predecessor's
+//     exit and the first mismatch re-walked from its true entry until all agree; the window's
+//     record-start marks, count, byte sum, exit and first invalid record go to scratch;
+//   * k_ba_wstitch (one workgroup per page): window w's entry must be window w-1's exit; a window
+//     whose guess was wrong is resolved again from the true entry (rare); window bases = running
+//     record / byte counts; the page's error (the first invalid record on the chain before `count`
+//     records) and limits;
+//   * k_ba_wemit (one workgroup per window): records numbered by block scans of the marks,
+//     lengths (data page -> aux) or cumulative offsets (dictionary page -> dcum) written.
 // ------------------------------------------------------------------------------------------------
 // 252-byte segments: neighbouring lanes' segments start 63 dwords apart, so their LDS reads fall in
 // different banks (a power-of-two stride would put a whole wave on one bank)
-constexpr int kChainSeg = 252;
-constexpr int kChainWin = kChainSeg * kBlock;      // 64512 bytes per window
-constexpr int kChainWords = (kChainSeg + 63) / 64; // mask words per segment
 
 struct ChainLds {
   uint32_t win[(kChainWin + 64) / 4];
@@ -43,6 +44,8 @@ struct ChainLds {
   uint8_t exitbad[kBlock];
   int32_t first_bad;
   int32_t stop;
+  int32_t guess;
+  int32_t pad;
   uint64_t wsum[4];
 };
 
@@ -60,9 +63,14 @@ __device__ __forceinline__ int chain_step(const ChainLds& C, int64_t wb, int64_t
   return PQH_OK;
 }
 
-// Walk segment [s0, s0 + kChainSeg) from `start` (must lie in the segment): marks + exit.
-__device__ void chain_walk(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t start) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = s0 + kChainSeg;
+__device__ __forceinline__ int64_t seg_end(int j, int64_t wb, int64_t wend) {
+  const int64_t s1 = wb + int64_t(j + 1) * kChainSeg;
+  return s1 < wend ? s1 : wend;
+}
+
+// Walk segment j [s0, s1) from `start` (must lie in the segment): marks + exit.
+__device__ void chain_walk(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t e0, int64_t start) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
   uint64_t m[kChainWords];
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) m[k] = 0;
@@ -93,10 +101,10 @@ __device__ __forceinline__ bool chain_has(const ChainLds& C, int j, int q) {
 }
 
 // Is segment j's stored result right for its true entry (the previous segment's exit)?  By
-// induction from segment 0 (whose start is the known entry), when every segment passes, all
+// induction from segment 0 (whose start is the window entry), when every segment passes, all
 // segments up to the first invalid exit are exact and that exit is the true end of the chain.
-__device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb, int64_t entry) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+__device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb, int64_t wend, int64_t entry) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
   int64_t T = entry;
   uint8_t pbad = 0;
   if (j > 0) {
@@ -107,187 +115,316 @@ __device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb,
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) empty = empty && C.mask[j][k] == 0;
   if (pbad) return true;  // the chain ended before j (exactly, if j-1 is right): nothing here counts
-  if (T >= s0 + kChainSeg) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
-  if (empty && C.exitbad[j] && C.exitv[j] == T) return true;  // the record at T itself is invalid
+  if (T >= s1) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
+  if (empty && C.exitbad[j] && C.exitv[j] == T) return true;       // the record at T itself is invalid
   return chain_has(C, j, int(T - s0));
 }
 
 // Make segment j right for the entry T (pbad: the chain already ended before it).
-__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t e0, int64_t T, uint8_t pbad) {
+__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t e0, int64_t T, uint8_t pbad) {
   const int64_t s0 = wb + int64_t(j) * kChainSeg;
-  if (pbad || T >= s0 + kChainSeg) {
+  if (pbad || T >= seg_end(j, wb, wend)) {
 #pragma unroll
     for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
     C.exitv[j] = int32_t(T);
     C.exitbad[j] = pbad;
   } else if (!chain_has(C, j, int(T - s0))) {
-    chain_walk(C, j, wb, e0, T);
+    chain_walk(C, j, wb, wend, e0, T);
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_walk(DevBatch b, const int32_t* ba_pages, int32_t n) {
-  __shared__ ChainLds C;
+// The record starts <= 3 bytes apart at x..x+3 that look like records (valid, and followed inside
+// the window by another valid one): the shortest wins.  The last byte of a string followed by a
+// small length field reads as a record ~256x longer than the true one a byte later.
+__device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, int64_t e0, int64_t s0, int64_t s1,
+                                               int64_t staged_end) {
+  auto plausible = [&](int64_t x, int32_t& l) {
+    int64_t nx, nx2;
+    int32_t l2;
+    if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
+    return nx + 4 <= staged_end && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
+  };
+  for (int64_t x = s0; x < s1 && x < e0; x++) {
+    int32_t l;
+    if (!plausible(x, l)) continue;
+    int64_t start = x;
+    for (int d = 1; d <= 3 && x + d < s1; d++) {
+      int32_t l2;
+      if (plausible(x + d, l2) && l2 < l) {
+        start = x + d;
+        l = l2;
+      }
+    }
+    return start;
+  }
+  return -1;
+}
+
+// Resolve the chain of the window [wb, wend) from `entry` (whole workgroup; C.win staged from wb).
+// Afterwards segment j's marks hold the true record starts in it, C.first_bad = the first segment
+// whose walk ended on an invalid record (kBlock if none).
+__device__ void chain_resolve(ChainLds& C, int64_t wb, int64_t wend, int64_t e0, int64_t entry) {
   const int j = threadIdx.x;
-  const int p = ba_pages[blockIdx.x];
+  {
+    const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
+    int64_t start = -1;
+    if (j == 0) start = entry;
+    else if (s0 < s1) start = chain_guess(C, wb, e0, s0, s1, wb + kChainWin);
+    if (start >= 0) {
+      chain_walk(C, j, wb, wend, e0, start);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      C.exitv[j] = int32_t(s1 > s0 ? s1 : s0);
+      C.exitbad[j] = 0;
+    }
+  }
+  __syncthreads();
+  // the first segment whose walk misses its true entry has an exact predecessor: re-walk it; repeat
+  for (;;) {
+    if (j == 0) C.stop = kBlock;
+    __syncthreads();
+    if (!chain_good(C, j, wb, wend, entry)) atomicMin(&C.stop, j);
+    __syncthreads();
+    const int sg = C.stop;
+    if (sg >= kBlock) break;
+    if (j == sg)
+      chain_fix(C, sg, wb, wend, e0, sg == 0 ? entry : int64_t(C.exitv[sg - 1]), sg == 0 ? 0 : C.exitbad[sg - 1]);
+    __syncthreads();
+  }
+  if (j == 0) C.first_bad = kBlock;
+  __syncthreads();
+  if (C.exitbad[j]) atomicMin(&C.first_bad, j);  // segments before the chain's end are exact
+  __syncthreads();
+}
+
+// Segment j's marks on the true chain (starts before its true entry dropped; none past the end).
+__device__ __forceinline__ int chain_marks(const ChainLds& C, int j, int64_t wb, int64_t entry, int fb,
+                                           uint64_t m[kChainWords]) {
+  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+  const int64_t T = j == 0 ? entry : int64_t(C.exitv[j - 1]);
+  const bool live = j <= fb;
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) {
+    m[k] = live ? C.mask[j][k] : 0;
+    const int64_t lo = T - s0 - 64 * k;
+    if (lo > 0) m[k] = lo >= 64 ? 0 : m[k] & ~((1ull << lo) - 1);
+    cnt += __popcll(m[k]);
+  }
+  return cnt;
+}
+
+struct BaPageCtx {
+  bool ok, dict;
+  int64_t count, entry, e0;
+  const uint8_t* img;
+};
+
+__device__ __forceinline__ BaPageCtx ba_page_ctx(const DevBatch& b, int p) {
+  BaPageCtx c;
   const DevPage P = b.pages[p];
   const PageState S = b.states[p];
-  const bool dict = P.page_type == PQH_DICTIONARY_PAGE;
-  if (S.err != kNoError && (dict || page_failed_before_values(S))) return;
-  int64_t count, entry, e0;
-  int32_t* out;
-  if (dict) {  // dictPageReader.read: num_values PLAIN entries over the whole page
-    count = P.num_values;
-    entry = 0;
-    e0 = P.image_len;
-    out = b.dcum + P.aux_base;
-  } else {
-    count = S.nn;
-    entry = S.val_s;
-    e0 = S.val_e;
-    out = b.chunks[P.chunk].aux + S.value_base;
+  c.dict = P.page_type == PQH_DICTIONARY_PAGE;
+  c.ok = !(S.err != kNoError && (c.dict || page_failed_before_values(S)));
+  c.count = c.dict ? P.num_values : S.nn;
+  c.entry = c.dict ? 0 : S.val_s;
+  c.e0 = c.dict ? P.image_len : S.val_e;
+  c.img = b.payload + P.image_off;
+  return c;
+}
+
+// Stage, resolve and summarise one window (whole workgroup); marks to scratch.
+__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry, BaWin* res,
+                          uint64_t* marks) {
+  const int j = threadIdx.x;
+  const int64_t wend = c.entry + (w + 1) * kChainStride;
+  BaWin r{int32_t(entry), int32_t(entry), 0, 0, 0, -1, 0, 0};
+  if (entry >= c.e0 || entry >= wend) {  // no record starts in the window (or no bytes left)
+    if (entry >= c.e0 && entry < wend) r.bad = PQH_ERR_EOF;
+    if (j == 0) *res = r;
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++) marks[j * kChainWords + k] = 0;
+    return;
   }
-  const uint8_t* img = b.payload + P.image_off;
-  int64_t done = 0;      // records emitted so far
-  int64_t cum = 0;       // dictionary: bytes of the entries so far
-  int code = PQH_OK;
-  while (done < count) {
-    if (entry >= e0) {  // no bytes left for the next length
-      code = PQH_ERR_EOF;
-      break;
-    }
-    // window [wb, wb + kChainWin) with wb 16-byte aligned (payload address) at or before entry
-    const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(entry)) & 15);
-    __syncthreads();
-    // the 16 B past e0 stay in the pad
-    stage_copy(reinterpret_cast<uint4*>(C.win), img + wb, (kChainWin + 64) / 16, e0 - wb);
-    __syncthreads();
-    // 1. speculative walks
-    {
-      const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = s0 + kChainSeg;
-      int64_t start = -1;
-      if (j == 0) {
-        start = entry;
-      } else {
-        // the first offset whose record is valid and is followed, inside the window, by another
-        // valid record: the bytes of a length field read at an offset of 1-3 give lengths of
-        // ~2^8..2^24 that land in the middle of string bytes (or outside the window)
-        // Among the plausible starts at x..x+3 the shortest record wins: the last byte of a string
-        // followed by a small length field reads as a plausible record ~256x longer than the true one
-        // that starts a byte later.
-        auto plausible = [&](int64_t x, int32_t& l) {
-          int64_t nx, nx2;
-          int32_t l2;
-          if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
-          return nx < wb + kChainWin && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
-        };
-        for (int64_t x = s0; x < s1 && x < e0; x++) {
-          int32_t l;
-          if (!plausible(x, l)) continue;
-          start = x;
-          for (int d = 1; d <= 3 && x + d < s1; d++) {
-            int32_t l2;
-            if (plausible(x + d, l2) && l2 < l) {
-              start = x + d;
-              l = l2;
-            }
-          }
-          break;
-        }
-      }
-      if (start >= 0) {
-        chain_walk(C, j, wb, e0, start);
-      } else {
-#pragma unroll
-        for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
-        C.exitv[j] = int32_t(s1);
-        C.exitbad[j] = 0;
-      }
-    }
-    __syncthreads();
-    // 2. resolution: a parallel check of every segment against its predecessor's exit, then the
-    // first mismatch (whose predecessor is exact) re-walks from its true entry; repeat.
-    for (int round = 0;; round++) {
-      // the first segment whose walk misses its true entry has a final predecessor: re-walk it
-      if (j == 0) C.stop = kBlock;
-      __syncthreads();
-      if (!chain_good(C, j, wb, entry)) atomicMin(&C.stop, j);
-      __syncthreads();
-      const int sg = C.stop;
-      if (sg >= kBlock) break;
-      if (j == sg) chain_fix(C, sg, wb, e0, sg == 0 ? entry : int64_t(C.exitv[sg - 1]), sg == 0 ? 0 : C.exitbad[sg - 1]);
-      __syncthreads();
-    }
-    // 3. number the records of the true chain, emit, find where the chain ends
-    if (j == 0) C.first_bad = kBlock;
-    __syncthreads();
-    if (C.exitbad[j]) atomicMin(&C.first_bad, j);  // segments before the chain's end are exact and valid
-    __syncthreads();
-    const int fb = C.first_bad;
+  const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(entry)) & 15);
+  __syncthreads();
+  stage_copy(reinterpret_cast<uint4*>(C.win), c.img + wb, (kChainWin + 64) / 16, c.e0 - wb);
+  __syncthreads();
+  chain_resolve(C, wb, wend, c.e0, entry);
+  const int fb = C.first_bad;
+  uint64_t m[kChainWords];
+  const int cnt = chain_marks(C, j, wb, entry, fb, m);
+  int64_t bytes = 0;
+  if (c.dict) {
     const int64_t s0 = wb + int64_t(j) * kChainSeg;
-    const int64_t T = j == 0 ? entry : int64_t(C.exitv[j - 1]);
-    const bool live = j <= fb;
-    uint64_t m[kChainWords];
-    int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kChainWords; k++) {
-      m[k] = live ? C.mask[j][k] : 0;
-      const int64_t lo = T - s0 - 64 * k;  // drop speculative starts before the true entry
-      if (lo > 0) m[k] = lo >= 64 ? 0 : m[k] & ~((1ull << lo) - 1);
-      cnt += __popcll(m[k]);
-    }
-    uint64_t tot;
-    const int64_t before = int64_t(block_exclusive_scan(uint64_t(cnt), C.wsum, &tot));
-    int64_t bytes = 0;
-    if (dict) {
-#pragma unroll
-      for (int k = 0; k < kChainWords; k++) {
-        uint64_t x = m[k];
-        while (x) {
-          const int64_t o = s0 + __builtin_ctzll(x) + 64 * k - wb;
-          x &= x - 1;
-          bytes += int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
-        }
-      }
-    }
-    uint64_t btot = 0;
-    const int64_t bbefore = dict ? int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot)) : 0;
-    int64_t r = done + before, c = cum + bbefore;
 #pragma unroll
     for (int k = 0; k < kChainWords; k++) {
       uint64_t x = m[k];
       while (x) {
         const int64_t o = s0 + __builtin_ctzll(x) + 64 * k - wb;
         x &= x - 1;
-        const int32_t l = int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
-        if (r < count) {
-          out[r] = dict ? int32_t(c) : l;
-          if (dict && r == count - 1) out[count] = int32_t(c + l);
-        }
-        r++;
-        c += l;
+        bytes += int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
       }
     }
-    done += int64_t(tot);  // segments after the chain's end hold no records
-    cum += int64_t(btot);
+  }
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) marks[j * kChainWords + k] = m[k];
+  uint64_t tot, btot;
+  block_exclusive_scan(uint64_t(cnt), C.wsum, &tot);
+  block_exclusive_scan(uint64_t(bytes), C.wsum, &btot);
+  if (j == 0) {
+    r.count = int32_t(tot);
+    r.bytes = int64_t(btot);
     if (fb < kBlock) {
-      code = C.exitbad[fb];
+      r.bad = C.exitbad[fb];
+      r.exit = C.exitv[fb];
+    } else {
+      // the last segment's exit: the first record start >= wend
+      r.exit = C.exitv[(wend - wb + kChainSeg - 1) / kChainSeg - 1];
+    }
+    *res = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, uint64_t* marks) {
+  __shared__ ChainLds C;
+  const int2 pw = wins[blockIdx.x];
+  const BaPageCtx c = ba_page_ctx(b, pw.x);
+  BaWin* r = res + blockIdx.x;
+  uint64_t* mk = marks + int64_t(blockIdx.x) * kBlock * kChainWords;
+  const int64_t Bw = c.entry + int64_t(pw.y) * kChainStride;
+  if (!c.ok || Bw >= c.e0) {
+    if (threadIdx.x == 0) *r = BaWin{-1, -1, 0, 0, 0, -1, 0, 0};
+    return;
+  }
+  int64_t entry = c.entry;
+  if (pw.y > 0) {  // guess the first record start >= B_w from the 2 KiB at B_w
+    constexpr int kGuess = 2048;
+    const int64_t wb = Bw - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(Bw)) & 15);
+    stage_copy(reinterpret_cast<uint4*>(C.win), c.img + wb, kGuess / 16, c.e0 - wb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int64_t g = chain_guess(C, wb, c.e0, Bw, wb + kGuess - 1024, wb + kGuess);
+      C.guess = int32_t(g < 0 ? Bw : g);
+    }
+    __syncthreads();
+    entry = C.guess;
+  }
+  ba_window(C, c, pw.y, entry, r, mk);
+}
+// One workgroup per PLAIN byte-array page: windows stitched in order (see above).
+__global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* ba_pages, const int2* pwin, BaWin* res,
+                                                     uint64_t* marks) {
+  __shared__ ChainLds C;
+  __shared__ BaWin cur;
+  const int p = ba_pages[blockIdx.x];
+  const int2 wr = pwin[blockIdx.x];
+  const BaPageCtx c = ba_page_ctx(b, p);
+  if (!c.ok) return;
+  int64_t done = 0, cum = 0, T = c.entry;
+  int code = PQH_OK;
+  int w = 0;
+  for (; w < wr.y && done < c.count; w++) {
+    BaWin* r = res + wr.x + w;
+    if (T >= c.e0) {  // no bytes left for the next length
+      code = PQH_ERR_EOF;
       break;
     }
-    entry = C.exitv[kBlock - 1];
+    __syncthreads();
+    if (threadIdx.x == 0) cur = *r;
+    __syncthreads();
+    if (cur.entry != T) {  // the window's guess was not its true entry: resolve it again
+      ba_window(C, c, w, T, r, marks + int64_t(wr.x + w) * kBlock * kChainWords);
+      __syncthreads();
+      if (threadIdx.x == 0) cur = *r;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      r->base = done;
+      r->cbase = cum;
+    }
+    done += cur.count;
+    cum += cur.bytes;
+    if (cur.bad) {
+      code = cur.bad;
+      w++;
+      break;
+    }
+    T = cur.exit;
   }
-  if (j == 0) {
-    if (done >= count) {  // all values read (records past `count` are never looked at)
-      if (dict) {
-        if (count == 0) out[0] = 0;
-        b.states[p].dict_n = int32_t(count);
+  if (threadIdx.x == 0) {
+    for (; w < wr.y; w++) res[wr.x + w].base = -1;  // windows past the chain's end or `count`
+    int32_t* out = c.dict ? b.dcum + b.pages[p].aux_base : nullptr;
+    if (done >= c.count) {  // all values read (records past `count` are never looked at)
+      if (c.dict) {
+        if (c.count == 0) out[0] = 0;
+        b.states[p].dict_n = int32_t(c.count);
       } else {
-        b.states[p].val_limit = int32_t(count);
+        b.states[p].val_limit = int32_t(c.count);
       }
-    } else if (dict) {
+    } else if (c.dict) {
       atomicMin(&b.states[p].err, (unsigned long long)err_key(0, done, code));
     } else {
       b.states[p].val_limit = int32_t(done);
       atomicMin(&b.states[p].err, (unsigned long long)err_key(3, done, code));
+    }
+  }
+}
+
+// One workgroup per window: records numbered and emitted (lengths or cumulative dictionary offsets).
+__global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* wins, const BaWin* res,
+                                                   const uint64_t* marks) {
+  __shared__ uint64_t wsum[4];
+  const BaWin r = res[blockIdx.x];
+  if (r.base < 0 || r.entry < 0) return;
+  const int p = wins[blockIdx.x].x;
+  const BaPageCtx c = ba_page_ctx(b, p);
+  if (!c.ok) return;
+  const int j = threadIdx.x;
+  const int64_t wb = r.entry - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(r.entry)) & 15);
+  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+  const uint64_t* mk = marks + int64_t(blockIdx.x) * kBlock * kChainWords + j * kChainWords;
+  uint64_t m[kChainWords];
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) {
+    m[k] = mk[k];
+    cnt += __popcll(m[k]);
+  }
+  auto len_at = [&](int64_t pos) {
+    typedef int32_t i32u __attribute__((aligned(1)));
+    return int32_t(*(const PQH_G i32u*)(c.img + pos));
+  };
+  int64_t bytes = 0;
+  if (c.dict) {
+#pragma unroll
+    for (int k = 0; k < kChainWords; k++) {
+      uint64_t x = m[k];
+      while (x) {
+        bytes += len_at(s0 + __builtin_ctzll(x) + 64 * k);
+        x &= x - 1;
+      }
+    }
+  }
+  uint64_t tot, btot;
+  const int64_t before = int64_t(block_exclusive_scan(uint64_t(cnt), wsum, &tot));
+  const int64_t bbefore = c.dict ? int64_t(block_exclusive_scan(uint64_t(bytes), wsum, &btot)) : 0;
+  PQH_G int32_t* out = c.dict ? (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base)
+                              : b.chunks[b.pages[p].chunk].aux + b.states[p].value_base;
+  int64_t idx = r.base + before, cu = r.cbase + bbefore;
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) {
+    uint64_t x = m[k];
+    while (x) {
+      const int32_t l = len_at(s0 + __builtin_ctzll(x) + 64 * k);
+      x &= x - 1;
+      if (idx < c.count) {
+        out[idx] = c.dict ? int32_t(cu) : l;
+        if (c.dict && idx == c.count - 1) out[c.count] = int32_t(cu + l);
+      }
+      idx++;
+      cu += l;
     }
   }
 }

@@ -163,6 +163,26 @@ enum TileKind : int32_t {
 
 constexpr int kBaTile = 2048;  // byte-array values per tile (one 256 x 8 block scan)
 
+// PLAIN byte-array chains (k_ba_wspec / k_ba_wstitch / k_ba_wemit): windows of 256 segments.
+constexpr int kChainSeg = 252;
+constexpr int kChainWin = kChainSeg * kBlock;      // 64512 bytes per window
+constexpr int kChainWords = (kChainSeg + 63) / 64; // mask words per segment
+constexpr int kChainStride = kChainWin - 16;       // window bases: the window staged from a 16-aligned
+                                                   // entry >= B_w still covers [entry, B_w+1)
+
+// Scratch per window (k_ba_wspec -> k_ba_wstitch -> k_ba_wemit).
+struct BaWin {
+  int32_t entry;   // the entry the window was resolved from (-1: nothing to do)
+  int32_t exit;    // first record start >= B_w+1, or where the chain ended
+  int32_t count;   // records on the chain in the window before the first invalid one
+  int32_t bad;     // error code of the first invalid record (0: none in the window)
+  int64_t bytes;   // byte sum of those records' lengths (dictionary pages)
+  int64_t base;    // k_ba_wstitch: records before the window (-1: not emitted)
+  int64_t cbase;   // k_ba_wstitch: bytes before the window
+  int64_t pad;
+};
+
+
 // Nesting outputs of a repeated chunk (pqh_batch_nesting): list offsets / presence per repetition
 // level and leaf validity, from the chunk's decoded level bytes.
 constexpr int kMaxNest = 8;

@@ -1034,9 +1034,24 @@ hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, in
   return hipGetLastError();
 }
 
-hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s) {
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint64_t* marks,
+                           hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_walk, dim3(n), dim3(256), 0, s, b, ba_pages, n);
+  hipLaunchKernelGGL(k_ba_wspec, dim3(n), dim3(256), 0, s, b, wins, res, marks);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
+                             uint64_t* marks, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_wstitch, dim3(n), dim3(256), 0, s, b, ba_pages, pwin, res, marks);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const uint64_t* marks,
+                           hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, wins, res, marks);
   return hipGetLastError();
 }
 

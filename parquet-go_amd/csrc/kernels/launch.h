@@ -47,7 +47,14 @@ hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n,
 hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
 // per-chunk offset scan, offsets + byte copy.
-hipError_t launch_ba_walk(const DevBatch& b, const int32_t* ba_pages, int32_t n, hipStream_t s);
+// PLAIN chains: every window of every PLAIN page resolved from a guessed entry, windows stitched
+// per page (wrong guesses resolved again), records emitted per window.
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint64_t* marks,
+                           hipStream_t s);
+hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
+                             uint64_t* marks, hipStream_t s);
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const uint64_t* marks,
+                           hipStream_t s);
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
