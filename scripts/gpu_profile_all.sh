@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 per workload: kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate passes
+# (gfx950 counter slots).  Outputs gpurun_out/prof_<w>_{trace,fetch,write}; summarise with
+#   python scripts/pmc_summary.py <tag> gpurun_out prof_<w>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=$PWD/gpurun_out
+mkdir -p "$OUT"
+run() {  # run <name> <timeout> <bench args> -- <rocprof args...>
+  local name=$1 to=$2 args=$3; shift 3
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$to" rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python bench.py $args > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 2 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for w in ${WORKLOADS:-c2 c3 c5}; do
+  A="--workload $w --steps 10 --warmup 2 --no-cpu"
+  [ "$w" = c2 ] && A="--steps 10 --warmup 2 --no-cpu"
+  run prof_${w}_trace 600 "$A" --kernel-trace --stats -T
+  run prof_${w}_fetch 600 "$A" --pmc FETCH_SIZE --kernel-trace -T
+  run prof_${w}_write 600 "$A" --pmc WRITE_SIZE --kernel-trace -T
+done

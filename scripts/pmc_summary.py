@@ -8,7 +8,7 @@ HBM traffic per launch = FETCH_SIZE x 2 + WRITE_SIZE (KB -> bytes): on gfx950 FE
 half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md §HBM); every read of the
 decode kernels is a 16-byte-per-lane coalesced load (copies, LDS staging) or an 8-byte load.
 
-usage: python scripts/pmc_summary.py <tag> [gpurun_out]
+usage: python scripts/pmc_summary.py <tag> [gpurun_out] [prefix (default prof)]
 """
 import csv
 import json
@@ -38,15 +38,16 @@ def durations(path):
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
+    pre = sys.argv[3] if len(sys.argv) > 3 else "prof"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles", tag)
     os.makedirs(out, exist_ok=True)
-    stats = os.path.join(src, "prof_trace", "run_kernel_stats.csv")
+    stats = os.path.join(src, pre + "_trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(out, "kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(src, "prof_fetch", "run_counter_collection.csv"))
-    write = per_kernel(os.path.join(src, "prof_write", "run_counter_collection.csv"))
-    dur = durations(os.path.join(src, "prof_trace", "run_kernel_trace.csv"))
+    fetch = per_kernel(os.path.join(src, pre + "_fetch", "run_counter_collection.csv"))
+    write = per_kernel(os.path.join(src, pre + "_write", "run_counter_collection.csv"))
+    dur = durations(os.path.join(src, pre + "_trace", "run_kernel_trace.csv"))
     kernels = {}
     for k in sorted(set(fetch) | set(write) | set(dur)):
         f = fetch.get(k)
@@ -58,7 +59,7 @@ def main():
                       "hbm_traffic_bytes_per_launch": traffic}
     summary = {"source": "rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE (separate passes)",
                "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md §HBM)", "kernels": kernels}
-    for name in ("bench.log", "prof_trace.log"):
+    for name in ("bench.log", pre + "_trace.log"):
         p = os.path.join(src, name)
         if os.path.exists(p):
             for line in open(p):
