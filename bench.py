@@ -8,7 +8,7 @@ Default workload = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data pa
 groups per GPU.  Multi-GPU: one process per GPU (torchrun), row groups sharded (each rank decodes
 its own 16 row groups, different seed), no data-path collective -> "scaling": "weak".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c5] [--rows R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c4|c5] [--rows R]
 """
 import argparse
 import json
@@ -90,7 +90,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -116,7 +116,7 @@ def main():
     kw = {}
     if args.rows:
         kw["rows"] = args.rows
-    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c5": 40}[args.workload] + 1000 * rank
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40}[args.workload] + 1000 * rank
     t0 = time.perf_counter()
     data = builder(seed=seed_kw, **kw)
     gen_s = time.perf_counter() - t0
@@ -209,7 +209,7 @@ def main():
             "vs_baseline": None,
             "dtype": "int32/int64/f32/f64/bool/flba16 (bit-exact integer/byte decode)" if args.workload == "c2"
             else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload == "c5"
-            else "int64",
+            else "int64/int32/bytes + u8 levels + int32 list offsets" if args.workload == "c4" else "int64",
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
             "config": {"workload": desc, "rows_per_gpu": f.num_rows, "row_groups_per_gpu": f.num_row_groups,
                        "pages_per_gpu": hb.num_pages, "parallelism": f"row-group sharded x{world}, no collective",

@@ -167,7 +167,7 @@ struct pqh_batch {
   int2* d_ba_wins = nullptr;        // (page, window) of every PLAIN chain window
   int2* d_ba_pwin = nullptr;        // per PLAIN page: (first window, windows)
   BaWin* d_ba_res = nullptr;
-  uint64_t* d_ba_marks = nullptr;
+  int32_t* d_ba_wrec = nullptr;     // per window: its records' lengths / cumulative bytes
   int32_t* d_ba_chunks = nullptr;
   int32_t* d_dcum = nullptr;
   int64_t* d_basums = nullptr;
@@ -541,8 +541,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wins), sizeof(int2) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pwin), sizeof(int2) * b->ba_pwin.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_res), sizeof(BaWin) * b->ba_wins.size())) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_marks),
-                   sizeof(uint64_t) * size_t(kBlock) * kChainWords * b->ba_wins.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wrec), sizeof(int32_t) * size_t(kChainRecs) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
@@ -722,13 +721,13 @@ int pqh_batch_run(pqh_batch* b) {
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
   if (e == hipSuccess && nbp) {
     const int32_t nw = int32_t(b->ba_wins.size());
-    e = timed(7, nw, s, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_marks, st); });
+    e = timed(7, nw, s, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
     if (e == hipSuccess)
       e = timed(20, nbp, s, [&](hipStream_t st) {
-        return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_marks, st);
+        return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_wrec, st);
       });
     if (e == hipSuccess)
-      e = timed(21, nw, s, [&](hipStream_t st) { return launch_ba_wemit(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_marks, st); });
+      e = timed(21, nw, s, [&](hipStream_t st) { return launch_ba_wemit(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
   }
   if (e == hipSuccess && ndt && b->delta_page_mode) {
     const int32_t nds = int32_t(b->delta_streams.size());

@@ -26,13 +26,14 @@
 //     252-byte segment and walks it from a speculative start (the shortest plausible record among
 //     four neighbouring offsets), the walks are checked in parallel against their predecessor's
 //     exit and the first mismatch re-walked from its true entry until all agree; the window's
-//     record-start marks, count, byte sum, exit and first invalid record go to scratch;
+//     records (lengths, or bytes before each record for dictionary pages), count, byte sum, exit and
+//     first invalid record go to scratch;
 //   * k_ba_wstitch (one workgroup per page): window w's entry must be window w-1's exit; a window
 //     whose guess was wrong is resolved again from the true entry (rare); window bases = running
 //     record / byte counts; the page's error (the first invalid record on the chain before `count`
 //     records) and limits;
-//   * k_ba_wemit (one workgroup per window): records numbered by block scans of the marks,
-//     lengths (data page -> aux) or cumulative offsets (dictionary page -> dcum) written.
+//   * k_ba_wemit (one workgroup per window): the window's records copied out at its base: lengths
+//     (data page -> aux) or cumulative offsets (dictionary page -> dcum).
 // ------------------------------------------------------------------------------------------------
 // 252-byte segments: neighbouring lanes' segments start 63 dwords apart, so their LDS reads fall in
 // different banks (a power-of-two stride would put a whole wave on one bank)
@@ -234,17 +235,19 @@ __device__ __forceinline__ BaPageCtx ba_page_ctx(const DevBatch& b, int p) {
   return c;
 }
 
-// Stage, resolve and summarise one window (whole workgroup); marks to scratch.
-__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry, BaWin* res,
-                          uint64_t* marks) {
+// Stage, resolve and summarise one window (whole workgroup).  Its records go to the window's scratch
+// in order: lengths (data pages) or the bytes before each record within the window (dictionary
+// pages; one more entry holds the window's total).
+__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry, BaWin* res, int32_t* wrec) {
   const int j = threadIdx.x;
   const int64_t wend = c.entry + (w + 1) * kChainStride;
   BaWin r{int32_t(entry), int32_t(entry), 0, 0, 0, -1, 0, 0};
   if (entry >= c.e0 || entry >= wend) {  // no record starts in the window (or no bytes left)
     if (entry >= c.e0 && entry < wend) r.bad = PQH_ERR_EOF;
-    if (j == 0) *res = r;
-#pragma unroll
-    for (int k = 0; k < kChainWords; k++) marks[j * kChainWords + k] = 0;
+    if (j == 0) {
+      *res = r;
+      wrec[0] = 0;
+    }
     return;
   }
   const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(entry)) & 15);
@@ -255,25 +258,29 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   const int fb = C.first_bad;
   uint64_t m[kChainWords];
   const int cnt = chain_marks(C, j, wb, entry, fb, m);
+  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+  auto len_lds = [&](int64_t pos) {
+    const int64_t o = pos - wb;
+    return int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
+  };
   int64_t bytes = 0;
   if (c.dict) {
-    const int64_t s0 = wb + int64_t(j) * kChainSeg;
 #pragma unroll
-    for (int k = 0; k < kChainWords; k++) {
-      uint64_t x = m[k];
-      while (x) {
-        const int64_t o = s0 + __builtin_ctzll(x) + 64 * k - wb;
-        x &= x - 1;
-        bytes += int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
-      }
-    }
+    for (int k = 0; k < kChainWords; k++)
+      for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(s0 + __builtin_ctzll(x) + 64 * k);
   }
+  uint64_t tot, btot = 0;
+  int32_t li = int32_t(block_exclusive_scan(uint64_t(cnt), C.wsum, &tot));
+  int64_t lb = c.dict ? int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot)) : 0;
 #pragma unroll
-  for (int k = 0; k < kChainWords; k++) marks[j * kChainWords + k] = m[k];
-  uint64_t tot, btot;
-  block_exclusive_scan(uint64_t(cnt), C.wsum, &tot);
-  block_exclusive_scan(uint64_t(bytes), C.wsum, &btot);
+  for (int k = 0; k < kChainWords; k++)
+    for (uint64_t x = m[k]; x; x &= x - 1) {
+      const int32_t l = len_lds(s0 + __builtin_ctzll(x) + 64 * k);
+      wrec[li++] = c.dict ? int32_t(lb) : l;
+      lb += l;
+    }
   if (j == 0) {
+    if (c.dict) wrec[tot] = int32_t(btot);
     r.count = int32_t(tot);
     r.bytes = int64_t(btot);
     if (fb < kBlock) {
@@ -287,12 +294,12 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, uint64_t* marks) {
+__global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, int32_t* wrec) {
   __shared__ ChainLds C;
   const int2 pw = wins[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, pw.x);
   BaWin* r = res + blockIdx.x;
-  uint64_t* mk = marks + int64_t(blockIdx.x) * kBlock * kChainWords;
+  int32_t* mk = wrec + int64_t(blockIdx.x) * kChainRecs;
   const int64_t Bw = c.entry + int64_t(pw.y) * kChainStride;
   if (!c.ok || Bw >= c.e0) {
     if (threadIdx.x == 0) *r = BaWin{-1, -1, 0, 0, 0, -1, 0, 0};
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, 
 }
 // One workgroup per PLAIN byte-array page: windows stitched in order (see above).
 __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* ba_pages, const int2* pwin, BaWin* res,
-                                                     uint64_t* marks) {
+                                                     int32_t* wrec) {
   __shared__ ChainLds C;
   __shared__ BaWin cur;
   const int p = ba_pages[blockIdx.x];
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
     if (threadIdx.x == 0) cur = *r;
     __syncthreads();
     if (cur.entry != T) {  // the window's guess was not its true entry: resolve it again
-      ba_window(C, c, w, T, r, marks + int64_t(wr.x + w) * kBlock * kChainWords);
+      ba_window(C, c, w, T, r, wrec + int64_t(wr.x + w) * kChainRecs);
       __syncthreads();
       if (threadIdx.x == 0) cur = *r;
       __syncthreads();
@@ -372,60 +379,23 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
   }
 }
 
-// One workgroup per window: records numbered and emitted (lengths or cumulative dictionary offsets).
+// One workgroup per window: its records' lengths (data page -> aux) or cumulative offsets
+// (dictionary page -> dcum) copied out at the window's base.
 __global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* wins, const BaWin* res,
-                                                   const uint64_t* marks) {
-  __shared__ uint64_t wsum[4];
+                                                   const int32_t* wrec) {
   const BaWin r = res[blockIdx.x];
   if (r.base < 0 || r.entry < 0) return;
   const int p = wins[blockIdx.x].x;
   const BaPageCtx c = ba_page_ctx(b, p);
   if (!c.ok) return;
-  const int j = threadIdx.x;
-  const int64_t wb = r.entry - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(r.entry)) & 15);
-  const int64_t s0 = wb + int64_t(j) * kChainSeg;
-  const uint64_t* mk = marks + int64_t(blockIdx.x) * kBlock * kChainWords + j * kChainWords;
-  uint64_t m[kChainWords];
-  int cnt = 0;
-#pragma unroll
-  for (int k = 0; k < kChainWords; k++) {
-    m[k] = mk[k];
-    cnt += __popcll(m[k]);
-  }
-  auto len_at = [&](int64_t pos) {
-    typedef int32_t i32u __attribute__((aligned(1)));
-    return int32_t(*(const PQH_G i32u*)(c.img + pos));
-  };
-  int64_t bytes = 0;
-  if (c.dict) {
-#pragma unroll
-    for (int k = 0; k < kChainWords; k++) {
-      uint64_t x = m[k];
-      while (x) {
-        bytes += len_at(s0 + __builtin_ctzll(x) + 64 * k);
-        x &= x - 1;
-      }
-    }
-  }
-  uint64_t tot, btot;
-  const int64_t before = int64_t(block_exclusive_scan(uint64_t(cnt), wsum, &tot));
-  const int64_t bbefore = c.dict ? int64_t(block_exclusive_scan(uint64_t(bytes), wsum, &btot)) : 0;
+  const int32_t* src = wrec + int64_t(blockIdx.x) * kChainRecs;
   PQH_G int32_t* out = c.dict ? (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base)
                               : b.chunks[b.pages[p].chunk].aux + b.states[p].value_base;
-  int64_t idx = r.base + before, cu = r.cbase + bbefore;
-#pragma unroll
-  for (int k = 0; k < kChainWords; k++) {
-    uint64_t x = m[k];
-    while (x) {
-      const int32_t l = len_at(s0 + __builtin_ctzll(x) + 64 * k);
-      x &= x - 1;
-      if (idx < c.count) {
-        out[idx] = c.dict ? int32_t(cu) : l;
-        if (c.dict && idx == c.count - 1) out[c.count] = int32_t(cu + l);
-      }
-      idx++;
-      cu += l;
-    }
+  for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
+    const int64_t idx = r.base + i;
+    if (idx >= c.count) break;
+    out[idx] = c.dict ? int32_t(r.cbase + src[i]) : src[i];
+    if (c.dict && idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
   }
 }
 

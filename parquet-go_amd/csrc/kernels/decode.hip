@@ -1034,24 +1034,24 @@ hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, in
   return hipGetLastError();
 }
 
-hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint64_t* marks,
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, int32_t* wrec,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_wspec, dim3(n), dim3(256), 0, s, b, wins, res, marks);
+  hipLaunchKernelGGL(k_ba_wspec, dim3(n), dim3(256), 0, s, b, wins, res, wrec);
   return hipGetLastError();
 }
 
 hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
-                             uint64_t* marks, hipStream_t s) {
+                             int32_t* wrec, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_wstitch, dim3(n), dim3(256), 0, s, b, ba_pages, pwin, res, marks);
+  hipLaunchKernelGGL(k_ba_wstitch, dim3(n), dim3(256), 0, s, b, ba_pages, pwin, res, wrec);
   return hipGetLastError();
 }
 
-hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const uint64_t* marks,
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const int32_t* wrec,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, wins, res, marks);
+  hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, wins, res, wrec);
   return hipGetLastError();
 }
 

@@ -49,11 +49,11 @@ hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, 
 // per-chunk offset scan, offsets + byte copy.
 // PLAIN chains: every window of every PLAIN page resolved from a guessed entry, windows stitched
 // per page (wrong guesses resolved again), records emitted per window.
-hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint64_t* marks,
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, int32_t* wrec,
                            hipStream_t s);
 hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
-                             uint64_t* marks, hipStream_t s);
-hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const uint64_t* marks,
+                             int32_t* wrec, hipStream_t s);
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const int32_t* wrec,
                            hipStream_t s);
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);

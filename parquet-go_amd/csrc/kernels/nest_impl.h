@@ -16,19 +16,34 @@
 
 constexpr int kNestPer = kNestTile / kBlock;  // 32 consecutive slots per thread
 
-// Flags of one slot: bit f = E_f (bit 0 = row start).
-__device__ __forceinline__ uint32_t nest_flags(const DevNest& N, int32_t d, int32_t r) {
-  uint32_t f = r == 0 ? 1u : 0u;
+// The flag masks of a thread's 32 slots (bit j = slot j): E_f, V_l, LV (see k_nest_write).
+__device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, int64_t s0, int m,
+                                           uint32_t E[kNestFlags], uint32_t V[kMaxNest], uint32_t& LV) {
+  const int L = N.levels;
 #pragma unroll
-  for (int l = 1; l <= kMaxNest; l++)
-    if (l <= N.levels && r <= l && d >= N.rep_def[l - 1]) f |= 1u << l;
-  return f;
-}
-
-__device__ __forceinline__ void nest_load(const DevNest& N, const DevChunk& C, int64_t s0, uint8_t* d, uint8_t* r) {
-  // 32 level bytes of each stream; the level buffers carry 64 bytes of slack past n
-  __builtin_memcpy(d, C.def_levels + s0, 32);
-  __builtin_memcpy(r, C.rep_levels + s0, 32);
+  for (int f = 0; f < kNestFlags; f++) E[f] = 0;
+#pragma unroll
+  for (int l = 0; l < kMaxNest; l++) V[l] = 0;
+  LV = 0;
+  if (m <= 0) return;
+  // 32 level bytes of each stream (the level buffers carry 64 bytes of slack past n)
+  uint32_t dw[8], rw[8];
+  __builtin_memcpy(dw, C.def_levels + s0, 32);
+  __builtin_memcpy(rw, C.rep_levels + s0, 32);
+#pragma unroll
+  for (int j = 0; j < kNestPer; j++) {
+    const uint32_t d = (dw[j >> 2] >> (8 * (j & 3))) & 0xff, r = (rw[j >> 2] >> (8 * (j & 3))) & 0xff;
+    const uint32_t in = j < m ? 1u << j : 0u;
+    E[0] |= r == 0 ? in : 0u;
+#pragma unroll
+    for (int l = 1; l <= kMaxNest; l++) {
+      if (l <= L) {
+        E[l] |= (r <= uint32_t(l) && d >= uint32_t(N.rep_def[l - 1])) ? in : 0u;
+        V[l - 1] |= d + 1 >= uint32_t(N.rep_def[l - 1]) ? in : 0u;
+      }
+    }
+    LV |= d == uint32_t(N.max_def) ? in : 0u;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_nest_count(DevBatch b, const Tile* tiles) {
@@ -39,19 +54,12 @@ __global__ __launch_bounds__(256) void k_nest_count(DevBatch b, const Tile* tile
   if (threadIdx.x < kNestFlags) cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t s0 = int64_t(t.k) * kNestTile + int64_t(threadIdx.x) * kNestPer;
+  const int m = s0 < N.n ? (N.n - s0 < kNestPer ? int(N.n - s0) : kNestPer) : 0;
+  uint32_t E[kNestFlags], V[kMaxNest], LV;
+  nest_masks(N, C, s0, m, E, V, LV);
   int32_t c[kNestFlags];
 #pragma unroll
-  for (int f = 0; f < kNestFlags; f++) c[f] = 0;
-  if (s0 < N.n) {
-    uint8_t d[32], r[32];
-    nest_load(N, C, s0, d, r);
-    const int m = N.n - s0 < kNestPer ? int(N.n - s0) : kNestPer;
-    for (int j = 0; j < m; j++) {
-      const uint32_t fl = nest_flags(N, d[j], r[j]);
-#pragma unroll
-      for (int f = 0; f < kNestFlags; f++) c[f] += (fl >> f) & 1;
-    }
-  }
+  for (int f = 0; f < kNestFlags; f++) c[f] = __popc(E[f]);
 #pragma unroll
   for (int f = 0; f < kNestFlags; f++) {
     int32_t x = c[f];
@@ -98,47 +106,89 @@ __global__ __launch_bounds__(256) void k_nest_scan(DevBatch b) {
   }
 }
 
+// Copy n staged elements (LDS, laid out from a 16-byte aligned origin: element i of the range at
+// lds[lead + i]) to dst[0..n) with 16-byte stores; the partial vectors at both ends byte by byte.
+template <class T>
+__device__ __forceinline__ void nest_flush(PQH_G T* dst, const T* lds, int lead, int n) {
+  constexpr int E = 16 / sizeof(T);  // elements per vector
+  const int total = lead + n;
+  const int nvec = (total + E - 1) / E;
+  PQH_G T* origin = dst - lead;
+  for (int v = threadIdx.x; v < nvec; v += kBlock) {
+    const int i0 = v * E;
+    if (i0 >= lead && i0 + E <= total) {
+      uint4 x;
+      __builtin_memcpy(&x, lds + i0, 16);
+      *reinterpret_cast<PQH_G uint4*>(origin + i0) = x;
+    } else {
+      for (int i = i0; i < i0 + E; i++)
+        if (i >= lead && i < total) origin[i] = lds[i];
+    }
+  }
+}
+
+// Write pass: the tile's list offsets / presence per level and its leaf validity are staged in LDS
+// (each output range of a tile is contiguous) and flushed with coalesced 16-byte stores.  Per thread
+// the 32 slots' flags are bit masks (bit j = slot j): E_f (element / list starts), V_l (list of
+// level l present), LV (leaf non-null), so counts are popcounts and positions prefix popcounts.
 __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tiles) {
   __shared__ uint64_t wsum[4];
+  __shared__ __attribute__((aligned(16))) int32_t st32[kNestTile + 4];
+  __shared__ __attribute__((aligned(16))) uint8_t st8[kNestTile + 16];
   const Tile t = tiles[blockIdx.x];
   const DevNest N = b.nests[t.page];
   const DevChunk C = b.chunks[N.chunk];
   const int64_t s0 = int64_t(t.k) * kNestTile + int64_t(threadIdx.x) * kNestPer;
   const int m = s0 < N.n ? (N.n - s0 < kNestPer ? int(N.n - s0) : kNestPer) : 0;
-  const uint8_t* dl = C.def_levels + s0;
-  const uint8_t* rl = C.rep_levels + s0;
   const int L = N.levels;
-  int32_t c[kNestFlags];
-#pragma unroll
-  for (int f = 0; f < kNestFlags; f++) c[f] = 0;
-  for (int j = 0; j < m; j++) {
-    const uint32_t x = nest_flags(N, dl[j], rl[j]);
-#pragma unroll
-    for (int f = 0; f < kNestFlags; f++) c[f] += (x >> f) & 1;
-  }
+  uint32_t E[kNestFlags], V[kMaxNest], LV;
+  nest_masks(N, C, s0, m, E, V, LV);
   const int64_t* base = b.nsums + int64_t(N.tile_base + t.k) * kNestFlags;
-  int64_t pos[kNestFlags];  // running index of each flag at this thread's next slot
+  int32_t lpos[kNestFlags], tot[kNestFlags];
+  int64_t gbase[kNestFlags];
 #pragma unroll
   for (int f = 0; f < kNestFlags; f++) {
-    pos[f] = 0;
+    lpos[f] = 0;
+    tot[f] = 0;
+    gbase[f] = 0;
     if (f <= L) {  // uniform
-      uint64_t tot;
-      pos[f] = base[f] + int64_t(block_exclusive_scan(uint64_t(c[f]), wsum, &tot));
+      uint64_t tt;
+      lpos[f] = int32_t(block_exclusive_scan(uint64_t(__popc(E[f])), wsum, &tt));
+      tot[f] = int32_t(tt);
+      gbase[f] = base[f];
     }
   }
-  for (int j = 0; j < m; j++) {  // the level bytes are L1-resident from the first loop
-    const int32_t d = dl[j];
-    const uint32_t x = nest_flags(N, d, rl[j]);
 #pragma unroll
-    for (int l = 1; l <= kMaxNest; l++) {
-      if (l <= L && ((x >> (l - 1)) & 1)) {  // a list of level l starts here
-        const int64_t k = pos[l - 1];
-        N.offsets[l - 1][k] = int32_t(pos[l]);
-        N.validity[l - 1][k] = d >= N.rep_def[l - 1] - 1;
-      }
-      if (l == L && ((x >> l) & 1)) N.leaf_valid[pos[l]] = d == N.max_def;
+  for (int l = 1; l <= kMaxNest; l++) {  // lists of level l start at the E_{l-1} slots
+    if (l > L) break;
+    const int lead32 = int(gbase[l - 1] & 3), lead8 = int(gbase[l - 1] & 15);
+    int32_t k = lpos[l - 1];
+    for (uint32_t x = E[l - 1]; x; x &= x - 1) {
+      const int j = __builtin_ctz(x);
+      st32[lead32 + k] = int32_t(gbase[l] + lpos[l] + __popc(E[l] & ((1u << j) - 1)));
+      st8[lead8 + k] = uint8_t((V[l - 1] >> j) & 1);
+      k++;
     }
-#pragma unroll
-    for (int f = 0; f < kNestFlags; f++) pos[f] += (x >> f) & 1;
+    __syncthreads();
+    nest_flush(N.offsets[l - 1] + gbase[l - 1], st32, lead32, tot[l - 1]);
+    nest_flush(N.validity[l - 1] + gbase[l - 1], st8, lead8, tot[l - 1]);
+    __syncthreads();
   }
+  // leaf validity at the E_L slots
+  uint32_t EL = 0;
+  int32_t lposL = 0, totL = 0;
+  int64_t gbaseL = 0;
+#pragma unroll
+  for (int f = 1; f < kNestFlags; f++)
+    if (f == L) {
+      EL = E[f];
+      lposL = lpos[f];
+      totL = tot[f];
+      gbaseL = gbase[f];
+    }
+  const int lead8 = int(gbaseL & 15);
+  int32_t k = lposL;
+  for (uint32_t x = EL; x; x &= x - 1) st8[lead8 + k++] = uint8_t((LV >> __builtin_ctz(x)) & 1);
+  __syncthreads();
+  nest_flush(N.leaf_valid + gbaseL, st8, lead8, totL);
 }
