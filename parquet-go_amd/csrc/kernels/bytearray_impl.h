@@ -573,6 +573,14 @@ __device__ __forceinline__ void block_copy(PQH_G uint8_t* dst, const PQH_G uint8
 // Byte copy of one value (unaligned on both sides; values average tens of bytes).
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len);
 
+// ceil(len / 8) unaligned 8-byte words (len > 0).
+__device__ __forceinline__ void copy_words(PQH_G uint8_t* dst, const uint8_t* src_, int64_t len) {
+  typedef uint64_t u64u __attribute__((aligned(1)));
+  const PQH_G u64u* s = (const PQH_G u64u*)(src_);
+  PQH_G u64u* d = (PQH_G u64u*)(dst);
+  for (int64_t k = 0; k < len; k += 8) d[k >> 3] = s[k >> 3];
+}
+
 // DELTA_BYTE_ARRAY tile (byteArrayDeltaDecoder.decodeValues, type_bytearray.go:213-240): offsets
 // from prefix + suffix lengths, the per-value checks in the reference's order (suffix read short,
 // negative total, prefix longer than the previous value), and each suffix copied into place after
@@ -748,7 +756,15 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     } else {  // PLAIN: value i's bytes follow its u32 length
       src = img + S.val_s + 4 * (i + 1) + rel;
     }
-    if (!is_dlba && src && l > 0 && o + l <= C.bytes_cap) copy_bytes(C.bytes + o, src, l);
+    if (!is_dlba && src && l > 0 && o + l <= C.bytes_cap) {
+      // every value but the thread's last is copied in whole 8-byte words: the bytes written past
+      // its end are overwritten by the thread's next value (the payload pad covers the over-read)
+      int64_t rest = 0;  // bytes of the thread's later values: they overwrite the word tail
+#pragma unroll
+      for (int q = j + 1; q < 8; q++) rest += len[q] > 0 ? len[q] : 0;
+      if (((l + 7) & ~7) - l <= rest && o + ((l + 7) & ~7) <= C.bytes_cap) copy_words(C.bytes + o, src, l);
+      else copy_bytes(C.bytes + o, src, l);
+    }
     o += l;
     offs[i] = o;
   }
