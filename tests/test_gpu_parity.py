@@ -523,11 +523,15 @@ def test_plain_chain_layouts(pq, ctx):
                 out.append(rng.bytes(int(rng.integers(200, 3000))) if u < 0.8 else b"")
             elif kind == "huge":
                 out.append(rng.bytes(int(rng.integers(60000, 140000))) if u < 0.3 else rng.bytes(5))
+            elif kind == "lookalike":  # strings of small little-endian u32s: most offsets parse as records
+                k = int(rng.integers(0, 6))
+                out.append(b"".join(int(rng.integers(0, 24)).to_bytes(4, "little") for _ in range(k)))
             else:
                 out.append(bytes(rng.integers(97, 123, int(rng.integers(8, 41))).astype(np.uint8)))
         return out
 
-    for kind, n in (("empty_runs", 40000), ("zeros", 30000), ("long", 400), ("huge", 12), ("ascii", 60000)):
+    for kind, n in (("empty_runs", 40000), ("zeros", 30000), ("long", 400), ("huge", 12), ("ascii", 60000),
+                    ("lookalike", 50000)):
         s = strings(n, kind)
         img = _plain_chain(s)
         cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, img)))
@@ -536,7 +540,7 @@ def test_plain_chain_layouts(pq, ctx):
         k = int(rng.integers(0, n))
         cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0,
                                   _plain_chain(s[:k]) + b"\x00\x00\x00\x80" + _plain_chain(s[k:]))))
-        d = s[: min(n, 3000)]
+        d = s[: min(n, 30000)]  # dictionary pages of several chain windows
         idx = rng.integers(0, len(d), 5000).astype(np.int32)
         w = max(1, int(len(d) - 1).bit_length())
         cases.append((col, (len(d), W.PLAIN, _plain_chain(d)),
