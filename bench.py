@@ -33,32 +33,58 @@ def package():
     return ge._package()
 
 
-def cpu_baseline(data, seconds):
-    """The oracle (plain-C restatement of the reference decoders, 1 core) on a bounded sample of
-    the same file: whole row groups until `seconds` of decode work (walk excluded)."""
+def cpu_baseline(data, seconds, threads=1):
+    """The oracle (plain-C restatement of the reference decoders) on a bounded sample of the same
+    file: whole row groups until `seconds` of single-thread decode work (walk excluded).  With
+    threads > 1 the same sample is decoded again chunk-parallel on a thread pool (the C decoder runs
+    without the GIL) -- SURVEY.md §8(d): "1 core and all host cores (page-parallel)"."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O
 
     fr = O.FileReader(data)
     ncols = len(fr.columns)
+
+    def decode(ch):
+        n = 0
+        for r in O.decode_chunk(ch):
+            if r.status:
+                raise RuntimeError(f"oracle failed: status {r.status}")
+            n += len(r.values) + (0 if r.def_levels is None else len(r.def_levels)) + \
+                (0 if r.rep_levels is None else len(r.rep_levels))
+        return n
+
     out_bytes = 0
     spent = 0.0
-    rgs = 0
+    sample = []
     for rg in range(len(fr.row_groups)):
         chunks = [fr.read_chunk(rg, ci) for ci in range(ncols)]
         t0 = time.perf_counter()
         for ch in chunks:
-            for r in O.decode_chunk(ch):
-                if r.status:
-                    raise RuntimeError(f"oracle failed on rg {rg}: status {r.status}")
-                out_bytes += len(r.values) + (0 if r.def_levels is None else len(r.def_levels)) + \
-                    (0 if r.rep_levels is None else len(r.rep_levels))
+            out_bytes += decode(ch)
         spent += time.perf_counter() - t0
-        rgs += 1
+        sample.append(chunks)
         if spent >= seconds:
             break
-    return {"value": round(out_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{rgs} of {len(fr.row_groups)} row groups ({out_bytes / 1e9:.3f} GB decoded) by oracle/refdecode.c "
-                      f"(C restatement of the reference Go decoders), single thread, {spent:.1f} s"}
+    rgs = len(sample)
+    res = {"value": round(out_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{rgs} of {len(fr.row_groups)} row groups ({out_bytes / 1e9:.3f} GB decoded) by oracle/refdecode.c "
+                     f"(C restatement of the reference Go decoders), single thread, {spent:.1f} s"}
+    multi = None
+    if threads > 1:
+        flat = [ch for chunks in sample for ch in chunks]
+        rg = rgs
+        while len(flat) < 2 * threads and rg < len(fr.row_groups):  # enough chunks to occupy the pool
+            flat += [fr.read_chunk(rg, ci) for ci in range(ncols)]
+            rg += 1
+        with ThreadPoolExecutor(threads) as ex:
+            t0 = time.perf_counter()
+            got = sum(ex.map(decode, flat))
+            el = time.perf_counter() - t0
+        multi = {"value": round(got / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+                 "sample": f"{rg} row groups ({len(flat)} chunks) decoded chunk-parallel on {threads} threads, "
+                           f"{el:.2f} s"}
+    return res, multi
 
 
 def pmc_traffic(kernel, workload, rows):
@@ -85,6 +111,26 @@ def pmc_traffic(kernel, workload, rows):
     return None, None
 
 
+def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
+    """Plain pinned host -> HBM copy rate on this box (the PCIe bound of the end-to-end mode)."""
+    import ctypes
+
+    h = ctypes.c_void_p()
+    ctx.check(ctx.L.pqh_host_alloc(ctx.h, ctypes.byref(h), nbytes))
+    d = ctx.malloc(nbytes)
+    try:
+        ctx.h2d(d, h.value, nbytes)
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.h2d(d, h.value, nbytes)
+        ctx.sync()
+        return round(nbytes * reps / (time.perf_counter() - t0) / 1e9, 2)
+    finally:
+        ctx.free(d)
+        ctx.L.pqh_host_free(ctx.h, h.value)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +140,7 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,11 +238,57 @@ def main():
                 "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
                 "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
     all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)
+    batch.close()
+
+    # End-to-end: one staged batch per row-group range holding its decompressed
+    # page images in pinned host memory; every pass copies each range to HBM on the copy stream
+    # while the previous range decodes on the compute stream.  Host decompression excluded.
+    e2e = None
+    if not args.no_e2e:
+        # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
+        # >= 1/16 of the payload each
+        nrg = f.num_row_groups
+        groups = min(nrg, 16)
+        cuts = [nrg * g // groups for g in range(groups + 1)]
+        staged, payload = [], 0
+        for g in range(groups):
+            hbr = f.load(cuts[g], cuts[g + 1], list(range(ncols)))
+            payload += hbr.payload_bytes
+            staged.append(native.Batch.staged(ctx, hbr))
+            hbr.close()
+        e2e_written = 0.0
+        for sb in staged:
+            sb.run_staged()
+        for g, sb in enumerate(staged):
+            sb.sync()
+            e2e_written += sb.traffic()[1]
+            for c in range(ncols * (cuts[g + 1] - cuts[g])):
+                if sb.chunk_out(c).status != native.OK:
+                    raise RuntimeError("staged decode failed")
+        e2e_steps = max(1, min(args.steps, 10))
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(e2e_steps):
+            for sb in staged:
+                sb.run_staged()
+        barrier_sync()
+        e2e_el = time.perf_counter() - t0
+        e2e_el, e2e_total = pkg.shard.reduce_step(e2e_el, e2e_written, device=f"cuda:{local}" if world > 1 else None)
+        e2e = {"mode": "pinned H2D on a copy stream, overlapped per row group with decode; host decompression excluded",
+               "payload_bytes_per_gpu": payload, "staged_batches": groups, "steps": e2e_steps, "ms_per_step": round(e2e_el / e2e_steps * 1e3, 3),
+               "gbps": round(e2e_total * e2e_steps / e2e_el / 1e9, 2),
+               "per_gpu_gbps": round(e2e_written * e2e_steps / e2e_el / 1e9, 2),
+               "payload_h2d_gbps_per_gpu": round(payload * e2e_steps / e2e_el / 1e9, 2),
+               "unstaged_h2d_s": round(h2d_s, 4)}
+        for sb in staged:
+            sb.close()
+        e2e["pinned_h2d_ceiling_gbps"] = pinned_h2d_rate(ctx, native)
     if rank == 0:
-        cpu = None
+        cpu = cpu_mt = None
         if world == 1 and not args.no_cpu:
             log("timing the CPU baseline (oracle) ...")
-            cpu = cpu_baseline(data, args.cpu_seconds)
+            # the GPU box grants this job 16 host cores (os.cpu_count() reports the whole machine)
+            cpu, cpu_mt = cpu_baseline(data, args.cpu_seconds, threads=min(16, os.cpu_count() or 1))
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -222,14 +315,11 @@ def main():
             "kernels": kernels,
             "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 3),
                      "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
-            # end-to-end per GPU: host decompression excluded, pinned H2D of the
-            # decompressed pages + one decode; never `value`
-            "e2e": {"payload_bytes": hb.payload_bytes, "h2d_s": round(h2d_s, 4), "decode_s": round(ms_per_step / 1e3, 5),
-                    "gbps": round(bytes_written / (h2d_s + ms_per_step / 1e3) / 1e9, 2)},
+            "e2e": e2e,
             "cpu_baseline": cpu,
+            "cpu_baseline_multicore": cpu_mt,
         }
         print(json.dumps(line), flush=True)
-    batch.close()
     hb.close()
     ctx.close()
     if world > 1:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 2
+#define PQH_ABI_VERSION 3
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -314,6 +314,18 @@ void pqh_host_batch_free(pqh_host_batch* hb);
 /* Upload a host batch (pinned staging, async H2D on the context stream) and plan it.  The
  * returned batch owns the device copy of the payload. */
 int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out);
+
+/* End-to-end mode ("pinned H2D on a side stream"; north star: "Decompressed page
+ * buffers are staged in HBM with pinned hipMemcpyAsync on a side stream").  Replaces the page-bytes
+ * hand-off of readPageBlock -> dataPageReaderV1/V2.read (chunk_reader.go:161-180, page_v2.go:79-131)
+ * for a whole batch.  pqh_batch_create_staged keeps a pinned host copy of hb's decompressed page
+ * images (the state host decompression leaves them in) plus an HBM payload buffer;
+ * pqh_batch_run_staged enqueues the pinned->HBM copy on the context's copy stream and the decode on
+ * the compute stream behind it, so successive staged batches (e.g. one per row group) overlap
+ * batch i+1's copy with batch i's decode.  A repeat run's copy waits for the previous decode of the
+ * same batch.  Asynchronous: pqh_batch_sync / pqh_sync wait. */
+int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out);
+int pqh_batch_run_staged(pqh_batch* batch);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,7 @@ struct pqh_ctx {
   int32_t device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // staged (end-to-end) runs: pinned -> HBM copies
   std::string err;
 };
 
@@ -149,6 +150,10 @@ struct pqh_batch {
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
   int64_t payload_bytes = 0;
+  void* h_staged = nullptr;           // staged batches: pinned host page images
+  size_t staged_bytes = 0;
+  hipEvent_t ev_copied = nullptr, ev_done = nullptr;
+  bool done_recorded = false;
   DevPage* d_pages = nullptr;
   DevChunk* d_chunks = nullptr;
   PageState* d_states = nullptr;
@@ -196,6 +201,9 @@ void free_batch(pqh_batch* b) {
   for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
   for (void* p : b->allocations) hipFree(p);
   if (b->owned_payload) hipFree(b->owned_payload);
+  if (b->h_staged) hipHostFree(b->h_staged);
+  if (b->ev_copied) hipEventDestroy(b->ev_copied);
+  if (b->ev_done) hipEventDestroy(b->ev_done);
 }
 
 int dalloc(pqh_batch* b, void** p, size_t bytes) {
@@ -249,6 +257,10 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) {
+    hipStreamSynchronize(ctx->copy_stream);
+    hipStreamDestroy(ctx->copy_stream);
+  }
   delete ctx;
 }
 
@@ -1027,6 +1039,7 @@ void pqh_batch_destroy(pqh_batch* b) {
   if (!b) return;
   hipSetDevice(b->ctx->device);
   hipStreamSynchronize(b->ctx->stream);
+  if (b->ctx->copy_stream) hipStreamSynchronize(b->ctx->copy_stream);
   free_batch(b);
   delete b;
 }
@@ -1054,6 +1067,64 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
     return rc;
   }
   (*out)->owned_payload = d;
+  return PQH_OK;
+}
+
+int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out) {
+  *out = nullptr;
+  if (!ctx || !hb) return set_err(ctx, PQH_ERR_ARG, "null argument");
+  hipSetDevice(ctx->device);
+  if (!ctx->copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  const size_t bytes = hb->payload.size();
+  void* h = nullptr;
+  HIP_TRY(ctx, hipHostMalloc(&h, bytes ? bytes : 16, hipHostMallocDefault));
+  if (bytes) memcpy(h, hb->payload.data(), bytes);
+  void* d = nullptr;
+  hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
+  // the first upload happens here so that planning (which reads nothing from the payload) and the
+  // first plain pqh_batch_run see the same bytes as the staged runs
+  if (e == hipSuccess && bytes) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    if (d) hipFree(d);
+    hipHostFree(h);
+    return set_err(ctx, PQH_ERR_HIP, std::string("staged payload: ") + hipGetErrorString(e));
+  }
+  int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
+                            int32_t(hb->pages.size()), d, hb->payload_bytes, out);
+  if (rc) {
+    hipFree(d);
+    hipHostFree(h);
+    return rc;
+  }
+  pqh_batch* b = *out;
+  b->owned_payload = d;
+  b->h_staged = h;
+  b->staged_bytes = bytes;
+  if (hipEventCreateWithFlags(&b->ev_copied, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming) != hipSuccess) {
+    pqh_batch_destroy(b);
+    *out = nullptr;
+    return set_err(ctx, PQH_ERR_HIP, "staged batch events");
+  }
+  return PQH_OK;
+}
+
+int pqh_batch_run_staged(pqh_batch* b) {
+  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
+  pqh_ctx* ctx = b->ctx;
+  if (!b->h_staged) return set_err(ctx, PQH_ERR_ARG, "batch was not created by pqh_batch_create_staged");
+  hipSetDevice(ctx->device);
+  // the copy must not overwrite page images a previous decode of this batch still reads
+  if (b->done_recorded) HIP_TRY(ctx, hipStreamWaitEvent(ctx->copy_stream, b->ev_done, 0));
+  if (b->staged_bytes)
+    HIP_TRY(ctx, hipMemcpyAsync(b->owned_payload, b->h_staged, b->staged_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+  HIP_TRY(ctx, hipEventRecord(b->ev_copied, ctx->copy_stream));
+  HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->ev_copied, 0));
+  int rc = pqh_batch_run(b);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipEventRecord(b->ev_done, ctx->stream));
+  b->done_recorded = true;
   return PQH_OK;
 }
 

@@ -71,7 +71,7 @@ class KernelStat(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 2  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 3  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -117,6 +117,8 @@ PROTOTYPES = [
     ("pqh_host_batch_decompress_seconds", f64, [vp]),
     ("pqh_host_batch_free", None, [vp]),
     ("pqh_batch_create_from_host", ctypes.c_int, [vp, vp, ctypes.POINTER(vp)]),
+    ("pqh_batch_create_staged", ctypes.c_int, [vp, vp, ctypes.POINTER(vp)]),
+    ("pqh_batch_run_staged", ctypes.c_int, [vp]),
 ]
 
 
@@ -325,6 +327,14 @@ class Batch:
         return cls(ctx, h)
 
     @classmethod
+    def staged(cls, ctx, hb):
+        """End-to-end batch: pinned host copy of hb's page images, copied to HBM on every run_staged
+        (copy stream) ahead of the decode (compute stream)."""
+        h = vp()
+        ctx.check(ctx.L.pqh_batch_create_staged(ctx.h, hb.h, ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
     def from_tables(cls, ctx, chunks, pages, d_payload, payload_bytes):
         ch = (Chunk * len(chunks))(*chunks)
         pg = (Page * len(pages))(*pages)
@@ -335,6 +345,9 @@ class Batch:
 
     def run(self):
         self.ctx.check(self.L.pqh_batch_run(self.h))
+
+    def run_staged(self):
+        self.ctx.check(self.L.pqh_batch_run_staged(self.h))
 
     def sync(self):
         self.ctx.check(self.L.pqh_batch_sync(self.h))

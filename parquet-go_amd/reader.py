@@ -89,13 +89,20 @@ class ColumnData:
         return [d[self.offsets[i]:self.offsets[i + 1]] for i in range(len(self.offsets) - 1)]
 
 
-def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, return_batch=False):
+def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, return_batch=False, staged_runs=0):
     """Walk (host) and decode (GPU) the chunks of `columns` in row groups [rg_begin, rg_end).
 
+    staged_runs > 0: end-to-end mode -- the page images stay in pinned host memory and each of the
+    `staged_runs` runs copies them to HBM on the copy stream ahead of the decode.
     Returns a list of ColumnData in (row group, column) order."""
     hb = file.load(rg_begin, rg_end, columns, validate_crc)
-    batch = native.Batch.from_host(ctx, hb)
-    batch.run()
+    if staged_runs:
+        batch = native.Batch.staged(ctx, hb)
+        for _ in range(staged_runs):
+            batch.run_staged()
+    else:
+        batch = native.Batch.from_host(ctx, hb)
+        batch.run()
     batch.sync()
     cols = file.columns()
     res = batch.page_results(hb.num_pages)

@@ -60,6 +60,33 @@ def test_c2_schema(pq, ctx, v2):
     assert checked == 4 * 6
 
 
+def test_staged_end_to_end(pq, ctx):
+    """End-to-end mode: one staged batch per row group (pinned page images, H2D on the copy stream,
+    decode on the compute stream), all enqueued before one sync, each run three times so repeat
+    copies must wait for the previous decode of the same batch."""
+    data = fixtures.flat_c2_like(n=40000, v2=True)
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    fr = O.FileReader(data)
+    hbs = [f.load(rg, rg + 1, list(range(ncols))) for rg in range(f.num_row_groups)]
+    batches = [pq.native.Batch.staged(ctx, hb) for hb in hbs]
+    for _ in range(3):
+        for b in batches:
+            b.run_staged()
+    for rg, (hb, b) in enumerate(zip(hbs, batches)):
+        b.sync()
+        for ci, ch in enumerate(hb.chunks()):
+            col = pq.reader.ColumnData(f.columns()[ci][0], f.columns()[ci][1:], b.chunk_out(ci), [], ctx, None)
+            assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"staged rg{rg} c{ci}")
+        b.close()
+        hb.close()
+    assert f.num_row_groups == 4
+    res = pq.reader.decode_chunks(ctx, f, 1, 3, [0, 3, 5], staged_runs=2)
+    for k, col in enumerate(res):
+        rg, ci = 1 + k // 3, [0, 3, 5][k % 3]
+        assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"staged multi-rg rg{rg} c{ci}")
+
+
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
 @pytest.mark.parametrize("compression", ["NONE", "SNAPPY", "GZIP"])
 def test_pyarrow_files(pq, ctx, version, compression):
