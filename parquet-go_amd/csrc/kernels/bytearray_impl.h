@@ -145,9 +145,38 @@ __device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, in
     if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
     return nx + 4 <= staged_end && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
   };
-  for (int64_t x = s0; x < s1 && x < e0; x++) {
+  // scan 16 positions per step from 5 dwords loaded together (independent LDS reads; the length at
+  // each byte offset is a funnel shift of two of them): a mask of the positions whose own record is
+  // valid, then the full test on those in order
+  const int64_t lim = s1 < e0 ? s1 : e0;
+  int64_t x = -1;
+  for (int64_t base = wb + ((s0 - wb) & ~int64_t(3)); base < lim && x < 0; base += 16) {
+    const int k = int((base - wb) >> 2);
+    uint32_t w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = C.win[k + i];
+    const int64_t ra = e0 - base;
+    const int32_t rel = int32_t(ra < 0x7fffffff ? ra : 0x7fffffff);           // bytes left at base
+    const int32_t lo = int32_t(s0 > base ? s0 - base : 0), hi = int32_t(lim - base < 16 ? lim - base : 16);
+    uint32_t cand = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int32_t len = int32_t(__builtin_amdgcn_alignbit(w[(i >> 2) + 1], w[i >> 2], uint32_t(i & 3) * 8));
+      const int32_t avail = rel - i;
+      if (i >= lo && i < hi && avail >= 4 && len >= 0 && (len == 0 || avail - 4 >= len)) cand |= 1u << i;
+    }
+    for (; cand; cand &= cand - 1) {
+      int32_t l;
+      const int64_t p = base + __builtin_ctz(cand);
+      if (plausible(p, l)) {
+        x = p;
+        break;
+      }
+    }
+  }
+  if (x >= 0) {
     int32_t l;
-    if (!plausible(x, l)) continue;
+    plausible(x, l);
     int64_t start = x;
     for (int d = 1; d <= 3 && x + d < s1; d++) {
       int32_t l2;
@@ -173,6 +202,13 @@ __device__ void chain_resolve(ChainLds& C, int64_t wb, int64_t wend, int64_t e0,
     else if (s0 < s1) start = chain_guess(C, wb, e0, s0, s1, wb + kChainWin);
     if (start >= 0) {
       chain_walk(C, j, wb, wend, e0, start);
+    } else if (s0 >= e0 && s0 < s1) {
+      // past the end of the bytes: what a walk from s0 gives (EOF at s0), so that the segments after
+      // the chain's end agree at once instead of being fixed one per round
+#pragma unroll
+      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      C.exitv[j] = int32_t(s0);
+      C.exitbad[j] = uint8_t(PQH_ERR_EOF);
     } else {
 #pragma unroll
       for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
