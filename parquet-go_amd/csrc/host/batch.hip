@@ -62,7 +62,7 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
 constexpr int kNumKernels = 22;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
-constexpr size_t kDeltaPageModeMin = 1024;
+constexpr size_t kDeltaPageModeMin = 256;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -134,8 +134,8 @@ struct pqh_batch {
   std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
   std::vector<Tile> delta_streams;  // k_delta_page work list: (page, 0, stream) with values
   bool delta_page_mode = false;
-  int32_t delta_int_pages = 0;      // page mode: DELTA_BINARY_PACKED pages first in delta_pages
-  int32_t delta_int_streams = 0;    //            and their streams first in delta_streams
+  int32_t delta_fused_pages = 0;    // page mode: delta pages / streams through k_delta_fused
+  int32_t delta_fused_streams = 0;
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
   std::vector<int32_t> ba_pages;    // PLAIN byte-array data + dictionary pages (chain walks)
@@ -517,19 +517,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
     if (b->delta_page_mode) {
-      // DELTA_BINARY_PACKED pages (chased + decoded by k_delta_fused after the value scan) before
-      // the length streams of byte-array pages (walked before the scan: all their errors are load
-      // errors that the scan must see)
-      auto is_int = [&](int32_t p) {
-        const int32_t k = b->hpages[size_t(p)].kind;
-        return k == K_DELTA32 || k == K_DELTA64;
-      };
-      std::stable_partition(b->delta_pages.begin(), b->delta_pages.end(), is_int);
-      std::stable_partition(b->delta_streams.begin(), b->delta_streams.end(),
-                            [&](const Tile& t) { return is_int(t.page); });
-      b->delta_int_pages = int32_t(std::count_if(b->delta_pages.begin(), b->delta_pages.end(), is_int));
-      b->delta_int_streams = int32_t(std::count_if(b->delta_streams.begin(), b->delta_streams.end(),
-                                                   [&](const Tile& t) { return is_int(t.page); }));
+      // every delta page is chased + decoded by k_delta_fused after the value scan and then walked
+      // exactly.  Byte-array length streams decode all their lengths at load, so an error anywhere
+      // in them is a load error; the scan does not need it: it only moves the value offsets of the
+      // pages after the failing one, inside a chunk whose result is that error.
+      b->delta_fused_pages = int32_t(b->delta_pages.size());
+      b->delta_fused_streams = int32_t(b->delta_streams.size());
     }
   }
 
@@ -712,9 +705,9 @@ int pqh_batch_run(pqh_batch* b) {
   hipError_t e;
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
-  // page mode: DELTA_BINARY_PACKED pages [0, ni) get their init errors now and are chased, decoded
-  // and walked after the value scan; byte-array length streams [ni, ndp) as in tile mode
-  int32_t ni = b->delta_page_mode ? b->delta_int_pages : 0;
+  // page mode: every delta page gets its init errors now and is chased, decoded and walked after
+  // the value scan; tile mode: speculative walk + exact walk now, tiles after the scan
+  int32_t ni = b->delta_page_mode ? b->delta_fused_pages : 0;
   if (const char* f = getenv("PQH_DELTA_FUSED"))  // experiments: "0" = speculative walk + k_delta_page
     if (f[0] == '0') ni = 0;
   if (e == hipSuccess && ni)
@@ -725,7 +718,7 @@ int pqh_batch_run(pqh_batch* b) {
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
   if (e == hipSuccess && ni) {
-    const int32_t nis = b->delta_int_streams;
+    const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, st); });
     if (e == hipSuccess)
       e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });

@@ -1634,7 +1634,8 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
     const DevChunk C = b.chunks[P.chunk];
     int32_t* lp = P.kind == K_DBA ? C.aux2 : C.aux;
     uint8_t* out = lens ? reinterpret_cast<uint8_t*>(lp + S.value_base) : C.values + S.value_base * P.value_size;
-    const int64_t vcap = lens ? int64_t(S.nn) : int64_t(kmax) << lbs;  // values to emit
+    const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+    const int64_t vcap = lens ? (before_values ? 0 : int64_t(S.nn)) : int64_t(kmax) << lbs;  // values to emit
     const int64_t img_len = P.image_len;
     int32_t est = 0;  // 0: the first tile measures block 0
     for (;;) {
