@@ -893,8 +893,9 @@ struct TileStageLds {
   uint64_t md[kTileBlocks];
   uint64_t wtot[2][4];
   uint64_t wtot2[2][4];
+  uint64_t mdb[kTileBlocks];  // expand_rows: minDelta sum of the tile's blocks before each block
+  int32_t narrow;             // expand_rows: every miniblock width <= kNarrowWidth
   int32_t fits;
-  int32_t pad;
 };
 
 // Stage the tile; returns false (uniformly) when its bytes exceed kTileStage.
@@ -1066,6 +1067,39 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
+// Inclusive wave64 scan of 32-bit values (wrapping), same DPP pattern as wave_incl_scan.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xa, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xc, 0xf, false));
+  return x;
+}
+
+// Packed deltas (without minDelta) of the N positions q.. of one miniblock whose width is <= 32;
+// md = the block's minDelta, blk = its tile-relative block.
+template <int N, class L>
+__device__ __forceinline__ void staged_u32(const L& T, int32_t q, int bb0, int lbs, int lmb, uint32_t* u, uint64_t& md,
+                                           int& blk) {
+  blk = (q >> lbs) - bb0;
+  const int r = q & ((1 << lbs) - 1);
+  const int m = r >> lmb;
+  const int wm = T.mbw[blk][m];
+  md = T.md[blk];
+  const uint32_t bit = uint32_t(T.mbbit[blk][m]) + uint32_t(r & ((1 << lmb) - 1)) * uint32_t(wm);
+  const uint32_t mask = wm >= 32 ? ~0u : (1u << wm) - 1;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const uint32_t bj = bit + uint32_t(j * wm), k = bj >> 5;
+    u[j] = __builtin_amdgcn_alignbit(T.data[k + 1], T.data[k], bj & 31) & mask;
+  }
+}
+
+// Widths up to this keep a row's (1024 values) sum of packed deltas inside 32 bits.
+constexpr int kNarrowWidth = 22;
+
 // delta + minDelta of the 2 positions p, p+1 (p even: one miniblock).
 template <class L>
 __device__ __forceinline__ void staged_delta2(const L& T, int64_t p, int bb0, int lbs, int lmb, uint64_t d[2]) {
@@ -1095,7 +1129,67 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int row = 0;
   if (is64) {
+    // Narrow tiles (every width <= kNarrowWidth, the common case): the packed deltas are scanned in
+    // 32 bits and the minDelta part is added per value from the blocks' running minDelta sums
+    // (mdb), which cuts the 64-bit DPP scans and adds.  Wrapping 64-bit arithmetic gives the same
+    // sums in any grouping, so both paths produce identical values.
+    const int nblk = int(((v1 - 1) >> lbs) - bb0) + 1;
+    if (threadIdx.x < 64) {
+      bool wide = (v0 & ((int64_t(1) << lbs) - 1)) != 0;
+      uint64_t m = 0;
+      if (lane < nblk) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) wide |= T.mbw[lane][k] > kNarrowWidth;
+        m = T.md[lane] << lbs;
+      }
+      const uint64_t incl = wave_incl_scan(m);
+      if (lane < nblk) T.mdb[lane] = incl - m;
+      const uint64_t wm = __ballot(wide);
+      if (lane == 0) T.narrow = wm == 0;
+    }
+    __syncthreads();
     uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
+    if (T.narrow) {
+      uint64_t cu = carry;  // carry + packed deltas of the rows so far
+      for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
+        const int64_t pa = r0 + 2 * int64_t(threadIdx.x), pb = pa + 2 * kBlock;
+        uint32_t a[2] = {0, 0}, c[2] = {0, 0};
+        uint64_t mda = 0, mdc = 0;
+        int ba = 0, bc = 0;
+        if (pa < v1) staged_u32<2>(T, int32_t(pa), bb0, lbs, lmb, a, mda, ba);
+        if (pb < v1) staged_u32<2>(T, int32_t(pb), bb0, lbs, lmb, c, mdc, bc);
+        a[1] = pa + 1 < v1 ? a[1] : 0;
+        c[1] = pb + 1 < v1 ? c[1] : 0;
+        const uint32_t sa = a[0] + a[1], sb = c[0] + c[1];
+        const uint32_t ia = wave_incl_scan32(sa), ib = wave_incl_scan32(sb);
+        if (lane == 63) {
+          T.wtot[row][wv] = ia;
+          T.wtot2[row][wv] = ib;
+        }
+        __syncthreads();
+        const uint32_t ta = uint32_t(T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3]);
+        uint32_t ua = ia - sa, ub = ta + ib - sb;
+        for (int k = 0; k < wv; k++) {
+          ua += uint32_t(T.wtot[row][k]);
+          ub += uint32_t(T.wtot2[row][k]);
+        }
+        if (pa < v1) {
+          const uint64_t va = cu + ua + T.mdb[ba] + uint64_t(uint32_t(pa) & ((1u << lbs) - 1)) * mda;
+          if (pa + 2 <= v1) __builtin_nontemporal_store(u64x2{va, va + a[0] + mda}, reinterpret_cast<u64x2*>(o64 + pa));
+          else o64[pa] = va;
+        }
+        if (pb < v1) {
+          const uint64_t vb = cu + ub + T.mdb[bc] + uint64_t(uint32_t(pb) & ((1u << lbs) - 1)) * mdc;
+          if (pb + 2 <= v1) __builtin_nontemporal_store(u64x2{vb, vb + c[0] + mdc}, reinterpret_cast<u64x2*>(o64 + pb));
+          else o64[pb] = vb;
+        }
+        cu += uint64_t(ta) + uint32_t(T.wtot2[row][0] + T.wtot2[row][1] + T.wtot2[row][2] + T.wtot2[row][3]);
+      }
+      // the value at v1: packed deltas + minDelta of every position in [v0, v1)
+      const int64_t t1 = v1 - v0;
+      const int bl = int((t1 - 1) >> lbs);
+      return cu + T.mdb[bl] + uint64_t(t1 - (int64_t(bl) << lbs)) * T.md[bl];
+    }
     for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
       const int64_t pa = r0 + 2 * int64_t(threadIdx.x), pb = pa + 2 * kBlock;
       uint64_t a[2] = {0, 0}, c[2] = {0, 0};
@@ -1131,33 +1225,39 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
     }
     return carry;
   }
+  // 32-bit values: every sum wraps modulo 2^32 (the int32 decoder's arithmetic), so the whole
+  // expansion runs in 32 bits (widths of 32-bit streams are <= 32)
   uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+  uint32_t c32 = uint32_t(carry);
   for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
-    uint64_t d[4] = {0, 0, 0, 0};
-    if (p < v1) staged_delta4(T, p, bb0, lbs, lmb, d);
+    uint32_t d[4] = {0, 0, 0, 0};
+    if (p < v1) {
+      uint64_t md;
+      int bk;
+      staged_u32<4>(T, int32_t(p), bb0, lbs, lmb, d, md, bk);
 #pragma unroll
-    for (int j = 0; j < 4; j++) d[j] = p + j < v1 ? d[j] : 0;
-    const uint64_t tsum = d[0] + d[1] + d[2] + d[3];
-    const uint64_t incl = wave_incl_scan(tsum);
+      for (int j = 0; j < 4; j++) d[j] = p + j < v1 ? d[j] + uint32_t(md) : 0;
+    }
+    const uint32_t tsum = d[0] + d[1] + d[2] + d[3];
+    const uint32_t incl = wave_incl_scan32(tsum);
     if (lane == 63) T.wtot[row][wv] = incl;
     __syncthreads();
-    uint64_t v = carry + incl - tsum;
-    for (int k = 0; k < wv; k++) v += T.wtot[row][k];
+    uint32_t v = c32 + incl - tsum;
+    for (int k = 0; k < wv; k++) v += uint32_t(T.wtot[row][k]);
     if (p + 4 <= v1) {
-      const uint32_t o4[4] = {uint32_t(v), uint32_t(v + d[0]), uint32_t(v + d[0] + d[1]),
-                              uint32_t(v + d[0] + d[1] + d[2])};
+      const uint32_t o4[4] = {v, v + d[0], v + d[0] + d[1], v + d[0] + d[1] + d[2]};
       __builtin_memcpy(o32 + p, o4, 16);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        if (p + j < v1) o32[p + j] = uint32_t(v);
+        if (p + j < v1) o32[p + j] = v;
         v += d[j];
       }
     }
-    carry += T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3];
+    c32 += uint32_t(T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3]);
   }
-  return carry;
+  return c32;
 }
 
 
@@ -1201,9 +1301,12 @@ struct PageTileLds {
   uint64_t md[kTileBlocks];
   uint64_t wtot[2][4];
   uint64_t wtot2[2][4];
+  uint64_t mdb[kTileBlocks];
   int64_t a0;
   int32_t nfit;
   int32_t end;
+  int32_t narrow;
+  int32_t pad;
 };
 
 __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* streams) {

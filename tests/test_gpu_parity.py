@@ -295,6 +295,36 @@ def test_delta_geometries(pq, ctx, delta_mode):
     assert compared == len(cases) and errors > 50
 
 
+def test_delta_width_edges(pq, ctx, delta_mode):
+    """Miniblock widths around the 32-bit scan limit of the int64 expansion (kNarrowWidth = 22:
+    a 1024-value row of packed deltas must fit in 32 bits) and at 32/64; every tile either narrow,
+    wide or alternating.  Deltas are 0 or all-ones in the width, so the row sums are the largest
+    the width allows."""
+    import delta_streams as DS
+    W = fixtures.W
+    rng = np.random.default_rng(35)
+    cases = []
+    for bits, widths in ((64, (21, 22, 23, 31, 32, 33, 63, 64)), (32, (22, 23, 31, 32))):
+        col = (W.INT32 if bits == 32 else W.INT64, 0, 0, 0)
+        for bs, mbc in ((128, 4), (1024, 8), (2048, 1)):
+            for w in widths:
+                n = 20000
+                top = (1 << w) - 1
+                # one 0 per 64 deltas keeps minDelta at the base, so the packed deltas reach `top`
+                deltas = np.where(np.arange(n) % 64 == 0, 0, top).astype(object)
+                if w >= 23:  # alternate blocks of width w with narrow ones
+                    narrow = (np.arange(n) // (bs * 8)) % 2 == 1
+                    deltas = np.where(narrow, np.arange(n) % 5, deltas)
+                base = int(rng.integers(-1000, 1000))
+                vals = [base]
+                for dlt in deltas[1:]:
+                    vals.append(vals[-1] + int(dlt) - (1 << (w - 1) if w == bits else 0))
+                img = DS.encode(vals, bits, bs, mbc, "omit")
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BINARY_PACKED, 0, 0, img)))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors == 0
+
+
 def test_delta_multi_tile_pages(pq, ctx, delta_mode):
     """Pages spanning several 8192-value delta tiles (tile sums + page scan)."""
     rng = np.random.default_rng(32)
