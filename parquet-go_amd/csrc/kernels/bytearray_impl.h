@@ -726,13 +726,33 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_ba_expand: per tile, 8 consecutive values per thread: block scan of lengths -> offsets, then
-// the bytes of each value copied from its source (page chain / DELTA_LENGTH data / dictionary).
-// DELTA_LENGTH reads past the page (io.ReadFull short) are found here: the first value whose bytes
-// do not fit is the page's error.
+// k_ba_expand: per kBaTile tile of a PLAIN / DELTA_LENGTH / dictionary page.
+//   * lengths (or dictionary keys) are read with value index = j * 256 + thread (coalesced) into
+//     LDS; each thread then scans 8 consecutive lengths (block scan) -> tile-relative offsets;
+//   * the offsets go out coalesced; DELTA_LENGTH reads past the page (io.ReadFull short) are found
+//     here: the first value whose bytes do not fit is the page's error;
+//   * bytes: DELTA_LENGTH strings are contiguous in the page (one cooperative copy); PLAIN and
+//     dictionary values are gathered by their threads into an LDS image of kBaOut bytes of the
+//     tile's output at a time, then written out in aligned 16-byte stores; tiles of more than
+//     kBaOutWindows windows copy each value straight to its place (neighbouring lanes write
+//     neighbouring strings).
 // ------------------------------------------------------------------------------------------------
+constexpr int kBaOut = 16384;       // LDS output window
+constexpr int kBaOutWindows = 64;  // tiles with more output bytes copy each value directly
+
+// Bytes [0, len) of a value into LDS at d (any alignment): bytes up to a 4-aligned d, then dwords.
+__device__ __forceinline__ void lds_put(uint8_t* d, const PQH_G uint8_t* src, int64_t len) {
+  typedef uint32_t u32u __attribute__((aligned(1)));
+  int64_t k = 0;
+  for (; k < len && ((reinterpret_cast<uintptr_t>(d) + uintptr_t(k)) & 3); k++) d[k] = src[k];
+  for (; k + 4 <= len; k += 4) *reinterpret_cast<uint32_t*>(d + k) = *reinterpret_cast<const PQH_G u32u*>(src + k);
+  for (; k < len; k++) d[k] = src[k];
+}
+
 __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles) {
   __shared__ uint64_t wsum[4];
+  __shared__ int64_t s_off[kBaTile + 1];  // lengths, then tile-relative exclusive offsets
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBaOut + 16];
   const Tile t = tiles[blockIdx.x];
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
@@ -743,21 +763,34 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
   const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
   if (v0 >= v1) return;
   const bool is_dict = P.kind == K_DICT, is_dlba = P.kind == K_DLBA, is_dba = P.kind == K_DBA;
-  const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
-  const int32_t* aux = C.aux + S.value_base;
-  const int64_t i0 = v0 + 8 * int64_t(threadIdx.x);
   if (is_dba) return;  // k_dba_expand
-  int64_t len[8];
+  const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
+  const int32_t* aux = C.aux + S.value_base + v0;
+  const int n = int(v1 - v0), tid = threadIdx.x;
   int32_t a[8];
-  int64_t tsum = 0;
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    a[j] = i0 + j < v1 ? aux[i0 + j] : 0;
-    len[j] = i0 + j < v1 ? ba_len(d, is_dict, a[j]) : 0;
-    tsum += len[j] > 0 ? len[j] : 0;
+    const int idx = j * kBlock + tid;
+    a[j] = idx < n ? aux[idx] : 0;
+    const int64_t l = idx < n ? ba_len(d, is_dict, a[j]) : 0;
+    s_off[idx] = l > 0 ? l : 0;
+  }
+  __syncthreads();
+  int64_t L[8], tsum = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    L[j] = s_off[8 * tid + j];
+    tsum += L[j];
   }
   uint64_t tot;
-  const int64_t excl = int64_t(block_exclusive_scan(uint64_t(tsum), wsum, &tot));
+  int64_t o = int64_t(block_exclusive_scan(uint64_t(tsum), wsum, &tot));
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    s_off[8 * tid + j] = o;
+    o += L[j];
+  }
+  if (tid == kBlock - 1) s_off[kBaTile] = o;
+  __syncthreads();
   const int64_t base = b.basums[P.batile_base + t.k];
   const PQH_G uint8_t* img = b.payload + P.image_off;
   int64_t data_s = 0, data_n = 0;
@@ -765,44 +798,22 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     data_s = b.dstates[t.page].end_pos;
     data_n = S.val_e - data_s;
   }
-  int64_t* offs = C.offsets + S.value_base + 1;
-  int64_t o = base + excl;
+  int64_t* offs = C.offsets + S.value_base + 1 + v0;
   int64_t first_bad = INT64_MAX;
   int bad_code = 0;
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    const int64_t i = i0 + j;
-    if (i >= v1) break;
-    const int64_t l = len[j] > 0 ? len[j] : 0;
-    const int64_t rel = o - S.byte_base;  // page-relative first byte
-    const uint8_t* src = nullptr;
-    if (is_dict) {
-      const uint32_t k = uint32_t(a[j]);
-      if (k < d.K) src = b.payload + d.base + 4 * int64_t(k + 1) + d.dcum[k];
-    } else if (is_dlba) {
-      const int64_t rem = data_n - rel;
-      if (len[j] > 0 && rem < len[j]) {
-        if (i < first_bad) {
-          first_bad = i;
-          bad_code = rem <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
-        }
-      } else {
-        src = img + data_s + rel;
+    const int idx = j * kBlock + tid;
+    if (idx >= n) break;
+    const int64_t e = s_off[idx + 1];
+    offs[idx] = base + e;
+    if (is_dlba) {
+      const int64_t l = e - s_off[idx], rem = data_n - (base + s_off[idx] - S.byte_base);
+      if (l > 0 && rem < l && v0 + idx < first_bad) {
+        first_bad = v0 + idx;
+        bad_code = rem <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;
       }
-    } else {  // PLAIN: value i's bytes follow its u32 length
-      src = img + S.val_s + 4 * (i + 1) + rel;
     }
-    if (!is_dlba && src && l > 0 && o + l <= C.bytes_cap) {
-      // every value but the thread's last is copied in whole 8-byte words: the bytes written past
-      // its end are overwritten by the thread's next value (the payload pad covers the over-read)
-      int64_t rest = 0;  // bytes of the thread's later values: they overwrite the word tail
-#pragma unroll
-      for (int q = j + 1; q < 8; q++) rest += len[q] > 0 ? len[q] : 0;
-      if (((l + 7) & ~7) - l <= rest && o + ((l + 7) & ~7) <= C.bytes_cap) copy_words(C.bytes + o, src, l);
-      else copy_bytes(C.bytes + o, src, l);
-    }
-    o += l;
-    offs[i] = o;
   }
   if (first_bad != INT64_MAX) atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, bad_code));
   if (is_dlba) {  // the tile's strings are contiguous in the page: one cooperative copy
@@ -811,5 +822,58 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     if (len_all > data_n - rel0) len_all = data_n - rel0;   // bytes past the page belong to the error
     if (len_all > C.bytes_cap - base) len_all = C.bytes_cap - base;
     if (len_all > 0) block_copy(C.bytes + base, img + data_s + rel0, len_all);
+    return;
+  }
+  // source of value idx (nullptr: an out-of-range dictionary key, whose page fails)
+  auto src_of = [&](int j, int idx) -> const PQH_G uint8_t* {
+    if (is_dict) {
+      const uint32_t k = uint32_t(a[j]);
+      return k < d.K ? b.payload + d.base + 4 * int64_t(k + 1) + d.dcum[k] : nullptr;
+    }
+    // PLAIN: value i's bytes follow its u32 length
+    return img + S.val_s + 4 * (v0 + idx + 1) + (base + s_off[idx] - S.byte_base);
+  };
+  PQH_G uint8_t* dst = C.bytes + base;
+  const int lead = int(reinterpret_cast<uintptr_t>(dst) & 15);
+  const int64_t end = lead + int64_t(tot);  // output bytes in coordinates of the aligned start A
+  if (end <= kBaOutWindows * int64_t(kBaOut) && base + int64_t(tot) <= C.bytes_cap) {
+    PQH_G uint8_t* A = dst - lead;
+    for (int64_t w0 = 0; w0 < end; w0 += kBaOut) {  // kBaOut bytes of output per pass
+      const int64_t w1 = w0 + kBaOut < end ? w0 + kBaOut : end;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int idx = j * kBlock + tid;
+        if (idx >= n) break;
+        const int64_t x0 = lead + s_off[idx], x1 = lead + s_off[idx + 1];
+        const int64_t c0 = x0 > w0 ? x0 : w0, c1 = x1 < w1 ? x1 : w1;
+        if (c0 < c1) {
+          const PQH_G uint8_t* src = src_of(j, idx);
+          if (src) lds_put(s_out + (c0 - w0), src + (c0 - x0), c1 - c0);
+        }
+      }
+      __syncthreads();
+      const int nb = int(w1 - w0);
+      for (int c = tid; c < (nb + 15) >> 4; c += kBlock) {
+        const int lo = c << 4;
+        const int64_t g = w0 + lo;
+        if (g >= lead && g + 16 <= end) {
+          typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(s_out + lo), reinterpret_cast<PQH_G v4u*>(A + g));
+        } else {
+          for (int q = 0; q < 16 && lo + q < nb; q++)
+            if (g + q >= lead && g + q < end) A[g + q] = s_out[lo + q];
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int idx = j * kBlock + tid;
+    if (idx >= n) break;
+    const int64_t o0 = s_off[idx], l = s_off[idx + 1] - o0;
+    const PQH_G uint8_t* src = l > 0 ? src_of(j, idx) : nullptr;
+    if (src && base + o0 + l <= C.bytes_cap) copy_bytes(dst + o0, src, l);
   }
 }

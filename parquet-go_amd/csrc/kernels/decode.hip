@@ -203,7 +203,25 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
           if (match == 0) cnt_lane += valid - pc;
         }
         if (match == 1) cnt_lane += ones;
+      } else if (w == 2 || w == 4 || w == 8) {
+        // whole fields per 64-bit word: t = word ^ (match in every field); OR-folding each
+        // field's bits into its low bit leaves that bit clear exactly for the matching values
+        const uint64_t lowm = w == 2 ? 0x5555555555555555ull : w == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
+        const uint64_t pat = lowm * uint64_t(uint32_t(match));
+        const int per = 64 / w;
+        const int64_t nw = (lim + per - 1) / per;
+#pragma unroll 4
+        for (int64_t c = lane; c < nw; c += 64) {
+          uint64_t t = ld64_masked(img + data + c * 8, end) ^ pat;
+          t |= t >> 1;
+          if (w >= 4) t |= t >> 2;
+          if (w == 8) t |= t >> 4;
+          const int64_t nv = lim - c * per;  // valid values in this word
+          const uint64_t valid = nv >= per ? lowm : (lowm & ((1ull << (nv * w)) - 1));
+          cnt_lane += __popcll(valid & ~t);
+        }
       } else {
+#pragma unroll 2
         for (int64_t g = lane; g * 8 < lim; g += 64) {
           const uint64_t q = ld64_masked(img + data + g * w, end);
           const uint64_t q2 = w > 8 ? ld64_masked(img + data + g * w + 8, end) : 0;
