@@ -138,6 +138,8 @@ struct pqh_batch {
   int32_t delta_fused_streams = 0;
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
+  std::vector<int32_t> ba_xlist;    // ba_tiles indices: DELTA_LENGTH tiles, then PLAIN / dictionary
+  int32_t ba_ncopy = 0;             //   (the first ba_ncopy go to k_ba_expand, the rest to k_ba_gather)
   std::vector<int32_t> ba_pages;    // PLAIN byte-array data + dictionary pages (chain walks)
   std::vector<int2> ba_wins, ba_pwin;
   std::vector<int32_t> ba_chunks;   // k_ba_scan work list
@@ -168,6 +170,7 @@ struct pqh_batch {
   uint64_t* d_dagg = nullptr;
   uint64_t* d_dpre = nullptr;
   Tile* d_batiles = nullptr;
+  int32_t* d_ba_xlist = nullptr;
   int32_t* d_ba_pages = nullptr;
   int2* d_ba_wins = nullptr;        // (page, window) of every PLAIN chain window
   int2* d_ba_pwin = nullptr;        // per PLAIN page: (first window, windows)
@@ -526,6 +529,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
   }
 
+  for (size_t i = 0; i < b->ba_tiles.size(); i++)
+    if (b->hpages[size_t(b->ba_tiles[i].page)].kind == K_DLBA) b->ba_xlist.push_back(int32_t(i));
+  b->ba_ncopy = int32_t(b->ba_xlist.size());
+  for (size_t i = 0; i < b->ba_tiles.size(); i++) {
+    const int32_t k = b->hpages[size_t(b->ba_tiles[i].page)].kind;
+    if (k != K_DLBA && k != K_DBA) b->ba_xlist.push_back(int32_t(i));
+  }
+
   // ---- device allocations ----
   int rc;
   const size_t ntiles = b->expand_tiles.size() + b->global_tiles.size();
@@ -542,6 +553,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dagg), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dpre), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_batiles), sizeof(Tile) * b->ba_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_xlist), sizeof(int32_t) * b->ba_xlist.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wins), sizeof(int2) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pwin), sizeof(int2) * b->ba_pwin.size())) ||
@@ -649,6 +661,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
                        hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !b->ba_tiles.empty())
     e = hipMemcpyAsync(b->d_batiles, b->ba_tiles.data(), sizeof(Tile) * b->ba_tiles.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !b->ba_xlist.empty())
+    e = hipMemcpyAsync(b->d_ba_xlist, b->ba_xlist.data(), sizeof(int32_t) * b->ba_xlist.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !b->ba_pages.empty())
     e = hipMemcpyAsync(b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !b->ba_wins.empty())
@@ -755,7 +769,9 @@ int pqh_batch_run(pqh_batch* b) {
     if (e == hipSuccess)
       e = timed(9, nbc, s, [&](hipStream_t st) { return launch_ba_scan(d, b->d_ba_chunks, nbc, b->d_batiles, st); });
     if (e == hipSuccess)
-      e = timed(10, nbt, s, [&](hipStream_t st) { return launch_ba_expand(d, b->d_batiles, nbt, st); });
+      e = timed(10, nbt, s, [&](hipStream_t st) {  // k_ba_expand + k_ba_gather
+        return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, int32_t(b->ba_xlist.size()) - b->ba_ncopy, st);
+      });
     if (e == hipSuccess && b->has_dba)
       e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });
   }

@@ -749,11 +749,10 @@ __device__ __forceinline__ void lds_put(uint8_t* d, const PQH_G uint8_t* src, in
   for (; k < len; k++) d[k] = src[k];
 }
 
-__global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles) {
-  __shared__ uint64_t wsum[4];
-  __shared__ int64_t s_off[kBaTile + 1];  // lengths, then tile-relative exclusive offsets
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBaOut + 16];
-  const Tile t = tiles[blockIdx.x];
+// kGather = false: DELTA_LENGTH tiles (contiguous strings); true: PLAIN and dictionary tiles.
+template <bool kGather>
+__device__ __forceinline__ void ba_expand_tile(const DevBatch& b, const Tile& t, uint64_t* wsum, int64_t* s_off,
+                                               uint8_t* s_out) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
   if (page_failed_before_values(S)) return;
@@ -763,7 +762,7 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
   const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
   if (v0 >= v1) return;
   const bool is_dict = P.kind == K_DICT, is_dlba = P.kind == K_DLBA, is_dba = P.kind == K_DBA;
-  if (is_dba) return;  // k_dba_expand
+  if (is_dba || is_dlba == kGather) return;  // k_dba_expand; the other kernel
   const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
   const int32_t* aux = C.aux + S.value_base + v0;
   const int n = int(v1 - v0), tid = threadIdx.x;
@@ -816,14 +815,14 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     }
   }
   if (first_bad != INT64_MAX) atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, bad_code));
-  if (is_dlba) {  // the tile's strings are contiguous in the page: one cooperative copy
+  if constexpr (!kGather) {  // the tile's strings are contiguous in the page: one cooperative copy
     const int64_t rel0 = base - S.byte_base;
     int64_t len_all = int64_t(tot);
     if (len_all > data_n - rel0) len_all = data_n - rel0;   // bytes past the page belong to the error
     if (len_all > C.bytes_cap - base) len_all = C.bytes_cap - base;
     if (len_all > 0) block_copy(C.bytes + base, img + data_s + rel0, len_all);
     return;
-  }
+  } else {
   // source of value idx (nullptr: an out-of-range dictionary key, whose page fails)
   auto src_of = [&](int j, int idx) -> const PQH_G uint8_t* {
     if (is_dict) {
@@ -840,15 +839,48 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     PQH_G uint8_t* A = dst - lead;
     for (int64_t w0 = 0; w0 < end; w0 += kBaOut) {  // kBaOut bytes of output per pass
       const int64_t w1 = w0 + kBaOut < end ? w0 + kBaOut : end;
+      // the thread's pieces, four at a time: the first 16 bytes of each come from one unaligned
+      // 16-byte load, the four loads in flight together (the payload pad covers the over-read);
+      // longer pieces continue with lds_put
+      typedef uint4 uint4_u __attribute__((aligned(1)));
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int idx = j * kBlock + tid;
-        if (idx >= n) break;
-        const int64_t x0 = lead + s_off[idx], x1 = lead + s_off[idx + 1];
-        const int64_t c0 = x0 > w0 ? x0 : w0, c1 = x1 < w1 ? x1 : w1;
-        if (c0 < c1) {
-          const PQH_G uint8_t* src = src_of(j, idx);
-          if (src) lds_put(s_out + (c0 - w0), src + (c0 - x0), c1 - c0);
+      for (int h = 0; h < 8; h += 4) {
+        uint4 v[4];
+        const PQH_G uint8_t* sp[4];
+        int32_t pl[4], pd[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+          const int j = h + jj, idx = j * kBlock + tid;
+          sp[jj] = nullptr;
+          pl[jj] = 0;
+          pd[jj] = 0;
+          if (idx < n) {
+            const int64_t x0 = lead + s_off[idx], x1 = lead + s_off[idx + 1];
+            const int64_t c0 = x0 > w0 ? x0 : w0, c1 = x1 < w1 ? x1 : w1;
+            if (c0 < c1) {
+              const PQH_G uint8_t* src = src_of(j, idx);
+              if (src) {
+                sp[jj] = src + (c0 - x0);
+                pl[jj] = int32_t(c1 - c0);
+                pd[jj] = int32_t(c0 - w0);
+              }
+            }
+          }
+          v[jj] = make_uint4(0, 0, 0, 0);
+          if (sp[jj]) {
+            const uint4 x = *reinterpret_cast<const PQH_G uint4_u*>(sp[jj]);
+            v[jj] = x;
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+          if (!sp[jj]) continue;
+          uint8_t* d = s_out + pd[jj];
+          const uint32_t wv[4] = {v[jj].x, v[jj].y, v[jj].z, v[jj].w};
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if (q < pl[jj]) d[q] = uint8_t(wv[q >> 2] >> (8 * (q & 3)));
+          if (pl[jj] > 16) lds_put(d + 16, sp[jj] + 16, pl[jj] - 16);
         }
       }
       __syncthreads();
@@ -876,4 +908,21 @@ __global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles
     const PQH_G uint8_t* src = l > 0 ? src_of(j, idx) : nullptr;
     if (src && base + o0 + l <= C.bytes_cap) copy_bytes(dst + o0, src, l);
   }
+  }
+}
+
+// The tile lists hold indices into the chunk-ordered tile table: DELTA_LENGTH tiles for
+// k_ba_expand, PLAIN / dictionary tiles for k_ba_gather (the gather needs more registers, which
+// would cost the copy kernel occupancy).
+__global__ __launch_bounds__(256) void k_ba_expand(DevBatch b, const Tile* tiles, const int32_t* list) {
+  __shared__ uint64_t wsum[4];
+  __shared__ int64_t s_off[kBaTile + 1];  // lengths, then tile-relative exclusive offsets
+  ba_expand_tile<false>(b, tiles[list[blockIdx.x]], wsum, s_off, nullptr);
+}
+
+__global__ __launch_bounds__(256) void k_ba_gather(DevBatch b, const Tile* tiles, const int32_t* list) {
+  __shared__ uint64_t wsum[4];
+  __shared__ int64_t s_off[kBaTile + 1];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBaOut + 16];
+  ba_expand_tile<true>(b, tiles[list[blockIdx.x]], wsum, s_off, s_out);
 }

@@ -1085,9 +1085,10 @@ hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n
   return hipGetLastError();
 }
 
-hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_expand, dim3(n), dim3(256), 0, s, b, tiles);
+hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n_copy, int32_t n_gather,
+                            hipStream_t s) {
+  if (n_copy > 0) hipLaunchKernelGGL(k_ba_expand, dim3(n_copy), dim3(256), 0, s, b, tiles, list);
+  if (n_gather > 0) hipLaunchKernelGGL(k_ba_gather, dim3(n_gather), dim3(256), 0, s, b, tiles, list + n_copy);
   return hipGetLastError();
 }
 

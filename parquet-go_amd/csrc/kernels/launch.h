@@ -57,7 +57,8 @@ hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const
                            hipStream_t s);
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
-hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n_copy, int32_t n_gather,
+                            hipStream_t s);
 // DELTA_BYTE_ARRAY: every value's shared prefix copied from the suffixes of earlier values.
 hipError_t launch_dba_prefix(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Nesting (levels -> list offsets / presence / leaf validity): counts, per-chunk scan, write.
