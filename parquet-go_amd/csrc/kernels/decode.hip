@@ -602,16 +602,19 @@ __device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, in
     }
     if (threadIdx.x == 0) stage[nvec * 4] = 0;  // the word after the last one (alignbit reads k+1)
     __syncthreads();
-    for (int64_t i0 = c0 + 8 * int64_t(threadIdx.x); i0 < c1; i0 += 8 * kBlock) {
+    // G values per thread and step (Sink::kGroup): 4 for 4-byte outputs, so that a wave's stores
+    // are one contiguous kilobyte
+    constexpr int G = Sink::kGroup;
+    for (int64_t i0 = c0 + G * int64_t(threadIdx.x); i0 < c1; i0 += G * kBlock) {
       uint32_t v[8];
       const uint32_t bit0 = lead_bits + uint32_t(i0 - c0) * uint32_t(w);
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t bit = bit0 + uint32_t(j * w);
+      for (int j = 0; j < G; j++) {
+        const uint32_t bit = bit0 + uint32_t(j) * uint32_t(w);
         const uint32_t lo = stage[bit >> 5], hi = stage[(bit >> 5) + 1];
         v[j] = __builtin_amdgcn_alignbit(hi, lo, bit & 31) & m;
       }
-      sink(i0, v, int(c1 - i0 < 8 ? c1 - i0 : 8));
+      sink(i0, v, int(c1 - i0 < G ? c1 - i0 : G));
     }
   }
 }
@@ -623,6 +626,7 @@ __device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& 
                               TileLds& L, uint32_t* stage, Sink& sink) {
   const uint8_t* end = img + e;
   if (w == 0) {  // all zeros
+    __syncthreads();  // LDS the sink reads (a staged dictionary) is ready
     for (int64_t i0 = t0 + 8 * int64_t(threadIdx.x); i0 < t1; i0 += 8 * kBlock) {
       uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       sink(i0, v, int(t1 - i0 < 8 ? t1 - i0 : 8));
@@ -632,6 +636,12 @@ __device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& 
   int64_t from = t0;
   int64_t rs = c.run_start, rl = c.run_len, pos = c.next_hdr & 0x7fffffff;
   int32_t data = c.data, bp = (c.next_hdr >> 31) & 1;
+  if (bp && rs + rl >= t1 && ((t0 - rs) & 7) == 0 && w <= 32) {
+    // the checkpoint's bit-packed run holds the whole tile (every reference-writer stream): no
+    // run list, straight to the staged unpack
+    bp_staged(img, e, w, data, rs, t0, t1, stage, sink);
+    return;
+  }
   while (from < t1) {
     if (threadIdx.x == 0) build_runs(img, w, t1, rs, rl, data, bp, pos, L);
     __syncthreads();
@@ -674,6 +684,7 @@ __device__ void expand_hybrid(const uint8_t* img, int64_t e, int w, const Ckpt& 
 // ------------------------------------------------------------------------------------------------
 // decodePackedArray into one byte per level slot.
 struct LevelSink {
+  static constexpr int kGroup = 8;
   uint8_t* out;
   __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
     if (cnt == 8) {
@@ -688,6 +699,7 @@ struct LevelSink {
 
 // booleanRLEDecoder.decodeValues (type_boolean.go:109-120): value == 1.
 struct BoolSink {
+  static constexpr int kGroup = 8;
   uint8_t* out;
   __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
     if (cnt == 8) {
@@ -703,28 +715,48 @@ struct BoolSink {
 // dictDecoder.decodeValues (type_dict.go:40-60): bounds-checked gather of dictionary entries.
 template <int VS>
 struct DictSink {
+  static constexpr int kGroup = VS == 4 ? 4 : 8;
   const uint8_t* dict;  // LDS (fused kernel) or global (large dictionaries)
   uint8_t* out;         // chunk values + value_base * vs
   uint32_t K;
   int vs;               // runtime size when VS == 0
   int64_t* first_bad;   // per-thread min failing index
   __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
-    bool ok = true;
-    for (int j = 0; j < cnt; j++)
-      if (v[j] >= K) {
-        if (i0 + j < *first_bad) *first_bad = i0 + j;
-        ok = false;
+    if constexpr (VS == 4) {  // full group of in-range keys: one 16-byte store
+      if (cnt == 4 && v[0] < K && v[1] < K && v[2] < K && v[3] < K) {
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(dict);
+        const uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
+        __builtin_memcpy(out + i0 * 4, &a, 16);
+        return;
       }
+    }
+    slow(i0, v, cnt);
+  }
+  __device__ __noinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
+    // unrolled over the group (v[] stays in registers); the first out-of-range key of the group
+    bool ok = true;
+    int jb = 8;
+#pragma unroll
+    for (int j = 7; j >= 0; j--)
+      if (j < cnt && v[j] >= K) jb = j;
+    if (jb < 8) {
+      ok = false;
+      if (i0 + jb < *first_bad) *first_bad = i0 + jb;
+    }
     if constexpr (VS == 4) {
       const uint32_t* d = reinterpret_cast<const uint32_t*>(dict);
-      if (ok && cnt == 8) {
+      if (ok && cnt == 4) {
+        uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
+        __builtin_memcpy(out + i0 * 4, &a, 16);
+      } else if (ok && cnt == 8) {
         uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
         uint4 c = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
         __builtin_memcpy(out + i0 * 4, &a, 16);
         __builtin_memcpy(out + i0 * 4 + 16, &c, 16);
       } else {
-        for (int j = 0; j < cnt; j++)
-          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 4, &d[v[j]], 4);
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (j < cnt && v[j] < K) __builtin_memcpy(out + (i0 + j) * 4, &d[v[j]], 4);
       }
     } else if constexpr (VS == 8) {
       const uint64_t* d = reinterpret_cast<const uint64_t*>(dict);
@@ -734,8 +766,9 @@ struct DictSink {
           __builtin_memcpy(out + (i0 + j) * 8, pr, 16);
         }
       } else {
-        for (int j = 0; j < cnt; j++)
-          if (v[j] < K) __builtin_memcpy(out + (i0 + j) * 8, &d[v[j]], 8);
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (j < cnt && v[j] < K) __builtin_memcpy(out + (i0 + j) * 8, &d[v[j]], 8);
       }
     } else {
       for (int j = 0; j < cnt; j++) {
@@ -757,19 +790,36 @@ struct DictSink {
 // Byte-array dictionary pages: the index stream becomes per-value keys (aux); lengths and bytes are
 // resolved against the dictionary's cumulative-bytes table by k_ba_sum / k_ba_expand.
 struct KeySink {
+  static constexpr int kGroup = 4;
   int32_t* out;  // chunk aux + value_base
   uint32_t K;
   int64_t* first_bad;
   __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
-    for (int j = 0; j < cnt; j++)
-      if (v[j] >= K && i0 + j < *first_bad) *first_bad = i0 + j;
-    if (cnt == 8) {
+    if (cnt == 4 && v[0] < K && v[1] < K && v[2] < K && v[3] < K) {
+      const uint4 a = make_uint4(v[0], v[1], v[2], v[3]);
+      __builtin_memcpy(out + i0, &a, 16);
+      return;
+    }
+    slow(i0, v, cnt);
+  }
+  __device__ __noinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
+    int jb = 8;
+#pragma unroll
+    for (int j = 7; j >= 0; j--)
+      if (j < cnt && v[j] >= K) jb = j;
+    if (jb < 8 && i0 + jb < *first_bad) *first_bad = i0 + jb;
+    if (cnt == 4) {
+      uint4 a = make_uint4(v[0], v[1], v[2], v[3]);
+      __builtin_memcpy(out + i0, &a, 16);
+    } else if (cnt == 8) {
       uint4 a = make_uint4(v[0], v[1], v[2], v[3]);
       uint4 c = make_uint4(v[4], v[5], v[6], v[7]);
       __builtin_memcpy(out + i0, &a, 16);
       __builtin_memcpy(out + i0 + 4, &c, 16);
     } else {
-      for (int j = 0; j < cnt; j++) out[i0 + j] = int32_t(v[j]);
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (j < cnt) out[i0 + j] = int32_t(v[j]);
     }
   }
 };
@@ -830,7 +880,8 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
       reinterpret_cast<uint32_t*>(dict_lds)[i] = x;
     }
     dict = dict_lds;
-    __syncthreads();
+    // no barrier here: expand_hybrid passes one (run list or the unpack's first stage) before any
+    // value is gathered
   }
   const uint8_t* img = b.payload + P.image_off;
   int64_t first_bad = INT64_MAX;
