@@ -15,8 +15,8 @@ run() {  # run <name> <timeout> <bench args> -- <rocprof args...>
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 for w in ${WORKLOADS:-c2 c3 c5}; do
-  A="--workload $w --steps 10 --warmup 2 --no-cpu"
-  [ "$w" = c2 ] && A="--steps 10 --warmup 2 --no-cpu"
+  A="--workload $w --steps 10 --warmup 2 --no-cpu --no-e2e"
+  [ "$w" = c2 ] && A="--steps 10 --warmup 2 --no-cpu --no-e2e"
   run prof_${w}_trace 600 "$A" --kernel-trace --stats -T
   run prof_${w}_fetch 600 "$A" --pmc FETCH_SIZE --kernel-trace -T
   run prof_${w}_write 600 "$A" --pmc WRITE_SIZE --kernel-trace -T
