@@ -1561,6 +1561,37 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
     int32_t d0 = -1;
     est = lds_block(data, loc0, eloc, plim, dlim, is64, mbc, gbytes, d0) ? d0 - loc0 : 64;
   }
+  {
+    // uniform spans (reference-writer streams of steady data): lane i parses the header predicted
+    // at loc0 + i*est; lanes 0..m-1 whose block is usable and ends exactly at the next prediction
+    // are the chain (by induction from lane 0, which sits on the true header loc0).  Taken when it
+    // covers nmax blocks or stops only because the next block runs past the window; anything else
+    // goes through the segment chase below.
+    const int32_t g = loc0 + est * lane;
+    int32_t dat = 0, dend = -1;
+    uint64_t md = 0, wd = 0;
+    const bool parsed = g < plim && g + 24 <= eloc && (dend = lds_hdr(data, g, is64, mbc, gbytes, dat, md, wd)) >= 0;
+    const bool usable = parsed && dend <= dlim && dend <= eloc;
+    const uint64_t cm = __ballot(usable && dend == g + est);
+    const int m = cm == ~0ull ? 64 : __builtin_ctzll(~cm);
+    bool take = m >= nmax;
+    if (!take && m > 0) {  // lane m: the true next header; accept if its block only overflows the window
+      const int ok = __builtin_amdgcn_readlane(int(parsed && dend > dlim && dend <= eloc), m);
+      take = ok != 0;
+    }
+    if (take && est > 0) {
+      const int n = m < nmax ? m : nmax;
+      if (lane < n) {
+        blkbit[lane] = dat * 8;
+        blkw[lane] = wd;
+        mdt[lane] = md;
+      }
+      n_out = n;
+      next_out = loc0 + est * n;
+      stop_out = false;
+      return;
+    }
+  }
   const int32_t S = est < 16 ? 16 : est;
   const int32_t s0 = loc0 + S * lane, s1 = s0 + S;
   int cnt = 0;
