@@ -23,7 +23,7 @@
 //     [B_w, B_w+1), B_w = entry + w * kChainStride;
 //   * k_ba_wspec (one workgroup per window): window w's entry (the first record start >= B_w) is
 //     guessed (window 0: the known entry), then resolved inside the window: each thread owns a
-//     252-byte segment and walks it from a speculative start (the shortest plausible record among
+//     124-byte segment and walks it from a speculative start (the shortest plausible record among
 //     four neighbouring offsets), the walks are checked in parallel against their predecessor's
 //     exit and the first mismatch re-walked from its true entry until all agree; the window's
 //     records (lengths, or bytes before each record for dictionary pages), count, byte sum, exit and
@@ -35,7 +35,7 @@
 //   * k_ba_wemit (one workgroup per window): the window's records copied out at its base: lengths
 //     (data page -> aux) or cumulative offsets (dictionary page -> dcum).
 // ------------------------------------------------------------------------------------------------
-// 252-byte segments: neighbouring lanes' segments start 63 dwords apart, so their LDS reads fall in
+// 124-byte segments: neighbouring lanes' segments start 31 dwords apart, so their LDS reads fall in
 // different banks (a power-of-two stride would put a whole wave on one bank)
 
 struct ChainLds {
