@@ -50,9 +50,13 @@ def c2(rows=100_000_000, row_groups=16, seed=10):
     return W.flat(c2_columns(rows, seed), per, v2=True, as_array=True)
 
 
-def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
+def c3_values(rows=1_000_000_000, seed=20):
     rng = np.random.default_rng(seed)
-    ts = np.cumsum(1_000_000 + rng.integers(0, 4096, rows), dtype=np.int64) + 1_700_000_000_000_000_000
+    return np.cumsum(1_000_000 + rng.integers(0, 4096, rows), dtype=np.int64) + 1_700_000_000_000_000_000
+
+
+def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
+    ts = c3_values(rows, seed)
     return W.flat([("ts", W.Column(W.INT64, ts, encoding=W.DELTA_BINARY_PACKED, use_dict=False), W.REQUIRED)],
                   rows_per_group, v2=False, as_array=True)
 
@@ -78,6 +82,13 @@ def _repeated_levels(rng, rows, mean, p_null, p_empty, p_null_elem, max_d):
 
 
 def c4(rows=20_000_000, row_groups=4, v2=False, seed=30):
+    schema, cols = c4_columns(rows, seed)
+    per = -(-rows // row_groups)
+    rg = [min(per, rows - i * per) for i in range(row_groups)]
+    return W.write(schema, cols, rg, v2=v2, as_array=True)
+
+
+def c4_columns(rows, seed=30):
     rng = np.random.default_rng(seed)
     ld, lr = _repeated_levels(rng, rows, 4.0, 0.05, 0.05, 0.05, 3)
     lv = rng.integers(-2**40, 2**40, int((ld == 3).sum()))
@@ -105,9 +116,7 @@ def c4(rows=20_000_000, row_groups=4, v2=False, seed=30):
     cols = [W.Column(W.INT64, lv, def_levels=ld, rep_levels=lr, use_dict=False),
             W.Column(W.BYTE_ARRAY, (kdata, koff), def_levels=kd, rep_levels=kr, use_dict=False),
             W.Column(W.INT32, vv, def_levels=vd, rep_levels=kr, use_dict=False)]
-    per = -(-rows // row_groups)
-    rg = [min(per, rows - i * per) for i in range(row_groups)]
-    return W.write(schema, cols, rg, v2=v2, as_array=True)
+    return schema, cols
 
 
 def c5_strings(rows, seed=40, chunk=4_000_000):

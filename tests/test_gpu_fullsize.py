@@ -1,0 +1,144 @@
+"""Full-size round trips at the BASELINE.json configurations: the generator's
+seeded column data is written in the reference writer's layout, decoded on the GPU in one batch,
+and every decoded chunk must equal the slice of the input it was written from -- values, definition
+levels, byte-array offsets and bytes, bit for bit.  The oracle checks the decoders at sizes it
+finishes in seconds (test_gpu_parity.py); these check the same kernels at the sizes the bench runs.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(pq):
+    return pq.native.Context(0)
+
+
+def _decode(pq, ctx, data):
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    hb = f.load(0, f.num_row_groups, list(range(ncols)))
+    b = pq.native.Batch.from_host(ctx, hb)
+    b.run()
+    b.sync()
+    rows = [f.row_group_num_rows(rg) for rg in range(f.num_row_groups)]
+    return f, hb, b, ncols, rows
+
+
+def _fixed_chunks(pq, ctx, b, ncols, rows, ci, col, size):
+    """Compare column ci chunk by chunk with the written Column (fixed-width values)."""
+    vstart = sstart = 0
+    for rg, n in enumerate(rows):
+        o = b.chunk_out(rg * ncols + ci)
+        assert o.status == pq.native.OK, (ci, rg, o.status)
+        if col.def_levels is not None:
+            want_def = col.def_levels[sstart:sstart + n]
+            got_def = ctx.d2h_array(o.def_levels, n)
+            assert np.array_equal(got_def, want_def), (ci, rg, "def levels")
+            nn = int(np.count_nonzero(want_def))
+        else:
+            nn = n
+        assert o.num_non_null == nn and o.value_size == size, (ci, rg)
+        got = ctx.d2h_array(o.values, nn * size)
+        assert np.array_equal(got, col.data[vstart * size:(vstart + nn) * size]), (ci, rg, "values")
+        vstart += nn
+        sstart += n
+
+
+def test_c2_full(pq, ctx):
+    """C2: 100M rows x 6 columns, V2, 16 row groups (the bench's default workload)."""
+    from parquet_go_amd import datasets, writer as W
+
+    rows = 100_000_000
+    cols = datasets.c2_columns(rows, 10)
+    data = W.flat(cols, -(-rows // 16), v2=True, as_array=True)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
+    assert f.num_row_groups == 16 and sum(rg_rows) == rows
+    for ci, (_, col, _) in enumerate(cols):
+        size = 16 if col.ptype == W.FIXED_LEN_BYTE_ARRAY else col.data.itemsize * len(col.data) // max(1, col.num_values)
+        _fixed_chunks(pq, ctx, b, ncols, rg_rows, ci, col, size)
+    b.close()
+    hb.close()
+
+
+def test_c3_full(pq, ctx):
+    """C3: 1,000,000,000 INT64 timestamps, DELTA_BINARY_PACKED 128/4, 128 row groups."""
+    from parquet_go_amd import datasets, writer as W
+
+    rows = 1_000_000_000
+    ts = datasets.c3_values(rows, 20)
+    data = W.flat([("ts", W.Column(W.INT64, ts, encoding=W.DELTA_BINARY_PACKED, use_dict=False), W.REQUIRED)],
+                  7_812_500, v2=False, as_array=True)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
+    assert f.num_row_groups == 128
+    start = 0
+    for rg, n in enumerate(rg_rows):
+        o = b.chunk_out(rg)
+        assert o.status == pq.native.OK and o.num_non_null == n, rg
+        got = ctx.d2h_array(o.values, n, np.int64)
+        assert np.array_equal(got, ts[start:start + n]), rg
+        start += n
+    b.close()
+    hb.close()
+
+
+def test_c5_full(pq, ctx):
+    """C5: 50M strings, dictionary pages then DELTA_LENGTH fallback, SNAPPY, 8 row groups."""
+    from parquet_go_amd import datasets, writer as W
+
+    rows = 50_000_000
+    sdata, soff = datasets.c5_strings(rows, 40)
+    col = W.Column(W.BYTE_ARRAY, (sdata, soff), encoding=W.DELTA_LENGTH_BYTE_ARRAY, dict_page_limit=1 << 20)
+    data = W.flat([("s", col, W.REQUIRED)], -(-rows // 8), v2=False, codec=W.SNAPPY, as_array=True)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
+    start = 0
+    for rg, n in enumerate(rg_rows):
+        o = b.chunk_out(rg)
+        assert o.status == pq.native.OK and o.num_non_null == n, rg
+        offs = ctx.d2h_array(o.offsets, n + 1, np.int64)
+        want = soff[start:start + n + 1] - soff[start]
+        assert np.array_equal(offs, want), (rg, "offsets")
+        got = ctx.d2h_array(o.bytes, int(offs[-1]))
+        assert np.array_equal(got, sdata[soff[start]:soff[start + n]]), (rg, "bytes")
+        start += n
+    b.close()
+    hb.close()
+
+
+def test_c4_full(pq, ctx):
+    """C4: 20M rows of LIST<optional int64> + MAP<string, optional int32>, 4 row groups: levels,
+    values and key strings of every chunk equal the written columns."""
+    from parquet_go_amd import datasets, writer as W
+
+    rows, rgs = 20_000_000, 4
+    schema, cols = datasets.c4_columns(rows, 30)
+    per = -(-rows // rgs)
+    data = W.write(schema, cols, [min(per, rows - i * per) for i in range(rgs)], as_array=True)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
+    max_def = [3, 2, 3]
+    for ci, col in enumerate(cols):
+        row_starts = np.flatnonzero(col.rep_levels == 0)
+        bounds = list(row_starts[::per]) + [len(col.rep_levels)]
+        vstart = 0
+        for rg in range(rgs):
+            s0, s1 = int(bounds[rg]), int(bounds[rg + 1])
+            o = b.chunk_out(rg * ncols + ci)
+            assert o.status == pq.native.OK and o.num_values == s1 - s0, (ci, rg)
+            d = col.def_levels[s0:s1]
+            assert np.array_equal(ctx.d2h_array(o.def_levels, s1 - s0), d), (ci, rg, "def")
+            assert np.array_equal(ctx.d2h_array(o.rep_levels, s1 - s0), col.rep_levels[s0:s1]), (ci, rg, "rep")
+            nn = int(np.count_nonzero(d == max_def[ci]))
+            assert o.num_non_null == nn, (ci, rg)
+            if col.offsets is None:
+                size = 8 if col.ptype == W.INT64 else 4
+                got = ctx.d2h_array(o.values, nn * size)
+                assert np.array_equal(got, col.data[vstart * size:(vstart + nn) * size]), (ci, rg, "values")
+            else:
+                offs = ctx.d2h_array(o.offsets, nn + 1, np.int64)
+                assert np.array_equal(offs, col.offsets[vstart:vstart + nn + 1] - col.offsets[vstart]), (ci, rg)
+                got = ctx.d2h_array(o.bytes, int(offs[-1]))
+                assert np.array_equal(got, col.data[col.offsets[vstart]:col.offsets[vstart + nn]]), (ci, rg, "bytes")
+            vstart += nn
+    b.close()
+    hb.close()
