@@ -238,6 +238,10 @@ typedef struct pqh_batch pqh_batch;
 int pqh_abi_version(void);
 int pqh_device_count(int32_t* count);
 int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out);
+/* Replace the context's flags (e.g. turn PQH_CTX_PROFILE on for a few runs).  Unprofiled batch runs
+ * replay the batch's launch sequence as one captured hipGraph; profiled runs launch each kernel
+ * between HIP events. */
+int pqh_ctx_set_flags(pqh_ctx* ctx, uint32_t flags);
 void pqh_ctx_destroy(pqh_ctx* ctx);
 const char* pqh_last_error(const pqh_ctx* ctx);
 /* The HIP stream all kernels of this context are enqueued on (a hipStream_t). */

@@ -196,6 +196,9 @@ struct pqh_batch {
   std::vector<double> k_read, k_written;  // per kernel kind algorithmic bytes of one run
   std::vector<hipEvent_t> event_pool;
   size_t event_next = 0;
+  hipGraph_t graph = nullptr;        // unprofiled runs: the captured launch sequence
+  hipGraphExec_t gexec = nullptr;
+  bool graph_failed = false;
 };
 
 namespace {
@@ -207,6 +210,8 @@ void free_batch(pqh_batch* b) {
   if (b->h_staged) hipHostFree(b->h_staged);
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
   if (b->ev_done) hipEventDestroy(b->ev_done);
+  if (b->gexec) hipGraphExecDestroy(b->gexec);
+  if (b->graph) hipGraphDestroy(b->graph);
 }
 
 int dalloc(pqh_batch* b, void** p, size_t bytes) {
@@ -270,6 +275,12 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
 const char* pqh_last_error(const pqh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 void* pqh_ctx_stream(pqh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int pqh_ctx_set_flags(pqh_ctx* ctx, uint32_t flags) {
+  if (!ctx) return set_err(nullptr, PQH_ERR_ARG, "null context");
+  ctx->flags = flags;
+  return PQH_OK;
+}
 
 int pqh_malloc(pqh_ctx* ctx, void** dptr, size_t bytes) {
   hipSetDevice(ctx->device);
@@ -692,16 +703,13 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   return PQH_OK;
 }
 
-int pqh_batch_run(pqh_batch* b) {
-  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
-  pqh_ctx* ctx = b->ctx;
-  hipSetDevice(ctx->device);
-  const bool prof = (ctx->flags & PQH_CTX_PROFILE) != 0;
-  hipStream_t s = ctx->stream;
+namespace {
+
+// Enqueue every kernel of one decode of the batch on stream s (timed with HIP events when prof).
+hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
              b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2};
-  b->synced = false;
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
@@ -781,6 +789,51 @@ int pqh_batch_run(pqh_batch* b) {
     if (e == hipSuccess) e = timed(12, nns, s, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
     if (e == hipSuccess)
       e = timed(13, nnt, s, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+  }
+  return e;
+}
+
+bool graphs_enabled() {
+  const char* g = getenv("PQH_GRAPH");
+  return !(g && g[0] == '0');
+}
+
+}  // namespace
+
+// A batch's launch sequence is fixed at plan time, so unprofiled runs replay it as one hipGraph
+// (captured on the first such run): one submission instead of one per kernel.  Profiled runs
+// launch directly, with HIP events around every kernel.
+int pqh_batch_run(pqh_batch* b) {
+  if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
+  pqh_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  const bool prof = (ctx->flags & PQH_CTX_PROFILE) != 0;
+  hipStream_t s = ctx->stream;
+  b->synced = false;
+  hipError_t e = hipSuccess;
+  if (!prof && graphs_enabled() && !b->graph_failed) {
+    if (!b->gexec) {
+      e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+      if (e == hipSuccess) {
+        const hipError_t le = enqueue_run(b, s, false);
+        hipGraph_t g = nullptr;
+        e = hipStreamEndCapture(s, &g);
+        if (e == hipSuccess) e = le;
+        if (e == hipSuccess) e = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
+        b->graph = g;
+      }
+      if (e != hipSuccess) {  // replay unavailable: launch directly from now on
+        (void)hipGetLastError();
+        if (b->gexec) hipGraphExecDestroy(b->gexec);
+        if (b->graph) hipGraphDestroy(b->graph);
+        b->gexec = nullptr;
+        b->graph = nullptr;
+        b->graph_failed = true;
+      }
+    }
+    e = b->gexec ? hipGraphLaunch(b->gexec, s) : enqueue_run(b, s, false);
+  } else {
+    e = enqueue_run(b, s, prof);
   }
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   return PQH_OK;

@@ -78,6 +78,7 @@ PROTOTYPES = [
     ("pqh_device_count", ctypes.c_int, [ctypes.POINTER(i32)]),
     ("pqh_ctx_create", ctypes.c_int, [i32, u32, ctypes.POINTER(vp)]),
     ("pqh_ctx_destroy", None, [vp]),
+    ("pqh_ctx_set_flags", ctypes.c_int, [vp, u32]),
     ("pqh_last_error", cp, [vp]),
     ("pqh_ctx_stream", vp, [vp]),
     ("pqh_malloc", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
@@ -170,6 +171,10 @@ class Context:
 
     def sync(self):
         self.check(self.L.pqh_sync(self.h))
+
+    def set_profile(self, on):
+        """Per-kernel HIP-event timing on (direct launches) or off (graph replay)."""
+        self.check(self.L.pqh_ctx_set_flags(self.h, CTX_PROFILE if on else 0))
 
     def malloc(self, n):
         p = vp()
