@@ -325,6 +325,55 @@ def test_delta_width_edges(pq, ctx, delta_mode):
     assert compared == len(cases) and errors == 0
 
 
+def test_edge_pages(pq, ctx, delta_mode):
+    """Edge cases the reference decoders meet at the boundaries: pages with no values, all-null
+    optional pages, single values, ragged counts (not a multiple of 8), dictionary index widths 0,
+    1, 32 and 33 (> 32 fails at init, type_dict.go:23-30), one-entry and empty dictionaries, DELTA
+    streams of 0/1/2 values and constant runs."""
+    import delta_streams as DS
+    W = fixtures.W
+    rng = np.random.default_rng(50)
+    cases = []
+
+    def v1_defs(defs):  # V1 page: u32 length + hybrid definition levels (maxD 1)
+        h = W.hybrid_encode(1, np.asarray(defs, np.int32))
+        return len(h).to_bytes(4, "little") + h
+
+    for ptype, size in ((W.INT32, 4), (W.INT64, 8), (W.FLOAT, 4), (W.DOUBLE, 8), (W.BOOLEAN, 0),
+                        (W.FIXED_LEN_BYTE_ARRAY, 16), (W.BYTE_ARRAY, 0)):
+        tl = 16 if ptype == W.FIXED_LEN_BYTE_ARRAY else 0
+        cases.append(((ptype, tl, 0, 0), None, (O.DATA_PAGE, 0, W.PLAIN, 0, 0, b"")))
+        cases.append(((ptype, tl, 1, 0), None, (O.DATA_PAGE, 37, W.PLAIN, 0, 0, v1_defs([0] * 37))))
+        one = (b"\x05\x00\x00\x00hello" if ptype == W.BYTE_ARRAY else
+               bytes([1]) if ptype == W.BOOLEAN else rng.bytes(size))
+        cases.append(((ptype, tl, 1, 0), None, (O.DATA_PAGE, 1, W.PLAIN, 0, 0, v1_defs([1]) + one)))
+        cases.append(((ptype, tl, 1, 0), None, (O.DATA_PAGE, 3, W.PLAIN, 0, 0, v1_defs([0, 1, 0]) + one)))
+    for n in (1, 7, 9, 63, 65, 1023):  # ragged boolean and level counts
+        bits = rng.integers(0, 2, n).astype(np.uint8)
+        cases.append(((W.BOOLEAN, 0, 0, 0), None,
+                      (O.DATA_PAGE, n, W.PLAIN, 0, 0, np.packbits(bits, bitorder="little").tobytes())))
+        defs = rng.integers(0, 2, n)
+        vals = rng.integers(-9, 9, int(defs.sum())).astype(np.int32).tobytes()
+        cases.append(((W.INT32, 0, 1, 0), None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, v1_defs(defs) + vals)))
+    d5 = np.arange(10, 15, dtype=np.int32).tobytes()
+    idx = rng.integers(0, 5, 200).astype(np.int32)
+    for w, body in ((0, b""), (1, W.hybrid_encode(1, idx % 2)), (3, W.hybrid_encode(3, idx)),
+                    (32, W.hybrid_encode(32, idx)), (33, W.hybrid_encode(3, idx))):
+        cases.append(((W.INT32, 0, 0, 0), (5, W.PLAIN, d5), (O.DATA_PAGE, 200, W.RLE_DICTIONARY, 0, 0, bytes([w]) + body)))
+    cases.append(((W.INT64, 0, 0, 0), (1, W.PLAIN, (7).to_bytes(8, "little")),
+                  (O.DATA_PAGE, 1000, W.RLE_DICTIONARY, 0, 0, bytes([1]) + W.hybrid_encode(1, np.zeros(1000, np.int32)))))
+    cases.append(((W.INT32, 0, 0, 0), (0, W.PLAIN, b""),
+                  (O.DATA_PAGE, 3, W.RLE_DICTIONARY, 0, 0, bytes([1]) + W.hybrid_encode(1, np.zeros(3, np.int32)))))
+    cases.append(((W.INT32, 0, 0, 0), (5, W.PLAIN, d5), (O.DATA_PAGE, 0, W.RLE_DICTIONARY, 0, 0, b"")))
+    for bits in (32, 64):
+        col = (W.INT32 if bits == 32 else W.INT64, 0, 0, 0)
+        for vals in ([], [5], [5, -3], [7] * 300, list(range(0, 3000, 3))):
+            img = DS.encode(vals, bits, 128, 4, "full")
+            cases.append((col, None, (O.DATA_PAGE, len(vals), W.DELTA_BINARY_PACKED, 0, 0, img)))
+    compared, errors = _run_cases(pq, ctx, cases)
+    assert compared == len(cases) and errors >= 2
+
+
 def test_delta_multi_tile_pages(pq, ctx, delta_mode):
     """Pages spanning several 8192-value delta tiles (tile sums + page scan)."""
     rng = np.random.default_rng(32)
