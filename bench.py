@@ -119,11 +119,11 @@ def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
     ctx.check(ctx.L.pqh_host_alloc(ctx.h, ctypes.byref(h), nbytes))
     d = ctx.malloc(nbytes)
     try:
-        ctx.h2d(d, h.value, nbytes)
+        ctx.h2d_pinned_async(d, h.value, nbytes)
         ctx.sync()
         t0 = time.perf_counter()
         for _ in range(reps):
-            ctx.h2d(d, h.value, nbytes)
+            ctx.h2d_pinned_async(d, h.value, nbytes)
         ctx.sync()
         return round(nbytes * reps / (time.perf_counter() - t0) / 1e9, 2)
     finally:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 3
+#define PQH_ABI_VERSION 4
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -251,8 +251,13 @@ int pqh_malloc(pqh_ctx* ctx, void** dptr, size_t bytes);
 int pqh_free(pqh_ctx* ctx, void* dptr);
 int pqh_host_alloc(pqh_ctx* ctx, void** hptr, size_t bytes); /* pinned */
 int pqh_host_free(pqh_ctx* ctx, void* hptr);
-int pqh_memcpy_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes); /* async, ctx stream */
-int pqh_memcpy_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes); /* async, ctx stream */
+/* Copies between HBM and pageable (or pinned) host memory, ordered after the work already on the
+ * context stream; they return when the host buffer is filled / reusable.  They stage through the
+ * context's pinned bounce buffer, so the HIP runtime never pins pageable memory on the fly. */
+int pqh_memcpy_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes);
+int pqh_memcpy_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Asynchronous copy on the context stream from PINNED host memory (pqh_host_alloc) to HBM. */
+int pqh_memcpy_h2d_pinned_async(pqh_ctx* ctx, void* dst, const void* pinned_src, size_t bytes);
 int pqh_sync(pqh_ctx* ctx);
 
 /* Plan a batch: copies the page/chunk tables, sizes and allocates scratch and outputs.

@@ -28,6 +28,12 @@ struct pqh_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // staged (end-to-end) runs: pinned -> HBM copies
   std::string err;
+  // Pinned bounce buffer for every copy between HBM and pageable host memory (two halves, so the
+  // host-side memcpy of one overlaps the DMA of the other).  Pageable copies never reach the HIP
+  // runtime: its on-the-fly pinning of pageable memory faulted ("illegal memory access") on a
+  // device-to-host copy into a fresh numpy buffer after earlier large transfers in the process.
+  uint8_t* bounce = nullptr;
+  hipEvent_t bounce_ev[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -65,6 +71,60 @@ constexpr int kNumKernels = 22;
 constexpr size_t kDeltaPageModeMin = 256;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// PQH_SYNC_EACH=1 (debugging): direct launches, each followed by a stream synchronisation, so a
+// kernel fault is reported against the kernel that caused it.
+bool sync_each_enabled() {
+  const char* f = getenv("PQH_SYNC_EACH");
+  return f && f[0] == '1';
+}
+thread_local const char* g_fail_kernel = nullptr;
+
+constexpr size_t kBounceHalf = size_t(16) << 20;
+
+hipError_t bounce_init(pqh_ctx* ctx) {
+  if (ctx->bounce) return hipSuccess;
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&ctx->bounce), 2 * kBounceHalf, hipHostMallocDefault);
+  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ctx->bounce_ev[i], hipEventDisableTiming);
+  return e;
+}
+
+// Pageable host -> device on the context stream; returns when the host buffer may be reused.
+hipError_t bounce_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  hipError_t e = bounce_init(ctx);
+  for (size_t off = 0, i = 0; off < bytes && e == hipSuccess; off += kBounceHalf, i++) {
+    const size_t n = std::min(kBounceHalf, bytes - off);
+    uint8_t* half = ctx->bounce + (i & 1) * kBounceHalf;
+    if (i >= 2) e = hipEventSynchronize(ctx->bounce_ev[i & 1]);  // that half's previous copy is done
+    if (e != hipSuccess) break;
+    memcpy(half, static_cast<const uint8_t*>(src) + off, n);
+    e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, half, n, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ctx->bounce_ev[i & 1], ctx->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  return e;
+}
+
+// Device -> pageable host, ordered after the work already on the context stream; synchronous.
+hipError_t bounce_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  hipError_t e = bounce_init(ctx);
+  const size_t nchunks = (bytes + kBounceHalf - 1) / kBounceHalf;
+  auto issue = [&](size_t i) {
+    const size_t off = i * kBounceHalf, n = std::min(kBounceHalf, bytes - off);
+    hipError_t r = hipMemcpyAsync(ctx->bounce + (i & 1) * kBounceHalf, static_cast<const uint8_t*>(src) + off, n,
+                                  hipMemcpyDeviceToHost, ctx->stream);
+    return r == hipSuccess ? hipEventRecord(ctx->bounce_ev[i & 1], ctx->stream) : r;
+  };
+  if (e == hipSuccess && nchunks) e = issue(0);
+  for (size_t i = 0; i < nchunks && e == hipSuccess; i++) {
+    if (i + 1 < nchunks) e = issue(i + 1);  // the other half is free: its memcpy below finished
+    if (e == hipSuccess) e = hipEventSynchronize(ctx->bounce_ev[i & 1]);
+    if (e != hipSuccess) break;
+    const size_t off = i * kBounceHalf;
+    memcpy(static_cast<uint8_t*>(dst) + off, ctx->bounce + (i & 1) * kBounceHalf, std::min(kBounceHalf, bytes - off));
+  }
+  return e;
+}
 
 }  // namespace
 
@@ -269,6 +329,9 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
     hipStreamSynchronize(ctx->copy_stream);
     hipStreamDestroy(ctx->copy_stream);
   }
+  for (hipEvent_t ev : ctx->bounce_ev)
+    if (ev) hipEventDestroy(ev);
+  if (ctx->bounce) hipHostFree(ctx->bounce);
   delete ctx;
 }
 
@@ -300,11 +363,15 @@ int pqh_host_free(pqh_ctx* ctx, void* hptr) {
   return PQH_OK;
 }
 int pqh_memcpy_h2d(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, bounce_h2d(ctx, dst, src, bytes));
   return PQH_OK;
 }
 int pqh_memcpy_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, bounce_d2h(ctx, dst, src, bytes));
+  return PQH_OK;
+}
+int pqh_memcpy_h2d_pinned_async(pqh_ctx* ctx, void* dst, const void* pinned_src, size_t bytes) {
+  HIP_TRY(ctx, hipMemcpyAsync(dst, pinned_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   return PQH_OK;
 }
 int pqh_sync(pqh_ctx* ctx) {
@@ -656,38 +723,33 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   }
   std::vector<Tile> all(b->expand_tiles);
   all.insert(all.end(), b->global_tiles.begin(), b->global_tiles.end());
+  // page mode: the (shorter) stream list takes the delta tile list's place
+  const std::vector<Tile>& dl = b->delta_page_mode ? b->delta_streams : b->delta_tiles;
+  struct Up {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  const Up ups[] = {
+      {b->d_pages, b->hpages.data(), sizeof(DevPage) * size_t(num_pages)},
+      {b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * size_t(num_chunks)},
+      {b->d_tiles, all.data(), sizeof(Tile) * ntiles},
+      {b->d_dtiles, dl.data(), b->delta_tiles.empty() ? 0 : sizeof(Tile) * dl.size()},
+      {b->d_delta_pages, b->delta_pages.data(), sizeof(int32_t) * b->delta_pages.size()},
+      {b->d_batiles, b->ba_tiles.data(), sizeof(Tile) * b->ba_tiles.size()},
+      {b->d_ba_xlist, b->ba_xlist.data(), sizeof(int32_t) * b->ba_xlist.size()},
+      {b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size()},
+      {b->d_ba_wins, b->ba_wins.data(), sizeof(int2) * b->ba_wins.size()},
+      {b->d_ba_pwin, b->ba_pwin.data(), sizeof(int2) * b->ba_pwin.size()},
+      {b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size()},
+      {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
+      {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
+  };
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
-  if (num_pages) e = hipMemcpyAsync(b->d_pages, b->hpages.data(), sizeof(DevPage) * size_t(num_pages), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && num_chunks)
-    e = hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * size_t(num_chunks), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && ntiles) e = hipMemcpyAsync(b->d_tiles, all.data(), sizeof(Tile) * ntiles, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->delta_tiles.empty()) {
-    // page mode: the (shorter) stream list takes the tile list's place
-    const std::vector<Tile>& dl = b->delta_page_mode ? b->delta_streams : b->delta_tiles;
-    e = hipMemcpyAsync(b->d_dtiles, dl.data(), sizeof(Tile) * dl.size(), hipMemcpyHostToDevice, s);
-  }
-  if (e == hipSuccess && !b->delta_pages.empty())
-    e = hipMemcpyAsync(b->d_delta_pages, b->delta_pages.data(), sizeof(int32_t) * b->delta_pages.size(),
-                       hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_tiles.empty())
-    e = hipMemcpyAsync(b->d_batiles, b->ba_tiles.data(), sizeof(Tile) * b->ba_tiles.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_xlist.empty())
-    e = hipMemcpyAsync(b->d_ba_xlist, b->ba_xlist.data(), sizeof(int32_t) * b->ba_xlist.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_pages.empty())
-    e = hipMemcpyAsync(b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_wins.empty())
-    e = hipMemcpyAsync(b->d_ba_wins, b->ba_wins.data(), sizeof(int2) * b->ba_wins.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_pwin.empty())
-    e = hipMemcpyAsync(b->d_ba_pwin, b->ba_pwin.data(), sizeof(int2) * b->ba_pwin.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->ba_chunks.empty())
-    e = hipMemcpyAsync(b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size(),
-                       hipMemcpyHostToDevice, s);
+  for (const Up& u : ups)
+    if (e == hipSuccess && u.bytes) e = bounce_h2d(ctx, u.dst, u.src, u.bytes);
   if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
-  if (e == hipSuccess && !b->nests.empty())
-    e = hipMemcpyAsync(b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && !b->nest_tiles.empty())
-    e = hipMemcpyAsync(b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     free_batch(b);
@@ -710,6 +772,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
              b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2};
+  const bool sync_each = sync_each_enabled();
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
@@ -721,6 +784,11 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     if (prof) {
       hipEventRecord(e1, st);
       b->pending.push_back(KernelRun{kind, e0, e1, items});
+    }
+    if (sync_each) {  // debugging: name the kernel whose launch or execution fails
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e == hipSuccess) e = hipGetLastError();
+      if (e != hipSuccess) g_fail_kernel = kKernelNames[kind];
     }
     return e;
   };
@@ -795,7 +863,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
 
 bool graphs_enabled() {
   const char* g = getenv("PQH_GRAPH");
-  return !(g && g[0] == '0');
+  return !(g && g[0] == '0') && !sync_each_enabled();
 }
 
 }  // namespace
@@ -833,9 +901,12 @@ int pqh_batch_run(pqh_batch* b) {
     }
     e = b->gexec ? hipGraphLaunch(b->gexec, s) : enqueue_run(b, s, false);
   } else {
+    g_fail_kernel = nullptr;
     e = enqueue_run(b, s, prof);
   }
-  if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
+  if (e != hipSuccess)
+    return set_err(ctx, PQH_ERR_HIP, std::string("launch") + (g_fail_kernel ? std::string(" ") + g_fail_kernel : "") +
+                                         ": " + hipGetErrorString(e));
   return PQH_OK;
 }
 
@@ -844,18 +915,28 @@ int pqh_batch_sync(pqh_batch* b) {
   pqh_ctx* ctx = b->ctx;
   hipSetDevice(ctx->device);
   b->states.resize(b->pages.size());
-  if (!b->pages.empty())
-    HIP_TRY(ctx, hipMemcpyAsync(b->states.data(), b->d_states, sizeof(PageState) * b->pages.size(),
-                                hipMemcpyDeviceToHost, ctx->stream));
+  if (!b->pages.empty()) HIP_TRY(ctx, bounce_d2h(ctx, b->states.data(), b->d_states, sizeof(PageState) * b->pages.size()));
   b->chunk_bytes.assign(b->chunks.size(), 0);
   if (!b->ba_chunks.empty())
-    HIP_TRY(ctx, hipMemcpyAsync(b->chunk_bytes.data(), b->d_chunk_bytes, sizeof(int64_t) * b->chunks.size(),
-                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, bounce_d2h(ctx, b->chunk_bytes.data(), b->d_chunk_bytes, sizeof(int64_t) * b->chunks.size()));
   b->nest_totals.assign(b->nests.size() * kNestFlags, 0);
   if (!b->nests.empty())
-    HIP_TRY(ctx, hipMemcpyAsync(b->nest_totals.data(), b->d_ntotals, sizeof(int64_t) * b->nest_totals.size(),
-                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, bounce_d2h(ctx, b->nest_totals.data(), b->d_ntotals, sizeof(int64_t) * b->nest_totals.size()));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  // The per-page results bound every later copy of the outputs (pqh_batch_chunk_out): refuse
+  // results that would reach past the planned output buffers instead of handing them out.
+  for (size_t p = 0; p < b->pages.size(); p++) {
+    const DevPage& P = b->hpages[p];
+    const PageState& S = b->states[p];
+    if (P.page_type == PQH_DICTIONARY_PAGE) continue;
+    const int64_t n = std::max(0, P.num_values);
+    if (S.nn < 0 || S.nn > n || S.value_base < 0 || S.value_base + S.nn > b->hchunks[size_t(P.chunk)].values_cap) {
+      char msg[160];
+      snprintf(msg, sizeof(msg), "device page state out of range: page %zu nn %d of %lld, value_base %lld", p, S.nn,
+               (long long)n, (long long)S.value_base);
+      return set_err(ctx, PQH_ERR_HIP, msg);
+    }
+  }
   // Byte-array outputs sized from an estimate (dictionary gathers): grow the chunks that came out
   // short (and decoded without error), then decode again.  Contents are deterministic, so this
   // happens at most once per batch.
@@ -879,8 +960,7 @@ int pqh_batch_sync(pqh_batch* b) {
     regrow = true;
   }
   if (regrow) {
-    HIP_TRY(ctx, hipMemcpyAsync(b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * b->hchunks.size(),
-                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, bounce_h2d(ctx, b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * b->hchunks.size()));
     int rc = pqh_batch_run(b);
     if (rc != PQH_OK) return rc;
     return pqh_batch_sync(b);
@@ -1113,11 +1193,7 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
   void* d = nullptr;
   const size_t bytes = hb->payload.size();
   HIP_TRY(ctx, hipMalloc(&d, bytes ? bytes : 16));
-  void* src = const_cast<uint8_t*>(hb->payload.data());
-  const bool pinned = bytes && hipHostRegister(src, bytes, hipHostRegisterDefault) == hipSuccess;
-  hipError_t e = bytes ? hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ctx->stream) : hipSuccess;
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  if (pinned) hipHostUnregister(src);
+  const hipError_t e = bounce_h2d(ctx, d, hb->payload.data(), bytes);
   if (e != hipSuccess) {
     hipFree(d);
     return set_err(ctx, PQH_ERR_HIP, std::string("payload upload: ") + hipGetErrorString(e));

@@ -71,7 +71,7 @@ class KernelStat(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 3  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 4  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -87,6 +87,7 @@ PROTOTYPES = [
     ("pqh_host_free", ctypes.c_int, [vp, vp]),
     ("pqh_memcpy_h2d", ctypes.c_int, [vp, vp, vp, ctypes.c_size_t]),
     ("pqh_memcpy_d2h", ctypes.c_int, [vp, vp, vp, ctypes.c_size_t]),
+    ("pqh_memcpy_h2d_pinned_async", ctypes.c_int, [vp, vp, vp, ctypes.c_size_t]),
     ("pqh_sync", ctypes.c_int, [vp]),
     ("pqh_batch_create", ctypes.c_int, [vp, ctypes.POINTER(Chunk), i32, ctypes.POINTER(Page), i32, vp, i64,
                                         ctypes.POINTER(vp)]),
@@ -186,7 +187,12 @@ class Context:
             self.L.pqh_free(self.h, p)
 
     def h2d(self, dst, src_ptr, n):
+        """Synchronous copy from pageable (or pinned) host memory."""
         self.check(self.L.pqh_memcpy_h2d(self.h, dst, src_ptr, n))
+
+    def h2d_pinned_async(self, dst, pinned_ptr, n):
+        """Asynchronous copy on the context stream from pqh_host_alloc memory."""
+        self.check(self.L.pqh_memcpy_h2d_pinned_async(self.h, dst, pinned_ptr, n))
 
     def d2h_array(self, src, n, dtype=np.uint8):
         out = np.empty(n, dtype=dtype)

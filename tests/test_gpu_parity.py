@@ -98,8 +98,6 @@ def test_nested_levels(pq, ctx, v2):
     _run_file(pq, ctx, fixtures.nested_list_map(n=6000, v2=v2))
 
 
-@pytest.mark.skip(reason="OPEN DEFECT: illegal memory access on MI355X (reproduced with PQH_GRAPH=0, "
-                         "so not graph replay); skipped so the suite does not fault the GPU. See DESIGN.md §7.")
 def test_large_pages_single_run(pq, ctx):
     """Reference-writer pages spanning many tiles (1 MiB page estimate, one bit-packed run)."""
     W = fixtures.W
