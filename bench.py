@@ -33,11 +33,13 @@ def package():
     return ge._package()
 
 
-def cpu_baseline(data, seconds, threads=1):
+def cpu_baseline(data, seconds, threads=1, verify=None):
     """The oracle (plain-C restatement of the reference decoders) on a bounded sample of the same
     file: whole row groups until `seconds` of single-thread decode work (walk excluded).  With
     threads > 1 the same sample is decoded again chunk-parallel on a thread pool (the C decoder runs
-    without the GIL) -- SURVEY.md §8(d): "1 core and all host cores (page-parallel)"."""
+    without the GIL) -- SURVEY.md §8(d): "1 core and all host cores (page-parallel)".
+    verify(rg, ci, results): called outside the timed region with the oracle's page results of every
+    sampled chunk, to check the GPU's outputs of the same chunk against them."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
@@ -45,24 +47,32 @@ def cpu_baseline(data, seconds, threads=1):
     fr = O.FileReader(data)
     ncols = len(fr.columns)
 
-    def decode(ch):
+    def run(ch):
+        res = O.decode_chunk(ch)
         n = 0
-        for r in O.decode_chunk(ch):
+        for r in res:
             if r.status:
                 raise RuntimeError(f"oracle failed: status {r.status}")
             n += len(r.values) + (0 if r.def_levels is None else len(r.def_levels)) + \
                 (0 if r.rep_levels is None else len(r.rep_levels))
-        return n
+        return n, res
+
+    def decode(ch):
+        return run(ch)[0]
 
     out_bytes = 0
     spent = 0.0
     sample = []
     for rg in range(len(fr.row_groups)):
         chunks = [fr.read_chunk(rg, ci) for ci in range(ncols)]
-        t0 = time.perf_counter()
-        for ch in chunks:
-            out_bytes += decode(ch)
-        spent += time.perf_counter() - t0
+        for ci, ch in enumerate(chunks):
+            t0 = time.perf_counter()
+            n, res = run(ch)
+            spent += time.perf_counter() - t0
+            out_bytes += n
+            if verify is not None:
+                verify(rg, ci, res)
+            del res
         sample.append(chunks)
         if spent >= seconds:
             break
@@ -109,6 +119,28 @@ def pmc_traffic(kernel, workload, rows):
         if k.get("hbm_traffic_bytes_per_launch"):
             return k["hbm_traffic_bytes_per_launch"], f"profiles/{tag}/pmc_summary.json"
     return None, None
+
+
+def check_chunk(ctx, batch, chunk, res, np):
+    """The GPU's outputs of one chunk equal the oracle's page results (values, byte-array offsets
+    and bytes, definition / repetition levels), bit for bit."""
+    o = batch.chunk_out(chunk)
+    if o.status != 0:
+        raise RuntimeError(f"chunk {chunk}: GPU status {o.status}")
+    want_vals = b"".join(r.values for r in res)
+    if o.value_size > 0:
+        got = ctx.d2h_array(o.values, o.num_non_null * o.value_size)
+        ok = got.tobytes() == want_vals
+    else:
+        offs = ctx.d2h_array(o.offsets, o.num_non_null + 1, np.int64)
+        lens = np.concatenate([np.diff(r.offsets) for r in res if r.offsets is not None] or [np.zeros(0, np.int64)])
+        ok = np.array_equal(np.diff(offs), lens) and ctx.d2h_array(o.bytes, int(offs[-1])).tobytes() == want_vals
+    for ptr, attr in ((o.def_levels, "def_levels"), (o.rep_levels, "rep_levels")):
+        if ptr:
+            want = np.concatenate([getattr(r, attr) for r in res])
+            ok = ok and np.array_equal(ctx.d2h_array(ptr, o.num_values), want)
+    if not ok:
+        raise RuntimeError(f"chunk {chunk}: GPU output differs from the oracle")
 
 
 def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
@@ -249,6 +281,21 @@ def main():
                 "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
                 "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
     all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)  # kernel time of one profiled step
+    cpu = cpu_mt = None
+    verified = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import numpy as np
+
+        log("timing the CPU baseline (oracle) and checking the GPU outputs of its sample ...")
+        nchk = [0]
+
+        def verify(rg, ci, res):
+            check_chunk(ctx, batch, rg * ncols + ci, res, np)
+            nchk[0] += 1
+
+        # the GPU box grants this job 16 host cores (os.cpu_count() reports the whole machine)
+        cpu, cpu_mt = cpu_baseline(data, args.cpu_seconds, threads=min(16, os.cpu_count() or 1), verify=verify)
+        verified = f"{nchk[0]} of {hb.num_chunks} chunks (the CPU sample) bit-exact vs the oracle"
     batch.close()
 
     # End-to-end: one staged batch per row-group range holding its decompressed
@@ -295,11 +342,6 @@ def main():
             sb.close()
         e2e["pinned_h2d_ceiling_gbps"] = pinned_h2d_rate(ctx, native)
     if rank == 0:
-        cpu = cpu_mt = None
-        if world == 1 and not args.no_cpu:
-            log("timing the CPU baseline (oracle) ...")
-            # the GPU box grants this job 16 host cores (os.cpu_count() reports the whole machine)
-            cpu, cpu_mt = cpu_baseline(data, args.cpu_seconds, threads=min(16, os.cpu_count() or 1))
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -330,6 +372,7 @@ def main():
             "e2e": e2e,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
+            "verified": verified,
         }
         print(json.dumps(line), flush=True)
     hb.close()

@@ -46,6 +46,73 @@ def _fixed_chunks(pq, ctx, b, ncols, rows, ci, col, size):
         sstart += n
 
 
+def test_c1_full(pq, ctx):
+    """C1 (BASELINE configs[0]) at full size: 10M required INT32 dictionary values (K = 4096, index
+    width bits.Len(4096) = 13, page_v1.go:184-191), reference-writer V1 pages of ~258k values whose
+    index stream is ONE bit-packed run (hybrid_encoder.go:55-70) spanning many tiles.  Every chunk
+    must equal the oracle's decode bit for bit, and the seeded input."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from parquet_go_amd import datasets
+
+    rows = 10_000_000
+    data = datasets.c1(rows=rows, seed=1)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
+    assert ncols == 1 and sum(rg_rows) == rows
+    pages = hb.pages()
+    big = [p for p in pages if p.page_type != O.DICTIONARY_PAGE]
+    assert max(p.num_values for p in big) > 200_000  # the reference writer's 1 MiB page estimate
+    rng = np.random.default_rng(1)
+    dictionary = rng.integers(-2**31, 2**31 - 1, 4096).astype(np.int32)
+    want_all = dictionary[np.random.default_rng(2).integers(0, 4096, rows)]
+    fr = O.FileReader(data)
+    start = 0
+    for rg, n in enumerate(rg_rows):
+        o = b.chunk_out(rg)
+        assert o.status == pq.native.OK and o.num_non_null == n, rg
+        got = ctx.d2h_array(o.values, n * 4)
+        res = O.decode_chunk(fr.read_chunk(rg, 0))
+        assert all(r.status == 0 for r in res)
+        assert got.tobytes() == b"".join(r.values for r in res), (rg, "oracle")
+        assert np.array_equal(got.view(np.int32), want_all[start:start + n]), (rg, "input")
+        start += n
+    b.close()
+    hb.close()
+
+
+def test_c1_pyarrow_variant(pq, ctx):
+    """The pyarrow-written C1 variant: dictionary indices of width 12 in mixed
+    RLE / bit-packed runs, 10M rows, V1 pages."""
+    import io
+
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pqa
+
+    rows = 10_000_000
+    rng = np.random.default_rng(5)
+    dictionary = rng.integers(-2**31, 2**31 - 1, 4000).astype(np.int32)
+    idx = rng.integers(0, 4000, rows)
+    idx[rng.random(rows) < 0.3] = 7  # runs of repeats -> RLE runs between bit-packed ones
+    idx = np.where(np.repeat(rng.random(rows // 100) < 0.2, 100)[:rows], 11, idx)
+    vals = dictionary[idx]
+    buf = io.BytesIO()
+    pqa.write_table(pa.table({"v": vals}), buf, row_group_size=2_500_000, data_page_version="1.0",
+                    compression="NONE", use_dictionary=True)
+    f, hb, b, ncols, rg_rows = _decode(pq, ctx, buf.getvalue())
+    start = 0
+    for rg, n in enumerate(rg_rows):
+        o = b.chunk_out(rg)
+        assert o.status == pq.native.OK and o.num_non_null == n, (rg, o.status)
+        got = ctx.d2h_array(o.values, n * 4).view(np.int32)
+        assert np.array_equal(got, vals[start:start + n]), rg
+        start += n
+    assert start == rows
+    b.close()
+    hb.close()
+
+
 def test_c2_full(pq, ctx):
     """C2: 100M rows x 6 columns, V2, 16 row groups (the bench's default workload)."""
     from parquet_go_amd import datasets, writer as W
