@@ -195,25 +195,42 @@ def main():
     kw = {}
     if args.rows:
         kw["rows"] = args.rows
-    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40}[args.workload] + 1000 * rank
+    # C3 (BASELINE configs[2]: 128 row groups of ONE file sharded across 1/2/4/8 GPUs) is strong
+    # scaling: every rank opens the same file and decodes its contiguous block of row groups
+    # (shard.row_group_block).  The other workloads give every rank its own file (weak scaling).
+    strong = args.workload == "c3"
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40}[args.workload] + (0 if strong else 1000 * rank)
     t0 = time.perf_counter()
-    data = builder(seed=seed_kw, **kw)
+    path = None
+    if strong and world > 1:
+        # generated once (rank 0) into a shared file that every rank memory-maps
+        shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+        path = os.path.join(shm, f"pqh_bench_{args.workload}_{seed_kw}_{os.environ.get('MASTER_PORT', '0')}.parquet")
+        if rank == 0:
+            builder(seed=seed_kw, **kw).tofile(path + ".part")
+            os.replace(path + ".part", path)
+        dist.barrier()
+        data = None
+    else:
+        data = builder(seed=seed_kw, **kw)
     gen_s = time.perf_counter() - t0
-    log(f"rank {rank}: generated {len(data) / 1e9:.2f} GB file in {gen_s:.1f}s")
+    log(f"rank {rank}: {'opened' if data is None else 'generated'} the {args.workload} file in {gen_s:.1f}s")
 
     # timed steps replay each batch's captured hipGraph (unprofiled); per-kernel HIP-event timing for
     # the roofline comes from separate profiled passes of the same batch
     ctx = native.Context(local, profile=False)
-    f = native.File(data)
+    f = native.File(data if data is not None else path)
     ncols = len(f.columns())
+    rg0, rg1 = pkg.shard.row_group_block(f.num_row_groups, world, rank) if strong else (0, f.num_row_groups)
+    my_rows = sum(f.row_group_num_rows(rg) for rg in range(rg0, rg1))
     t0 = time.perf_counter()
-    hb = f.load(0, f.num_row_groups, list(range(ncols)))
+    hb = f.load(rg0, rg1, list(range(ncols)))
     walk_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     batch = native.Batch.from_host(ctx, hb)
     h2d_s = time.perf_counter() - t0
-    log(f"rank {rank}: walked {hb.num_pages} pages / {hb.num_chunks} chunks in {walk_s:.2f}s, "
-        f"payload {hb.payload_bytes / 1e9:.2f} GB uploaded in {h2d_s:.2f}s")
+    log(f"rank {rank}: row groups [{rg0}, {rg1}) of {f.num_row_groups}: walked {hb.num_pages} pages / "
+        f"{hb.num_chunks} chunks in {walk_s:.2f}s, payload {hb.payload_bytes / 1e9:.2f} GB uploaded in {h2d_s:.2f}s")
 
     batch.run()
     batch.sync()
@@ -241,7 +258,12 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     # whole job: max step time over ranks, sum of decoded bytes (shard.py; RCCL for N > 1)
-    elapsed, total_written = pkg.shard.reduce_step(elapsed, bytes_written, device=f"cuda:{local}" if world > 1 else None)
+    dev = f"cuda:{local}" if world > 1 else None
+    elapsed, total_written = pkg.shard.reduce_step(elapsed, bytes_written, device=dev)
+    # the sharded decode's one exchange: every rank's block, checked to tile the file (strong mode)
+    blocks = pkg.shard.gather_blocks(rg0, rg1, my_rows, bytes_written, device=dev)
+    if strong:
+        pkg.shard.check_cover(blocks, f.num_row_groups, f.num_rows)
     batch.sync()
     # profiled passes: every kernel between HIP events on the decode stream
     ctx.set_profile(True)
@@ -274,7 +296,7 @@ def main():
     if dom is not None:
         avg_ms = dom.total_ms / dom.launches
         ach = (dom.bytes_read + dom.bytes_written) / (avg_ms * 1e-3) / 1e9
-        traffic, src = pmc_traffic(dom.name.decode(), desc, f.num_rows)
+        traffic, src = pmc_traffic(dom.name.decode(), desc, my_rows)
         roof = {"bound": "hbm", "kernel": dom.name.decode(), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": round(traffic) if traffic else None, "traffic_source": src,
@@ -305,12 +327,12 @@ def main():
     if not args.no_e2e:
         # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
         # >= 1/16 of the payload each
-        nrg = f.num_row_groups
+        nrg = rg1 - rg0
         groups = min(nrg, 16)
         cuts = [nrg * g // groups for g in range(groups + 1)]
         staged, payload = [], 0
         for g in range(groups):
-            hbr = f.load(cuts[g], cuts[g + 1], list(range(ncols)))
+            hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)))
             payload += hbr.payload_bytes
             staged.append(native.Batch.staged(ctx, hbr))
             hbr.close()
@@ -352,15 +374,21 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "launch": "hipGraph replay per step (profiled direct launches: %.4f ms/step)" % prof_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int32/int64/f32/f64/bool/flba16 (bit-exact integer/byte decode)" if args.workload == "c2"
             else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload == "c5"
             else "int64/int32/bytes + u8 levels + int32 list offsets" if args.workload == "c4" else "int64",
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
-            "config": {"workload": desc, "rows_per_gpu": f.num_rows, "row_groups_per_gpu": f.num_row_groups,
-                       "pages_per_gpu": hb.num_pages, "parallelism": f"row-group sharded x{world}, no collective",
+            "config": {"workload": desc, "rows_total": f.num_rows if strong else f.num_rows * world,
+                       "rows_per_gpu": my_rows, "row_groups_per_gpu": rg1 - rg0,
+                       "pages_per_gpu": hb.num_pages,
+                       "parallelism": (f"row groups of one file sharded in contiguous blocks over {world} GPU(s)"
+                                       if strong else f"one file of {f.num_row_groups} row groups per GPU x{world}")
+                       + "; no data-path collective",
                        "mode": "HBM-resident"},
+            "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
+                       for r, b in enumerate(blocks)],
             "per_gpu_gbps": round(bytes_written * args.steps / elapsed / 1e9, 2),
             "algo_read_bytes_per_step": bytes_read,
             "decoded_bytes_per_step": bytes_written,
@@ -376,8 +404,12 @@ def main():
         }
         print(json.dumps(line), flush=True)
     hb.close()
+    f.close()
     ctx.close()
     if world > 1:
+        dist.barrier()
+        if path and rank == 0:
+            os.unlink(path)
         dist.destroy_process_group()
 
 

@@ -47,10 +47,14 @@ def _worker(rank, world, port, path, q):
                     blobs.append((rg, ci, bytes(r.values)))
                     nbytes += len(r.values)
         t, total = shard.reduce_step(0.5 + rank, nbytes)
+        # the bench's exchange: every rank's block, checked to tile the file
+        rows = sum(fr.row_group_num_rows(rg) for rg in range(rg0, rg1))
+        blocks = shard.gather_blocks(rg0, rg1, rows, nbytes)
+        shard.check_cover(blocks, len(fr.row_groups), sum(fr.row_group_num_rows(g) for g in range(len(fr.row_groups))))
         gathered = [None] * world
         dist.all_gather_object(gathered, blobs)
         if rank == 0:
-            q.put((t, total, [b for g in gathered for b in g]))
+            q.put((t, total, [b for g in gathered for b in g], blocks, shard.global_row_offsets(blocks)))
     finally:
         dist.destroy_process_group()
 
@@ -86,7 +90,7 @@ def test_two_rank_gloo_shards(tmp_path):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, str(path), q)) for r in range(2)]
     for p in procs:
         p.start()
-    t, total, blobs = q.get(timeout=240)
+    t, total, blobs, blocks, offsets = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -98,3 +102,6 @@ def test_two_rank_gloo_shards(tmp_path):
                 want.append((rg, ci, bytes(r.values)))
     assert blobs == want
     assert t == 1.5 and total == sum(len(b[2]) for b in want)
+    # the plan the bench uses (shard.row_group_block) for 9 row groups over 2 ranks
+    assert [b[:3] for b in blocks] == [(0, 5, 5000), (5, 9, 4000)] and offsets == [0, 5000]
+    assert sum(b[3] for b in blocks) == total
