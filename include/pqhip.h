@@ -221,6 +221,19 @@ typedef struct pqh_page_result {
   int64_t level_offset; /* first level slot of this page in pqh_chunk_out.{def,rep}_levels */
 } pqh_page_result;
 
+/* One readValues(size) result materialised on the host (pqh_batch_page_read). */
+typedef struct pqh_page_values {
+  int32_t status;       /* the reference's readValues error for this call, PQH_OK if none */
+  int32_t phase;        /* enum pqh_phase of that error */
+  int64_t index;        /* its level-slot / value index inside the page (as pqh_page_result) */
+  int64_t num_slots;    /* level slots returned: min(count, num_values - first) */
+  int64_t num_non_null; /* notNull of those slots (helpers.go:143-145) */
+  int64_t values_read;  /* values decodeValues produced (< num_non_null on a value error) */
+  int64_t num_bytes;    /* BYTE_ARRAY: bytes of the returned values */
+  int32_t value_size;   /* bytes per fixed-width value, 0 for BYTE_ARRAY */
+  int32_t reserved;
+} pqh_page_values;
+
 typedef struct pqh_kernel_stat {
   char name[32];
   int32_t launches;     /* launches timed */
@@ -275,6 +288,20 @@ int pqh_batch_chunk_out(const pqh_batch* batch, int32_t chunk, pqh_chunk_out* ou
  * PQH_ERR_NOT_IMPLEMENTED. */
 int pqh_batch_nesting(const pqh_batch* batch, int32_t chunk, pqh_nest_out* out);
 int pqh_batch_page_results(const pqh_batch* batch, pqh_page_result* out, int32_t num_pages);
+/* Compat path: one page's pageReader.readValues(size) result (reference
+ * interfaces.go:11-18, page_v1.go:33-63, page_v2.go:31-60) copied to HOST buffers after
+ * pqh_batch_sync, for a cgo shim that boxes it into []interface{} + packedArray levels.
+ * Level slots [first, first + count) of the page (count clipped to the page, as readValues clips
+ * size); def_levels / rep_levels receive num_slots bytes each (NULL = skip); fixed-width values
+ * go to `values` (num_non_null * value_size bytes), byte arrays to offsets (num_non_null + 1,
+ * relative to the first returned value) + data (num_bytes).  With NULL value buffers only the
+ * sizes are filled in.  On a readValues error (out->status != PQH_OK) nothing is copied, as the
+ * reference returns nil slices.  Errors are those of the whole-page call the reference makes
+ * (ColumnStore.readNextPage, data_store.go:236-260); a ranged call reports a level error once its
+ * range reaches the failing slot and a value error once its values reach the failing value. */
+int pqh_batch_page_read(const pqh_batch* batch, int32_t page, int64_t first, int64_t count, void* values,
+                        int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data,
+                        int64_t data_cap, uint8_t* def_levels, uint8_t* rep_levels, pqh_page_values* out);
 /* Kernel timing accumulated since the last reset (requires PQH_CTX_PROFILE). */
 int pqh_batch_kernel_stats(const pqh_batch* batch, pqh_kernel_stat* out, int32_t max_stats,
                            int32_t* num_stats);
@@ -305,6 +332,23 @@ int32_t pqh_file_num_columns(const pqh_file* f);
 /* Leaf column metadata; path is the dot-joined schema path (Column.FlatName). */
 int pqh_file_column(const pqh_file* f, int32_t column, pqh_column* out, char* path,
                     int32_t path_capacity);
+
+/* The schema as a flat DFS list (FileMetaData.schema, root first), with the levels the reader
+ * derives for every node (readGroupSchema / readColumnSchema, schema.go:893-990): what the record
+ * assembly (Column.getData, schema.go:216-312) walks. */
+typedef struct pqh_schema_element {
+  int32_t physical_type; /* enum pqh_physical_type, -1 for groups */
+  int32_t type_length;
+  int32_t repetition;    /* 0 REQUIRED, 1 OPTIONAL, 2 REPEATED, -1 unset (root) */
+  int32_t num_children;  /* 0 for leaves */
+  int32_t column;        /* leaves: index for pqh_file_column / pqh_file_load, else -1 */
+  int32_t max_def;       /* the node's maximum definition level */
+  int32_t max_rep;       /* the node's maximum repetition level */
+  int32_t reserved;
+} pqh_schema_element;
+int32_t pqh_file_num_schema_elements(const pqh_file* f);
+int pqh_file_schema_element(const pqh_file* f, int32_t index, pqh_schema_element* out, char* name,
+                            int32_t name_capacity);
 
 /* Walk and decompress the pages of the given leaf columns for row groups [rg_begin, rg_end),
  * producing a page table and one payload of page images (8-byte aligned images). */

@@ -1088,6 +1088,96 @@ int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num
   return PQH_OK;
 }
 
+// readValues(size) of one page as the reference's pageReader returns it (page_v1.go:33-63,
+// page_v2.go:31-60), materialised in host memory from the batch's device outputs: level slots
+// [first, first + count) of the page, their definition / repetition levels and the dense values of
+// the non-null ones.  Sizes only when the buffers are NULL.
+int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t count, void* values,
+                        int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data, int64_t data_cap,
+                        uint8_t* def_levels, uint8_t* rep_levels, pqh_page_values* out) {
+  if (!b || !out || page < 0 || size_t(page) >= b->pages.size() || first < 0 || count < 0)
+    return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad page read arguments");
+  if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
+  pqh_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  memset(out, 0, sizeof(*out));
+  const DevPage& P = b->hpages[size_t(page)];
+  const PageState& S = b->states[size_t(page)];
+  const DevChunk& C = b->hchunks[size_t(P.chunk)];
+  out->value_size = C.value_size;
+  if (P.page_type == PQH_DICTIONARY_PAGE) return set_err(ctx, PQH_ERR_ARG, "dictionary pages have no readValues");
+  const int64_t n = std::max(0, P.num_values);
+  // dataPageReaderV1/V2.readValues: size is clipped to the values left in the page
+  const int64_t s0 = std::min(first, n), s1 = std::min(n, s0 + count);
+  out->num_slots = s1 - s0;
+  if (S.err != kNoError) {
+    const int phase = int(S.err >> 56);
+    const int64_t idx = int64_t((S.err >> 8) & 0xffffffffffffull);
+    out->status = int32_t(S.err & 0xff);
+    out->phase = phase;
+    out->index = idx;
+    // the whole-page call (readNextPage, data_store.go:241) fails; a ranged call fails when its
+    // range reaches the failing level slot (load errors fail every call, value errors below)
+    if (phase == PQH_PHASE_LOAD || ((phase == PQH_PHASE_REP || phase == PQH_PHASE_DEF) && idx < s1)) return PQH_OK;
+    if (phase != PQH_PHASE_VALUES) {
+      out->status = PQH_OK;
+      out->phase = 0;
+      out->index = 0;
+    }
+  }
+  if (s1 == s0) return PQH_OK;
+  // levels of the range, and the non-null values before / inside it
+  std::vector<uint8_t> defs;
+  int64_t nn0 = s0, nn1 = s1 - s0;
+  if (C.max_def > 0) {
+    defs.resize(size_t(s1));
+    HIP_TRY(ctx, bounce_d2h(ctx, defs.data(), C.def_levels + P.level_base, size_t(s1)));
+    nn0 = 0;
+    nn1 = 0;
+    for (int64_t i = 0; i < s1; i++) (i < s0 ? nn0 : nn1) += defs[size_t(i)] == C.max_def;
+    if (def_levels) memcpy(def_levels, defs.data() + s0, size_t(s1 - s0));
+  }
+  if (C.max_rep > 0 && rep_levels)
+    HIP_TRY(ctx, bounce_d2h(ctx, rep_levels, C.rep_levels + P.level_base + s0, size_t(s1 - s0)));
+  if (out->status != PQH_OK) {  // a value error: decodeValues of this range meets it?
+    if (out->index < nn0 + nn1) {
+      out->num_non_null = nn1;
+      // decodeValues' count: values before the failing one, except the two checks that return 0
+      // (type_dict.go:52-54, type_bytearray.go:223-229)
+      const bool zero = out->status == PQH_ERR_DICT_INDEX || out->status == PQH_ERR_DBA_PREFIX;
+      out->values_read = zero ? 0 : std::max<int64_t>(0, out->index - nn0);
+      return PQH_OK;
+    }
+    out->status = PQH_OK;
+    out->phase = 0;
+    out->index = 0;
+  }
+  out->num_non_null = nn1;
+  out->values_read = nn1;
+  const int64_t v0 = S.value_base + nn0;
+  if (C.value_size > 0) {
+    const int64_t bytes = nn1 * C.value_size;
+    if (values) {
+      if (values_cap < bytes) return set_err(ctx, PQH_ERR_ARG, "values buffer too small");
+      HIP_TRY(ctx, bounce_d2h(ctx, values, C.values + v0 * C.value_size, size_t(bytes)));
+    }
+    return PQH_OK;
+  }
+  // byte arrays: offsets relative to the range's first value, then the bytes
+  std::vector<int64_t> offs(size_t(nn1 + 1));
+  HIP_TRY(ctx, bounce_d2h(ctx, offs.data(), C.offsets + v0, sizeof(int64_t) * size_t(nn1 + 1)));
+  out->num_bytes = offs.back() - offs.front();
+  if (offsets) {
+    if (offsets_cap < nn1 + 1) return set_err(ctx, PQH_ERR_ARG, "offsets buffer too small");
+    for (int64_t i = 0; i <= nn1; i++) offsets[i] = offs[size_t(i)] - offs.front();
+  }
+  if (data && out->num_bytes > 0) {
+    if (data_cap < out->num_bytes) return set_err(ctx, PQH_ERR_ARG, "data buffer too small");
+    HIP_TRY(ctx, bounce_d2h(ctx, data, C.bytes + offs.front(), size_t(out->num_bytes)));
+  }
+  return PQH_OK;
+}
+
 int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   if (!b || chunk < 0 || size_t(chunk) >= b->chunks.size()) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad chunk");
   if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");

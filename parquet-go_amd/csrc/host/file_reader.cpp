@@ -11,6 +11,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -59,7 +60,15 @@ struct SchemaEl {
 
 }  // namespace
 
+// One schema element as the reader's Column tree sees it (schema.go:893-990).
+struct SchemaNode {
+  SchemaEl el;
+  int32_t column = -1;  // leaf: index into pqh_file::columns
+  int32_t d = 0, r = 0;
+};
+
 struct pqh_file {
+  std::vector<SchemaNode> schema;
   int fd = -1;
   void* map = nullptr;
   size_t map_len = 0;
@@ -158,6 +167,8 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
     return false;
   }
   st.push_back({root.num_children, 0, 0, "", {}});
+  f->schema.assign(s.size(), SchemaNode{});
+  f->schema[0].el = root;
   for (size_t i = 1; i < s.size(); i++) {
     while (!st.empty() && st.back().remaining == 0) st.pop_back();
     if (st.empty()) {
@@ -188,6 +199,7 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
       cm.col = pqh_column{e.type, e.type_length, d, r, {0, 0, 0, 0, 0, 0, 0, 0}};
       for (size_t k = 0; k < rd.size() && k < PQH_MAX_NEST; k++) cm.col.rep_def[k] = rd[k];
       cm.path = path;
+      f->schema[i] = SchemaNode{e, int32_t(f->columns.size()), d, r};
       f->columns.push_back(cm);
     } else {
       if (!e.has_children || e.num_children <= 0) {
@@ -199,6 +211,7 @@ bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
         r++;
         rd.push_back(d);
       }
+      f->schema[i] = SchemaNode{e, -1, d, r};
       st.push_back({e.num_children, d, r, path, rd});
     }
   }
@@ -459,6 +472,27 @@ int64_t pqh_file_row_group_num_rows(const pqh_file* f, int32_t rg) {
   return rg >= 0 && size_t(rg) < f->rgs.size() ? f->rgs[size_t(rg)].num_rows : -1;
 }
 int32_t pqh_file_num_columns(const pqh_file* f) { return int32_t(f->columns.size()); }
+
+int32_t pqh_file_num_schema_elements(const pqh_file* f) { return f ? int32_t(f->schema.size()) : 0; }
+
+int pqh_file_schema_element(const pqh_file* f, int32_t i, pqh_schema_element* out, char* name, int32_t cap) {
+  if (!f || !out || i < 0 || size_t(i) >= f->schema.size()) return PQH_ERR_ARG;
+  const SchemaNode& n = f->schema[size_t(i)];
+  out->physical_type = n.el.has_type ? n.el.type : -1;
+  out->type_length = n.el.type_length;
+  out->repetition = n.el.has_rep ? n.el.rep : -1;
+  out->num_children = n.el.has_children ? n.el.num_children : 0;
+  out->column = n.column;
+  out->max_def = n.d;
+  out->max_rep = n.r;
+  out->reserved = 0;
+  if (name && cap > 0) {
+    const size_t k = std::min(n.el.name.size(), size_t(cap - 1));
+    memcpy(name, n.el.name.data(), k);
+    name[k] = 0;
+  }
+  return PQH_OK;
+}
 
 int pqh_file_column(const pqh_file* f, int32_t column, pqh_column* out, char* path, int32_t cap) {
   if (!f || column < 0 || size_t(column) >= f->columns.size()) return PQH_ERR_ARG;

@@ -65,6 +65,16 @@ class PageResult(ctypes.Structure):
                 ("value_offset", i64), ("level_offset", i64)]
 
 
+class SchemaElement(ctypes.Structure):
+    _fields_ = [("physical_type", i32), ("type_length", i32), ("repetition", i32), ("num_children", i32),
+                ("column", i32), ("max_def", i32), ("max_rep", i32), ("reserved", i32)]
+
+
+class PageValues(ctypes.Structure):
+    _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_slots", i64), ("num_non_null", i64),
+                ("values_read", i64), ("num_bytes", i64), ("value_size", i32), ("reserved", i32)]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", i32), ("work_items", i32), ("total_ms", f64),
                 ("bytes_read", f64), ("bytes_written", f64)]
@@ -96,6 +106,8 @@ PROTOTYPES = [
     ("pqh_batch_chunk_out", ctypes.c_int, [vp, i32, ctypes.POINTER(ChunkOut)]),
     ("pqh_batch_nesting", ctypes.c_int, [vp, i32, ctypes.POINTER(NestOut)]),
     ("pqh_batch_page_results", ctypes.c_int, [vp, ctypes.POINTER(PageResult), i32]),
+    ("pqh_batch_page_read", ctypes.c_int, [vp, i32, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp,
+                                           ctypes.POINTER(PageValues)]),
     ("pqh_batch_kernel_stats", ctypes.c_int, [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]),
     ("pqh_batch_reset_stats", ctypes.c_int, [vp]),
     ("pqh_batch_traffic", ctypes.c_int, [vp, ctypes.POINTER(f64), ctypes.POINTER(f64)]),
@@ -109,6 +121,8 @@ PROTOTYPES = [
     ("pqh_file_row_group_num_rows", i64, [vp, i32]),
     ("pqh_file_num_columns", i32, [vp]),
     ("pqh_file_column", ctypes.c_int, [vp, i32, ctypes.POINTER(Column), ctypes.c_char_p, i32]),
+    ("pqh_file_num_schema_elements", i32, [vp]),
+    ("pqh_file_schema_element", ctypes.c_int, [vp, i32, ctypes.POINTER(SchemaElement), ctypes.c_char_p, i32]),
     ("pqh_file_load", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]),
     ("pqh_host_batch_num_chunks", i32, [vp]),
     ("pqh_host_batch_num_pages", i32, [vp]),
@@ -302,6 +316,16 @@ class File:
             out.append((buf.value.decode(), c.physical_type, c.type_length, c.max_def, c.max_rep))
         return out
 
+    def schema(self):
+        """[(name, SchemaElement)] in DFS order, root first."""
+        out = []
+        buf = ctypes.create_string_buffer(1024)
+        for i in range(self.L.pqh_file_num_schema_elements(self.h)):
+            e = SchemaElement()
+            _check(self.L.pqh_file_schema_element(self.h, i, ctypes.byref(e), buf, 1024))
+            out.append((buf.value.decode(), e))
+        return out
+
     def load(self, rg_begin, rg_end, columns, validate_crc=False):
         cols = (i32 * len(columns))(*columns)
         h = vp()
@@ -377,6 +401,33 @@ class Batch:
         arr = (PageResult * max(n, 1))()
         self.ctx.check(self.L.pqh_batch_page_results(self.h, arr, n))
         return [arr[i] for i in range(n)]
+
+    def page_read(self, page, first=0, count=None):
+        """readValues(count) of one page from level slot `first` (the compat path of the cgo shim):
+        (PageValues, values or (offsets, data), def levels or None, rep levels or None) as host
+        numpy arrays; values are None when the call fails."""
+        if count is None:
+            count = 1 << 62
+        pv = PageValues()
+        self.ctx.check(self.L.pqh_batch_page_read(self.h, page, first, count, None, 0, None, 0, None, 0, None, None,
+                                                  ctypes.byref(pv)))
+        ns = pv.num_slots
+        d = np.empty(ns, np.uint8)
+        r = np.empty(ns, np.uint8)
+        vals = offs = data = None
+        if pv.status == OK:
+            if pv.value_size > 0:
+                vals = np.empty(pv.num_non_null * pv.value_size, np.uint8)
+            else:
+                offs = np.empty(pv.num_non_null + 1, np.int64)
+                data = np.empty(max(pv.num_bytes, 1), np.uint8)
+        p = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+        self.ctx.check(self.L.pqh_batch_page_read(
+            self.h, page, first, count, p(vals), 0 if vals is None else vals.nbytes, p(offs),
+            0 if offs is None else len(offs), p(data), 0 if data is None else data.nbytes, p(d), p(r), ctypes.byref(pv)))
+        if data is not None:
+            data = data[:pv.num_bytes]
+        return pv, (vals if pv.value_size > 0 else (offs, data)), d, r
 
     def kernel_stats(self):
         arr = (KernelStat * 32)()

@@ -29,8 +29,9 @@ class DecodeError(RuntimeError):
 class ColumnData:
     """One decoded column chunk (dense not-null values + level bytes), host copy."""
 
-    def __init__(self, path, column, out, page_results, ctx, nest=None):
+    def __init__(self, path, column, out, page_results, ctx, nest=None, page_info=None):
         self.path = path
+        self.page_info = page_info or []  # [(page_type, num_values, PageResult)] of the chunk's pages
         self.physical_type, self.type_length, self.max_def, self.max_rep = column
         self.status = out.status
         self.error_page, self.error_phase, self.error_index = out.error_page, out.error_phase, out.error_index
@@ -106,15 +107,18 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
     batch.sync()
     cols = file.columns()
     res = batch.page_results(hb.num_pages)
+    pages = hb.pages()
     out = []
     chunks = hb.chunks()
     for i, ch in enumerate(chunks):
         path, pt, tl, md, mr = cols[columns[i % len(columns)]]
-        pr = [res[p] for p in range(ch.first_page, ch.first_page + ch.num_pages)]
+        span = range(ch.first_page, ch.first_page + ch.num_pages)
+        pr = [res[p] for p in span]
         o = batch.chunk_out(i)
         if ch.host_status != native.OK and o.status == native.OK:
             o.status = ch.host_status
-        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None))
+        info = [(pages[p].page_type, pages[p].num_values, res[p]) for p in span]
+        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None, info))
     if return_batch:
         return out, batch, hb
     batch.close()
@@ -123,6 +127,10 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
 
 
 class FileReader:
+    """FileReader (file_reader.go:32-351) over the GPU decode.  The row-group cursor follows the
+    reference: rowGroupPosition is 1-based once a group is loaded, advanceIfNeeded loads the next
+    group when the current one is exhausted or skipped, io.EOF past the last group (EOFError)."""
+
     def __init__(self, source, *columns, device=0, validate_crc=False, ctx=None):
         self.file = native.File(source)
         self.ctx = ctx or native.Context(device)
@@ -139,8 +147,12 @@ class FileReader:
             self.selected = sorted(set(sel))
         else:
             self.selected = list(range(len(allc)))
-        self.row_group = 0
-        self._loaded = None
+        self._schema = None
+        self.row_group_position = 0  # f.rowGroupPosition
+        self.current_record = 0       # f.currentRecord
+        self.skip_row_group = False   # f.skipRowGroup
+        self._loaded = None           # decoded chunks of row group row_group_position - 1
+        self._rows = None             # records.RowAssembler over them
 
     @classmethod
     def NewFileReader(cls, source, *columns, **kw):
@@ -155,25 +167,67 @@ class FileReader:
     def Columns(self):
         return [self._paths[i] for i in self.selected]
 
-    def SeekToRowGroup(self, rg):
-        if rg < 0 or rg >= self.RowGroupCount():
-            raise IndexError("row group out of range")
-        self.row_group = rg
-        self._loaded = None
+    def _read_row_group(self):  # readRowGroup (file_reader.go:200-207)
+        if self.RowGroupCount() <= self.row_group_position:
+            raise EOFError("EOF")
+        self.row_group_position += 1
+        rg = self.row_group_position - 1
+        self._loaded = decode_chunks(self.ctx, self.file, rg, rg + 1, self.selected, self.validate_crc)
+        self._rows = None
+
+    def _advance_if_needed(self):  # advanceIfNeeded (file_reader.go:226-238)
+        if (self.row_group_position == 0 or self.skip_row_group
+                or self.current_record >= self.file.row_group_num_rows(self.row_group_position - 1)):
+            try:
+                self._read_row_group()
+            except EOFError:
+                self.skip_row_group = True
+                raise
+            self.current_record = 0
+            self.skip_row_group = False
+
+    def SeekToRowGroup(self, position):
+        """file_reader.go:186-198: rowGroupPosition = position - 1, then readRowGroup, which loads
+        RowGroups[position - 1] -- so, as in the reference, position 1 is the first row group and
+        position 0 fails (the reference's index -1 panic, recovered into an error)."""
+        if position < 1:
+            raise IndexError(f"index out of range [{position - 1}]")
+        self.row_group_position = position - 1
+        self.current_record = 0
+        self._read_row_group()
 
     def SkipRowGroup(self):
-        self.row_group += 1
-        self._loaded = None
+        self.skip_row_group = True
 
     def PreLoad(self):
-        if self._loaded is None:
-            self._loaded = decode_chunks(self.ctx, self.file, self.row_group, self.row_group + 1, self.selected,
-                                         self.validate_crc)
+        self._advance_if_needed()
         return self
 
+    def RowGroupNumRows(self):
+        self._advance_if_needed()
+        return self.file.row_group_num_rows(self.row_group_position - 1)
+
     def ReadColumns(self):
+        """The columnar throughput path: {path: ColumnData} of the current row group."""
         self.PreLoad()
         return {c.path: c.raise_for_status() for c in self._loaded}
+
+    def NextRow(self):
+        """NextRow (file_reader.go:258-272): the next record as a dict (records.py), loading the
+        next row group when needed; EOFError after the last row."""
+        from . import records
+
+        self._advance_if_needed()
+        if self._rows is None:
+            for c in self._loaded:  # readRowGroupData fails on any chunk error (chunk_reader.go:394-400)
+                c.raise_for_status()
+            if self._schema is None:
+                self._schema = self.file.schema()
+            cols = {self.selected[i]: (c, c.physical_type, c.path) for i, c in enumerate(self._loaded)}
+            self._rows = records.RowAssembler(self._schema, cols,
+                                              self.file.row_group_num_rows(self.row_group_position - 1))
+        self.current_record += 1
+        return self._rows.next_row()
 
     def close(self):
         self.file.close()
