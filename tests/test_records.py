@@ -9,6 +9,7 @@ KAT rows written to a file.  GPU: the same files read row by row through reader.
 assembly over the oracle's per-page readValues results."""
 import json
 import os
+import struct
 
 import numpy as np
 import pytest
@@ -141,13 +142,15 @@ def oracle_rows(data):
 
 
 def _norm(v):
-    """bytes -> str so KAT rows (JSON) and Go []byte values compare."""
+    """bytes -> str so KAT rows (JSON) and Go []byte values compare; floats by bit pattern."""
     if isinstance(v, dict):
         return {k: _norm(x) for k, x in v.items()}
     if isinstance(v, list):
         return [_norm(x) for x in v]
     if isinstance(v, (bytes, bytearray)):
         return bytes(v).decode("latin-1")
+    if isinstance(v, float):  # NaN != NaN: compare float values by their bits
+        return ("f64", struct.pack("<d", v))
     return v
 
 
