@@ -196,9 +196,11 @@ struct pqh_batch {
   bool delta_page_mode = false;
   int32_t delta_fused_pages = 0;    // page mode: delta pages / streams through k_delta_fused
   int32_t delta_fused_streams = 0;
+  int32_t delta_lens_streams = 0;   // the last of delta_streams: DELTA_LENGTH_BYTE_ARRAY pages
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
-  std::vector<int32_t> ba_xlist;    // ba_tiles indices: DELTA_LENGTH tiles, then PLAIN / dictionary
+  std::vector<int32_t> ba_xlist;    // ba_tiles indices: DELTA_LENGTH tiles, then PLAIN / dictionary, then k_ba_sum's
+  int32_t ba_sum_off = 0;           // start of k_ba_sum's list in ba_xlist
   int32_t ba_ncopy = 0;             //   (the first ba_ncopy go to k_ba_expand, the rest to k_ba_gather)
   std::vector<int32_t> ba_pages;    // PLAIN byte-array data + dictionary pages (chain walks)
   std::vector<int2> ba_wins, ba_pwin;
@@ -604,6 +606,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       // pages after the failing one, inside a chunk whose result is that error.
       b->delta_fused_pages = int32_t(b->delta_pages.size());
       b->delta_fused_streams = int32_t(b->delta_streams.size());
+      // DELTA_LENGTH streams last: k_delta_fused<true> sums their tiles' bytes
+      std::stable_partition(b->delta_streams.begin(), b->delta_streams.end(),
+                            [&](const Tile& t) { return b->hpages[size_t(t.page)].kind != K_DLBA; });
+      b->delta_lens_streams = int32_t(std::count_if(b->delta_streams.begin(), b->delta_streams.end(),
+                                                    [&](const Tile& t) { return b->hpages[size_t(t.page)].kind == K_DLBA; }));
     }
   }
 
@@ -613,6 +620,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   for (size_t i = 0; i < b->ba_tiles.size(); i++) {
     const int32_t k = b->hpages[size_t(b->ba_tiles[i].page)].kind;
     if (k != K_DLBA && k != K_DBA) b->ba_xlist.push_back(int32_t(i));
+  }
+  // k_ba_sum's work list (after the copy + gather lists): every tile, except that in page mode a
+  // DELTA_LENGTH page is represented by its tile 0 (its sums come from the delta kernels; the
+  // tile-0 workgroup checks that and otherwise sums the whole page)
+  b->ba_sum_off = int32_t(b->ba_xlist.size());
+  for (size_t i = 0; i < b->ba_tiles.size(); i++) {
+    const Tile& t = b->ba_tiles[i];
+    if (!(b->delta_page_mode && b->hpages[size_t(t.page)].kind == K_DLBA && t.k > 0)) b->ba_xlist.push_back(int32_t(i));
   }
 
   // ---- device allocations ----
@@ -809,7 +824,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
-    e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, st); });
+    e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
     if (e == hipSuccess)
       e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
   }
@@ -841,12 +856,15 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   if (e == hipSuccess && ng)
     e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
   if (e == hipSuccess && nbt) {
-    e = timed(8, nbt, s, [&](hipStream_t st) { return launch_ba_sum(d, b->d_batiles, nbt, st); });
+    const int32_t nsum = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
+    e = timed(8, nsum, s, [&](hipStream_t st) {
+      return launch_ba_sum(d, b->d_batiles, b->d_ba_xlist + b->ba_sum_off, nsum, b->delta_page_mode, st);
+    });
     if (e == hipSuccess)
       e = timed(9, nbc, s, [&](hipStream_t st) { return launch_ba_scan(d, b->d_ba_chunks, nbc, b->d_batiles, st); });
     if (e == hipSuccess)
       e = timed(10, nbt, s, [&](hipStream_t st) {  // k_ba_expand + k_ba_gather
-        return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, int32_t(b->ba_xlist.size()) - b->ba_ncopy, st);
+        return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, b->ba_sum_off - b->ba_ncopy, st);
       });
     if (e == hipSuccess && b->has_dba)
       e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });

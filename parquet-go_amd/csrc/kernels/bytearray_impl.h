@@ -496,16 +496,15 @@ __device__ __forceinline__ int64_t block_sum64(int64_t x, int64_t* wsum) {
 // ------------------------------------------------------------------------------------------------
 // k_ba_sum: bytes of each kBaTile tile; first negative DELTA_LENGTH length; EOF past valuesCount.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles) {
-  __shared__ int64_t wsum[4];
-  const Tile t = tiles[blockIdx.x];
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
+// Tile k of byte-array page `page`.
+__device__ void ba_tile_sum(const DevBatch& b, int page, int32_t k, int64_t* wsum) {
+  const DevPage P = b.pages[page];
+  const PageState S = b.states[page];
   int64_t s = 0;
   if (!page_failed_before_values(S)) {
     const DevChunk C = b.chunks[P.chunk];
-    const int64_t lim = ba_limit(b, t.page, P, S);
-    const int64_t v0 = int64_t(t.k) * kBaTile;
+    const int64_t lim = ba_limit(b, page, P, S);
+    const int64_t v0 = int64_t(k) * kBaTile;
     const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
     const bool is_dict = P.kind == K_DICT;
     const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
@@ -523,17 +522,41 @@ __global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles) {
       }
     }
     s2 = block_sum64(dba ? s2 : 0, wsum);
-    if (threadIdx.x == 0) b.basums2[P.batile_base + t.k] = s2;
+    if (threadIdx.x == 0) b.basums2[P.batile_base + k] = s2;
     if (P.kind == K_DLBA || dba) {
       if (first_neg != INT64_MAX)  // make([]byte, negative) panics (re-panicked, file_reader.go:179-181)
-        atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_neg, PQH_ERR_NEGATIVE_DLBA_LENGTH));
-      const int64_t vc = b.dstates[dba ? b.num_pages + t.page : t.page].limit;
-      if (t.k == 0 && threadIdx.x == 0 && S.nn > vc)  // lens exhausted: io.EOF (type_bytearray.go:118-121)
-        atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
+        atomicMin(&b.states[page].err, (unsigned long long)err_key(3, first_neg, PQH_ERR_NEGATIVE_DLBA_LENGTH));
+      const int64_t vc = b.dstates[dba ? b.num_pages + page : page].limit;
+      if (k == 0 && threadIdx.x == 0 && S.nn > vc)  // lens exhausted: io.EOF (type_bytearray.go:118-121)
+        atomicMin(&b.states[page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
     }
   }
   s = block_sum64(s, wsum);
-  if (threadIdx.x == 0) b.basums[P.batile_base + t.k] = s;
+  if (threadIdx.x == 0) b.basums[P.batile_base + k] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_ba_sum: bytes of each kBaTile tile; first negative DELTA_LENGTH length; EOF past valuesCount.
+// dlba_pages (page mode): a DELTA_LENGTH page is listed once (tile 0); its sums and negative-length
+// checks were done by k_delta_fused / k_delta_page unless the page's stream left that path (summed
+// == 0), in which case this workgroup sums every tile of the page.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles, const int32_t* list, int dlba_pages) {
+  __shared__ int64_t wsum[4];
+  const Tile t = tiles[list[blockIdx.x]];
+  const DevPage P = b.pages[t.page];
+  if (P.kind == K_DLBA && b.dstates[t.page].summed) {
+    const PageState S = b.states[t.page];
+    const int64_t vc = b.dstates[t.page].limit;
+    if (t.k == 0 && threadIdx.x == 0 && !page_failed_before_values(S) && S.nn > vc)
+      atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
+    return;
+  }
+  if (P.kind == K_DLBA && dlba_pages) {
+    for (int32_t k = 0; k < P.batile_n; k++) ba_tile_sum(b, t.page, k, wsum);
+    return;
+  }
+  ba_tile_sum(b, t.page, t.k, wsum);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -124,6 +124,9 @@ struct DeltaState {
   int32_t rec_base;       // first DeltaBlock of this stream within the page's records
   int32_t head_blocks;    // blocks [0, head_blocks) already decoded by k_delta_fused (no records)
   uint64_t head_carry;    // value at position head_blocks * block_size (bits)
+  int64_t head_neg;       // DELTA_LENGTH: first negative length among the head blocks (INT64_MAX: none)
+  int32_t summed;         // DELTA_LENGTH: k_delta_page left complete kBaTile byte sums in basums
+  int32_t pad2;
 };
 // DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
 // DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).

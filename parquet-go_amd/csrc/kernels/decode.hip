@@ -1061,9 +1061,11 @@ hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int3
   return hipGetLastError();
 }
 
-hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_delta_fused, dim3(n), dim3(256), 0, s, b, streams);
+// streams [0, n - n_lens): DELTA_BINARY_PACKED / DELTA_BYTE_ARRAY prefixes; [n - n_lens, n):
+// DELTA_LENGTH_BYTE_ARRAY lengths (with their tile byte sums)
+hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, int32_t n_lens, hipStream_t s) {
+  if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_fused<false>, dim3(n - n_lens), dim3(256), 0, s, b, streams);
+  if (n_lens > 0) hipLaunchKernelGGL(k_delta_fused<true>, dim3(n_lens), dim3(256), 0, s, b, streams + (n - n_lens));
   return hipGetLastError();
 }
 
@@ -1124,9 +1126,10 @@ hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const
   return hipGetLastError();
 }
 
-hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n, bool dlba_pages,
+                         hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_sum, dim3(n), dim3(256), 0, s, b, tiles);
+  hipLaunchKernelGGL(k_ba_sum, dim3(n), dim3(256), 0, s, b, tiles, list, int(dlba_pages));
   return hipGetLastError();
 }
 

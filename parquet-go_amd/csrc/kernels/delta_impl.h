@@ -543,6 +543,8 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   D.rec_base = 0;
   D.head_blocks = 0;
   D.head_carry = 0;
+  D.head_neg = INT64_MAX;
+  D.summed = 0;
   int64_t pos = vs;
   int st;
   int32_t vc;
@@ -688,10 +690,13 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   const int64_t spec_hr = rfl64(uint64_t(b.dstates[p].end_pos));
   const int head_in = __builtin_amdgcn_readfirstlane(b.dstates[p].head_blocks);
   const uint64_t carry_in = rfl64(b.dstates[p].head_carry);
+  const int64_t neg_in = int64_t(rfl64(uint64_t(b.dstates[p].head_neg)));
   DeltaState D, D1;
   D.mode = D1.mode = DM_NONE;
   D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.head_blocks = 0;
   D.head_carry = 0;
+  D.head_neg = INT64_MAX;
+  D.summed = D.pad2 = 0;
   D.first = 0;
   D.end_pos = 0;
   D1 = D;
@@ -724,6 +729,7 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   if (head_in > 0 && D.mode == DM_FAST && D.nblocks >= head_in && spec_r == head_in) {
     D.head_blocks = head_in;
     D.head_carry = carry_in;
+    D.head_neg = neg_in;
   }
   if (lane == 0) {
     b.dstates[p] = D;
@@ -1118,13 +1124,30 @@ __device__ __forceinline__ void staged_delta2(const L& T, int64_t p, int bb0, in
   }
 }
 
+// DELTA_LENGTH_BYTE_ARRAY lengths: the byte sum of every kBaTile tile of the page accumulated while
+// the lengths are in registers (what k_ba_sum would re-read), and the first negative length
+// (make([]byte, negative) panics, file_reader.go:179-181).  Positions >= lim are not counted.
+struct LenSums {
+  int64_t* tsum;  // basums + the page's batile_base (atomic adds; zeroed before the first producer)
+  int64_t lim;
+  int64_t neg;    // first negative length seen (INT64_MAX: none)
+};
+
+// One wave's partial sums of tile `tile` into tsum (one atomic per wave and tile).
+__device__ __forceinline__ void flush_tile_sum(LenSums& ls, int64_t tile, uint64_t acc) {
+  const uint64_t tot = wave_incl_scan(acc);
+  if ((threadIdx.x & 63) == 63 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(ls.tsum + tile), tot);
+}
+
 // Rows of 1024 positions of a staged tile, one block scan each (wave totals double-buffered by row
 // parity).  Every store instruction writes 16 contiguous bytes per lane, 1 KiB per wave: int32
 // values 4 consecutive per thread; int64 values 2 consecutive per thread in each half row (two
-// independent scans).  Returns the carry after the tile.
-template <class L>
+// independent scans).  Returns the carry after the tile.  kSum (int32 DELTA_LENGTH lengths): each
+// lane also sums its lengths of the wave's current kBaTile tile in a register, flushed (one wave
+// reduction + one atomic) when the wave moves on to the next tile.
+template <bool kSum = false, class L>
 __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, int lbs, int lmb, uint8_t* out,
-                                                bool is64, uint64_t carry) {
+                                                bool is64, uint64_t carry, LenSums* ls = nullptr) {
   const int bb0 = int(v0 >> lbs);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int row = 0;
@@ -1229,6 +1252,10 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
   // expansion runs in 32 bits (widths of 32-bit streams are <= 32)
   uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
   uint32_t c32 = uint32_t(carry);
+  // kSum: acc = this lane's lengths of tile tacc (wave-uniform) not yet flushed
+  int64_t tacc = (v0 + 4 * 64 * wv) / kBaTile;
+  uint64_t acc = 0;
+  const int64_t lim_e = kSum ? (v1 < ls->lim ? v1 : ls->lim) : 0;
   for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
     uint32_t d[4] = {0, 0, 0, 0};
@@ -1245,18 +1272,47 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
     __syncthreads();
     uint32_t v = c32 + incl - tsum;
     for (int k = 0; k < wv; k++) v += uint32_t(T.wtot[row][k]);
+    const uint32_t o4[4] = {v, v + d[0], v + d[0] + d[1], v + d[0] + d[1] + d[2]};
     if (p + 4 <= v1) {
-      const uint32_t o4[4] = {v, v + d[0], v + d[0] + d[1], v + d[0] + d[1] + d[2]};
       __builtin_memcpy(o32 + p, o4, 16);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (p + j < v1) o32[p + j] = v;
-        v += d[j];
+      for (int j = 0; j < 4; j++)
+        if (p + j < v1) o32[p + j] = o4[j];
+    }
+    if constexpr (kSum) {
+      // the lane's 4 lengths: non-negative int32 pairs add without overflow in 32 bits
+      uint64_t rs;
+      if (p + 4 <= lim_e && ((o4[0] | o4[1] | o4[2] | o4[3]) >> 31) == 0) {
+        rs = uint64_t(o4[0] + o4[1]) + uint64_t(o4[2] + o4[3]);
+      } else {
+        rs = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (p + j >= lim_e) break;
+          if (int32_t(o4[j]) < 0) ls->neg = p + j < ls->neg ? p + j : ls->neg;
+          else rs += o4[j];
+        }
+      }
+      const int64_t w0 = r0 + 4 * 64 * wv;  // the wave's 256 positions of this row: [w0, w0 + 256)
+      const int64_t t0 = w0 / kBaTile;       // wave-uniform; advances by <= 1 per row
+      if (t0 != tacc) {
+        flush_tile_sum(*ls, tacc, acc);
+        acc = 0;
+        tacc = t0;
+      }
+      if ((w0 + 255) / kBaTile != t0) {  // the row crosses into tile t0 + 1 inside this wave
+        const bool lo = p < (t0 + 1) * kBaTile;
+        flush_tile_sum(*ls, t0, acc + (lo ? rs : 0));
+        acc = lo ? 0 : rs;
+        tacc = t0 + 1;
+      } else {
+        acc += rs;
       }
     }
     c32 += uint32_t(T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3]);
   }
+  if constexpr (kSum) flush_tile_sum(*ls, tacc, acc);
   return c32;
 }
 
@@ -1324,6 +1380,17 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
   const int64_t nblk = (vlim + c.D.block_size - 1) >> lbs;
   const int64_t e = c.P.image_len;
   const int tid = threadIdx.x;
+  // DELTA_LENGTH: the tile byte sums of the page (k_delta_fused added the head's when the walk
+  // accepted it; otherwise they start again from zero) and the first negative length
+  __shared__ unsigned long long s_neg;
+  const bool sums = c.P.kind == K_DLBA;
+  LenSums ls{b.basums + c.P.batile_base, vlim < c.S.val_limit ? vlim : c.S.val_limit, INT64_MAX};
+  if (sums) {
+    if (c.D.head_blocks == 0)
+      for (int k = tid; k < c.P.batile_n; k += kBlock) ls.tsum[k] = 0;
+    if (tid == 0) s_neg = uint64_t(c.D.head_neg);
+    __syncthreads();
+  }
   // blocks [0, head_blocks) were decoded by k_delta_fused
   uint64_t carry = c.D.head_blocks ? c.D.head_carry : c.D.first;
   for (int64_t blk0 = c.D.head_blocks; blk0 < nblk;) {
@@ -1368,8 +1435,19 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
     const int64_t v0 = blk0 << lbs;
     int64_t v1 = (blk0 + nfit) << lbs;
     if (v1 > vlim) v1 = vlim;
-    carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+    if (sums) carry = expand_rows<true>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
+    else carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
     blk0 += nfit;
+  }
+  if (sums) {
+    if (ls.neg != INT64_MAX) atomicMin(&s_neg, (unsigned long long)ls.neg);
+    __syncthreads();
+    if (tid == 0) {
+      if (s_neg != (~0ull >> 1))  // make([]byte, negative) panics (re-panicked, file_reader.go:179-181)
+        atomicMin(&b.states[streams[blockIdx.x].page].err,
+                  (unsigned long long)err_key(3, int64_t(s_neg), PQH_ERR_NEGATIVE_DLBA_LENGTH));
+      b.dstates[streams[blockIdx.x].page].summed = 1;
+    }
   }
 }
 
@@ -1713,6 +1791,9 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
 // no block records are written.  The chase stops at the first header the common-case parse rejects
 // or a block that runs past the stream; k_delta_walk resumes there with the exact semantics (and the
 // records of the remaining blocks) and k_delta_page decodes the rest.
+// kLens: the DELTA_LENGTH streams' launch (tile byte sums in the row loop); the other streams run
+// the instantiation without them, which keeps its register budget (occupancy) unchanged.
+template <bool kLens>
 __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* streams) {
   __shared__ PageTileLds T;
   __shared__ int32_t s_blkbit[kTileBlocks];
@@ -1722,6 +1803,7 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
   __shared__ int32_t s_geo[5];  // kmax (0 = nothing to do), block size, miniblocks, values per miniblock, vc
   __shared__ int32_t s_n, s_stop;
   __shared__ int16_t s_lst[kChaseCap][64];
+  __shared__ unsigned long long s_neg;
   const Tile t = streams[blockIdx.x];
   if (t.kind != 0) return;  // DELTA_BYTE_ARRAY suffix lengths: k_delta_walk + k_delta_page
   const int p = t.page;
@@ -1752,13 +1834,20 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
           s_geo[3] = D.mbvc;
           s_first = D.first;
           s_h = h0;
+          s_geo[4] = vc;
         }
       }
     }
-    if (tid == 0) s_geo[0] = kmax;
+    if (tid == 0) {
+      s_geo[0] = kmax;
+      s_neg = ~0ull >> 1;
+    }
   }
   __syncthreads();
   const int kmax = s_geo[0];
+  // DELTA_LENGTH: tile byte sums + first negative length of the head (k_delta_init zeroed the sums)
+  const bool sums = kLens && P.kind == K_DLBA && kmax > 0;
+  LenSums ls{b.basums + P.batile_base, sums ? (S.val_limit < s_geo[4] ? S.val_limit : s_geo[4]) : 0, INT64_MAX};
   int r = 0;
   int64_t h = s_h;
   uint64_t carry = s_first;
@@ -1805,18 +1894,28 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
       const int64_t v0 = int64_t(r) << lbs;
       int64_t v1 = int64_t(r + n) << lbs;
       if (v1 > vcap) v1 = vcap;
-      if (v0 < v1) carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+      if (v0 < v1) {
+        if constexpr (kLens) {
+          if (sums) carry = expand_rows<true>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
+          else carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+        } else {
+          carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
+        }
+      }
       est = int32_t((s_h - h) / n);  // mean block span so far: the next tile's lane segments
       r += n;
       h = s_h;
       if (s_stop || r >= kmax || v1 >= vcap) break;
     }
   }
+  if (sums && ls.neg != INT64_MAX) atomicMin(&s_neg, (unsigned long long)ls.neg);
+  __syncthreads();
   if (tid == 0) {
     b.dstates[p].nblocks = r;
     b.dstates[p].end_pos = h;
     b.dstates[p].head_blocks = r;
     b.dstates[p].head_carry = carry;
+    b.dstates[p].head_neg = int64_t(s_neg);  // counts only if k_delta_walk accepts the head
   }
 }
 
@@ -1834,6 +1933,8 @@ __global__ __launch_bounds__(256) void k_delta_init(DevBatch b, const int32_t* d
   const PageState S = b.states[p];
   const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
   if (P.host_err != kNoError || !load_ok) return;
+  if (P.kind == K_DLBA)  // k_delta_fused / k_delta_page add the tile byte sums of its lengths
+    for (int k = lane; k < P.batile_n; k += 64) b.basums[P.batile_base + k] = 0;
   Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
   win_load(w, S.val_s, lane);
   DeltaState D;

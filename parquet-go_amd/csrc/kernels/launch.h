@@ -42,7 +42,7 @@ hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, 
 // Page mode (many delta streams): init errors of the DELTA_BINARY_PACKED pages before the value
 // scan; whole blocks chased and decoded in one workgroup per stream (before the exact walk).
 hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
-hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
+hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, int32_t n_lens, hipStream_t s);
 // Many delta streams: one workgroup per (page, stream), its tiles in order with a running carry.
 hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,
@@ -55,7 +55,8 @@ hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const i
                              int32_t* wrec, hipStream_t s);
 hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const int32_t* wrec,
                            hipStream_t s);
-hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n, bool dlba_pages,
+                         hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
 hipError_t launch_ba_expand(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n_copy, int32_t n_gather,
                             hipStream_t s);
