@@ -621,13 +621,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     const int32_t k = b->hpages[size_t(b->ba_tiles[i].page)].kind;
     if (k != K_DLBA && k != K_DBA) b->ba_xlist.push_back(int32_t(i));
   }
-  // k_ba_sum's work list (after the copy + gather lists): every tile, except that in page mode a
-  // DELTA_LENGTH page is represented by its tile 0 (its sums come from the delta kernels; the
-  // tile-0 workgroup checks that and otherwise sums the whole page)
+  // k_ba_sum's work list (after the copy + gather lists): every tile, except that PLAIN pages (and in
+  // page mode DELTA_LENGTH pages) are represented by their tile 0: their sums come from k_ba_wemit
+  // (the delta kernels); the tile-0 workgroup checks that and otherwise sums the whole page
   b->ba_sum_off = int32_t(b->ba_xlist.size());
   for (size_t i = 0; i < b->ba_tiles.size(); i++) {
     const Tile& t = b->ba_tiles[i];
-    if (!(b->delta_page_mode && b->hpages[size_t(t.page)].kind == K_DLBA && t.k > 0)) b->ba_xlist.push_back(int32_t(i));
+    const int32_t kind = b->hpages[size_t(t.page)].kind;
+    if (t.k == 0 || !(kind == K_PLAIN_BA || (b->delta_page_mode && kind == K_DLBA))) b->ba_xlist.push_back(int32_t(i));
   }
 
   // ---- device allocations ----

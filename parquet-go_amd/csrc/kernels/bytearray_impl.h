@@ -365,6 +365,10 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
   const int2 wr = pwin[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, p);
   if (!c.ok) return;
+  if (!c.dict) {  // k_ba_wemit adds the tile byte sums of the page's lengths
+    const DevPage P = b.pages[p];
+    for (int k = threadIdx.x; k < P.batile_n; k += kBlock) b.basums[P.batile_base + k] = 0;
+  }
   int64_t done = 0, cum = 0, T = c.entry;
   int code = PQH_OK;
   int w = 0;
@@ -412,11 +416,14 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
       b.states[p].val_limit = int32_t(done);
       atomicMin(&b.states[p].err, (unsigned long long)err_key(3, done, code));
     }
+    if (!c.dict) b.states[p].ba_summed = 1;
   }
 }
 
 // One workgroup per window: its records' lengths (data page -> aux) or cumulative offsets
-// (dictionary page -> dcum) copied out at the window's base.
+// (dictionary page -> dcum) copied out at the window's base.  Data pages: the lengths before the
+// page's value limit are also added to the page's kBaTile byte sums (k_ba_wstitch zeroed them), so
+// k_ba_sum does not read them again.
 __global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* wins, const BaWin* res,
                                                    const int32_t* wrec) {
   const BaWin r = res[blockIdx.x];
@@ -425,14 +432,34 @@ __global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* wins, 
   const BaPageCtx c = ba_page_ctx(b, p);
   if (!c.ok) return;
   const int32_t* src = wrec + int64_t(blockIdx.x) * kChainRecs;
-  PQH_G int32_t* out = c.dict ? (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base)
-                              : b.chunks[b.pages[p].chunk].aux + b.states[p].value_base;
-  for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
-    const int64_t idx = r.base + i;
-    if (idx >= c.count) break;
-    out[idx] = c.dict ? int32_t(r.cbase + src[i]) : src[i];
-    if (c.dict && idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
+  if (c.dict) {
+    PQH_G int32_t* out = (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base);
+    for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
+      const int64_t idx = r.base + i;
+      if (idx >= c.count) break;
+      out[idx] = int32_t(r.cbase + src[i]);
+      if (idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
+    }
+    return;
   }
+  const PageState S = b.states[p];
+  const DevPage P = b.pages[p];
+  PQH_G int32_t* out = b.chunks[P.chunk].aux + S.value_base;
+  const int64_t lim = S.val_limit < c.count ? S.val_limit : c.count;
+  const int wv = threadIdx.x >> 6;
+  WaveTileSum wts{(r.base + 64 * wv) / kBaTile, 0};
+  for (int32_t i0 = 0; i0 < r.count; i0 += kBlock) {  // uniform trip count (wave-wide sums)
+    const int32_t i = i0 + int32_t(threadIdx.x);
+    const int64_t idx = r.base + i;
+    int32_t l = 0;
+    if (i < r.count && idx < c.count) {
+      l = src[i];
+      out[idx] = l;
+    }
+    const int64_t w0 = r.base + i0 + 64 * wv;
+    wave_tile_add(wts, b.basums + P.batile_base, w0, w0 + 63, idx, idx < lim && l > 0 ? uint64_t(l) : 0);
+  }
+  flush_tile_sum(b.basums + P.batile_base, wts.tacc, wts.acc);
 }
 
 // Values of a byte-array data page that decode before the first error known so far.
@@ -537,22 +564,24 @@ __device__ void ba_tile_sum(const DevBatch& b, int page, int32_t k, int64_t* wsu
 
 // ------------------------------------------------------------------------------------------------
 // k_ba_sum: bytes of each kBaTile tile; first negative DELTA_LENGTH length; EOF past valuesCount.
-// dlba_pages (page mode): a DELTA_LENGTH page is listed once (tile 0); its sums and negative-length
-// checks were done by k_delta_fused / k_delta_page unless the page's stream left that path (summed
-// == 0), in which case this workgroup sums every tile of the page.
+// A PLAIN page, and in page mode (dlba_pages) a DELTA_LENGTH page, is listed once (tile 0): its sums
+// (and negative-length checks) were accumulated by k_ba_wemit / k_delta_fused + k_delta_page unless
+// the page left that path (ba_summed == 0), in which case this workgroup sums every tile of it.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles, const int32_t* list, int dlba_pages) {
   __shared__ int64_t wsum[4];
   const Tile t = tiles[list[blockIdx.x]];
   const DevPage P = b.pages[t.page];
-  if (P.kind == K_DLBA && b.dstates[t.page].summed) {
+  if (b.states[t.page].ba_summed) {
     const PageState S = b.states[t.page];
-    const int64_t vc = b.dstates[t.page].limit;
-    if (t.k == 0 && threadIdx.x == 0 && !page_failed_before_values(S) && S.nn > vc)
-      atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
+    if (P.kind == K_DLBA) {
+      const int64_t vc = b.dstates[t.page].limit;
+      if (t.k == 0 && threadIdx.x == 0 && !page_failed_before_values(S) && S.nn > vc)
+        atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, vc, PQH_ERR_EOF));
+    }
     return;
   }
-  if (P.kind == K_DLBA && dlba_pages) {
+  if (P.kind == K_PLAIN_BA || (P.kind == K_DLBA && dlba_pages)) {
     for (int32_t k = 0; k < P.batile_n; k++) ba_tile_sum(b, t.page, k, wsum);
     return;
   }
@@ -564,43 +593,47 @@ __global__ __launch_bounds__(256) void k_ba_sum(DevBatch b, const Tile* tiles, c
 // chunk are contiguous and in page order) -> each tile's first output offset, each page's first
 // byte (byte_base), the chunk's byte total.
 // ------------------------------------------------------------------------------------------------
-__device__ int64_t chunk_scan(int64_t* sums, int32_t n, const Tile* tiles, PageState* states, int64_t* wsum,
-                              int64_t& carry) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t == 0) carry = 0;
-  __syncthreads();
-  for (int base = 0; base < n; base += kBlock) {
-    const int i = base + t;
-    const int64_t x = i < n ? sums[i] : 0;
-    int64_t incl = x;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int64_t y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int64_t before = carry;
-    for (int k = 0; k < wv; k++) before += wsum[k];
-    if (i < n) {
-      const int64_t start = before + incl - x;
-      sums[i] = start;
-      if (states && tiles[i].k == 0) states[tiles[i].page].byte_base = start;
-    }
-    __syncthreads();
-    if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
+// Each thread scans a contiguous run of ceil(n / 256) tiles (independent loads, one block scan), so
+// a chunk of thousands of tiles costs one pass instead of one barrier round per 256 tiles.
+__device__ int64_t chunk_scan(int64_t* sums, int32_t n, const Tile* tiles, PageState* states, uint64_t* wsum) {
+  const int per = (n + kBlock - 1) / kBlock;
+  const int i0 = int(threadIdx.x) * per, i1 = i0 + per < n ? i0 + per : n;
+  uint64_t local = 0;
+  for (int i = i0; i < i1; i += 8) {  // 8 loads in flight
+    int64_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = i + k < i1 ? sums[i + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) local += uint64_t(x[k]);
   }
-  return carry;
+  uint64_t total;
+  int64_t run = int64_t(block_exclusive_scan(local, wsum, &total));
+  for (int i = i0; i < i1; i += 8) {
+    int64_t x[8];
+    Tile tl[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      x[k] = i + k < i1 ? sums[i + k] : 0;
+      if (states && i + k < i1) tl[k] = tiles[i + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (i + k >= i1) break;
+      sums[i + k] = run;
+      if (states && tl[k].k == 0) states[tl[k].page].byte_base = run;
+      run += x[k];
+    }
+  }
+  return int64_t(total);
 }
 
 __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_chunks, const Tile* tiles) {
-  __shared__ int64_t wsum[4];
-  __shared__ int64_t carry;
+  __shared__ uint64_t wsum[4];
   const int c = ba_chunks[blockIdx.x];
   const DevChunk C = b.chunks[c];
   if (threadIdx.x == 0 && C.offsets) C.offsets[0] = 0;
-  const int64_t total = chunk_scan(b.basums + C.batile_base, C.batile_n, tiles + C.batile_base, b.states, wsum, carry);
-  if (C.aux2) chunk_scan(b.basums2 + C.batile_base, C.batile_n, tiles + C.batile_base, nullptr, wsum, carry);
+  const int64_t total = chunk_scan(b.basums + C.batile_base, C.batile_n, tiles + C.batile_base, b.states, wsum);
+  if (C.aux2) chunk_scan(b.basums2 + C.batile_base, C.batile_n, tiles + C.batile_base, nullptr, wsum);
   if (threadIdx.x == 0) b.chunk_bytes[c] = total;
 }
 

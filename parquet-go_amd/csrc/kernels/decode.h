@@ -105,6 +105,9 @@ struct PageState {
   int32_t val_s, val_e;    // values section / value hybrid stream
   int32_t val_limit;       // values before the first phase-3 stream error (== nn if none)
   int32_t dict_n;          // dictionary pages: entries decoded
+  int32_t ba_summed;       // byte-array data page: its kBaTile byte sums were accumulated by the
+                           // length producers (k_ba_wemit / k_delta_page), so k_ba_sum skips it
+  int32_t pad;
   int64_t value_base;      // first value of the page in the chunk's dense values
   int64_t byte_base;       // byte arrays: first byte
 };
@@ -125,8 +128,6 @@ struct DeltaState {
   int32_t head_blocks;    // blocks [0, head_blocks) already decoded by k_delta_fused (no records)
   uint64_t head_carry;    // value at position head_blocks * block_size (bits)
   int64_t head_neg;       // DELTA_LENGTH: first negative length among the head blocks (INT64_MAX: none)
-  int32_t summed;         // DELTA_LENGTH: k_delta_page left complete kBaTile byte sums in basums
-  int32_t pad2;
 };
 // DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
 // DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).

@@ -269,6 +269,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
   S.val_s = S.val_e = 0;
   S.val_limit = 0;
   S.dict_n = 0;
+  S.ba_summed = S.pad = 0;
   S.value_base = 0;
   S.byte_base = 0;
   uint64_t err = P.host_err;

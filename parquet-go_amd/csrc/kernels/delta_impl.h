@@ -544,7 +544,6 @@ __device__ uint64_t delta_walk(Win& w, int64_t vs, bool is64, int64_t nn, DeltaB
   D.head_blocks = 0;
   D.head_carry = 0;
   D.head_neg = INT64_MAX;
-  D.summed = 0;
   int64_t pos = vs;
   int st;
   int32_t vc;
@@ -696,7 +695,6 @@ __global__ __launch_bounds__(256) void k_delta_walk(DevBatch b, const int32_t* d
   D.block_size = D.mb_count = D.mbvc = D.nblocks = D.limit = D.rec_base = D.head_blocks = 0;
   D.head_carry = 0;
   D.head_neg = INT64_MAX;
-  D.summed = D.pad2 = 0;
   D.first = 0;
   D.end_pos = 0;
   D1 = D;
@@ -1134,9 +1132,34 @@ struct LenSums {
 };
 
 // One wave's partial sums of tile `tile` into tsum (one atomic per wave and tile).
-__device__ __forceinline__ void flush_tile_sum(LenSums& ls, int64_t tile, uint64_t acc) {
+__device__ __forceinline__ void flush_tile_sum(int64_t* tsum, int64_t tile, uint64_t acc) {
   const uint64_t tot = wave_incl_scan(acc);
-  if ((threadIdx.x & 63) == 63 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(ls.tsum + tile), tot);
+  if ((threadIdx.x & 63) == 63 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(tsum + tile), tot);
+}
+
+// Running kBaTile sums of one wave (call with the whole wave): lane x at position pos, the wave's
+// positions [wfirst, wlast] (wave-uniform, ascending from call to call by less than a tile).  A lane
+// keeps the sum of the wave's current tile `tacc` in `acc`; the wave flushes it when it moves on.
+struct WaveTileSum {
+  int64_t tacc;
+  uint64_t acc;
+};
+__device__ __forceinline__ void wave_tile_add(WaveTileSum& w, int64_t* tsum, int64_t wfirst, int64_t wlast, int64_t pos,
+                                              uint64_t x) {
+  const int64_t t0 = wfirst / kBaTile;
+  if (t0 != w.tacc) {
+    flush_tile_sum(tsum, w.tacc, w.acc);
+    w.acc = 0;
+    w.tacc = t0;
+  }
+  if (wlast / kBaTile != t0) {  // the wave's positions cross into tile t0 + 1
+    const bool lo = pos < (t0 + 1) * kBaTile;
+    flush_tile_sum(tsum, t0, w.acc + (lo ? x : 0));
+    w.acc = lo ? 0 : x;
+    w.tacc = t0 + 1;
+  } else {
+    w.acc += x;
+  }
 }
 
 // Rows of 1024 positions of a staged tile, one block scan each (wave totals double-buffered by row
@@ -1252,9 +1275,7 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
   // expansion runs in 32 bits (widths of 32-bit streams are <= 32)
   uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
   uint32_t c32 = uint32_t(carry);
-  // kSum: acc = this lane's lengths of tile tacc (wave-uniform) not yet flushed
-  int64_t tacc = (v0 + 4 * 64 * wv) / kBaTile;
-  uint64_t acc = 0;
+  WaveTileSum wts{(v0 + 4 * 64 * wv) / kBaTile, 0};
   const int64_t lim_e = kSum ? (v1 < ls->lim ? v1 : ls->lim) : 0;
   for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
@@ -1294,25 +1315,12 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
           else rs += o4[j];
         }
       }
-      const int64_t w0 = r0 + 4 * 64 * wv;  // the wave's 256 positions of this row: [w0, w0 + 256)
-      const int64_t t0 = w0 / kBaTile;       // wave-uniform; advances by <= 1 per row
-      if (t0 != tacc) {
-        flush_tile_sum(*ls, tacc, acc);
-        acc = 0;
-        tacc = t0;
-      }
-      if ((w0 + 255) / kBaTile != t0) {  // the row crosses into tile t0 + 1 inside this wave
-        const bool lo = p < (t0 + 1) * kBaTile;
-        flush_tile_sum(*ls, t0, acc + (lo ? rs : 0));
-        acc = lo ? 0 : rs;
-        tacc = t0 + 1;
-      } else {
-        acc += rs;
-      }
+      const int64_t w0 = r0 + 4 * 64 * wv;  // the wave's 256 positions of this row
+      wave_tile_add(wts, ls->tsum, w0, w0 + 255, p, rs);
     }
     c32 += uint32_t(T.wtot[row][0] + T.wtot[row][1] + T.wtot[row][2] + T.wtot[row][3]);
   }
-  if constexpr (kSum) flush_tile_sum(*ls, tacc, acc);
+  if constexpr (kSum) flush_tile_sum(ls->tsum, wts.tacc, wts.acc);
   return c32;
 }
 
@@ -1446,7 +1454,7 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
       if (s_neg != (~0ull >> 1))  // make([]byte, negative) panics (re-panicked, file_reader.go:179-181)
         atomicMin(&b.states[streams[blockIdx.x].page].err,
                   (unsigned long long)err_key(3, int64_t(s_neg), PQH_ERR_NEGATIVE_DLBA_LENGTH));
-      b.dstates[streams[blockIdx.x].page].summed = 1;
+      b.states[streams[blockIdx.x].page].ba_summed = 1;
     }
   }
 }

@@ -70,37 +70,40 @@ __global__ __launch_bounds__(256) void k_nest_count(DevBatch b, const Tile* tile
   if (threadIdx.x < kNestFlags) b.nsums[int64_t(N.tile_base + t.k) * kNestFlags + threadIdx.x] = cnt[threadIdx.x];
 }
 
-// One workgroup per nested chunk: exclusive scan of every flag over the chunk's tiles.
+// One workgroup per nested chunk: exclusive scan of every flag over the chunk's tiles (each thread
+// a contiguous run of ceil(tile_n / 256) tiles: one block scan per flag).
 __global__ __launch_bounds__(256) void k_nest_scan(DevBatch b) {
-  __shared__ int64_t wsum[4];
-  __shared__ int64_t carry;
+  __shared__ uint64_t wsum[4];
   const DevNest& N = b.nests[blockIdx.x];  // by reference: the per-level arrays are indexed at run time
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (N.tile_n + kBlock - 1) / kBlock;
+  const int i0 = int(threadIdx.x) * per, i1 = i0 + per < N.tile_n ? i0 + per : N.tile_n;
   for (int f = 0; f <= N.levels; f++) {
-    if (t == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < N.tile_n; base += kBlock) {
-      const int i = base + t;
-      int64_t* slot = b.nsums + int64_t(N.tile_base + i) * kNestFlags + f;
-      const int64_t x = i < N.tile_n ? *slot : 0;
-      int64_t incl = x;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int64_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) wsum[wv] = incl;
-      __syncthreads();
-      int64_t before = carry;
-      for (int k = 0; k < wv; k++) before += wsum[k];
-      if (i < N.tile_n) *slot = before + incl - x;
-      __syncthreads();
-      if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-      __syncthreads();
+    int64_t* slot = b.nsums + int64_t(N.tile_base) * kNestFlags + f;
+    uint64_t local = 0;
+    for (int i = i0; i < i1; i += 8) {  // 8 loads in flight
+      int64_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = i + k < i1 ? slot[int64_t(i + k) * kNestFlags] : 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) local += uint64_t(x[k]);
     }
-    if (t == 0) {
-      N.totals[f] = carry;
+    uint64_t total;
+    int64_t run = int64_t(block_exclusive_scan(local, wsum, &total));
+    for (int i = i0; i < i1; i += 8) {
+      int64_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = i + k < i1 ? slot[int64_t(i + k) * kNestFlags] : 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (i + k >= i1) break;
+        slot[int64_t(i + k) * kNestFlags] = run;
+        run += x[k];
+      }
+    }
+    if (threadIdx.x == 0) {
+      N.totals[f] = int64_t(total);
       // closing offset of level f: its element total after its lists (level f+1's lists = E_f)
-      if (f >= 1) N.offsets[f - 1][N.totals[f - 1]] = int32_t(carry);
+      if (f >= 1) N.offsets[f - 1][N.totals[f - 1]] = int32_t(total);
     }
     __syncthreads();
   }
