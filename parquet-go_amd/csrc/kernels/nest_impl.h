@@ -16,7 +16,23 @@
 
 constexpr int kNestPer = kNestTile / kBlock;  // 32 consecutive slots per thread
 
-// The flag masks of a thread's 32 slots (bit j = slot j): E_f, V_l, LV (see k_nest_write).
+// Bytes of x that are >= t (t <= 128, every byte of x < 128): 0x80 in each such byte.  Subtracting
+// t from each byte with its top bit forced on never borrows across bytes.
+__device__ __forceinline__ uint32_t ge8(uint32_t x, uint32_t t) {
+  return ((x | 0x80808080u) - t * 0x01010101u) & 0x80808080u;
+}
+
+// Byte flags (0x80 per byte) -> bits 0..3.
+__device__ __forceinline__ uint32_t pack4(uint32_t m) {
+  uint32_t t = m >> 7;
+  t |= t >> 7;
+  t |= t >> 14;
+  return t & 0xfu;
+}
+
+// The flag masks of a thread's 32 slots (bit j = slot j): E_f, V_l, LV (see k_nest_write).  Four
+// slots per dword compare at once (ge8); bytes >= 128 (a corrupt stream of 8-bit levels) or levels
+// >= 128 take the per-slot path.
 __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, int64_t s0, int m,
                                            uint32_t E[kNestFlags], uint32_t V[kMaxNest], uint32_t& LV) {
   const int L = N.levels;
@@ -30,6 +46,33 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
   uint32_t dw[8], rw[8];
   __builtin_memcpy(dw, C.def_levels + s0, 32);
   __builtin_memcpy(rw, C.rep_levels + s0, 32);
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) hi |= dw[k] | rw[k];
+  const uint32_t in = m >= kNestPer ? ~0u : (1u << m) - 1;
+  if ((hi & 0x80808080u) == 0 && N.max_def < 128) {
+    const uint32_t M = uint32_t(N.max_def);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t d = dw[k], r = rw[k];
+      E[0] |= pack4(~ge8(r, 1) & 0x80808080u) << (4 * k);
+#pragma unroll
+      for (int l = 1; l <= kMaxNest; l++) {
+        if (l <= L) {
+          const uint32_t D = uint32_t(N.rep_def[l - 1]);
+          E[l] |= pack4(~ge8(r, uint32_t(l) + 1) & ge8(d, D)) << (4 * k);
+          V[l - 1] |= pack4(ge8(d, D - 1)) << (4 * k);
+        }
+      }
+      LV |= pack4(ge8(d, M) & ~ge8(d, M + 1)) << (4 * k);
+    }
+#pragma unroll
+    for (int f = 0; f < kNestFlags; f++) E[f] &= in;
+#pragma unroll
+    for (int l = 0; l < kMaxNest; l++) V[l] &= in;
+    LV &= in;
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kNestPer; j++) {
     const uint32_t d = (dw[j >> 2] >> (8 * (j & 3))) & 0xff, r = (rw[j >> 2] >> (8 * (j & 3))) & 0xff;
@@ -191,7 +234,12 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
     }
   const int lead8 = int(gbaseL & 15);
   int32_t k = lposL;
-  for (uint32_t x = EL; x; x &= x - 1) st8[lead8 + k++] = uint8_t((LV >> __builtin_ctz(x)) & 1);
+  if (EL == ~0u) {  // every slot of the thread is an element: its 32 leaf flags in order
+#pragma unroll
+    for (int j = 0; j < kNestPer; j++) st8[lead8 + k + j] = uint8_t((LV >> j) & 1);
+  } else {
+    for (uint32_t x = EL; x; x &= x - 1) st8[lead8 + k++] = uint8_t((LV >> __builtin_ctz(x)) & 1);
+  }
   __syncthreads();
   nest_flush(N.leaf_valid + gbaseL, st8, lead8, totL);
 }
