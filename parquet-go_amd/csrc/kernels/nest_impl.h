@@ -179,7 +179,10 @@ __device__ __forceinline__ void nest_flush(PQH_G T* dst, const T* lds, int lead,
 // level l present), LV (leaf non-null), so counts are popcounts and positions prefix popcounts.
 __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tiles) {
   __shared__ uint64_t wsum[4];
-  __shared__ __attribute__((aligned(16))) int32_t st32[kNestTile + 4];
+  // list offsets are staged kListPart at a time (a tile rarely starts more lists than that), which
+  // halves the LDS of a workgroup (occupancy)
+  constexpr int kListPart = kNestTile / 2;
+  __shared__ __attribute__((aligned(16))) int32_t st32[kListPart + 4];
   __shared__ __attribute__((aligned(16))) uint8_t st8[kNestTile + 16];
   const Tile t = tiles[blockIdx.x];
   const DevNest N = b.nests[t.page];
@@ -208,17 +211,20 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
   for (int l = 1; l <= kMaxNest; l++) {  // lists of level l start at the E_{l-1} slots
     if (l > L) break;
     const int lead32 = int(gbase[l - 1] & 3), lead8 = int(gbase[l - 1] & 15);
-    int32_t k = lpos[l - 1];
-    for (uint32_t x = E[l - 1]; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
-      st32[lead32 + k] = int32_t(gbase[l] + lpos[l] + __popc(E[l] & ((1u << j) - 1)));
-      st8[lead8 + k] = uint8_t((V[l - 1] >> j) & 1);
-      k++;
+    for (int p0 = 0; p0 < tot[l - 1]; p0 += kListPart) {  // uniform
+      int32_t k = lpos[l - 1];
+      for (uint32_t x = E[l - 1]; x; x &= x - 1, k++) {
+        const int j = __builtin_ctz(x);
+        if (k < p0 || k >= p0 + kListPart) continue;
+        st32[lead32 + k - p0] = int32_t(gbase[l] + lpos[l] + __popc(E[l] & ((1u << j) - 1)));
+        st8[lead8 + k - p0] = uint8_t((V[l - 1] >> j) & 1);
+      }
+      __syncthreads();
+      const int cnt = tot[l - 1] - p0 < kListPart ? tot[l - 1] - p0 : kListPart;
+      nest_flush(N.offsets[l - 1] + gbase[l - 1] + p0, st32, lead32, cnt);
+      nest_flush(N.validity[l - 1] + gbase[l - 1] + p0, st8, lead8, cnt);
+      __syncthreads();
     }
-    __syncthreads();
-    nest_flush(N.offsets[l - 1] + gbase[l - 1], st32, lead32, tot[l - 1]);
-    nest_flush(N.validity[l - 1] + gbase[l - 1], st8, lead8, tot[l - 1]);
-    __syncthreads();
   }
   // leaf validity at the E_L slots
   uint32_t EL = 0;

@@ -583,6 +583,33 @@ def test_nesting_c4_multi_tile(pq, ctx):
     assert _check_nesting(pq, ctx, datasets.c4(rows=150_000, row_groups=2)) == 6
 
 
+def test_nesting_sparse_lists(pq, ctx):
+    """Mostly null / empty lists: nest tiles starting more than half a tile of lists (the list
+    offsets are staged in parts), for one and two repetition levels."""
+    import io
+
+    import pyarrow as pa
+    import pyarrow.parquet as pqa
+
+    rng = np.random.default_rng(11)
+    n = 40000
+
+    def row():
+        u = rng.random()
+        if u < 0.45:
+            return None
+        if u < 0.9:
+            return []
+        return [int(rng.integers(0, 1000)) for _ in range(rng.poisson(2))]
+
+    a = [row() for _ in range(n)]
+    b = [None if rng.random() < 0.5 else [row() for _ in range(rng.poisson(0.5))] for _ in range(n)]
+    t = pa.table({"a": pa.array(a, pa.list_(pa.int64())), "b": pa.array(b, pa.list_(pa.list_(pa.int64())))})
+    buf = io.BytesIO()
+    pqa.write_table(t, buf, row_group_size=n, data_page_size=1 << 20, use_dictionary=False)
+    assert _check_nesting(pq, ctx, buf.getvalue()) == 2
+
+
 def test_nesting_deep_lists(pq, ctx):
     """list<list<int32>> and list<struct<list<string>>> from pyarrow (max_rep 2)."""
     import io
