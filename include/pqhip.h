@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 4
+#define PQH_ABI_VERSION 5
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -159,6 +159,21 @@ typedef struct pqh_page {
   int32_t chunk;                  /* index of the owning pqh_chunk */
   int32_t reserved;
 } pqh_page;
+
+/* Device-side decompression: where one page's source bytes lie and how its image
+ * is rebuilt in HBM (pqh_file_load_ex with PQH_LOAD_DEVICE_SNAPPY).  The image of page i of the host
+ * batch is codec page i. */
+typedef struct pqh_codec_page {
+  int64_t src_offset;   /* page bytes in the source payload: the compressed block (SNAPPY, after the
+                           raw prefix), or the finished image (codec 0: copied) */
+  int64_t image_offset; /* == pqh_page.image_offset: where the image goes in the image buffer */
+  int32_t src_len;      /* source bytes, raw prefix included */
+  int32_t image_len;    /* == pqh_page.image_len: the header's uncompressed page size */
+  int32_t raw_len;      /* leading bytes stored uncompressed (DataPageV2 levels, page_v2.go:116-125) */
+  int32_t codec;        /* PQH_CODEC_SNAPPY, or PQH_CODEC_UNCOMPRESSED for a plain copy */
+  int32_t chunk;        /* owning chunk in the host batch */
+  int32_t reserved;
+} pqh_codec_page;
 
 /* A column chunk: a contiguous range of pages; a dictionary page, if any, comes first
  * (chunk_reader.go:195-227). */
@@ -378,6 +393,24 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
  * batch i+1's copy with batch i's decode.  A repeat run's copy waits for the previous decode of the
  * same batch.  Asynchronous: pqh_batch_sync / pqh_sync wait. */
 int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out);
+/* Device codecs: load with PQH_LOAD_DEVICE_SNAPPY and the pages of SNAPPY chunks stay compressed in
+ * the host batch's payload (the SOURCE payload); pqh_host_batch_image_bytes is the size of the page
+ * images they rebuild.  Batches made from such a host batch (pqh_batch_create_from_host /
+ * pqh_batch_create_staged) upload (or stage) the source payload and begin every run with k_snappy
+ * (one wave per page) rebuilding the images in HBM.  A chunk whose page fails to decompress, or
+ * whose decoded size differs from the header, reports PQH_ERR_DECOMPRESS like the host walker
+ * (readPageBlock / newBlockReader, compress.go:131-152): it fails the whole chunk unless a page
+ * before it already failed on the host. */
+#define PQH_LOAD_DEVICE_SNAPPY 1u
+int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
+                     int32_t validate_crc, uint32_t flags, pqh_host_batch** out);
+int32_t pqh_host_batch_num_codec_pages(const pqh_host_batch* hb);
+const pqh_codec_page* pqh_host_batch_codec_pages(const pqh_host_batch* hb);
+int64_t pqh_host_batch_image_bytes(const pqh_host_batch* hb);
+/* Decompress pages on the device, synchronously (the k_snappy step of a batch run, on its own):
+ * d_src / d_dst as described by `pages` (host array), status[i] = PQH_OK or PQH_ERR_DECOMPRESS. */
+int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_pages, const void* d_src,
+                         void* d_dst, int32_t* status);
 int pqh_batch_run_staged(pqh_batch* batch);
 
 #ifdef __cplusplus

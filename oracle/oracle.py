@@ -387,6 +387,78 @@ def decompress(codec, data, uncompressed_size):
     return pa.decompress(bytes(data), decompressed_size=uncompressed_size, codec=name, asbytes=True)
 
 
+class SnappyCorrupt(Exception):
+    pass
+
+
+def snappy_decode(src):
+    """github.com/golang/snappy v0.0.4 Decode (decode.go: decodedLen + decode), restated: the
+    reference's SNAPPY codec (compress.go:43-49).  Returns the block or raises SnappyCorrupt
+    (ErrCorrupt / ErrTooLarge).  Pinned against pyarrow's snappy on valid blocks
+    (tests/test_codec_oracle.py)."""
+    src = bytes(src)
+    # decodedLen: binary.Uvarint (n <= 0 on a missing terminator or a 64-bit overflow)
+    v, shift, n = 0, 0, 0
+    for i, c in enumerate(src[:10]):
+        if i == 9 and c > 1:
+            raise SnappyCorrupt("uvarint overflow")
+        v |= (c & 0x7F) << shift
+        shift += 7
+        if c < 0x80:
+            n = i + 1
+            break
+    if n == 0 or v > 0xFFFFFFFF:
+        raise SnappyCorrupt("decodedLen")
+    dst = bytearray(v)
+    d, s = 0, n
+    while s < len(src):
+        tag = src[s]
+        kind = tag & 3
+        if kind == 0:
+            x = tag >> 2
+            if x < 60:
+                s += 1
+            else:
+                k = x - 59
+                s += 1 + k
+                if s > len(src):
+                    raise SnappyCorrupt("literal header")
+                x = int.from_bytes(src[s - k:s], "little")
+            length = x + 1
+            if length > len(dst) - d or length > len(src) - s:
+                raise SnappyCorrupt("literal")
+            dst[d:d + length] = src[s:s + length]
+            d += length
+            s += length
+            continue
+        if kind == 1:
+            s += 2
+            if s > len(src):
+                raise SnappyCorrupt("copy1 header")
+            length = 4 + ((tag >> 2) & 7)
+            offset = ((tag & 0xE0) << 3) | src[s - 1]
+        elif kind == 2:
+            s += 3
+            if s > len(src):
+                raise SnappyCorrupt("copy2 header")
+            length = 1 + (tag >> 2)
+            offset = src[s - 2] | (src[s - 1] << 8)
+        else:
+            s += 5
+            if s > len(src):
+                raise SnappyCorrupt("copy4 header")
+            length = 1 + (tag >> 2)
+            offset = int.from_bytes(src[s - 4:s], "little")
+        if offset <= 0 or d < offset or length > len(dst) - d:
+            raise SnappyCorrupt("copy")
+        for i in range(length):  # forward, overlap-safe
+            dst[d + i] = dst[d + i - offset]
+        d += length
+    if d != len(dst):
+        raise SnappyCorrupt("short")
+    return bytes(dst)
+
+
 class Page:
     def __init__(self, page_type, num_values, encoding, def_len, rep_len, image):
         self.page_type = page_type

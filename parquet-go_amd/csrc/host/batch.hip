@@ -64,8 +64,8 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_ba_wspec",   "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
-                              "k_delta_fused", "k_ba_wstitch", "k_ba_wemit"};
-constexpr int kNumKernels = 22;
+                              "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy"};
+constexpr int kNumKernels = 23;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -213,6 +213,14 @@ struct pqh_batch {
   size_t expand_lds = 0;            // dynamic LDS of k_expand: largest staged dictionary
   const uint8_t* d_payload = nullptr;
   void* owned_payload = nullptr;
+  // device codecs: source payload (compressed pages) and the page table k_snappy rebuilds the
+  // images (owned_payload) from at the start of every run
+  void* d_src = nullptr;
+  size_t src_bytes = 0;
+  pqh_codec_page* d_codec = nullptr;
+  int32_t codec_n = 0;
+  int32_t* d_codec_status = nullptr;
+  std::vector<int32_t> codec_status;  // host copy after sync (per page)
   int64_t payload_bytes = 0;
   void* h_staged = nullptr;           // staged batches: pinned host page images
   size_t staged_bytes = 0;
@@ -269,12 +277,15 @@ void free_batch(pqh_batch* b) {
   for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
   for (void* p : b->allocations) hipFree(p);
   if (b->owned_payload) hipFree(b->owned_payload);
+  if (b->d_src) hipFree(b->d_src);
   if (b->h_staged) hipHostFree(b->h_staged);
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
   if (b->ev_done) hipEventDestroy(b->ev_done);
   if (b->gexec) hipGraphExecDestroy(b->gexec);
   if (b->graph) hipGraphDestroy(b->graph);
 }
+
+int32_t codec_fail_page(const pqh_batch* b, int32_t chunk);
 
 int dalloc(pqh_batch* b, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
@@ -808,9 +819,14 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     }
     return e;
   };
-  hipError_t e;
+  hipError_t e = hipSuccess;
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
-  e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
+  if (b->codec_n)  // device codecs: the page images first
+    e = timed(22, b->codec_n, s, [&](hipStream_t st) {
+      return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
+                           static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
+    });
+  if (e == hipSuccess) e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
   // page mode: every delta page gets its init errors now and is chased, decoded and walked after
   // the value scan; tile mode: speculative walk + exact walk now, tiles after the scan
   int32_t ni = b->delta_page_mode ? b->delta_fused_pages : 0;
@@ -941,6 +957,9 @@ int pqh_batch_sync(pqh_batch* b) {
   b->nest_totals.assign(b->nests.size() * kNestFlags, 0);
   if (!b->nests.empty())
     HIP_TRY(ctx, bounce_d2h(ctx, b->nest_totals.data(), b->d_ntotals, sizeof(int64_t) * b->nest_totals.size()));
+  b->codec_status.assign(size_t(b->codec_n), PQH_OK);
+  if (b->codec_n)
+    HIP_TRY(ctx, bounce_d2h(ctx, b->codec_status.data(), b->d_codec_status, sizeof(int32_t) * size_t(b->codec_n)));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   // The per-page results bound every later copy of the outputs (pqh_batch_chunk_out): refuse
   // results that would reach past the planned output buffers instead of handing them out.
@@ -1125,6 +1144,11 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   const DevChunk& C = b->hchunks[size_t(P.chunk)];
   out->value_size = C.value_size;
   if (P.page_type == PQH_DICTIONARY_PAGE) return set_err(ctx, PQH_ERR_ARG, "dictionary pages have no readValues");
+  if (codec_fail_page(b, P.chunk) >= 0) {  // readChunk failed: no page of the chunk is ever read
+    out->status = PQH_ERR_DECOMPRESS;
+    out->phase = PQH_PHASE_LOAD;
+    return PQH_OK;
+  }
   const int64_t n = std::max(0, P.num_values);
   // dataPageReaderV1/V2.readValues: size is clipped to the values left in the page
   const int64_t s0 = std::min(first, n), s1 = std::min(n, s0 + count);
@@ -1197,6 +1221,29 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   return PQH_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Device codecs: the page of `chunk` whose image failed to decompress, if it decides the chunk's
+// result (-1 otherwise).  The reference walks a chunk's pages in order (readChunk) and decompresses
+// each one before looking at the next header, so the failing page wins over walker errors after it
+// (the host walker stopped there: host_status) and over every decode error; a page-level load error
+// found by the planner at or before it (P.host_err of a chunk the walker finished) wins instead.
+int32_t codec_fail_page(const pqh_batch* b, int32_t chunk) {
+  if (b->codec_status.empty()) return -1;
+  const DevChunk& D = b->hchunks[size_t(chunk)];
+  const bool walker_failed = b->chunks[size_t(chunk)].host_status != PQH_OK;
+  for (int32_t i = 0; i < D.num_pages; i++) {
+    const int32_t p = D.first_page + i;
+    if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) return p;
+    if (!walker_failed && b->hpages[size_t(p)].host_err != kNoError) return -1;
+  }
+  return -1;
+}
+}  // namespace
+
+extern "C" {
+
 int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   if (!b || chunk < 0 || size_t(chunk) >= b->chunks.size()) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad chunk");
   if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
@@ -1225,6 +1272,13 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
     if (b->hpages[size_t(p)].page_type != PQH_DICTIONARY_PAGE) nn += S.nn;
   }
   out->num_non_null = nn;
+  const int32_t k = codec_fail_page(b, chunk);
+  if (k >= 0) {  // readPageBlock failed at page k: the chunk fails there, before any decode
+    out->status = PQH_ERR_DECOMPRESS;
+    out->error_page = k;
+    out->error_phase = PQH_PHASE_LOAD;
+    out->error_index = 0;
+  }
   return PQH_OK;
 }
 
@@ -1295,10 +1349,67 @@ void pqh_batch_destroy(pqh_batch* b) {
   delete b;
 }
 
+}  // extern "C"
+
+namespace {
+// Device codecs: the image buffer (zeroed, with its pad) the decode reads, planned over the host
+// batch's tables; the source payload at d_src (already in HBM or uploaded by the caller) is
+// decompressed into it at the start of every run.
+int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_batch** out) {
+  void* img = nullptr;
+  const size_t ibytes = size_t(hb->image_bytes) + PQH_PAYLOAD_PAD;
+  HIP_TRY(ctx, hipMalloc(&img, ibytes));
+  hipError_t e = hipMemsetAsync(img, 0, ibytes, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    hipFree(img);
+    return set_err(ctx, PQH_ERR_HIP, std::string("image buffer: ") + hipGetErrorString(e));
+  }
+  int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
+                            int32_t(hb->pages.size()), img, hb->image_bytes, out);
+  if (rc) {
+    hipFree(img);
+    return rc;
+  }
+  pqh_batch* b = *out;
+  b->owned_payload = img;
+  b->d_src = d_src;
+  b->src_bytes = hb->payload.size();
+  b->codec_n = int32_t(hb->codec_pages.size());
+  if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec), sizeof(pqh_codec_page) * size_t(b->codec_n))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec_status), sizeof(int32_t) * size_t(b->codec_n)))) {
+    pqh_batch_destroy(b);
+    *out = nullptr;
+    return rc;
+  }
+  e = bounce_h2d(ctx, b->d_codec, hb->codec_pages.data(), sizeof(pqh_codec_page) * size_t(b->codec_n));
+  if (e != hipSuccess) {
+    pqh_batch_destroy(b);
+    *out = nullptr;
+    return set_err(ctx, PQH_ERR_HIP, std::string("codec pages: ") + hipGetErrorString(e));
+  }
+  return PQH_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** out) {
   *out = nullptr;
   if (!ctx || !hb) return set_err(ctx, PQH_ERR_ARG, "null argument");
   hipSetDevice(ctx->device);
+  if (!hb->codec_pages.empty()) {  // source payload to HBM; images rebuilt by every run
+    void* src = nullptr;
+    HIP_TRY(ctx, hipMalloc(&src, hb->payload.size()));
+    hipError_t e = bounce_h2d(ctx, src, hb->payload.data(), hb->payload.size());
+    if (e != hipSuccess) {
+      hipFree(src);
+      return set_err(ctx, PQH_ERR_HIP, std::string("source upload: ") + hipGetErrorString(e));
+    }
+    const int rc = create_codec_batch(ctx, hb, src, out);
+    if (rc) hipFree(src);
+    return rc;
+  }
   void* d = nullptr;
   const size_t bytes = hb->payload.size();
   HIP_TRY(ctx, hipMalloc(&d, bytes ? bytes : 16));
@@ -1337,15 +1448,17 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
     hipHostFree(h);
     return set_err(ctx, PQH_ERR_HIP, std::string("staged payload: ") + hipGetErrorString(e));
   }
-  int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
-                            int32_t(hb->pages.size()), d, hb->payload_bytes, out);
+  int rc = hb->codec_pages.empty() ? pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()),
+                                                       hb->pages.data(), int32_t(hb->pages.size()), d,
+                                                       hb->payload_bytes, out)
+                                    : create_codec_batch(ctx, hb, d, out);
   if (rc) {
     hipFree(d);
     hipHostFree(h);
     return rc;
   }
   pqh_batch* b = *out;
-  b->owned_payload = d;
+  if (hb->codec_pages.empty()) b->owned_payload = d;  // else: d is the source buffer (b->d_src)
   b->h_staged = h;
   b->staged_bytes = bytes;
   if (hipEventCreateWithFlags(&b->ev_copied, hipEventDisableTiming) != hipSuccess ||
@@ -1357,6 +1470,26 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
   return PQH_OK;
 }
 
+int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_pages, const void* d_src,
+                         void* d_dst, int32_t* status) {
+  if (!ctx || num_pages < 0 || (num_pages && (!pages || !status))) return set_err(ctx, PQH_ERR_ARG, "bad arguments");
+  if (num_pages == 0) return PQH_OK;
+  hipSetDevice(ctx->device);
+  pqh_codec_page* dp = nullptr;
+  int32_t* ds = nullptr;
+  hipError_t e = hipMalloc(&dp, sizeof(pqh_codec_page) * size_t(num_pages));
+  if (e == hipSuccess) e = hipMalloc(&ds, sizeof(int32_t) * size_t(num_pages));
+  if (e == hipSuccess) e = bounce_h2d(ctx, dp, pages, sizeof(pqh_codec_page) * size_t(num_pages));
+  if (e == hipSuccess)
+    e = launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
+  if (e == hipSuccess) e = bounce_d2h(ctx, status, ds, sizeof(int32_t) * size_t(num_pages));
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (dp) hipFree(dp);
+  if (ds) hipFree(ds);
+  if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("pqh_decompress_pages: ") + hipGetErrorString(e));
+  return PQH_OK;
+}
+
 int pqh_batch_run_staged(pqh_batch* b) {
   if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
   pqh_ctx* ctx = b->ctx;
@@ -1364,8 +1497,9 @@ int pqh_batch_run_staged(pqh_batch* b) {
   hipSetDevice(ctx->device);
   // the copy must not overwrite page images a previous decode of this batch still reads
   if (b->done_recorded) HIP_TRY(ctx, hipStreamWaitEvent(ctx->copy_stream, b->ev_done, 0));
-  if (b->staged_bytes)
-    HIP_TRY(ctx, hipMemcpyAsync(b->owned_payload, b->h_staged, b->staged_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+  if (b->staged_bytes)  // the page images, or with device codecs the source bytes
+    HIP_TRY(ctx, hipMemcpyAsync(b->codec_n ? b->d_src : b->owned_payload, b->h_staged, b->staged_bytes,
+                                hipMemcpyHostToDevice, ctx->copy_stream));
   HIP_TRY(ctx, hipEventRecord(b->ev_copied, ctx->copy_stream));
   HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->ev_copied, 0));
   int rc = pqh_batch_run(b);

@@ -320,10 +320,56 @@ bool parse_page_header(TReader& r, PageHdr& h) {
 
 struct ChunkWork {
   pqh_chunk chunk;
-  std::vector<pqh_page> pages;  // image_offset relative to `bytes`
+  std::vector<pqh_page> pages;  // image_offset relative to `bytes` (device codecs: to the image space)
   std::vector<uint8_t> bytes;
   double seconds = 0;
+  bool device_codecs = false;   // bytes = source bytes; images rebuilt on the device
+  std::vector<pqh_codec_page> cps;
+  int64_t image = 0;            // device codecs: image space used so far
 };
+
+// Device codecs: the page's source bytes (raw prefix a, then b) go to `bytes`; its image (of
+// image_len bytes) gets a place in the image space.
+void append_source(ChunkWork& w, pqh_page& pg, const uint8_t* a, size_t na, const uint8_t* b, size_t nb,
+                   int64_t image_len, int32_t codec) {
+  const size_t off = (w.bytes.size() + 63) & ~size_t(63);
+  w.bytes.resize(off + na + nb);
+  if (na) memcpy(w.bytes.data() + off, a, na);
+  if (nb) memcpy(w.bytes.data() + off + na, b, nb);
+  const int64_t img = (w.image + 63) & ~int64_t(63);
+  w.image = img + image_len;
+  pg.image_offset = img;
+  pg.image_len = int32_t(image_len);
+  pqh_codec_page cp;
+  memset(&cp, 0, sizeof(cp));
+  cp.src_offset = int64_t(off);
+  cp.image_offset = img;
+  cp.src_len = int32_t(na + nb);
+  cp.image_len = int32_t(image_len);
+  cp.raw_len = codec == PQH_CODEC_SNAPPY ? int32_t(na) : 0;
+  cp.codec = codec;
+  w.cps.push_back(cp);
+}
+
+// The decoded length a snappy block announces (its uvarint header), -1 if malformed.
+int64_t snappy_announced(const uint8_t* p, size_t n) {
+  uint64_t v = 0;
+  for (size_t i = 0; i < n && i < 10; i++) {
+    if (i == 9 && p[i] > 1) return -1;
+    v |= uint64_t(p[i] & 0x7f) << (7 * i);
+    if (p[i] < 0x80) return v > 0xffffffffull ? -1 : int64_t(v);
+  }
+  return -1;
+}
+
+// Device codecs: can a SNAPPY block of n bytes decode to exactly `expected` bytes?  (A wrong or
+// malformed announced length, or more output than the format can encode in n bytes, fails exactly
+// as the host decode would: readPageBlock's ErrCorrupt / size check, compress.go:131-152.)
+bool snappy_plausible(const uint8_t* p, size_t n, int64_t expected) {
+  if (expected < 0) return false;
+  const int64_t v = snappy_announced(p, n);
+  return v == expected && v <= 22 * int64_t(n) + 64;  // a 3-byte copy element yields <= 64 bytes
+}
 
 void append_image(ChunkWork& w, pqh_page& pg, const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
   size_t off = (w.bytes.size() + 63) & ~size_t(63);
@@ -369,13 +415,26 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
     pg.num_values = h.num_values;
     pg.encoding = h.encoding;
     pg.chunk = 0;
+    const bool dev = w.device_codecs && m.codec == PQH_CODEC_SNAPPY;
+    // whole-block pages (V1 data / dictionary): decompressed here, or left for the device
+    auto whole_block = [&]() -> bool {
+      if (dev) {
+        if (!snappy_plausible(block, size_t(got), h.usize)) return false;
+        append_source(w, pg, block, 0, block, size_t(got), h.usize, PQH_CODEC_SNAPPY);
+        w.cps.back().raw_len = 0;
+        return true;
+      }
+      if (!decompress_block(m.codec, block, size_t(got), size_t(h.usize), out) || int64_t(out.size()) != h.usize)
+        return false;
+      if (w.device_codecs) append_source(w, pg, out.data(), out.size(), nullptr, 0, int64_t(out.size()), PQH_CODEC_UNCOMPRESSED);
+      else append_image(w, pg, out.data(), out.size(), nullptr, 0);
+      return true;
+    };
     if (h.type == PQH_DICTIONARY_PAGE) {
       if (have_dict) return fail(PQH_ERR_DICT_PAGE);
       if (!h.has_dict) return fail(PQH_ERR_PAGE_HEADER);
       if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
-      if (!decompress_block(m.codec, block, size_t(got), size_t(h.usize), out) || int64_t(out.size()) != h.usize)
-        return fail(PQH_ERR_DECOMPRESS);
-      append_image(w, pg, out.data(), out.size(), nullptr, 0);
+      if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
       w.pages.push_back(pg);
       have_dict = true;
       if (m.has_dict_offset && m.dict_page_offset != pos) {  // seek to DataPageOffset
@@ -387,9 +446,7 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
     if (h.type == PQH_DATA_PAGE) {
       if (!h.has_dp) return fail(PQH_ERR_PAGE_HEADER);
       if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
-      if (!decompress_block(m.codec, block, size_t(got), size_t(h.usize), out) || int64_t(out.size()) != h.usize)
-        return fail(PQH_ERR_DECOMPRESS);
-      append_image(w, pg, out.data(), out.size(), nullptr, 0);
+      if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
     } else if (h.type == PQH_DATA_PAGE_V2) {
       if (!h.has_v2) return fail(PQH_ERR_PAGE_HEADER);
       if (h.num_values < 0 || h.rep_len < 0 || h.def_len < 0) return fail(PQH_ERR_PAGE_HEADER);
@@ -397,10 +454,20 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if (levels > got) return fail(PQH_ERR_PAGE_HEADER);  // slice out of range in the reference
       if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
       // the values section is decompressed regardless of is_compressed (page_v2.go:125)
-      if (!decompress_block(m.codec, block + levels, size_t(got - levels), size_t(h.usize - levels), out) ||
-          int64_t(out.size()) != int64_t(h.usize) - levels)
-        return fail(PQH_ERR_DECOMPRESS);
-      append_image(w, pg, block, size_t(levels), out.data(), out.size());
+      if (dev) {
+        if (!snappy_plausible(block + levels, size_t(got - levels), int64_t(h.usize) - levels))
+          return fail(PQH_ERR_DECOMPRESS);
+        append_source(w, pg, block, size_t(levels), block + levels, size_t(got - levels), h.usize, PQH_CODEC_SNAPPY);
+      } else {
+        if (!decompress_block(m.codec, block + levels, size_t(got - levels), size_t(h.usize - levels), out) ||
+            int64_t(out.size()) != int64_t(h.usize) - levels)
+          return fail(PQH_ERR_DECOMPRESS);
+        if (w.device_codecs)
+          append_source(w, pg, block, size_t(levels), out.data(), out.size(), int64_t(levels) + int64_t(out.size()),
+                        PQH_CODEC_UNCOMPRESSED);
+        else
+          append_image(w, pg, block, size_t(levels), out.data(), out.size());
+      }
       pg.def_levels_byte_length = h.def_len;
       pg.rep_levels_byte_length = h.rep_len;
     } else {
@@ -508,6 +575,11 @@ int pqh_file_column(const pqh_file* f, int32_t column, pqh_column* out, char* pa
 
 int pqh_file_load(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
                   int32_t validate_crc, pqh_host_batch** out) {
+  return pqh_file_load_ex(f, rg_begin, rg_end, columns, num_columns, validate_crc, 0, out);
+}
+
+int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
+                     int32_t validate_crc, uint32_t flags, pqh_host_batch** out) {
   *out = nullptr;
   if (!f) return PQH_ERR_ARG;
   if (rg_begin < 0 || rg_end > int32_t(f->rgs.size()) || rg_begin > rg_end)
@@ -516,6 +588,16 @@ int pqh_file_load(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* 
     if (columns[i] < 0 || size_t(columns[i]) >= f->columns.size()) return file_error(f, PQH_ERR_ARG, "bad column");
   const int64_t nchunks = int64_t(rg_end - rg_begin) * num_columns;
   std::vector<ChunkWork> work(static_cast<size_t>(nchunks));
+  // device codecs only when some selected chunk is SNAPPY (otherwise the plain layout)
+  bool dev = false;
+  if (flags & PQH_LOAD_DEVICE_SNAPPY)
+    for (int32_t rg = rg_begin; rg < rg_end && !dev; rg++)
+      for (int32_t i = 0; i < num_columns && !dev; i++) {
+        const RowGroupMeta& g = f->rgs[size_t(rg)];
+        dev = size_t(columns[i]) < g.chunks.size() && g.chunks[size_t(columns[i])].has_meta &&
+              g.chunks[size_t(columns[i])].codec == PQH_CODEC_SNAPPY;
+      }
+  for (auto& w : work) w.device_codecs = dev;
   std::atomic<int64_t> next{0};
   auto worker = [&]() {
     for (;;) {
@@ -545,28 +627,43 @@ int pqh_file_load(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* 
   size_t total = 0;
   for (auto& w : work) total = ((total + 63) & ~size_t(63)) + w.bytes.size();
   hb->payload.reserve(total + PQH_PAYLOAD_PAD);
+  int64_t image = 0;
   for (auto& w : work) {
     size_t base = (hb->payload.size() + 63) & ~size_t(63);
     hb->payload.resize(base);
     hb->payload.insert(hb->payload.end(), w.bytes.begin(), w.bytes.end());
+    const int64_t ibase = dev ? (image + 63) & ~int64_t(63) : int64_t(base);
     pqh_chunk c = w.chunk;
     c.first_page = int32_t(hb->pages.size());
     c.num_pages = int32_t(w.pages.size());
     const int32_t ci = int32_t(hb->chunks.size());
-    for (auto pg : w.pages) {
-      pg.image_offset += int64_t(base);
+    for (size_t i = 0; i < w.pages.size(); i++) {
+      pqh_page pg = w.pages[i];
+      pg.image_offset += ibase;
       pg.chunk = ci;
       hb->pages.push_back(pg);
+      if (dev) {
+        pqh_codec_page cp = w.cps[i];
+        cp.src_offset += int64_t(base);
+        cp.image_offset += ibase;
+        cp.chunk = ci;
+        hb->codec_pages.push_back(cp);
+      }
     }
+    if (dev) image = ibase + w.image;
     hb->chunks.push_back(c);
     hb->decompress_seconds += w.seconds;
   }
+  hb->image_bytes = dev ? image : 0;
   hb->payload_bytes = int64_t(hb->payload.size());
   hb->payload.resize(hb->payload.size() + PQH_PAYLOAD_PAD, 0);
   *out = hb;
   return PQH_OK;
 }
 
+int32_t pqh_host_batch_num_codec_pages(const pqh_host_batch* hb) { return int32_t(hb->codec_pages.size()); }
+const pqh_codec_page* pqh_host_batch_codec_pages(const pqh_host_batch* hb) { return hb->codec_pages.data(); }
+int64_t pqh_host_batch_image_bytes(const pqh_host_batch* hb) { return hb->image_bytes; }
 int32_t pqh_host_batch_num_chunks(const pqh_host_batch* hb) { return int32_t(hb->chunks.size()); }
 int32_t pqh_host_batch_num_pages(const pqh_host_batch* hb) { return int32_t(hb->pages.size()); }
 const pqh_chunk* pqh_host_batch_chunks(const pqh_host_batch* hb) { return hb->chunks.data(); }

@@ -13,6 +13,11 @@ struct pqh_host_batch {
   std::vector<uint8_t> payload;  // page images, 8-byte aligned, PQH_PAYLOAD_PAD zero bytes at the end
   int64_t payload_bytes = 0;     // without the pad
   double decompress_seconds = 0;
+  // device codecs (PQH_LOAD_DEVICE_SNAPPY): payload holds the SOURCE bytes of every page, and
+  // codec_pages[i] rebuilds page i's image at pages[i].image_offset of an image buffer of
+  // image_bytes (+ PQH_PAYLOAD_PAD)
+  std::vector<pqh_codec_page> codec_pages;
+  int64_t image_bytes = 0;
 };
 
 namespace pqhip {

@@ -1005,6 +1005,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 #include "delta_impl.h"
 #include "bytearray_impl.h"
 #include "nest_impl.h"
+#include "snappy_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
@@ -1047,6 +1048,13 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s) {
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_expand, dim3(n), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
+                         hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, pages, src, dst, status);
   return hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "decode.h"
+#include "pqhip.h"
 
 namespace pqhip {
 
@@ -27,6 +28,9 @@ struct DevBatch {
 };
 
 hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
+// Device codecs: one wave per page rebuilding its image from its (SNAPPY) source bytes.
+hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
+                         hipStream_t s);
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.

@@ -65,6 +65,14 @@ class PageResult(ctypes.Structure):
                 ("value_offset", i64), ("level_offset", i64)]
 
 
+class CodecPage(ctypes.Structure):
+    _fields_ = [("src_offset", i64), ("image_offset", i64), ("src_len", i32), ("image_len", i32),
+                ("raw_len", i32), ("codec", i32), ("chunk", i32), ("reserved", i32)]
+
+
+LOAD_DEVICE_SNAPPY = 1
+
+
 class SchemaElement(ctypes.Structure):
     _fields_ = [("physical_type", i32), ("type_length", i32), ("repetition", i32), ("num_children", i32),
                 ("column", i32), ("max_def", i32), ("max_rep", i32), ("reserved", i32)]
@@ -81,7 +89,7 @@ class KernelStat(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 4  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 5  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -124,6 +132,12 @@ PROTOTYPES = [
     ("pqh_file_num_schema_elements", i32, [vp]),
     ("pqh_file_schema_element", ctypes.c_int, [vp, i32, ctypes.POINTER(SchemaElement), ctypes.c_char_p, i32]),
     ("pqh_file_load", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]),
+    ("pqh_file_load_ex", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.c_uint32,
+                                        ctypes.POINTER(vp)]),
+    ("pqh_host_batch_num_codec_pages", i32, [vp]),
+    ("pqh_host_batch_codec_pages", ctypes.POINTER(CodecPage), [vp]),
+    ("pqh_host_batch_image_bytes", i64, [vp]),
+    ("pqh_decompress_pages", ctypes.c_int, [vp, ctypes.POINTER(CodecPage), i32, vp, vp, ctypes.POINTER(i32)]),
     ("pqh_host_batch_num_chunks", i32, [vp]),
     ("pqh_host_batch_num_pages", i32, [vp]),
     ("pqh_host_batch_chunks", ctypes.POINTER(Chunk), [vp]),
@@ -208,6 +222,13 @@ class Context:
         """Asynchronous copy on the context stream from pqh_host_alloc memory."""
         self.check(self.L.pqh_memcpy_h2d_pinned_async(self.h, dst, pinned_ptr, n))
 
+    def decompress_pages(self, pages, d_src, d_dst):
+        """k_snappy on its own: rebuild `pages` (CodecPage list) from d_src into d_dst; statuses."""
+        arr = (CodecPage * max(1, len(pages)))(*pages)
+        st = (i32 * max(1, len(pages)))()
+        self.check(self.L.pqh_decompress_pages(self.h, arr, len(pages), d_src, d_dst, st))
+        return [st[i] for i in range(len(pages))]
+
     def d2h_array(self, src, n, dtype=np.uint8):
         out = np.empty(n, dtype=dtype)
         nbytes = out.nbytes
@@ -250,6 +271,16 @@ class HostBatch:
     def pages(self):
         p = self.L.pqh_host_batch_pages(self.h)
         return [p[i] for i in range(self.num_pages)]
+
+    def codec_pages(self):
+        n = self.L.pqh_host_batch_num_codec_pages(self.h)
+        p = self.L.pqh_host_batch_codec_pages(self.h)
+        return [p[i] for i in range(n)]
+
+    @property
+    def image_bytes(self):
+        """Device codecs: bytes of the page images the source payload decompresses to (else 0)."""
+        return self.L.pqh_host_batch_image_bytes(self.h)
 
     def payload(self):
         n = self.L.pqh_host_batch_payload_bytes(self.h)
@@ -326,10 +357,13 @@ class File:
             out.append((buf.value.decode(), e))
         return out
 
-    def load(self, rg_begin, rg_end, columns, validate_crc=False):
+    def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False):
+        """Walk the pages of `columns` in row groups [rg_begin, rg_end).  device_snappy: SNAPPY
+        pages stay compressed (the batch decompresses them on the device, k_snappy)."""
         cols = (i32 * len(columns))(*columns)
         h = vp()
-        rc = self.L.pqh_file_load(self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc), ctypes.byref(h))
+        rc = self.L.pqh_file_load_ex(self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc),
+                                     LOAD_DEVICE_SNAPPY if device_snappy else 0, ctypes.byref(h))
         if rc != OK:
             raise PqhError(rc, (self.L.pqh_file_error(self.h) or b"").decode())
         return HostBatch(self.L, h)

@@ -1,0 +1,94 @@
+"""Device-codec groundwork on the CPU.
+
+* oracle.snappy_decode (a restatement of github.com/golang/snappy v0.0.4 decode.go, the
+  reference's SNAPPY codec at compress.go:43-49) pinned against pyarrow's snappy on valid blocks,
+  and its corruption rules on hand-built blocks;
+* the host walker's device-codec layout (pqh_file_load_ex + PQH_LOAD_DEVICE_SNAPPY): every page's
+  source bytes rebuild exactly the image the host-decompressing walker produces, and the checks the
+  walker still makes itself (announced length, impossible expansion) fail the chunk as before.
+"""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import fixtures
+from oracle import oracle as O
+from snappy_blocks import literal, copy1, copy2, copy4, block, sample_blocks
+
+
+def test_snappy_oracle_matches_pyarrow():
+    for raw in sample_blocks():
+        comp = pa.compress(raw, codec="snappy", asbytes=True)
+        assert O.snappy_decode(comp) == raw
+
+
+def test_snappy_oracle_hand_built():
+    # literals of every length-header size, copies of every kind, overlapping copies
+    raw = b"abcdefgh" * 3
+    blk = block(len(raw) + 8 + 70000 + 5, literal(raw) + copy1(8, 8) + literal(b"z" * 70000) + copy2(5, 1))
+    out = O.snappy_decode(blk)
+    assert out == raw + raw[-8:] + b"z" * 70000 + b"z" * 5
+    assert O.snappy_decode(block(10, literal(b"ab") + copy4(8, 2))) == b"ab" * 5
+    for bad in (block(5, literal(b"abc")),                  # short output
+                block(3, literal(b"abcd")),                 # literal past the output
+                block(6, literal(b"ab") + copy2(4, 3)),     # offset before the output start
+                block(6, literal(b"ab") + copy2(4, 0)),     # offset 0
+                block(4, literal(b"ab"))[:-1],              # literal past the input
+                b"\xff" * 11,                               # uvarint without a terminator
+                b"\x80\x80\x80\x80\x80\x80\x80\x80\x80\x02"):  # 64-bit overflow
+        with pytest.raises(O.SnappyCorrupt):
+            O.snappy_decode(bad)
+    # a non-canonical (padded) uvarint is accepted by binary.Uvarint
+    assert O.snappy_decode(b"\x83\x80\x00" + literal(b"xyz")) == b"xyz"
+
+
+@pytest.mark.parametrize("v2", [False, True])
+def test_device_codec_layout(pq, v2):
+    data = fixtures.flat_all_types(n=6000, v2=v2, codec=O.SNAPPY, page=16 * 1024, rows_per_group=3000)
+    f = pq.native.File(data)
+    cols = list(range(len(f.columns())))
+    host = f.load(0, f.num_row_groups, cols)
+    dev = f.load(0, f.num_row_groups, cols, device_snappy=True)
+    hp, dp, cps = host.pages(), dev.pages(), dev.codec_pages()
+    assert len(hp) == len(dp) == len(cps) and dev.image_bytes > 0
+    hpay, src = host.payload(), dev.payload()
+    snappy_pages = 0
+    for a, b, c in zip(hp, dp, cps):
+        assert (a.page_type, a.num_values, a.encoding, a.image_len) == (b.page_type, b.num_values, b.encoding, b.image_len)
+        assert (c.image_offset, c.image_len) == (b.image_offset, b.image_len) and b.image_offset % 64 == 0
+        want = bytes(hpay[a.image_offset:a.image_offset + a.image_len])
+        s = bytes(src[c.src_offset:c.src_offset + c.src_len])
+        if c.codec == O.SNAPPY:
+            got = s[:c.raw_len] + O.snappy_decode(s[c.raw_len:])
+            snappy_pages += 1
+        else:
+            got = s
+        assert got == want
+    assert snappy_pages == len(cps)
+
+
+def test_device_codec_plain_files_keep_the_host_layout(pq):
+    data = fixtures.flat_all_types(n=3000, codec=O.UNCOMPRESSED)
+    f = pq.native.File(data)
+    hb = f.load(0, f.num_row_groups, [0, 1], device_snappy=True)
+    assert hb.codec_pages() == [] and hb.image_bytes == 0
+
+
+def test_device_codec_walker_checks(pq):
+    """Announced lengths that cannot match fail the chunk on the host, as decoding would."""
+    W = pq.writer
+    vals = np.arange(5000, dtype=np.int64)
+    data = bytearray(W.flat([("v", W.Column(W.INT64, vals, use_dict=False), W.REQUIRED)], 5000, codec=O.SNAPPY))
+    f = pq.native.File(bytes(data))
+    hb = f.load(0, 1, [0], device_snappy=True)
+    cp = hb.codec_pages()[0]
+    assert hb.chunks()[0].host_status == 0
+    # find the page's compressed block in the file and break its announced length
+    blk = bytes(hb.payload()[cp.src_offset:cp.src_offset + cp.src_len])
+    pos = bytes(data).find(blk)
+    assert pos > 0
+    data[pos] ^= 0x01
+    for dev in (False, True):
+        f2 = pq.native.File(bytes(data))
+        hb2 = f2.load(0, 1, [0], device_snappy=dev)
+        assert hb2.chunks()[0].host_status == {v: k for k, v in pq.native.STATUS.items()}["DECOMPRESS"]

@@ -1,0 +1,167 @@
+"""Device SNAPPY (k_snappy) against the oracle.
+
+* pqh_decompress_pages on its own: hand-built blocks covering every element kind, bulk literals,
+  batch-cap boundaries and long chains of tiny overlapping copies; pyarrow-compressed data of
+  several kinds; and a seeded mutation fuzzer -- the device's status and bytes must equal
+  oracle.snappy_decode (golang/snappy decode.go restated), ErrCorrupt <-> PQH_ERR_DECOMPRESS.
+* whole files decoded with the pages of SNAPPY chunks decompressed on the device (plain batches and
+  staged end-to-end batches) must equal the oracle's decode chunk by chunk, bit for bit.
+* a chunk whose compressed page is corrupt reports PQH_ERR_DECOMPRESS, as the host walker does.
+"""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import fixtures
+from oracle import oracle as O
+from parity import assert_chunk, oracle_chunk
+from snappy_blocks import edge_blocks, sample_blocks
+
+pytestmark = pytest.mark.gpu
+
+DECOMPRESS = 23
+
+
+@pytest.fixture(scope="module")
+def ctx(pq):
+    return pq.native.Context(0)
+
+
+def _device_decompress(pq, ctx, blocks, sizes):
+    """Every block as one codec page; returns [(status, bytes)]."""
+    N = pq.native
+    src, pages, soff, ioff = [], [], 0, 0
+    for blk, size in zip(blocks, sizes):
+        pad = (-soff) % 64
+        src.append(b"\0" * pad + blk)
+        soff += pad
+        ioff = (ioff + 63) & ~63
+        pages.append(N.CodecPage(soff, ioff, len(blk), size, 0, O.SNAPPY, 0, 0))
+        soff += len(blk)
+        ioff += size
+    s = np.frombuffer(b"".join(src) + b"\0" * N.PAYLOAD_PAD, np.uint8).copy()
+    ds, dd = ctx.malloc(len(s)), ctx.malloc(ioff + N.PAYLOAD_PAD)
+    try:
+        ctx.h2d(ds, s.ctypes.data, len(s))
+        st = ctx.decompress_pages(pages, ds, dd)
+        img = ctx.d2h_array(dd, ioff) if ioff else np.zeros(0, np.uint8)
+    finally:
+        ctx.free(ds)
+        ctx.free(dd)
+    return [(st[i], img[p.image_offset:p.image_offset + p.image_len].tobytes()) for i, p in enumerate(pages)]
+
+
+def _expect(blk, size):
+    try:
+        raw = O.snappy_decode(blk)
+    except O.SnappyCorrupt:
+        return DECOMPRESS, None
+    return (0, raw) if len(raw) == size else (DECOMPRESS, None)
+
+
+def _check(pq, ctx, blocks, sizes):
+    got = _device_decompress(pq, ctx, blocks, sizes)
+    bad = 0
+    for i, (blk, size) in enumerate(zip(blocks, sizes)):
+        st, raw = _expect(blk, size)
+        assert got[i][0] == st, f"block {i}: device status {got[i][0]} vs oracle {st}"
+        if st == 0:
+            assert got[i][1] == raw, f"block {i}: bytes differ"
+        bad += st != 0
+    return bad
+
+
+def test_snappy_edge_blocks(pq, ctx):
+    cases = edge_blocks()
+    assert _check(pq, ctx, [c[0] for c in cases], [len(c[1]) for c in cases]) == 0
+
+
+def test_snappy_pyarrow_blocks(pq, ctx):
+    raws = sample_blocks()
+    blocks = [pa.compress(r, codec="snappy", asbytes=True) for r in raws]
+    assert _check(pq, ctx, blocks, [len(r) for r in raws]) == 0
+
+
+def test_snappy_mutation_fuzz(pq, ctx):
+    rng = np.random.default_rng(97)
+    raws = sample_blocks(seed=9) + [c[1] for c in edge_blocks()]
+    blocks, sizes = [], []
+    for r in raws:
+        comp = pa.compress(r, codec="snappy", asbytes=True) if len(r) else b"\0"
+        for k in range(12):
+            b = bytearray(comp)
+            mode = k % 4
+            if mode == 0 and len(b) > 1:
+                for _ in range(int(rng.integers(1, 4))):
+                    b[int(rng.integers(1, len(b)))] = int(rng.integers(0, 256))
+            elif mode == 1:
+                b = b[:int(rng.integers(0, len(b) + 1))]
+            elif mode == 2 and len(b) > 1:
+                i = int(rng.integers(1, len(b)))
+                b[i] ^= 1 << int(rng.integers(0, 8))
+            blocks.append(bytes(b))
+            sizes.append(len(r) + (int(rng.integers(-2, 3)) if mode == 3 else 0))
+    bad = _check(pq, ctx, blocks, [max(0, s) for s in sizes])
+    assert bad > 20
+
+
+def _files():
+    yield "writer-v1", fixtures.flat_all_types(n=8000, v2=False, codec=O.SNAPPY, page=16 * 1024, rows_per_group=4000)
+    yield "writer-v2", fixtures.flat_all_types(n=8000, v2=True, codec=O.SNAPPY, page=16 * 1024, rows_per_group=4000)
+    yield "pyarrow-v1", fixtures.pyarrow_file(n=20000, version="1.0", compression="SNAPPY")
+    yield "pyarrow-v2", fixtures.pyarrow_file(n=20000, version="2.0", compression="SNAPPY")
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_device_snappy_files(pq, ctx, staged):
+    checked = 0
+    for name, data in _files():
+        f = pq.native.File(data)
+        ncols = len(f.columns())
+        res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(ncols)), device_snappy=True,
+                                      staged_runs=2 if staged else 0)
+        fr = O.FileReader(data)
+        for k, col in enumerate(res):
+            rg, ci = divmod(k, ncols)
+            if col.status == pq.native.NOT_IMPLEMENTED:
+                continue
+            assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"{name} rg{rg} {col.path}")
+            checked += 1
+    assert checked > 40
+
+
+def test_device_snappy_corrupt_page_fails_its_chunk(pq, ctx):
+    """A corrupt compressed page (announced length intact): the chunk fails with DECOMPRESS on the
+    device exactly when the host decoder (and golang/snappy) rejects the block."""
+    W = pq.writer
+    rng = np.random.default_rng(3)
+    vals = np.repeat(rng.integers(0, 1 << 40, 3000), 8)
+    data = W.flat([("v", W.Column(W.INT64, vals, use_dict=False), W.REQUIRED),
+                   ("w", W.Column(W.INT64, vals[::-1].copy(), use_dict=False), W.REQUIRED)], len(vals),
+                  codec=O.SNAPPY, max_page_size=8 * 1024)
+    f = pq.native.File(data)
+    failed = ok = 0
+    for trial in range(12):
+        hb = f.load(0, 1, [0, 1], device_snappy=True)
+        cps = hb.codec_pages()
+        src = hb.payload()  # writable view of the host batch's source bytes
+        victim = cps[int(rng.integers(0, len(cps)))]
+        lo = victim.src_offset + victim.raw_len + 3  # past the announced length
+        i = int(rng.integers(lo, victim.src_offset + victim.src_len))
+        src[i] ^= 1 << int(rng.integers(0, 8))
+        blk = bytes(src[victim.src_offset + victim.raw_len:victim.src_offset + victim.src_len])
+        st, _ = _expect(blk, victim.image_len - victim.raw_len)
+        b = pq.native.Batch.from_host(ctx, hb)
+        b.run()
+        b.sync()
+        out = b.chunk_out(victim.chunk)
+        if st:
+            assert out.status == DECOMPRESS, f"trial {trial}: device status {out.status}"
+            failed += 1
+        else:
+            ok += 1
+        other = b.chunk_out(1 - victim.chunk)
+        assert other.status == 0
+        b.close()
+        hb.close()
+    assert failed >= 3, (failed, ok)
