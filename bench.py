@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5z"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -199,7 +199,7 @@ def main():
     # scaling: every rank opens the same file and decodes its contiguous block of row groups
     # (shard.row_group_block).  The other workloads give every rank its own file (weak scaling).
     strong = args.workload == "c3"
-    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40}[args.workload] + (0 if strong else 1000 * rank)
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40, "c5z": 41}[args.workload] + (0 if strong else 1000 * rank)
     t0 = time.perf_counter()
     path = None
     if strong and world > 1:
@@ -323,46 +323,80 @@ def main():
     # End-to-end: one staged batch per row-group range holding its decompressed
     # page images in pinned host memory; every pass copies each range to HBM on the copy stream
     # while the previous range decodes on the compute stream.  Host decompression excluded.
-    e2e = None
-    if not args.no_e2e:
+    # device_snappy: the ranges hold the pages of SNAPPY chunks still compressed,
+    # so H2D moves compressed bytes and every decode starts with k_snappy.
+    def e2e_pass(device_snappy):
         # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
         # >= 1/16 of the payload each
         nrg = rg1 - rg0
         groups = min(nrg, 16)
         cuts = [nrg * g // groups for g in range(groups + 1)]
-        staged, payload = [], 0
+        staged, payload, images = [], 0, 0
         for g in range(groups):
-            hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)))
+            hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)), device_snappy=device_snappy)
             payload += hbr.payload_bytes
+            images += hbr.image_bytes or hbr.payload_bytes
             staged.append(native.Batch.staged(ctx, hbr))
             hbr.close()
-        e2e_written = 0.0
+        written = 0.0
         for sb in staged:
             sb.run_staged()
         for g, sb in enumerate(staged):
             sb.sync()
-            e2e_written += sb.traffic()[1]
+            written += sb.traffic()[1]
             for c in range(ncols * (cuts[g + 1] - cuts[g])):
                 if sb.chunk_out(c).status != native.OK:
                     raise RuntimeError("staged decode failed")
-        e2e_steps = max(1, min(args.steps, 10))
+        steps = max(1, min(args.steps, 10))
         barrier_sync()
         t0 = time.perf_counter()
-        for _ in range(e2e_steps):
+        for _ in range(steps):
             for sb in staged:
                 sb.run_staged()
         barrier_sync()
-        e2e_el = time.perf_counter() - t0
-        e2e_el, e2e_total = pkg.shard.reduce_step(e2e_el, e2e_written, device=f"cuda:{local}" if world > 1 else None)
-        e2e = {"mode": "pinned H2D on a copy stream, overlapped per row group with decode; host decompression excluded",
-               "payload_bytes_per_gpu": payload, "staged_batches": groups, "steps": e2e_steps, "ms_per_step": round(e2e_el / e2e_steps * 1e3, 3),
-               "gbps": round(e2e_total * e2e_steps / e2e_el / 1e9, 2),
-               "per_gpu_gbps": round(e2e_written * e2e_steps / e2e_el / 1e9, 2),
-               "payload_h2d_gbps_per_gpu": round(payload * e2e_steps / e2e_el / 1e9, 2),
-               "unstaged_h2d_s": round(h2d_s, 4)}
+        el = time.perf_counter() - t0
+        el, total = pkg.shard.reduce_step(el, written, device=f"cuda:{local}" if world > 1 else None)
+        out = {"mode": ("pinned H2D of the COMPRESSED pages on a copy stream, k_snappy + decode on the compute "
+                        "stream, overlapped per row group" if device_snappy else
+                        "pinned H2D on a copy stream, overlapped per row group with decode; host decompression excluded"),
+               "payload_bytes_per_gpu": payload, "image_bytes_per_gpu": images, "staged_batches": groups,
+               "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+               "gbps": round(total * steps / el / 1e9, 2),
+               "per_gpu_gbps": round(written * steps / el / 1e9, 2),
+               "payload_h2d_gbps_per_gpu": round(payload * steps / el / 1e9, 2)}
         for sb in staged:
             sb.close()
+        return out
+
+    e2e = e2e_dev = None
+    if not args.no_e2e:
+        e2e = e2e_pass(False)
+        e2e["unstaged_h2d_s"] = round(h2d_s, 4)
         e2e["pinned_h2d_ceiling_gbps"] = pinned_h2d_rate(ctx, native)
+        probe = f.load(rg0, rg0 + 1, list(range(ncols)), device_snappy=True)
+        has_snappy = len(probe.codec_pages()) > 0
+        probe.close()
+        if has_snappy:
+            e2e_dev = e2e_pass(True)
+            # k_snappy alone: HBM-resident batch of the rank's row groups, profiled runs
+            hd = f.load(rg0, rg1, list(range(ncols)), device_snappy=True)
+            bd = native.Batch.from_host(ctx, hd)
+            bd.run()
+            bd.sync()
+            ctx.set_profile(True)
+            bd.reset_stats()
+            for _ in range(3):
+                bd.run()
+            bd.sync()
+            ks = [s for s in bd.kernel_stats() if s.name.decode() == "k_snappy" and s.launches]
+            ctx.set_profile(False)
+            if ks:
+                ms = ks[0].total_ms / ks[0].launches
+                e2e_dev["k_snappy"] = {"avg_ms": round(ms, 4), "pages": ks[0].work_items,
+                                       "compressed_bytes": hd.payload_bytes, "image_bytes": hd.image_bytes,
+                                       "decompressed_gbps": round(hd.image_bytes / (ms * 1e-3) / 1e9, 1)}
+            bd.close()
+            hd.close()
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -377,7 +411,7 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int32/int64/f32/f64/bool/flba16 (bit-exact integer/byte decode)" if args.workload == "c2"
-            else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload == "c5"
+            else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload in ("c5", "c5z")
             else "int64/int32/bytes + u8 levels + int32 list offsets" if args.workload == "c4" else "int64",
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
             "config": {"workload": desc, "rows_total": f.num_rows if strong else f.num_rows * world,
@@ -398,6 +432,7 @@ def main():
             "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 3),
                      "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
             "e2e": e2e,
+            "e2e_device_snappy": e2e_dev,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
             "verified": verified,

@@ -148,6 +148,35 @@ def c5(rows=50_000_000, row_groups=8, seed=40, codec=W.SNAPPY):
                    dict_page_limit=1 << 20)
     return W.flat([("s", col, W.REQUIRED)], per, v2=False, codec=codec, as_array=True)
 
+def c5z_strings(rows, seed=41, chunk=2_000_000):
+    """(data, offsets) of `rows` URL-like strings "https://<host>/<section>/<item>?id=<n>": a few
+    hundred hosts / sections, sequential ids -- text that SNAPPY compresses (unlike C5's random
+    letters), for the device-SNAPPY end-to-end measurement."""
+    rng = np.random.default_rng(seed)
+    hosts = [f"www.{w}.example.com".encode() for w in ("alpha", "bravo", "charlie", "delta", "echo", "foxtrot")]
+    sections = [f"{a}-{b}".encode() for a in ("news", "shop", "blog", "docs", "media") for b in range(40)]
+    parts, lens = [], []
+    for a in range(0, rows, chunk):
+        n = min(chunk, rows - a)
+        h = rng.integers(0, len(hosts), n)
+        sc = rng.integers(0, len(sections), n)
+        it = rng.integers(0, 5000, n)
+        for i in range(n):
+            s = b"https://" + hosts[h[i]] + b"/" + sections[sc[i]] + b"/item" + str(it[i]).encode() + \
+                b"?id=" + str(a + i).encode()
+            parts.append(s)
+            lens.append(len(s))
+    offsets = np.zeros(rows + 1, np.int64)
+    np.cumsum(np.array(lens, np.int64), out=offsets[1:])
+    return np.frombuffer(b"".join(parts) + b"\0", np.uint8), offsets
+
+
+def c5z(rows=10_000_000, row_groups=8, seed=41, codec=W.SNAPPY):
+    """Supplementary (not a BASELINE config): compressible strings, DELTA_LENGTH_BYTE_ARRAY, SNAPPY."""
+    per = -(-rows // row_groups)
+    col = W.Column(W.BYTE_ARRAY, c5z_strings(rows, seed), encoding=W.DELTA_LENGTH_BYTE_ARRAY, use_dict=False)
+    return W.flat([("url", col, W.REQUIRED)], per, v2=False, codec=codec, as_array=True)
+
 
 WORKLOADS = {
     "c1": ("C1: 10M rows, required INT32 dictionary K=4096 (width 13), UNCOMPRESSED, data page V1", c1),
@@ -158,4 +187,6 @@ WORKLOADS = {
            "UNCOMPRESSED", c4),
     "c5": ("C5: required BYTE_ARRAY strings U[8,40] ~half unique, RLE_DICTIONARY (dict page <= 1 MiB) "
            "then DELTA_LENGTH_BYTE_ARRAY fallback, SNAPPY, 8 row groups", c5),
+    "c5z": ("C5z (supplementary, not a BASELINE config): 10M URL-like strings, DELTA_LENGTH_BYTE_ARRAY, "
+            "SNAPPY-compressible, 8 row groups", c5z),
 }
