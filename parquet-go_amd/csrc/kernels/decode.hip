@@ -1054,7 +1054,7 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
 hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                          hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, pages, src, dst, status);
+  hipLaunchKernelGGL(k_snappy, dim3(n), dim3(256), 0, s, pages, src, dst, status);
   return hipGetLastError();
 }
 

@@ -14,39 +14,55 @@
 //            output, a copy offset of 0 or before the output start, a short output; plus the
 //            reference's size check against the page header -> PQH_ERR_DECOMPRESS.
 //
-// One wave per page.  The element chain is sequential by definition; it is resolved 64 input bytes
-// at a time: every lane decodes the element that WOULD start at its byte, the wave then follows
-// the true chain from the window's first element with readlane steps, and a wave scan places the
-// chain's elements in the output.  The batch's output bytes are then produced lane-parallel: a
-// byte of a literal comes from the input; a byte of a copy maps to an earlier output position
-// (periodically for overlapping copies) which is either written by an earlier batch (read back
-// from HBM) or resolved again inside this batch.  Literals longer than one batch are copied in
-// bulk.  DataPageV2 pages copy their uncompressed level prefix first (page_v2.go:116-125).
+// One workgroup per page.  The element chain is sequential by definition; it is resolved 64 input
+// bytes at a time by wave 0 from an LDS stage of the compressed input: every lane decodes the
+// element that WOULD start at its byte, the wave follows the true chain from the window's first
+// element with readlane steps, and a wave scan places the chain's elements in the output.  Up to
+// kSnapOut output bytes (kSnapMaxE elements) form a batch; all 256 threads then produce the batch's
+// bytes: an output byte -> element map (max-scan of the elements' start markers) finds each byte's
+// element; a literal byte comes from the stage (or HBM), a copy byte maps to an earlier output
+// position (periodically for overlapping copies) that is resolved again inside the batch or read
+// back from HBM, written by an earlier batch.  Literals longer than a batch are copied in bulk.
+// DataPageV2 pages copy their uncompressed level prefix first (page_v2.go:116-125).
 #pragma once
 
-constexpr int kSnapBatch = 4096;  // output bytes resolved per batch (literals beyond: bulk copy)
+constexpr int kSnapStage = 8192;  // compressed input bytes staged in LDS per batch
+constexpr int kSnapOut = 8192;    // output bytes per batch (a longer literal: bulk copy)
+constexpr int kSnapMaxE = 1024;   // elements per batch
 
 struct SnapLds {
-  int32_t out[65];  // element output start (stream-relative); out[m] = the batch's end
-  int32_t src[64];  // literal: input position of its bytes; copy: offset
-  int32_t len[64];
-  uint8_t lit[64];
+  uint8_t in[kSnapStage + 96];    // the stage: block bytes [a0, a0 + kSnapStage + 96)
+  int32_t eout[kSnapMaxE + 1];    // element output start, batch-relative; eout[nE] = the batch's size
+  int32_t esrc[kSnapMaxE];        // literal: block position of its bytes; copy: offset
+  int32_t elen[kSnapMaxE];
+  uint16_t emap[kSnapOut];        // batch output byte -> element
+  uint8_t elit[kSnapMaxE];
+  int32_t wmax[4];
+  int32_t nE, bend, p_next, bad, bulk_len, bulk_src;
 };
 
-// n bytes from src to dst by one wave (any alignment): 16-byte stores once dst is aligned, each fed
-// by an unaligned 16-byte load (the source payload keeps PQH_PAYLOAD_PAD readable bytes past it).
-__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
-  const int lane = threadIdx.x & 63;
+// n bytes from src to dst by the workgroup (any alignment): 16-byte stores once dst is aligned,
+// each fed by an unaligned 16-byte load (the source payload keeps PQH_PAYLOAD_PAD readable bytes).
+__device__ __forceinline__ void snap_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const int tid = threadIdx.x;
   const int64_t head0 = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15);
   const int64_t head = head0 < n ? head0 : n;
-  if (lane < head) dst[lane] = src[lane];
+  if (tid < head) dst[tid] = src[tid];
   typedef uint4 uint4_u __attribute__((aligned(1)));
   const int64_t units = (n - head) >> 4;
   const uint4_u* sp = reinterpret_cast<const uint4_u*>(src + head);
   uint4* dp = reinterpret_cast<uint4*>(dst + head);
-  for (int64_t u = lane; u < units; u += 64) dp[u] = sp[u];
+  int64_t u = tid;
+  for (; u + 3 * kBlock < units; u += 4 * kBlock) {  // four loads in flight
+    const uint4 x0 = sp[u], x1 = sp[u + kBlock], x2 = sp[u + 2 * kBlock], x3 = sp[u + 3 * kBlock];
+    dp[u] = x0;
+    dp[u + kBlock] = x1;
+    dp[u + 2 * kBlock] = x2;
+    dp[u + 3 * kBlock] = x3;
+  }
+  for (; u < units; u += kBlock) dp[u] = sp[u];
   const int64_t done = head + units * 16;
-  if (lane < n - done) dst[done + lane] = src[done + lane];
+  if (tid < n - done) dst[done + tid] = src[done + tid];
 }
 
 __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
@@ -59,10 +75,119 @@ __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
   return incl - x;
 }
 
-// Decode one snappy block src[0, n) into dst[0, expected).  Whole wave; returns PQH_OK or
+// Wave 0: the elements of one batch from block position p (the stage holds [a0, ...)), output
+// starting at d.  Results in E (nE, bend, p_next, bad, bulk_*).
+__device__ void snappy_parse(SnapLds& E, int64_t n, int32_t p, int64_t a0, int32_t d, int32_t total) {
+  const int lane = threadIdx.x & 63;
+  int32_t pos = p, k = 0, T = 0, bulk_len = 0, bulk_src = 0;
+  bool bad = false;
+  for (;;) {
+    if (pos >= n || pos - a0 > kSnapStage - 64) break;  // done, or the stage is used up
+    // ---- every lane: the element that would start at byte q
+    const int32_t q = pos + lane;
+    const int32_t o8 = int32_t(q - a0);
+    uint64_t w;
+    __builtin_memcpy(&w, E.in + o8, 8);
+    const uint32_t tag = uint32_t(w & 0xff);
+    int32_t hdr, off = 0;
+    int64_t len;
+    const bool lit = (tag & 3) == 0;
+    if (lit) {
+      const uint32_t x = tag >> 2;
+      if (x < 60) {
+        hdr = 1;
+        len = int64_t(x) + 1;
+      } else {
+        const int kb = int(x) - 59;
+        hdr = 1 + kb;
+        len = int64_t((w >> 8) & (kb == 4 ? 0xffffffffull : ((1ull << (8 * kb)) - 1))) + 1;
+      }
+    } else if ((tag & 3) == 1) {
+      hdr = 2;
+      len = 4 + ((tag >> 2) & 7);
+      off = int32_t(((tag >> 5) << 8) | ((w >> 8) & 0xff));
+    } else if ((tag & 3) == 2) {
+      hdr = 3;
+      len = 1 + (tag >> 2);
+      off = int32_t((w >> 8) & 0xffff);
+    } else {
+      hdr = 5;
+      len = 1 + (tag >> 2);
+      const uint64_t ov = (w >> 8) & 0xffffffffull;
+      off = ov > 0x7fffffffull ? 0x7fffffff : int32_t(ov);  // beyond any output position: invalid
+    }
+    const bool hdr_ok = int64_t(q) + hdr <= n;
+    const int64_t nx64 = int64_t(q) + hdr + (lit ? len : 0);
+    const int32_t nxt = nx64 > n ? int32_t(n) + 1 : int32_t(nx64);  // past the input: invalid below
+    // ---- the true chain from pos (wave-uniform)
+    uint64_t chain = 0;
+    int32_t exitp = pos;
+    for (int32_t c = pos; c < pos + 64 && c < n;) {
+      const int l = c - pos;
+      chain |= 1ull << l;
+      if (!__builtin_amdgcn_readlane(int(hdr_ok), l)) {
+        bad = true;
+        break;
+      }
+      c = __builtin_amdgcn_readlane(nxt, l);
+      exitp = c;
+    }
+    if (bad) break;
+    const bool on = (chain >> lane) & 1;
+    const int idx = __popcll(chain & ((1ull << lane) - 1));
+    const int64_t excl = wave_excl_scan64(on ? len : 0);
+    const int64_t eo = int64_t(d) + T + excl;  // stream output position
+    bool ebad = false;
+    if (on) {
+      if (lit) ebad = nx64 > n || eo + len > total;
+      else ebad = off == 0 || off > eo || eo + len > total;
+    }
+    if (__ballot(ebad)) {
+      bad = true;
+      break;
+    }
+    // every chain element now lies inside the output: lengths and positions fit 32 bits
+    const uint64_t fit = __ballot(on && T + excl + len <= kSnapOut && k + idx < kSnapMaxE);
+    const int m = __popcll(fit);
+    if (m == 0) {
+      if (k == 0) {  // a literal longer than a batch (the window's first element, lane 0): bulk copy
+        bulk_len = __builtin_amdgcn_readfirstlane(int32_t(len));
+        bulk_src = pos + __builtin_amdgcn_readfirstlane(hdr);
+        pos = __builtin_amdgcn_readfirstlane(nxt);
+      }
+      break;
+    }
+    if (on && idx < m) {
+      E.eout[k + idx] = T + int32_t(excl);
+      E.elen[k + idx] = int32_t(len);
+      E.elit[k + idx] = lit;
+      E.esrc[k + idx] = lit ? q + hdr : off;
+    }
+    const int last = 63 - __builtin_clzll(fit);  // lane of the last element taken
+    T += __builtin_amdgcn_readlane(int32_t(excl + len), last);
+    k += m;
+    if (m < __popcll(chain)) {  // batch full: the next batch starts at the first element not taken
+      const uint64_t rest = chain & ~fit;
+      pos += __builtin_ctzll(rest);
+      break;
+    }
+    pos = exitp;
+  }
+  if (lane == 0) {
+    E.nE = k;
+    E.bend = T;
+    E.eout[k] = T;
+    E.p_next = pos;
+    E.bad = bad;
+    E.bulk_len = bulk_len;
+    E.bulk_src = bulk_src;
+  }
+}
+
+// Decode one snappy block src[0, n) into dst[0, expected).  Whole workgroup; returns PQH_OK or
 // PQH_ERR_DECOMPRESS (uniform).
 __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expected, SnapLds& E) {
-  const int lane = threadIdx.x & 63;
+  const int tid = threadIdx.x;
   // decodedLen: binary.Uvarint, at most 10 bytes; > 0xffffffff is ErrCorrupt
   uint64_t v = 0;
   int hl = 0;
@@ -80,138 +205,125 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
   const int32_t total = int32_t(v);
   int32_t p = hl, d = 0;
   while (p < n) {
-    // ---- every lane: the element that would start at byte q
-    const int32_t q = p + lane;
-    uint64_t w = 0;
-    __builtin_memcpy(&w, src + q, 8);  // in the page's bytes or the payload pad
-    const uint32_t tag = uint32_t(w & 0xff);
-    int32_t hdr, off = 0;
-    int64_t len;
-    bool lit = (tag & 3) == 0;
-    if (lit) {
-      const uint32_t x = tag >> 2;
-      if (x < 60) {
-        hdr = 1;
-        len = int64_t(x) + 1;
-      } else {
-        const int k = int(x) - 59;
-        hdr = 1 + k;
-        len = int64_t((w >> 8) & (k == 4 ? 0xffffffffull : ((1ull << (8 * k)) - 1))) + 1;
+    // ---- stage the compressed bytes from p (16-byte aligned start; the source payload is padded)
+    const int64_t a0 = p - int64_t((reinterpret_cast<uintptr_t>(src) + uintptr_t(p)) & 15);
+    __syncthreads();  // the previous batch's readers of the stage are done
+    {  // up to the block's end rounded to 16 bytes (inside the payload pad): bytes past it never
+       // decide a valid element
+      const uint4* sp = reinterpret_cast<const uint4*>(src + a0);
+      uint4* lp = reinterpret_cast<uint4*>(E.in);
+      const int64_t avail = (n - a0 + 15) >> 4;
+      const int nu = avail < (kSnapStage + 96) / 16 ? int(avail) : (kSnapStage + 96) / 16;
+      for (int u = tid; u < nu; u += kBlock) lp[u] = sp[u];
+    }
+    __syncthreads();
+    if (tid < 64) snappy_parse(E, n, p, a0, d, total);
+    __syncthreads();
+    if (E.bad) return PQH_ERR_DECOMPRESS;
+    const int32_t nE = E.nE, T = E.bend;
+    if (nE == 0) {
+      if (E.bulk_len > 0) {
+        snap_copy(dst + d, src + E.bulk_src, E.bulk_len);
+        d += E.bulk_len;
       }
-    } else if ((tag & 3) == 1) {
-      hdr = 2;
-      len = 4 + ((tag >> 2) & 7);
-      off = int32_t(((tag >> 5) << 8) | ((w >> 8) & 0xff));
-    } else if ((tag & 3) == 2) {
-      hdr = 3;
-      len = 1 + (tag >> 2);
-      off = int32_t((w >> 8) & 0xffff);
-    } else {
-      hdr = 5;
-      len = 1 + (tag >> 2);
-      const uint64_t o = (w >> 8) & 0xffffffffull;
-      off = o > 0x7fffffffull ? 0x7fffffff : int32_t(o);  // beyond any output position: invalid
-    }
-    const bool hdr_ok = int64_t(q) + hdr <= n;
-    const int64_t nx64 = int64_t(q) + hdr + (lit ? len : 0);
-    const int32_t nxt = nx64 > n ? int32_t(n) + 1 : int32_t(nx64);  // past the input: invalid below
-    // ---- the true chain from p (the window's first element), wave-uniform
-    uint64_t chain = 0;
-    bool bad = false;
-    for (int32_t pos = p; pos < p + 64 && pos < n;) {
-      const int l = pos - p;
-      chain |= 1ull << l;
-      if (!__builtin_amdgcn_readlane(int(hdr_ok), l)) {
-        bad = true;
-        break;
-      }
-      pos = __builtin_amdgcn_readlane(nxt, l);
-    }
-    if (bad) return PQH_ERR_DECOMPRESS;
-    const bool on = (chain >> lane) & 1;
-    const int idx = __popcll(chain & ((1ull << lane) - 1));
-    // ---- output positions of the chain's elements; checks of every element (decode.go order: all
-    // of them fail as ErrCorrupt, so which one does not matter)
-    const int64_t excl = wave_excl_scan64(on ? len : 0);
-    const int64_t eo = int64_t(d) + excl;
-    bool ebad = false;
-    if (on) {
-      if (lit) ebad = nx64 > n || eo + len > total;
-      else ebad = off == 0 || off > eo || eo + len > total;
-    }
-    if (__ballot(ebad)) return PQH_ERR_DECOMPRESS;
-    // every chain element now lies inside the output: lengths and positions fit 32 bits
-    const int32_t ln32 = int32_t(len);
-    // ---- batch: the chain's first m elements whose output fits kSnapBatch (copies are <= 64 bytes)
-    const uint64_t fit = __ballot(on && excl + len <= kSnapBatch);
-    const int m = __popcll(fit);
-    if (m == 0) {  // a literal longer than a batch (the chain's first element, lane 0): bulk copy
-      const int32_t l0 = __builtin_amdgcn_readfirstlane(ln32);
-      const int32_t h0 = __builtin_amdgcn_readfirstlane(hdr);
-      wave_copy(dst + d, src + p + h0, l0);
-      __syncthreads();
-      d += l0;
-      p = __builtin_amdgcn_readfirstlane(nxt);
+      p = E.p_next;
+      __syncthreads();  // the bulk bytes are visible to the next batches' reads
       continue;
     }
-    const int last = 63 - __builtin_clzll(fit);  // lane of element m-1 (fit is a prefix of the chain)
-    const int32_t p_next = __builtin_amdgcn_readlane(nxt, last);
-    const int32_t bend = d + __builtin_amdgcn_readlane(int32_t(excl) + ln32, last);
-    if (on && idx < m) {
-      E.out[idx] = int32_t(eo);
-      E.len[idx] = ln32;
-      E.lit[idx] = lit;
-      E.src[idx] = lit ? q + hdr : off;
-    }
-    if (lane == 0) E.out[m] = bend;
+    // ---- output byte -> element: start markers, then a max-scan (element ids rise with output)
+    for (int i = tid; i < T; i += kBlock) E.emap[i] = 0;
     __syncthreads();
-    // ---- the batch's output bytes, lane-parallel
-    for (int32_t b = d + lane; b < bend; b += 64) {
-      int32_t pos = b;
-      uint8_t val;
-      for (;;) {
-        int lo = 0, hi = m;  // E.out[lo] <= pos < E.out[hi]
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (E.out[mid] <= pos) lo = mid;
-          else hi = mid;
-        }
-        const int32_t rel = pos - E.out[lo];
-        if (E.lit[lo]) {
-          val = src[E.src[lo] + rel];
-          break;
-        }
-        const int32_t o = E.src[lo];
-        const int32_t s = E.out[lo] - o + (o < E.len[lo] ? rel % o : rel);  // overlapping copies repeat
-        if (s < d) {  // written by an earlier batch
-          val = dst[s];
-          break;
-        }
-        pos = s;
+    for (int e = tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
+    __syncthreads();
+    {
+      constexpr int per = kSnapOut / kBlock;  // 32 entries per thread
+      const int i0 = tid * per;
+      int32_t mx = 0;
+      for (int i = i0; i < i0 + per && i < T; i++) mx = E.emap[i] > mx ? E.emap[i] : mx;
+      int32_t incl = mx;  // inclusive max over the threads before
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(incl, o, 64);
+        if ((tid & 63) >= o) incl = y > incl ? y : incl;
       }
-      dst[b] = val;
+      if ((tid & 63) == 63) E.wmax[tid >> 6] = incl;
+      __syncthreads();
+      int32_t run = __shfl_up(incl, 1, 64);
+      if ((tid & 63) == 0) run = 0;
+      for (int wv = 0; wv < (tid >> 6); wv++) run = E.wmax[wv] > run ? E.wmax[wv] : run;
+      for (int i = i0; i < i0 + per && i < T; i++) {
+        run = E.emap[i] > run ? E.emap[i] : run;
+        E.emap[i] = uint16_t(run);
+      }
+    }
+    __syncthreads();
+    // ---- the batch's bytes: resolved in LDS, the HBM reads of 8 bytes issued together
+    const int64_t s_lo = a0, s_hi = a0 + kSnapStage + 96;
+    for (int b0 = 0; b0 < T; b0 += 8 * kBlock) {
+      int32_t ga[8];
+      uint8_t val[8];
+      uint8_t from[8];  // 0 resolved, 1 dst (an earlier batch), 2 src (a literal outside the stage)
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int32_t b = b0 + j * kBlock + tid;
+        from[j] = 0;
+        val[j] = 0;
+        ga[j] = 0;
+        if (b >= T) continue;
+        int32_t pos = b;
+        for (;;) {
+          const int e = E.emap[pos];
+          const int32_t rel = pos - E.eout[e];
+          if (E.elit[e]) {
+            const int32_t sp = E.esrc[e] + rel;
+            if (sp >= s_lo && sp < s_hi) {
+              val[j] = E.in[sp - s_lo];
+            } else {
+              from[j] = 2;
+              ga[j] = sp;
+            }
+            break;
+          }
+          const int32_t o = E.esrc[e];
+          const int32_t sabs = d + E.eout[e] - o + (o < E.elen[e] ? rel % o : rel);  // overlapping copies repeat
+          if (sabs >= d) {
+            pos = sabs - d;
+            continue;
+          }
+          from[j] = 1;
+          ga[j] = sabs;
+          break;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (from[j]) val[j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int32_t b = b0 + j * kBlock + tid;
+        if (b < T) dst[d + b] = val[j];
+      }
     }
     __syncthreads();  // this batch's bytes are visible to the next batches' reads
-    d = bend;
-    p = p_next;
+    d += T;
+    p = E.p_next;
   }
   return d == total ? PQH_OK : PQH_ERR_DECOMPRESS;
 }
 
-// One wave per page: its image rebuilt at image_offset from its source bytes (codec 0: copied).
-__global__ __launch_bounds__(64) void k_snappy(const pqh_codec_page* cps, const uint8_t* src_all, uint8_t* dst_all,
-                                               int32_t* status) {
+// One workgroup per page: its image rebuilt at image_offset from its source bytes (codec 0: copied).
+__global__ __launch_bounds__(256) void k_snappy(const pqh_codec_page* cps, const uint8_t* src_all, uint8_t* dst_all,
+                                                int32_t* status) {
   __shared__ SnapLds E;
   const pqh_codec_page cp = cps[blockIdx.x];
   const uint8_t* src = src_all + cp.src_offset;
   uint8_t* dst = dst_all + cp.image_offset;
   int rc = PQH_OK;
   if (cp.codec != PQH_CODEC_SNAPPY) {
-    wave_copy(dst, src, cp.src_len < cp.image_len ? cp.src_len : cp.image_len);
+    snap_copy(dst, src, cp.src_len < cp.image_len ? cp.src_len : cp.image_len);
     if (cp.src_len != cp.image_len) rc = PQH_ERR_DECOMPRESS;
   } else {
     const int32_t raw = cp.raw_len < cp.src_len ? cp.raw_len : cp.src_len;
-    wave_copy(dst, src, raw < cp.image_len ? raw : cp.image_len);  // DataPageV2 levels: never compressed
+    snap_copy(dst, src, raw < cp.image_len ? raw : cp.image_len);  // DataPageV2 levels: never compressed
     if (raw > cp.image_len) rc = PQH_ERR_DECOMPRESS;
     else rc = snappy_block(src + raw, cp.src_len - raw, dst + raw, int64_t(cp.image_len) - raw, E);
   }
