@@ -35,7 +35,8 @@ struct SnapLds {
   int32_t eout[kSnapMaxE + 1];    // element output start, batch-relative; eout[nE] = the batch's size
   int32_t esrc[kSnapMaxE];        // literal: block position of its bytes; copy: offset
   int32_t elen[kSnapMaxE];
-  uint16_t emap[kSnapOut];        // batch output byte -> element
+  uint16_t emap[kSnapOut];        // batch output byte -> element; then (as int16) the byte's pointer
+  uint8_t out[kSnapOut];          // the batch's output bytes
   uint8_t elit[kSnapMaxE];
   int32_t wmax[4];
   int32_t nE, bend, p_next, bad, bulk_len, bulk_src;
@@ -77,11 +78,18 @@ __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
 
 // Wave 0: the elements of one batch from block position p (the stage holds [a0, ...)), output
 // starting at d.  Results in E (nE, bend, p_next, bad, bulk_*).
-__device__ void snappy_parse(SnapLds& E, int64_t n, int32_t p, int64_t a0, int32_t d, int32_t total) {
+// Every position / count here is wave-uniform; readfirstlane makes that visible to the compiler so
+// that the readlane chain steps take their lane index from an SGPR (a lane index it believes
+// divergent turns each readlane into a loop over the wave).
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ void snappy_parse(SnapLds& E, int32_t n_, int32_t p, int32_t a0_, int32_t d_, int32_t total_) {
   const int lane = threadIdx.x & 63;
-  int32_t pos = p, k = 0, T = 0, bulk_len = 0, bulk_src = 0;
+  const int32_t n = uni(n_), a0 = uni(a0_), d = uni(d_), total = uni(total_);
+  int32_t pos = uni(p), k = 0, T = 0, bulk_len = 0, bulk_src = 0;
   bool bad = false;
   for (;;) {
+    pos = uni(pos);
     if (pos >= n || pos - a0 > kSnapStage - 64) break;  // done, or the stage is used up
     // ---- every lane: the element that would start at byte q
     const int32_t q = pos + lane;
@@ -123,13 +131,13 @@ __device__ void snappy_parse(SnapLds& E, int64_t n, int32_t p, int64_t a0, int32
     uint64_t chain = 0;
     int32_t exitp = pos;
     for (int32_t c = pos; c < pos + 64 && c < n;) {
-      const int l = c - pos;
+      const int l = uni(c - pos);
       chain |= 1ull << l;
       if (!__builtin_amdgcn_readlane(int(hdr_ok), l)) {
         bad = true;
         break;
       }
-      c = __builtin_amdgcn_readlane(nxt, l);
+      c = uni(__builtin_amdgcn_readlane(nxt, l));
       exitp = c;
     }
     if (bad) break;
@@ -163,9 +171,9 @@ __device__ void snappy_parse(SnapLds& E, int64_t n, int32_t p, int64_t a0, int32
       E.elit[k + idx] = lit;
       E.esrc[k + idx] = lit ? q + hdr : off;
     }
-    const int last = 63 - __builtin_clzll(fit);  // lane of the last element taken
-    T += __builtin_amdgcn_readlane(int32_t(excl + len), last);
-    k += m;
+    const int last = uni(63 - __builtin_clzll(fit));  // lane of the last element taken
+    T = uni(T + __builtin_amdgcn_readlane(int32_t(excl + len), last));
+    k = uni(k + m);
     if (m < __popcll(chain)) {  // batch full: the next batch starts at the first element not taken
       const uint64_t rest = chain & ~fit;
       pos += __builtin_ctzll(rest);
@@ -194,7 +202,7 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
   {
     bool done = false;
     for (int i = 0; i < 10 && i < n && !done; i++) {
-      const uint8_t c = src[i];
+      const uint8_t c = uint8_t(uni(src[i]));
       if (i == 9 && c > 1) return PQH_ERR_DECOMPRESS;  // overflows 64 bits
       v |= uint64_t(c & 0x7f) << (7 * i);
       hl = i + 1;
@@ -202,11 +210,14 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
     }
     if (!done || v > 0xffffffffull || int64_t(v) != expected) return PQH_ERR_DECOMPRESS;
   }
-  const int32_t total = int32_t(v);
-  int32_t p = hl, d = 0;
-  while (p < n) {
+  const int32_t total = uni(int32_t(v));
+  int32_t p = uni(hl), d = 0;
+  const int32_t n32 = uni(int32_t(n));
+  while (p < n32) {
+    p = uni(p);
+    d = uni(d);
     // ---- stage the compressed bytes from p (16-byte aligned start; the source payload is padded)
-    const int64_t a0 = p - int64_t((reinterpret_cast<uintptr_t>(src) + uintptr_t(p)) & 15);
+    const int32_t a0 = uni(p - int32_t((reinterpret_cast<uintptr_t>(src) + uintptr_t(p)) & 15));
     __syncthreads();  // the previous batch's readers of the stage are done
     {  // up to the block's end rounded to 16 bytes (inside the payload pad): bytes past it never
        // decide a valid element
@@ -217,16 +228,17 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       for (int u = tid; u < nu; u += kBlock) lp[u] = sp[u];
     }
     __syncthreads();
-    if (tid < 64) snappy_parse(E, n, p, a0, d, total);
+    if (tid < 64) snappy_parse(E, n32, p, a0, d, total);
     __syncthreads();
-    if (E.bad) return PQH_ERR_DECOMPRESS;
-    const int32_t nE = E.nE, T = E.bend;
+    if (uni(E.bad)) return PQH_ERR_DECOMPRESS;
+    const int32_t nE = uni(E.nE), T = uni(E.bend);
     if (nE == 0) {
-      if (E.bulk_len > 0) {
-        snap_copy(dst + d, src + E.bulk_src, E.bulk_len);
-        d += E.bulk_len;
+      const int32_t bl = uni(E.bulk_len);
+      if (bl > 0) {
+        snap_copy(dst + d, src + uni(E.bulk_src), bl);
+        d += bl;
       }
-      p = E.p_next;
+      p = uni(E.p_next);
       __syncthreads();  // the bulk bytes are visible to the next batches' reads
       continue;
     }
@@ -256,56 +268,108 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       }
     }
     __syncthreads();
-    // ---- the batch's bytes: resolved in LDS, the HBM reads of 8 bytes issued together
-    const int64_t s_lo = a0, s_hi = a0 + kSnapStage + 96;
-    for (int b0 = 0; b0 < T; b0 += 8 * kBlock) {
+    // ---- the batch's bytes.  Each byte is either known at once (a literal byte: from the stage or
+    // HBM; a copy byte whose source precedes the batch: read back from HBM) or points at an earlier
+    // byte of the batch; pointer jumping then resolves every chain in O(log length) rounds.
+    constexpr int kPer = kSnapOut / kBlock;  // 32 bytes per thread: b = i * kBlock + tid
+    const int32_t s_lo = a0, s_hi = a0 + kSnapStage + 96;
+    int16_t ptr[kPer];
+    uint8_t val[kPer];
+#pragma unroll
+    for (int i0 = 0; i0 < kPer; i0 += 8) {
       int32_t ga[8];
-      uint8_t val[8];
-      uint8_t from[8];  // 0 resolved, 1 dst (an earlier batch), 2 src (a literal outside the stage)
+      uint8_t from[8];  // 0 resolved / in-batch pointer, 1 dst (an earlier batch), 2 src (literal outside the stage)
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        const int32_t b = b0 + j * kBlock + tid;
+        const int32_t b = (i0 + j) * kBlock + tid;
         from[j] = 0;
-        val[j] = 0;
         ga[j] = 0;
+        val[i0 + j] = 0;
+        ptr[i0 + j] = -1;
         if (b >= T) continue;
-        int32_t pos = b;
-        for (;;) {
-          const int e = E.emap[pos];
-          const int32_t rel = pos - E.eout[e];
-          if (E.elit[e]) {
-            const int32_t sp = E.esrc[e] + rel;
-            if (sp >= s_lo && sp < s_hi) {
-              val[j] = E.in[sp - s_lo];
-            } else {
-              from[j] = 2;
-              ga[j] = sp;
-            }
-            break;
+        const int e = E.emap[b];
+        const int32_t rel = b - E.eout[e];
+        if (E.elit[e]) {
+          const int32_t sp = E.esrc[e] + rel;
+          if (sp >= s_lo && sp < s_hi) {
+            val[i0 + j] = E.in[sp - s_lo];
+          } else {
+            from[j] = 2;
+            ga[j] = sp;
           }
-          const int32_t o = E.esrc[e];
-          const int32_t sabs = d + E.eout[e] - o + (o < E.elen[e] ? rel % o : rel);  // overlapping copies repeat
-          if (sabs >= d) {
-            pos = sabs - d;
-            continue;
-          }
+          continue;
+        }
+        const int32_t o = E.esrc[e];
+        const int32_t sabs = d + E.eout[e] - o + (o < E.elen[e] ? rel % o : rel);  // overlapping copies repeat
+        if (sabs >= d) {
+          ptr[i0 + j] = int16_t(sabs - d);
+        } else {
           from[j] = 1;
           ga[j] = sabs;
-          break;
         }
       }
 #pragma unroll
-      for (int j = 0; j < 8; j++)
-        if (from[j]) val[j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+      for (int j = 0; j < 8; j++)  // the HBM reads of 8 bytes in flight together
+        if (from[j]) val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+    }
+    __syncthreads();  // emap no longer read: it becomes the pointer array
+    int16_t* P = reinterpret_cast<int16_t*>(E.emap);
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int32_t b = b0 + j * kBlock + tid;
-        if (b < T) dst[d + b] = val[j];
+    for (int i = 0; i < kPer; i++) {
+      const int32_t b = i * kBlock + tid;
+      if (b < T) {
+        P[b] = ptr[i];
+        E.out[b] = val[i];
       }
+    }
+    __syncthreads();
+    for (;;) {
+      // read half: a pointer to a resolved byte takes its value, otherwise jumps to its target's pointer
+      int pending = 0;
+#pragma unroll
+      for (int i = 0; i < kPer; i++) {
+        if (ptr[i] < 0) continue;
+        const int16_t q = P[ptr[i]];
+        if (q < 0) val[i] = E.out[ptr[i]];
+        else pending = 1;
+        ptr[i] = q;
+      }
+      const int more = __syncthreads_or(pending);
+      // write half
+#pragma unroll
+      for (int i = 0; i < kPer; i++) {
+        const int32_t b = i * kBlock + tid;
+        if (b < T) {
+          P[b] = ptr[i];
+          E.out[b] = val[i];
+        }
+      }
+      __syncthreads();
+      if (!more) break;
+    }
+    // ---- the batch to HBM: bytes until dst is 16-byte aligned, then 16-byte stores
+    {
+      uint8_t* o = dst + d;
+      const int32_t head0 = int32_t((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
+      const int32_t head = head0 < T ? head0 : T;
+      if (tid < head) o[tid] = E.out[tid];
+      const int32_t units = (T - head) >> 4;
+      for (int32_t u = tid; u < units; u += kBlock) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int32_t x = head + 16 * u + 4 * q;
+          w[q] = uint32_t(E.out[x]) | (uint32_t(E.out[x + 1]) << 8) | (uint32_t(E.out[x + 2]) << 16) |
+                 (uint32_t(E.out[x + 3]) << 24);
+        }
+        *reinterpret_cast<uint4*>(o + head + 16 * u) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      const int32_t done = head + units * 16;
+      if (tid < T - done) o[done + tid] = E.out[done + tid];
     }
     __syncthreads();  // this batch's bytes are visible to the next batches' reads
     d += T;
-    p = E.p_next;
+    p = uni(E.p_next);
   }
   return d == total ? PQH_OK : PQH_ERR_DECOMPRESS;
 }
