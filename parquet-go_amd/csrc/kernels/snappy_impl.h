@@ -30,13 +30,13 @@ constexpr int kSnapStage = 8192;  // compressed input bytes staged in LDS per ba
 constexpr int kSnapOut = 8192;    // output bytes per batch (a longer literal: bulk copy)
 constexpr int kSnapMaxE = 1024;   // elements per batch
 
-struct SnapLds {
+struct __attribute__((aligned(16))) SnapLds {
   uint8_t in[kSnapStage + 96];    // the stage: block bytes [a0, a0 + kSnapStage + 96)
+  uint16_t emap[kSnapOut];        // batch output byte -> element; then (as int16) the byte's pointer
+  uint8_t out[kSnapOut];          // the batch's output bytes
   int32_t eout[kSnapMaxE + 1];    // element output start, batch-relative; eout[nE] = the batch's size
   int32_t esrc[kSnapMaxE];        // literal: block position of its bytes; copy: offset
   int32_t elen[kSnapMaxE];
-  uint16_t emap[kSnapOut];        // batch output byte -> element; then (as int16) the byte's pointer
-  uint8_t out[kSnapOut];          // the batch's output bytes
   uint8_t elit[kSnapMaxE];
   int32_t wmax[4];
   int32_t nE, bend, p_next, bad, bulk_len, bulk_src;
@@ -94,8 +94,9 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, int32_t n_, int32_t p, 
     // ---- every lane: the element that would start at byte q
     const int32_t q = pos + lane;
     const int32_t o8 = int32_t(q - a0);
-    uint64_t w;
-    __builtin_memcpy(&w, E.in + o8, 8);
+    // bytes q..q+4 from two aligned LDS dwords
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(E.in);
+    const uint64_t w = ((uint64_t(in32[(o8 >> 2) + 1]) << 32) | in32[o8 >> 2]) >> (8 * (o8 & 3));
     const uint32_t tag = uint32_t(w & 0xff);
     int32_t hdr, off = 0;
     int64_t len;
@@ -127,23 +128,38 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, int32_t n_, int32_t p, 
     const bool hdr_ok = int64_t(q) + hdr <= n;
     const int64_t nx64 = int64_t(q) + hdr + (lit ? len : 0);
     const int32_t nxt = nx64 > n ? int32_t(n) + 1 : int32_t(nx64);  // past the input: invalid below
-    // ---- the true chain from pos (wave-uniform)
-    uint64_t chain = 0;
-    int32_t exitp = pos;
-    for (int32_t c = pos; c < pos + 64 && c < n;) {
-      const int l = uni(c - pos);
-      chain |= 1ull << l;
-      if (!__builtin_amdgcn_readlane(int(hdr_ok), l)) {
-        bad = true;
-        break;
+    // ---- the true chain from pos: pointer doubling over the window's lanes.  R = lanes on the path
+    // from this lane within 2^k steps, J = the lane 2^k steps on (64: the path left the window).
+    const bool here = q < n;
+    uint64_t R = here ? 1ull << lane : 0;
+    int32_t J = here ? (nxt - pos < 64 ? nxt - pos : 64) : 64;
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const int32_t src_lane = J < 64 ? J : lane;
+      const uint64_t Rn = __shfl(R, src_lane, 64);
+      const int32_t Jn = __shfl(J, src_lane, 64);
+      if (J < 64) {
+        R |= Rn;
+        J = Jn;
       }
-      c = uni(__builtin_amdgcn_readlane(nxt, l));
-      exitp = c;
     }
-    if (bad) break;
+    const uint64_t chain = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(R >> 32)))) << 32) |
+                           uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(R)));  // lane 0's path
     const bool on = (chain >> lane) & 1;
+    if (__ballot(on && !hdr_ok)) {  // an element header past the input
+      bad = true;
+      break;
+    }
+    const int32_t exitp = uni(__builtin_amdgcn_readlane(nxt, 63 - __builtin_clzll(chain)));
     const int idx = __popcll(chain & ((1ull << lane) - 1));
-    const int64_t excl = wave_excl_scan64(on ? len : 0);
+    // output positions: a 32-bit DPP scan unless some element is 16 MiB or longer
+    int64_t excl;
+    if (__ballot(on && len >= (1 << 24)) == 0) {
+      const uint32_t x = on ? uint32_t(len) : 0u;
+      excl = int64_t(wave_incl_scan32(x) - x);
+    } else {
+      excl = wave_excl_scan64(on ? len : 0);
+    }
     const int64_t eo = int64_t(d) + T + excl;  // stream output position
     bool ebad = false;
     if (on) {
@@ -243,29 +259,54 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       continue;
     }
     // ---- output byte -> element: start markers, then a max-scan (element ids rise with output)
-    for (int i = tid; i < T; i += kBlock) E.emap[i] = 0;
+    {  // every thread owns 32 consecutive entries (64 bytes: four 16-byte LDS accesses)
+      uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
+#pragma unroll
+      for (int k = 0; k < 4; k++) m4[k] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
     for (int e = tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
     __syncthreads();
     {
-      constexpr int per = kSnapOut / kBlock;  // 32 entries per thread
-      const int i0 = tid * per;
-      int32_t mx = 0;
-      for (int i = i0; i < i0 + per && i < T; i++) mx = E.emap[i] > mx ? E.emap[i] : mx;
-      int32_t incl = mx;  // inclusive max over the threads before
+      uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
+      uint32_t wv[16];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint4 x = m4[k];
+        wv[4 * k] = x.x;
+        wv[4 * k + 1] = x.y;
+        wv[4 * k + 2] = x.z;
+        wv[4 * k + 3] = x.w;
+      }
+      uint32_t mx = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
+        mx = a > mx ? a : mx;
+        mx = c > mx ? c : mx;
+      }
+      int32_t incl = int32_t(mx);  // inclusive max over the threads before
       for (int o = 1; o < 64; o <<= 1) {
         const int32_t y = __shfl_up(incl, o, 64);
         if ((tid & 63) >= o) incl = y > incl ? y : incl;
       }
       if ((tid & 63) == 63) E.wmax[tid >> 6] = incl;
       __syncthreads();
-      int32_t run = __shfl_up(incl, 1, 64);
-      if ((tid & 63) == 0) run = 0;
-      for (int wv = 0; wv < (tid >> 6); wv++) run = E.wmax[wv] > run ? E.wmax[wv] : run;
-      for (int i = i0; i < i0 + per && i < T; i++) {
-        run = E.emap[i] > run ? E.emap[i] : run;
-        E.emap[i] = uint16_t(run);
+      int32_t runv = __shfl_up(incl, 1, 64);
+      if ((tid & 63) == 0) runv = 0;
+      for (int w8 = 0; w8 < (tid >> 6); w8++) runv = E.wmax[w8] > runv ? E.wmax[w8] : runv;
+      uint32_t run = uint32_t(runv);
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
+        run = a > run ? a : run;
+        a = run;
+        run = c > run ? c : run;
+        c = run;
+        wv[k] = a | (c << 16);
       }
+#pragma unroll
+      for (int k = 0; k < 4; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
     }
     __syncthreads();
     // ---- the batch's bytes.  Each byte is either known at once (a literal byte: from the stage or
