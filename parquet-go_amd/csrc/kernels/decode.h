@@ -95,22 +95,23 @@ struct DevChunk {
   int32_t batile_n;
 };
 
-// Written by the prologue (one wave per page) and the scan kernel.
+// Written by the prologue (one wave per page) and the scan kernel.  64 bytes.
 struct PageState {
   unsigned long long err;  // min err_key, kNoError if none
   int32_t nn;              // not-null count
-  int32_t width;           // bit width of the value hybrid stream (dictionary / RLE boolean)
+  int16_t width;           // bit width of the value hybrid stream (dictionary / RLE boolean)
+  int16_t ba_summed;       // byte-array data page: its kBaTile byte sums were accumulated by the
+                           // length producers (k_ba_wemit / k_delta_page), so k_ba_sum skips it
   int32_t rep_s, rep_e;    // byte ranges in the image; s < 0 = uninitialised decoder
   int32_t def_s, def_e;
   int32_t val_s, val_e;    // values section / value hybrid stream
   int32_t val_limit;       // values before the first phase-3 stream error (== nn if none)
   int32_t dict_n;          // dictionary pages: entries decoded
-  int32_t ba_summed;       // byte-array data page: its kBaTile byte sums were accumulated by the
-                           // length producers (k_ba_wemit / k_delta_page), so k_ba_sum skips it
-  int32_t pad;
   int64_t value_base;      // first value of the page in the chunk's dense values
   int64_t byte_base;       // byte arrays: first byte
 };
+
+static_assert(sizeof(PageState) == 64, "PageState is one 64-byte record");
 
 // DELTA_BINARY_PACKED (deltabp_decoder.go): per page, written by k_delta_walk.
 enum DeltaMode : int32_t { DM_NONE = 0, DM_FAST = 1, DM_SERIAL = 2 };

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
   S.val_s = S.val_e = 0;
   S.val_limit = 0;
   S.dict_n = 0;
-  S.ba_summed = S.pad = 0;
+  S.ba_summed = 0;
   S.value_base = 0;
   S.byte_base = 0;
   uint64_t err = P.host_err;
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
         } else {
           const int w = img[vs];
           if (w > 32) err = err_key(0, 3, PQH_ERR_DICT_BIT_WIDTH);
-          S.width = w;
+          S.width = int16_t(w);
           hs = vs + 1;
         }
       } else if (P.kind == K_RLE_BOOL) {  // booleanRLEDecoder.init -> initSize (type_boolean.go:104-107)
