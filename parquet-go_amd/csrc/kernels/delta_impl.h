@@ -910,6 +910,7 @@ __device__ bool stage_tile(const DevBatch& b, const DevPage& P, const DeltaState
   const int lbs = __builtin_ctz(uint32_t(D.block_size));
   const int bb0 = int(v0 >> lbs), nb = int(((v1 - 1) >> lbs)) - bb0 + 1;
   const int mbc = D.mb_count, gbytes = D.mbvc / 8;
+  if (nb > kTileBlocks || bb0 + nb > D.nblocks) return false;  // (uniform) not stageable
   __shared__ int64_t s_start, s_end;
   if (threadIdx.x < nb) {
     const DeltaBlock r = load_block(recs, bb0 + threadIdx.x, img, P.kind == K_DELTA64, mbc);
@@ -926,6 +927,8 @@ __device__ bool stage_tile(const DevBatch& b, const DevPage& P, const DeltaState
   }
   __syncthreads();
   const int64_t start = s_start, end = s_end;
+  // the blocks' data must lie inside the page image (records are offsets into it)
+  if (start < 0 || end < start || end > int64_t(P.image_len)) return false;
   const int64_t a0 = start - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(start)) & 15);
   const int64_t nvec = (end - a0 + 15) >> 4;
   if (nvec * 16 > kTileStage) return false;
