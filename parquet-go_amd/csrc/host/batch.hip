@@ -64,8 +64,9 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_ba_wspec",   "k_ba_sum",    "k_ba_scan",    "k_ba_expand",
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
-                              "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy"};
-constexpr int kNumKernels = 23;
+                              "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
+                              "k_ba_wcopy"};
+constexpr int kNumKernels = 24;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -204,6 +205,8 @@ struct pqh_batch {
   int32_t ba_ncopy = 0;             //   (the first ba_ncopy go to k_ba_expand, the rest to k_ba_gather)
   std::vector<int32_t> ba_pages;    // PLAIN byte-array data + dictionary pages (chain walks)
   std::vector<int2> ba_wins, ba_pwin;
+  std::vector<int2> ba_wlist;       // {window, page}: dictionary pages' windows (k_ba_wemit), then data pages' (k_ba_wcopy)
+  int32_t ba_wdict = 0;             // dictionary windows at the front of ba_wlist
   std::vector<int32_t> ba_chunks;   // k_ba_scan work list
   std::vector<int64_t> chunk_bytes; // host copy after sync
   std::vector<DevNest> nests;       // repeated chunks with nesting outputs
@@ -244,6 +247,7 @@ struct pqh_batch {
   int32_t* d_ba_pages = nullptr;
   int2* d_ba_wins = nullptr;        // (page, window) of every PLAIN chain window
   int2* d_ba_pwin = nullptr;        // per PLAIN page: (first window, windows)
+  int2* d_ba_wlist = nullptr;
   BaWin* d_ba_res = nullptr;
   int32_t* d_ba_wrec = nullptr;     // per window: its records' lengths / cumulative bytes
   int32_t* d_ba_chunks = nullptr;
@@ -607,6 +611,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       b->ba_pwin.push_back(make_int2(int32_t(b->ba_wins.size()), nw));
       for (int32_t w = 0; w < nw; w++) b->ba_wins.push_back(make_int2(p, w));
     }
+    for (int dict = 1; dict >= 0; dict--) {
+      for (size_t i = 0; i < b->ba_wins.size(); i++) {
+        const int32_t p = b->ba_wins[i].x;
+        if ((b->hpages[size_t(p)].page_type == PQH_DICTIONARY_PAGE) == bool(dict))
+          b->ba_wlist.push_back(make_int2(int32_t(i), p));
+      }
+      if (dict) b->ba_wdict = int32_t(b->ba_wlist.size());
+    }
     b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
@@ -628,12 +640,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   for (size_t i = 0; i < b->ba_tiles.size(); i++)
     if (b->hpages[size_t(b->ba_tiles[i].page)].kind == K_DLBA) b->ba_xlist.push_back(int32_t(i));
   b->ba_ncopy = int32_t(b->ba_xlist.size());
-  for (size_t i = 0; i < b->ba_tiles.size(); i++) {
+  for (size_t i = 0; i < b->ba_tiles.size(); i++) {  // dictionary tiles (PLAIN pages: k_ba_wcopy)
     const int32_t k = b->hpages[size_t(b->ba_tiles[i].page)].kind;
-    if (k != K_DLBA && k != K_DBA) b->ba_xlist.push_back(int32_t(i));
+    if (k != K_DLBA && k != K_DBA && k != K_PLAIN_BA) b->ba_xlist.push_back(int32_t(i));
   }
   // k_ba_sum's work list (after the copy + gather lists): every tile, except that PLAIN pages (and in
-  // page mode DELTA_LENGTH pages) are represented by their tile 0: their sums come from k_ba_wemit
+  // page mode DELTA_LENGTH pages) are represented by their tile 0: their sums come from k_ba_wstitch
   // (the delta kernels); the tile-0 workgroup checks that and otherwise sums the whole page
   b->ba_sum_off = int32_t(b->ba_xlist.size());
   for (size_t i = 0; i < b->ba_tiles.size(); i++) {
@@ -662,6 +674,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wins), sizeof(int2) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pwin), sizeof(int2) * b->ba_pwin.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wlist), sizeof(int2) * b->ba_wlist.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_res), sizeof(BaWin) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wrec), sizeof(int32_t) * size_t(kChainRecs) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
@@ -768,6 +781,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       {b->d_ba_pages, b->ba_pages.data(), sizeof(int32_t) * b->ba_pages.size()},
       {b->d_ba_wins, b->ba_wins.data(), sizeof(int2) * b->ba_wins.size()},
       {b->d_ba_pwin, b->ba_pwin.data(), sizeof(int2) * b->ba_pwin.size()},
+      {b->d_ba_wlist, b->ba_wlist.data(), sizeof(int2) * b->ba_wlist.size()},
       {b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size()},
       {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
       {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
@@ -854,7 +868,9 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
         return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_wrec, st);
       });
     if (e == hipSuccess)
-      e = timed(21, nw, s, [&](hipStream_t st) { return launch_ba_wemit(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
+      e = timed(21, b->ba_wdict, s, [&](hipStream_t st) {
+        return launch_ba_wemit(d, b->d_ba_wlist, b->ba_wdict, b->d_ba_res, b->d_ba_wrec, st);
+      });
   }
   if (e == hipSuccess && ndt && b->delta_page_mode) {
     const int32_t nds = int32_t(b->delta_streams.size());
@@ -882,6 +898,11 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     if (e == hipSuccess)
       e = timed(10, nbt, s, [&](hipStream_t st) {  // k_ba_expand + k_ba_gather
         return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, b->ba_sum_off - b->ba_ncopy, st);
+      });
+    const int32_t nwd = int32_t(b->ba_wlist.size()) - b->ba_wdict;
+    if (e == hipSuccess && nwd)
+      e = timed(23, nwd, s, [&](hipStream_t st) {
+        return launch_ba_wcopy(d, b->d_ba_wlist + b->ba_wdict, nwd, b->d_ba_res, b->d_ba_wrec, st);
       });
     if (e == hipSuccess && b->has_dba)
       e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });
@@ -1016,7 +1037,7 @@ int pqh_batch_sync(pqh_batch* b) {
   b->event_next = 0;
   // algorithmic bytes of one run: page bytes read once, dictionaries once per
   // chunk, decoded bytes written; attributed to the kernel that moves them.
-  double wr = 0;
+  double wr = 0, plain_written = 0;
   std::fill(b->k_read.begin(), b->k_read.end(), 0.0);
   std::fill(b->k_written.begin(), b->k_written.end(), 0.0);
   for (size_t p = 0; p < b->pages.size(); p++) {
@@ -1064,7 +1085,14 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[kd] += vals;
         break;
       }
-      case K_PLAIN_BA:  // walked by k_ba_wspec / k_ba_wstitch / k_ba_wemit, bytes moved by k_ba_expand
+      case K_PLAIN_BA:  // walked by k_ba_wspec / k_ba_wstitch; values read and offsets + bytes written by k_ba_wcopy
+        b->k_read[23] += S.val_e - S.val_s;
+        if (S.err == kNoError) {
+          const double w = double(S.nn) * 8 + double(S.val_e - S.val_s - 4 * int64_t(S.nn));
+          b->k_written[23] += w;
+          plain_written += w;
+        }
+        break;
       case K_DLBA:
       case K_DBA:
         b->k_read[10] += S.val_e - S.val_s;
@@ -1089,6 +1117,7 @@ int pqh_batch_sync(pqh_batch* b) {
     wr += w;
     b->k_written[10] += w;
   }
+  b->k_written[10] -= plain_written;  // the PLAIN pages' share went to k_ba_wcopy
   for (size_t i = 0; i < b->nests.size(); i++) {  // list offsets (4 B) + presence (1 B) per list, leaf validity
     const DevNest& N = b->nests[i];
     double w = 0;

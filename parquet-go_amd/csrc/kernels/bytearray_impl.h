@@ -50,6 +50,16 @@ struct ChainLds {
   uint64_t wsum[4];
 };
 
+// Workgroup sum (every thread gets it).
+__device__ __forceinline__ int64_t block_sum64(int64_t x, int64_t* wsum) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  __syncthreads();
+  if (lane == 0) wsum[wv] = x;
+  __syncthreads();
+  return wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
 // One record at page offset p (window-relative o): 0 and the next offset, or the error code.
 __device__ __forceinline__ int chain_step(const ChainLds& C, int64_t wb, int64_t e0, int64_t p, int64_t& next,
                                           int32_t& len) {
@@ -272,8 +282,8 @@ __device__ __forceinline__ BaPageCtx ba_page_ctx(const DevBatch& b, int p) {
 }
 
 // Stage, resolve and summarise one window (whole workgroup).  Its records go to the window's scratch
-// in order: lengths (data pages) or the bytes before each record within the window (dictionary
-// pages; one more entry holds the window's total).
+// in order as the bytes of the records before each one within the window (one more entry holds the
+// window's total): record i's length is wrec[i + 1] - wrec[i].
 __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry, BaWin* res, int32_t* wrec) {
   const int j = threadIdx.x;
   const int64_t wend = c.entry + (w + 1) * kChainStride;
@@ -300,23 +310,21 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
     return int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
   };
   int64_t bytes = 0;
-  if (c.dict) {
 #pragma unroll
-    for (int k = 0; k < kChainWords; k++)
-      for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(s0 + __builtin_ctzll(x) + 64 * k);
-  }
+  for (int k = 0; k < kChainWords; k++)
+    for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(s0 + __builtin_ctzll(x) + 64 * k);
   uint64_t tot, btot = 0;
   int32_t li = int32_t(block_exclusive_scan(uint64_t(cnt), C.wsum, &tot));
-  int64_t lb = c.dict ? int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot)) : 0;
+  int64_t lb = int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot));
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
     for (uint64_t x = m[k]; x; x &= x - 1) {
       const int32_t l = len_lds(s0 + __builtin_ctzll(x) + 64 * k);
-      wrec[li++] = c.dict ? int32_t(lb) : l;
+      wrec[li++] = int32_t(lb);
       lb += l;
     }
   if (j == 0) {
-    if (c.dict) wrec[tot] = int32_t(btot);
+    wrec[tot] = int32_t(btot);
     r.count = int32_t(tot);
     r.bytes = int64_t(btot);
     if (fb < kBlock) {
@@ -365,13 +373,10 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
   const int2 wr = pwin[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, p);
   if (!c.ok) return;
-  if (!c.dict) {  // k_ba_wemit adds the tile byte sums of the page's lengths
-    const DevPage P = b.pages[p];
-    for (int k = threadIdx.x; k < P.batile_n; k += kBlock) b.basums[P.batile_base + k] = 0;
-  }
   int64_t done = 0, cum = 0, T = c.entry;
+  int64_t last_base = 0, last_cbase = 0;  // the last window taken: records and bytes before it
   int code = PQH_OK;
-  int w = 0;
+  int w = 0, last = -1;
   for (; w < wr.y && done < c.count; w++) {
     BaWin* r = res + wr.x + w;
     if (T >= c.e0) {  // no bytes left for the next length
@@ -391,6 +396,9 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
       r->base = done;
       r->cbase = cum;
     }
+    last = w;
+    last_base = done;
+    last_cbase = cum;
     done += cur.count;
     cum += cur.bytes;
     if (cur.bad) {
@@ -399,6 +407,17 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
       break;
     }
     T = cur.exit;
+  }
+  if (!c.dict) {
+    // the page's bytes before its value limit (min(count, records on the chain)) go to tile 0 of its
+    // byte sums, the other tiles get 0: k_ba_scan turns them into the page's byte_base, and
+    // k_ba_wcopy places every window at byte_base + cbase
+    int64_t total = cum;
+    if (done > c.count && last >= 0) {  // the last window holds records past `count`
+      total = last_cbase + wrec[int64_t(wr.x + last) * kChainRecs + (c.count - last_base)];
+    }
+    const DevPage P = b.pages[p];
+    for (int k = threadIdx.x; k < P.batile_n; k += kBlock) b.basums[P.batile_base + k] = k == 0 ? total : 0;
   }
   if (threadIdx.x == 0) {
     for (; w < wr.y; w++) res[wr.x + w].base = -1;  // windows past the chain's end or `count`
@@ -420,46 +439,24 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
   }
 }
 
-// One workgroup per window: its records' lengths (data page -> aux) or cumulative offsets
-// (dictionary page -> dcum) copied out at the window's base.  Data pages: the lengths before the
-// page's value limit are also added to the page's kBaTile byte sums (k_ba_wstitch zeroed them), so
-// k_ba_sum does not read them again.
-__global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* wins, const BaWin* res,
+// Dictionary pages, one workgroup per window (list: {window, page}): the window's records as
+// cumulative offsets (dcum) at its base.  Data-page windows go to k_ba_wcopy.
+__global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* list, const BaWin* res,
                                                    const int32_t* wrec) {
-  const BaWin r = res[blockIdx.x];
+  const int2 wl = list[blockIdx.x];
+  const BaWin r = res[wl.x];
   if (r.base < 0 || r.entry < 0) return;
-  const int p = wins[blockIdx.x].x;
+  const int p = wl.y;
   const BaPageCtx c = ba_page_ctx(b, p);
-  if (!c.ok) return;
-  const int32_t* src = wrec + int64_t(blockIdx.x) * kChainRecs;
-  if (c.dict) {
-    PQH_G int32_t* out = (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base);
-    for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
-      const int64_t idx = r.base + i;
-      if (idx >= c.count) break;
-      out[idx] = int32_t(r.cbase + src[i]);
-      if (idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
-    }
-    return;
-  }
-  const PageState S = b.states[p];
-  const DevPage P = b.pages[p];
-  PQH_G int32_t* out = b.chunks[P.chunk].aux + S.value_base;
-  const int64_t lim = S.val_limit < c.count ? S.val_limit : c.count;
-  const int wv = threadIdx.x >> 6;
-  WaveTileSum wts{(r.base + 64 * wv) / kBaTile, 0};
-  for (int32_t i0 = 0; i0 < r.count; i0 += kBlock) {  // uniform trip count (wave-wide sums)
-    const int32_t i = i0 + int32_t(threadIdx.x);
+  if (!c.ok || !c.dict) return;
+  const int32_t* src = wrec + int64_t(wl.x) * kChainRecs;
+  PQH_G int32_t* out = (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base);
+  for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
     const int64_t idx = r.base + i;
-    int32_t l = 0;
-    if (i < r.count && idx < c.count) {
-      l = src[i];
-      out[idx] = l;
-    }
-    const int64_t w0 = r.base + i0 + 64 * wv;
-    wave_tile_add(wts, b.basums + P.batile_base, w0, w0 + 63, idx, idx < lim && l > 0 ? uint64_t(l) : 0);
+    if (idx >= c.count) break;
+    out[idx] = int32_t(r.cbase + src[i]);
+    if (idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
   }
-  flush_tile_sum(b.basums + P.batile_base, wts.tacc, wts.acc);
 }
 
 // Values of a byte-array data page that decode before the first error known so far.
@@ -509,15 +506,6 @@ __device__ __forceinline__ int64_t ba_len(const BaDict& d, bool is_dict, int32_t
   if (!is_dict) return a;
   const uint32_t k = uint32_t(a);
   return k < d.K ? int64_t(d.dcum[k + 1]) - d.dcum[k] : 0;
-}
-
-__device__ __forceinline__ int64_t block_sum64(int64_t x, int64_t* wsum) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-  __syncthreads();
-  if (lane == 0) wsum[wv] = x;
-  __syncthreads();
-  return wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -981,4 +969,179 @@ __global__ __launch_bounds__(256) void k_ba_gather(DevBatch b, const Tile* tiles
   __shared__ int64_t s_off[kBaTile + 1];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kBaOut + 16];
   ba_expand_tile<true>(b, tiles[list[blockIdx.x]], wsum, s_off, s_out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_ba_wcopy: PLAIN byte-array data pages, after k_ba_scan, by chain windows (list: {window, page}).
+// A window's records are consecutive values of its page; k_ba_wspec left the bytes before each
+// record within the window (exclusive offsets) in the window's scratch, and the records' bytes are
+// the window's page bytes with the u32 length fields dropped (byteArrayPlainDecoder.next,
+// type_bytearray.go:24-45): record i's bytes start at entry + 4 (i + 1) + offset_i.
+//   * the window's page bytes (aligned 16-byte loads) and its offsets are staged in LDS, all loads
+//     in flight together;
+//   * one thread per record writes its chunk offset and copies its bytes from the stage (dwords
+//     through alignbit, stored unaligned; neighbouring lanes write neighbouring records);
+//   * the grid is persistent: a few workgroups per CU loop over the windows, the next window's
+//     metadata chain (window -> page, state -> chunk) loading while this one is copied;
+//   * a window whose last record runs past the stage (a string of more than ~1 KiB at its end)
+//     copies straight from the page: short records per thread, long ones by the workgroup.
+// ------------------------------------------------------------------------------------------------
+constexpr int kWStage = 33024;  // staged page bytes: a window plus ~1 KiB of overrun
+constexpr int kWV = (kWStage / 16 + kBlock - 1) / kBlock;  // 9 page vectors per thread
+constexpr int kWP = (kChainRecs / 2 + kBlock) / kBlock;    // 16 offset pairs per thread
+constexpr int kWGrid = 3 * 256;                             // resident workgroups (3 per CU)
+
+struct WcopyLds {
+  uint32_t stage[kWStage / 4 + 4];
+  uint16_t offs[kChainRecs + 8];  // the window's exclusive offsets (staged windows: < 2^16)
+};
+
+// One window's geometry and destination (wave-uniform; loaded one window ahead).
+struct WGeo {
+  int32_t wi, n;     // window, records to emit (0: nothing)
+  int32_t in_lead;   // page bytes before the entry in its 16-byte vector
+  int32_t nvec;      // staged 16-byte vectors (0: the window is not staged)
+  int64_t entry;
+  int64_t obase;     // chunk-relative first output byte of the window
+  int64_t cap;       // output bytes the chunk can take from the window on
+  const PQH_G uint8_t* img;
+  PQH_G uint8_t* dst;
+  PQH_G int64_t* offs_out;
+};
+
+__device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const BaWin* res, int t) {
+  WGeo g{};
+  const int2 wl = list[t];
+  const BaWin r = res[wl.x];
+  const DevPage P = b.pages[wl.y];
+  const PageState S = b.states[wl.y];
+  g.wi = wl.x;
+  g.n = 0;
+  if (r.base < 0 || r.entry < 0 || page_failed_before_values(S)) return g;
+  int64_t n = ba_limit(b, wl.y, P, S) - r.base;
+  if (n > r.count) n = r.count;
+  if (n <= 0) return g;
+  const DevChunk C = b.chunks[P.chunk];
+  g.n = int32_t(n);
+  g.img = b.payload + P.image_off;
+  g.entry = r.entry;
+  g.in_lead = int32_t(reinterpret_cast<uintptr_t>(g.img + r.entry) & 15);
+  // exit - entry >= the page bytes of the records (lengths and strings)
+  const int64_t span = g.in_lead + (int64_t(r.exit) - r.entry);
+  g.nvec = span <= kWStage ? int32_t((span + 15) >> 4) : 0;
+  g.obase = S.byte_base + r.cbase;
+  g.cap = C.bytes_cap - g.obase;
+  g.dst = C.bytes + g.obase;
+  g.offs_out = (PQH_G int64_t*)(C.offsets + S.value_base + 1 + r.base);
+  return g;
+}
+
+__global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const int2* list, int32_t nlist, const BaWin* res,
+                                                   const int32_t* wrec) {
+  __shared__ WcopyLds L;
+  const int tid = threadIdx.x;
+  int t = blockIdx.x;
+  if (t >= nlist) return;
+  WGeo g = wgeo(b, list, res, t);
+  for (;;) {
+    const int tn = t + int(gridDim.x);
+    WGeo gn{};
+    if (tn < nlist) gn = wgeo(b, list, res, tn);  // in flight during this window
+    const int n = g.n;
+    const PQH_G int32_t* wo = (const PQH_G int32_t*)(wrec + int64_t(g.wi) * kChainRecs);
+    typedef uint32_t u32u __attribute__((aligned(1)));
+    if (n > 0 && g.nvec) {
+      // page vectors and offset pairs: every load unconditional (clamped addresses) and every LDS
+      // store too (out-of-range ones to spare slots), so all of them stay in flight together
+      const PQH_G uint8_t* wb = g.img + g.entry - g.in_lead;
+      uint4 x[kWV];
+      int2 ov[kWP];
+#pragma unroll
+      for (int j = 0; j < kWV; j++) {
+        const int k = tid + j * kBlock;
+        x[j] = *reinterpret_cast<const PQH_G uint4*>(wb + (k < g.nvec ? 16 * k : 0));
+      }
+#pragma unroll
+      for (int j = 0; j < kWP; j++) {  // offsets 0 .. n (n + 1 entries; wrec holds the total at count)
+        const int k = tid + j * kBlock;
+        ov[j] = *reinterpret_cast<const PQH_G int2*>(wo + (2 * k <= n ? 2 * k : 0));
+      }
+      constexpr int kSpareVec = kWStage / 16;
+      constexpr int kSpareRec = kChainRecs + 1;
+#pragma unroll
+      for (int j = 0; j < kWV; j++) {
+        const int k = tid + j * kBlock;
+        reinterpret_cast<uint4*>(L.stage)[k < g.nvec ? k : kSpareVec] = x[j];
+      }
+#pragma unroll
+      for (int j = 0; j < kWP; j++) {
+        const int k = tid + j * kBlock;
+        L.offs[2 * k <= n ? 2 * k : kSpareRec] = uint16_t(ov[j].x);
+        L.offs[2 * k + 1 <= n ? 2 * k + 1 : kSpareRec] = uint16_t(ov[j].y);
+      }
+      __syncthreads();
+      typedef uint64_t u64u __attribute__((aligned(1)));
+      typedef uint16_t u16u __attribute__((aligned(1)));
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      typedef v4u v4uu __attribute__((aligned(1)));
+      for (int i = tid; i < n; i += kBlock) {
+        const int o = L.offs[i], e = L.offs[i + 1];
+        g.offs_out[i] = g.obase + e;
+        int l = e - o;
+        if (o + l > g.cap) l = g.cap > o ? int(g.cap - o) : 0;
+        const int sx = g.in_lead + 4 * (i + 1) + o;
+        const int w0 = sx >> 2;
+        const uint32_t sh = uint32_t(sx & 3) * 8;
+        PQH_G uint8_t* d = g.dst + o;
+        if (l <= 16) {  // short strings: five stage dwords, predicated stores, no per-byte loop
+          const uint32_t a0 = L.stage[w0], a1 = L.stage[w0 + 1], a2 = L.stage[w0 + 2], a3 = L.stage[w0 + 3],
+                         a4 = L.stage[w0 + 4];
+          const uint32_t v0 = __builtin_amdgcn_alignbit(a1, a0, sh), v1 = __builtin_amdgcn_alignbit(a2, a1, sh),
+                         v2 = __builtin_amdgcn_alignbit(a3, a2, sh), v3 = __builtin_amdgcn_alignbit(a4, a3, sh);
+          const int nw = l >> 2, tl = l & 3;
+          if (nw == 4) {
+            const v4u x4 = {v0, v1, v2, v3};
+            *reinterpret_cast<PQH_G v4uu*>(d) = x4;
+          } else {
+            if (nw >= 2) *reinterpret_cast<PQH_G u64u*>(d) = uint64_t(v0) | (uint64_t(v1) << 32);
+            if (nw & 1) *reinterpret_cast<PQH_G u32u*>(d + 4 * (nw & 2)) = (nw & 2) ? v2 : v0;
+            const uint32_t tv = nw == 0 ? v0 : nw == 1 ? v1 : nw == 2 ? v2 : v3;
+            PQH_G uint8_t* dt = d + 4 * nw;
+            if (tl & 2) *reinterpret_cast<PQH_G u16u*>(dt) = uint16_t(tv);
+            if (tl & 1) dt[tl & 2] = uint8_t(tv >> (8 * (tl & 2)));
+          }
+        } else {
+          int k = 0;
+          for (; k + 4 <= l; k += 4) {
+            const int q = sx + k;
+            *reinterpret_cast<PQH_G u32u*>(d + k) =
+                __builtin_amdgcn_alignbit(L.stage[(q >> 2) + 1], L.stage[q >> 2], uint32_t(q & 3) * 8);
+          }
+          for (; k < l; k++) {
+            const int q = sx + k;
+            d[k] = uint8_t(L.stage[q >> 2] >> (8 * (q & 3)));
+          }
+        }
+      }
+      __syncthreads();  // the stage is read before the next window's stores
+    } else if (n > 0) {
+      // a record runs past the stage: straight from the page
+      const PQH_G uint8_t* src0 = g.img + g.entry;
+      constexpr int kLong = 512;
+      for (int i = tid; i < n; i += kBlock) {
+        const int64_t o = wo[i], l = wo[i + 1] - o;
+        g.offs_out[i] = g.obase + o + l;
+        if (l > 0 && l < kLong && o + l <= g.cap) copy_bytes(g.dst + o, src0 + 4 * (i + 1) + o, l);
+      }
+      for (int i = 0; i < n; i++) {  // uniform: the long records by the whole workgroup
+        const int64_t o = wo[i], l = wo[i + 1] - o;
+        if (l < kLong && o + l <= g.cap) continue;
+        const int64_t cl = o + l <= g.cap ? l : g.cap - o;
+        if (cl > 0) block_copy(g.dst + o, src0 + 4 * (i + 1) + o, cl);
+      }
+    }
+    if (tn >= nlist) break;
+    g = gn;
+    t = tn;
+  }
 }

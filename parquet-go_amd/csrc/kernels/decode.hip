@@ -733,7 +733,7 @@ struct DictSink {
     }
     slow(i0, v, cnt);
   }
-  __device__ __noinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
+  __device__ __forceinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
     // unrolled over the group (v[] stays in registers); the first out-of-range key of the group
     bool ok = true;
     int jb = 8;
@@ -803,7 +803,7 @@ struct KeySink {
     }
     slow(i0, v, cnt);
   }
-  __device__ __noinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
+  __device__ __forceinline__ void slow(int64_t i0, const uint32_t* v, int cnt) const {
     int jb = 8;
 #pragma unroll
     for (int j = 7; j >= 0; j--)
@@ -1128,10 +1128,17 @@ hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const i
   return hipGetLastError();
 }
 
-hipError_t launch_ba_wemit(const DevBatch& b, const int2* wins, int32_t n, const BaWin* res, const int32_t* wrec,
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, wins, res, wrec);
+  hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, list, res, wrec);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
+                           hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_wcopy, dim3(n < kWGrid ? n : kWGrid), dim3(256), 0, s, b, list, n, res, wrec);
   return hipGetLastError();
 }
 
