@@ -27,6 +27,7 @@ struct pqh_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // staged (end-to-end) runs: pinned -> HBM copies
+  hipStream_t side = nullptr;         // unprofiled runs: branches beside the main launch sequence
   std::string err;
   // Pinned bounce buffer for every copy between HBM and pageable host memory (two halves, so the
   // host-side memcpy of one overlaps the DMA of the other).  Pageable copies never reach the HIP
@@ -229,6 +230,7 @@ struct pqh_batch {
   size_t staged_bytes = 0;
   hipEvent_t ev_copied = nullptr, ev_done = nullptr;
   bool done_recorded = false;
+  hipEvent_t ev_dep[4] = {nullptr, nullptr, nullptr, nullptr};  // fork / join points of the side branches
   DevPage* d_pages = nullptr;
   DevChunk* d_chunks = nullptr;
   PageState* d_states = nullptr;
@@ -285,6 +287,8 @@ void free_batch(pqh_batch* b) {
   if (b->h_staged) hipHostFree(b->h_staged);
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
   if (b->ev_done) hipEventDestroy(b->ev_done);
+  for (hipEvent_t e : b->ev_dep)
+    if (e) hipEventDestroy(e);
   if (b->gexec) hipGraphExecDestroy(b->gexec);
   if (b->graph) hipGraphDestroy(b->graph);
 }
@@ -329,7 +333,9 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
   pqh_ctx* c = new pqh_ctx();
   c->device = device;
   c->flags = flags;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+    if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return set_err(nullptr, PQH_ERR_HIP, "stream creation failed");
   }
@@ -342,6 +348,10 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipStreamDestroy(ctx->stream);
+  if (ctx->side) {
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
+  }
   if (ctx->copy_stream) {
     hipStreamSynchronize(ctx->copy_stream);
     hipStreamDestroy(ctx->copy_stream);
@@ -792,6 +802,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     if (e == hipSuccess && u.bytes) e = bounce_h2d(ctx, u.dst, u.src, u.bytes);
   if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  for (hipEvent_t& ev : b->ev_dep)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     free_batch(b);
     delete b;
@@ -834,6 +846,18 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     return e;
   };
   hipError_t e = hipSuccess;
+  // Unprofiled runs put two independent branches on the context's side stream, beside the main
+  // sequence: the PLAIN byte-array chain (k_ba_wspec / wstitch / wemit read only the prologue's
+  // page states; latency bound, so it overlaps the bandwidth-bound kernels) and the nesting kernels
+  // (read only the levels k_expand wrote; they overlap the byte-array copies).  Both rejoin before
+  // anything that reads their results.  Profiled and synchronised runs stay on one stream, so every
+  // kernel is timed alone.
+  const char* fk = getenv("PQH_FORK");
+  hipStream_t side = (!prof && !sync_each && b->ctx->side && !(fk && fk[0] == '0')) ? b->ctx->side : nullptr;
+  auto dep = [&](hipStream_t from, hipStream_t to, int k) -> hipError_t {  // `to` waits for `from`'s work so far
+    hipError_t r = hipEventRecord(b->ev_dep[k], from);
+    return r == hipSuccess ? hipStreamWaitEvent(to, b->ev_dep[k], 0) : r;
+  };
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   if (b->codec_n)  // device codecs: the page images first
     e = timed(22, b->codec_n, s, [&](hipStream_t st) {
@@ -841,6 +865,33 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
                            static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
     });
   if (e == hipSuccess) e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
+  const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
+  bool chain_open = false;  // the chain branch has not rejoined the main stream yet
+  if (e == hipSuccess && nbp) {
+    hipStream_t cs = s;
+    if (side) {
+      e = dep(s, side, 0);
+      cs = side;
+      chain_open = true;
+    }
+    const int32_t nw = int32_t(b->ba_wins.size());
+    if (e == hipSuccess)
+      e = timed(7, nw, cs, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
+    if (e == hipSuccess)
+      e = timed(20, nbp, cs, [&](hipStream_t st) {
+        return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_wrec, st);
+      });
+    if (e == hipSuccess && b->ba_wdict)
+      e = timed(21, b->ba_wdict, cs, [&](hipStream_t st) {
+        return launch_ba_wemit(d, b->d_ba_wlist, b->ba_wdict, b->d_ba_res, b->d_ba_wrec, st);
+      });
+    if (e == hipSuccess && side) e = hipEventRecord(b->ev_dep[1], side);
+  }
+  auto join_chain = [&]() -> hipError_t {
+    if (!chain_open) return hipSuccess;
+    chain_open = false;
+    return hipStreamWaitEvent(s, b->ev_dep[1], 0);
+  };
   // page mode: every delta page gets its init errors now and is chased, decoded and walked after
   // the value scan; tile mode: speculative walk + exact walk now, tiles after the scan
   int32_t ni = b->delta_page_mode ? b->delta_fused_pages : 0;
@@ -859,19 +910,6 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     if (e == hipSuccess)
       e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
   }
-  const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
-  if (e == hipSuccess && nbp) {
-    const int32_t nw = int32_t(b->ba_wins.size());
-    e = timed(7, nw, s, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
-    if (e == hipSuccess)
-      e = timed(20, nbp, s, [&](hipStream_t st) {
-        return launch_ba_wstitch(d, b->d_ba_pages, b->d_ba_pwin, nbp, b->d_ba_res, b->d_ba_wrec, st);
-      });
-    if (e == hipSuccess)
-      e = timed(21, b->ba_wdict, s, [&](hipStream_t st) {
-        return launch_ba_wemit(d, b->d_ba_wlist, b->ba_wdict, b->d_ba_res, b->d_ba_wrec, st);
-      });
-  }
   if (e == hipSuccess && ndt && b->delta_page_mode) {
     const int32_t nds = int32_t(b->delta_streams.size());
     e = timed(17, nds, s, [&](hipStream_t st) { return launch_delta_page(d, b->d_dtiles, nds, st); });
@@ -883,11 +921,28 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   }
   if (e == hipSuccess && ndp)  // pages outside the fast-path geometry (most launches exit at once)
     e = timed(14, ndp, s, [&](hipStream_t st) { return launch_delta_serial(d, b->d_delta_pages, ndp, st); });
+  // byte-array dictionary keys are checked against the dictionary sizes the chain branch found
+  if (e == hipSuccess && b->ba_wdict) e = join_chain();
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
   if (e == hipSuccess && ne)
     e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
   if (e == hipSuccess && ng)
     e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
+  const int32_t nnt = int32_t(b->nest_tiles.size()), nns = int32_t(b->nests.size());
+  bool nest_open = false;
+  if (e == hipSuccess && nnt) {  // nesting: the levels are complete
+    hipStream_t ns = s;
+    if (side) {
+      e = dep(s, side, 2);
+      ns = side;
+      nest_open = true;
+    }
+    if (e == hipSuccess) e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
+    if (e == hipSuccess) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    if (e == hipSuccess)
+      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+  }
+  if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
   if (e == hipSuccess && nbt) {
     const int32_t nsum = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
     e = timed(8, nsum, s, [&](hipStream_t st) {
@@ -907,12 +962,14 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     if (e == hipSuccess && b->has_dba)
       e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });
   }
-  const int32_t nnt = int32_t(b->nest_tiles.size()), nns = int32_t(b->nests.size());
-  if (e == hipSuccess && nnt) {
-    e = timed(11, nnt, s, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
-    if (e == hipSuccess) e = timed(12, nns, s, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
-    if (e == hipSuccess)
-      e = timed(13, nnt, s, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+  // rejoin whatever is still open (also after a failed launch, so the main stream's sync covers it)
+  if (chain_open) {
+    const hipError_t r = join_chain();
+    if (e == hipSuccess) e = r;
+  }
+  if (nest_open) {
+    const hipError_t r = dep(side, s, 3);
+    if (e == hipSuccess) e = r;
   }
   return e;
 }
