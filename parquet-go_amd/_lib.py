@@ -52,9 +52,9 @@ def hip():
     if _hip is None:
         from . import native
 
-        _hip = native.bind(_load("libpqhip.so", "build_hip"))
+        _hip = native.bind(_load(os.environ.get("PQH_HIP_LIB", "libpqhip.so"), "build_hip"))
     return _hip
 
 
 def hip_path():
-    return os.path.join(LIBDIR, "libpqhip.so")
+    return os.path.join(LIBDIR, os.environ.get("PQH_HIP_LIB", "libpqhip.so"))

@@ -58,11 +58,13 @@ def build_gen(force=False):
 
 
 def build_hip(force=False):
-    out = os.path.join(LIBDIR, "libpqhip.so")
+    # PQH_HIP_LIB names an experiment variant (built with its own PQH_HIPFLAGS, loaded with the same
+    # variable set); the product is libpqhip.so
+    out = os.path.join(LIBDIR, os.environ.get("PQH_HIP_LIB", "libpqhip.so"))
     if force or _stale(out, HOST_SRCS + HIP_SRCS):
         os.makedirs(LIBDIR, exist_ok=True)
         objs = []
-        bdir = os.path.join(PKG, "build")
+        bdir = os.path.join(PKG, "build", os.path.basename(out))
         os.makedirs(bdir, exist_ok=True)
         for s in HIP_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")

@@ -864,7 +864,10 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
                            static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
     });
-  if (e == hipSuccess) e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, st); });
+  // repeated columns carry long level streams: a workgroup per page splits their notNull count
+  const bool wide = std::any_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& c) { return c.max_rep > 0; });
+  if (e == hipSuccess)
+    e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, wide, st); });
   const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
   bool chain_open = false;  // the chain branch has not rejoined the main stream yet
   if (e == hipSuccess && nbp) {

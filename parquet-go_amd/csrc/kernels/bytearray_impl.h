@@ -60,12 +60,14 @@ __device__ __forceinline__ int64_t block_sum64(int64_t x, int64_t* wsum) {
   return wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-// One record at page offset p (window-relative o): 0 and the next offset, or the error code.
-__device__ __forceinline__ int chain_step(const ChainLds& C, int64_t wb, int64_t e0, int64_t p, int64_t& next,
+// Every position below is a byte offset in the page image (32 bits: pages are < 2 GiB); wb is the
+// window's stage base, e0 the end of the page's value bytes.
+// One record at page offset p: 0 and the next offset, or the error code.
+__device__ __forceinline__ int chain_step(const ChainLds& C, int32_t wb, int32_t e0, int32_t p, int32_t& next,
                                           int32_t& len) {
-  const int64_t avail = e0 - p;
+  const int32_t avail = e0 - p;
   if (avail < 4) return avail <= 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF;  // binary.Read(u32)
-  const int64_t o = p - wb;
+  const int32_t o = p - wb;
   const uint32_t w0 = C.win[o >> 2], w1 = C.win[(o >> 2) + 1];
   len = int32_t(__builtin_amdgcn_alignbit(w1, w0, uint32_t(o & 3) * 8));
   if (len < 0) return PQH_ERR_NEGATIVE_LENGTH;
@@ -74,28 +76,27 @@ __device__ __forceinline__ int chain_step(const ChainLds& C, int64_t wb, int64_t
   return PQH_OK;
 }
 
-__device__ __forceinline__ int64_t seg_end(int j, int64_t wb, int64_t wend) {
-  const int64_t s1 = wb + int64_t(j + 1) * kChainSeg;
+__device__ __forceinline__ int32_t seg_end(int j, int32_t wb, int32_t wend) {
+  const int32_t s1 = wb + (j + 1) * kChainSeg;
   return s1 < wend ? s1 : wend;
 }
 
 // Walk segment j [s0, s1) from `start` (must lie in the segment): marks + exit.
-__device__ void chain_walk(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t e0, int64_t start) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
+__device__ void chain_walk(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t e0, int32_t start) {
+  const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
   uint64_t m[kChainWords];
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) m[k] = 0;
-  int64_t p = start;
+  int32_t p = start;
   uint8_t bad = 0;
   while (p < s1) {
-    int64_t nx;
-    int32_t l;
+    int32_t nx, l;
     const int st = chain_step(C, wb, e0, p, nx, l);
     if (st) {
       bad = uint8_t(st);
       break;
     }
-    const int q = int(p - s0);
+    const int q = p - s0;
 #pragma unroll
     for (int k = 0; k < kChainWords; k++)
       if ((q >> 6) == k) m[k] |= 1ull << (q & 63);
@@ -103,7 +104,7 @@ __device__ void chain_walk(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t
   }
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) C.mask[j][k] = m[k];
-  C.exitv[j] = int32_t(p);
+  C.exitv[j] = p;
   C.exitbad[j] = bad;
 }
 
@@ -114,9 +115,9 @@ __device__ __forceinline__ bool chain_has(const ChainLds& C, int j, int q) {
 // Is segment j's stored result right for its true entry (the previous segment's exit)?  By
 // induction from segment 0 (whose start is the window entry), when every segment passes, all
 // segments up to the first invalid exit are exact and that exit is the true end of the chain.
-__device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb, int64_t wend, int64_t entry) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
-  int64_t T = entry;
+__device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int32_t wb, int32_t wend, int32_t entry) {
+  const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
+  int32_t T = entry;
   uint8_t pbad = 0;
   if (j > 0) {
     T = C.exitv[j - 1];
@@ -128,18 +129,18 @@ __device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int64_t wb,
   if (pbad) return true;  // the chain ended before j (exactly, if j-1 is right): nothing here counts
   if (T >= s1) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
   if (empty && C.exitbad[j] && C.exitv[j] == T) return true;       // the record at T itself is invalid
-  return chain_has(C, j, int(T - s0));
+  return chain_has(C, j, T - s0);
 }
 
 // Make segment j right for the entry T (pbad: the chain already ended before it).
-__device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t e0, int64_t T, uint8_t pbad) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg;
+__device__ void chain_fix(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t e0, int32_t T, uint8_t pbad) {
+  const int32_t s0 = wb + j * kChainSeg;
   if (pbad || T >= seg_end(j, wb, wend)) {
 #pragma unroll
     for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
-    C.exitv[j] = int32_t(T);
+    C.exitv[j] = T;
     C.exitbad[j] = pbad;
-  } else if (!chain_has(C, j, int(T - s0))) {
+  } else if (!chain_has(C, j, T - s0)) {
     chain_walk(C, j, wb, wend, e0, T);
   }
 }
@@ -147,27 +148,25 @@ __device__ void chain_fix(ChainLds& C, int j, int64_t wb, int64_t wend, int64_t 
 // The record starts <= 3 bytes apart at x..x+3 that look like records (valid, and followed inside
 // the window by another valid one): the shortest wins.  The last byte of a string followed by a
 // small length field reads as a record ~256x longer than the true one a byte later.
-__device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, int64_t e0, int64_t s0, int64_t s1,
-                                               int64_t staged_end) {
-  auto plausible = [&](int64_t x, int32_t& l) {
-    int64_t nx, nx2;
-    int32_t l2;
+__device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, int32_t e0, int32_t s0, int32_t s1,
+                                               int32_t staged_end) {
+  auto plausible = [&](int32_t x, int32_t& l) {
+    int32_t nx, nx2, l2;
     if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
     return nx + 4 <= staged_end && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
   };
   // scan 16 positions per step from 5 dwords loaded together (independent LDS reads; the length at
   // each byte offset is a funnel shift of two of them): a mask of the positions whose own record is
   // valid, then the full test on those in order
-  const int64_t lim = s1 < e0 ? s1 : e0;
-  int64_t x = -1;
-  for (int64_t base = wb + ((s0 - wb) & ~int64_t(3)); base < lim && x < 0; base += 16) {
-    const int k = int((base - wb) >> 2);
+  const int32_t lim = s1 < e0 ? s1 : e0;
+  int32_t x = -1;
+  for (int32_t base = wb + ((s0 - wb) & ~3); base < lim && x < 0; base += 16) {
+    const int k = (base - wb) >> 2;
     uint32_t w[5];
 #pragma unroll
     for (int i = 0; i < 5; i++) w[i] = C.win[k + i];
-    const int64_t ra = e0 - base;
-    const int32_t rel = int32_t(ra < 0x7fffffff ? ra : 0x7fffffff);           // bytes left at base
-    const int32_t lo = int32_t(s0 > base ? s0 - base : 0), hi = int32_t(lim - base < 16 ? lim - base : 16);
+    const int32_t rel = e0 - base;  // bytes left at base
+    const int32_t lo = s0 > base ? s0 - base : 0, hi = lim - base < 16 ? lim - base : 16;
     uint32_t cand = 0;
 #pragma unroll
     for (int i = 0; i < 16; i++) {
@@ -177,7 +176,7 @@ __device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, in
     }
     for (; cand; cand &= cand - 1) {
       int32_t l;
-      const int64_t p = base + __builtin_ctz(cand);
+      const int32_t p = base + __builtin_ctz(cand);
       if (plausible(p, l)) {
         x = p;
         break;
@@ -187,7 +186,7 @@ __device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, in
   if (x >= 0) {
     int32_t l;
     plausible(x, l);
-    int64_t start = x;
+    int32_t start = x;
     for (int d = 1; d <= 3 && x + d < s1; d++) {
       int32_t l2;
       if (plausible(x + d, l2) && l2 < l) {
@@ -203,26 +202,31 @@ __device__ __forceinline__ int64_t chain_guess(const ChainLds& C, int64_t wb, in
 // Resolve the chain of the window [wb, wend) from `entry` (whole workgroup; C.win staged from wb).
 // Afterwards segment j's marks hold the true record starts in it, C.first_bad = the first segment
 // whose walk ended on an invalid record (kBlock if none).
-__device__ void chain_resolve(ChainLds& C, int64_t wb, int64_t wend, int64_t e0, int64_t entry) {
+__device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0, int32_t entry) {
   const int j = threadIdx.x;
   {
-    const int64_t s0 = wb + int64_t(j) * kChainSeg, s1 = seg_end(j, wb, wend);
-    int64_t start = -1;
-    if (j == 0) start = entry;
+    const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
+    int32_t start = -1;
+    if (s0 <= entry) start = entry;  // the segment holding the entry (segments before it stay empty)
     else if (s0 < s1) start = chain_guess(C, wb, e0, s0, s1, wb + kChainWin);
-    if (start >= 0) {
+    if (s1 <= entry) {
+#pragma unroll
+      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      C.exitv[j] = entry;
+      C.exitbad[j] = 0;
+    } else if (start >= 0) {
       chain_walk(C, j, wb, wend, e0, start);
     } else if (s0 >= e0 && s0 < s1) {
       // past the end of the bytes: what a walk from s0 gives (EOF at s0), so that the segments after
       // the chain's end agree at once instead of being fixed one per round
 #pragma unroll
       for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
-      C.exitv[j] = int32_t(s0);
+      C.exitv[j] = s0;
       C.exitbad[j] = uint8_t(PQH_ERR_EOF);
     } else {
 #pragma unroll
       for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
-      C.exitv[j] = int32_t(s1 > s0 ? s1 : s0);
+      C.exitv[j] = s1 > s0 ? s1 : s0;
       C.exitbad[j] = 0;
     }
   }
@@ -235,8 +239,7 @@ __device__ void chain_resolve(ChainLds& C, int64_t wb, int64_t wend, int64_t e0,
     __syncthreads();
     const int sg = C.stop;
     if (sg >= kBlock) break;
-    if (j == sg)
-      chain_fix(C, sg, wb, wend, e0, sg == 0 ? entry : int64_t(C.exitv[sg - 1]), sg == 0 ? 0 : C.exitbad[sg - 1]);
+    if (j == sg) chain_fix(C, sg, wb, wend, e0, sg == 0 ? entry : C.exitv[sg - 1], sg == 0 ? 0 : C.exitbad[sg - 1]);
     __syncthreads();
   }
   if (j == 0) C.first_bad = kBlock;
@@ -246,16 +249,16 @@ __device__ void chain_resolve(ChainLds& C, int64_t wb, int64_t wend, int64_t e0,
 }
 
 // Segment j's marks on the true chain (starts before its true entry dropped; none past the end).
-__device__ __forceinline__ int chain_marks(const ChainLds& C, int j, int64_t wb, int64_t entry, int fb,
+__device__ __forceinline__ int chain_marks(const ChainLds& C, int j, int32_t wb, int32_t entry, int fb,
                                            uint64_t m[kChainWords]) {
-  const int64_t s0 = wb + int64_t(j) * kChainSeg;
-  const int64_t T = j == 0 ? entry : int64_t(C.exitv[j - 1]);
+  const int32_t s0 = wb + j * kChainSeg;
+  const int32_t T = j == 0 ? entry : C.exitv[j - 1];
   const bool live = j <= fb;
   int cnt = 0;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) {
     m[k] = live ? C.mask[j][k] : 0;
-    const int64_t lo = T - s0 - 64 * k;
+    const int32_t lo = T - s0 - 64 * k;
     if (lo > 0) m[k] = lo >= 64 ? 0 : m[k] & ~((1ull << lo) - 1);
     cnt += __popcll(m[k]);
   }
@@ -281,52 +284,78 @@ __device__ __forceinline__ BaPageCtx ba_page_ctx(const DevBatch& b, int p) {
   return c;
 }
 
-// Stage, resolve and summarise one window (whole workgroup).  Its records go to the window's scratch
-// in order as the bytes of the records before each one within the window (one more entry holds the
-// window's total): record i's length is wrec[i + 1] - wrec[i].
-__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry, BaWin* res, int32_t* wrec) {
+// Window w is staged from B_w = entry + w * kChainStride rounded down to 16 bytes: its records start
+// in [entry_w, B_w+1) with entry_w >= B_w, so [wb, B_w+1) spans at most kChainWin bytes whatever the
+// true entry turns out to be.
+__device__ __forceinline__ int64_t ba_wbase(const BaPageCtx& c, int64_t w) {
+  const int64_t Bw = c.entry + w * kChainStride;
+  return Bw - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(Bw)) & 15);
+}
+
+// The whole window in one round trip: every thread's vectors loaded together, then stored.
+__device__ __forceinline__ void ba_stage(ChainLds& C, const BaPageCtx& c, int64_t wb) {
+  constexpr int kNv = (kChainWin + 64) / 16, kPer = (kNv + kBlock - 1) / kBlock;
+  const PQH_G uint8_t* src = (const PQH_G uint8_t*)(c.img + wb);
+  const int64_t limit = c.e0 - wb;
+  uint4 x[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int k = int(threadIdx.x) + j * kBlock;
+    const bool ok = k < kNv && 16 * int64_t(k) < limit;
+    x[j] = *reinterpret_cast<const PQH_G uint4*>(src + (ok ? 16 * k : 0));
+    if (!ok) x[j] = make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int k = int(threadIdx.x) + j * kBlock;
+    if (k < kNv) reinterpret_cast<uint4*>(C.win)[k] = x[j];
+  }
+}
+
+// Resolve and summarise one window (whole workgroup; C.win staged from ba_wbase(c, w)).  Its records
+// go to the window's scratch in order as the bytes of the records before each one within the window
+// (one more entry holds the window's total): record i's length is wrec[i + 1] - wrec[i].
+__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res, int32_t* wrec) {
   const int j = threadIdx.x;
-  const int64_t wend = c.entry + (w + 1) * kChainStride;
-  BaWin r{int32_t(entry), int32_t(entry), 0, 0, 0, -1, 0, 0};
-  if (entry >= c.e0 || entry >= wend) {  // no record starts in the window (or no bytes left)
-    if (entry >= c.e0 && entry < wend) r.bad = PQH_ERR_EOF;
+  const int64_t wend64 = c.entry + (w + 1) * kChainStride;
+  BaWin r{int32_t(entry64), int32_t(entry64), 0, 0, 0, -1, 0, 0};
+  if (entry64 >= c.e0 || entry64 >= wend64) {  // no record starts in the window (or no bytes left)
+    if (entry64 >= c.e0 && entry64 < wend64) r.bad = PQH_ERR_EOF;
     if (j == 0) {
       *res = r;
       wrec[0] = 0;
     }
     return;
   }
-  const int64_t wb = entry - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(entry)) & 15);
-  __syncthreads();
-  stage_copy(reinterpret_cast<uint4*>(C.win), c.img + wb, (kChainWin + 64) / 16, c.e0 - wb);
-  __syncthreads();
-  chain_resolve(C, wb, wend, c.e0, entry);
+  const int32_t wb = int32_t(ba_wbase(c, w)), wend = int32_t(wend64), entry = int32_t(entry64);
+  chain_resolve(C, wb, wend, int32_t(c.e0), entry);
   const int fb = C.first_bad;
   uint64_t m[kChainWords];
   const int cnt = chain_marks(C, j, wb, entry, fb, m);
-  const int64_t s0 = wb + int64_t(j) * kChainSeg;
-  auto len_lds = [&](int64_t pos) {
-    const int64_t o = pos - wb;
+  const int32_t o0 = j * kChainSeg;  // the segment's first byte in the stage
+  auto len_lds = [&](int32_t o) {
     return int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
   };
-  int64_t bytes = 0;
+  int32_t bytes = 0;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
-    for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(s0 + __builtin_ctzll(x) + 64 * k);
-  uint64_t tot, btot = 0;
-  int32_t li = int32_t(block_exclusive_scan(uint64_t(cnt), C.wsum, &tot));
-  int64_t lb = int64_t(block_exclusive_scan(uint64_t(bytes), C.wsum, &btot));
+    for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(o0 + __builtin_ctzll(x) + 64 * k);
+  // records and bytes of the window both fit 32 bits: one scan of the pair
+  uint64_t tot;
+  const uint64_t ex = block_exclusive_scan((uint64_t(uint32_t(cnt)) << 32) | uint32_t(bytes), C.wsum, &tot);
+  int32_t li = int32_t(ex >> 32), lb = int32_t(uint32_t(ex));
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
     for (uint64_t x = m[k]; x; x &= x - 1) {
-      const int32_t l = len_lds(s0 + __builtin_ctzll(x) + 64 * k);
-      wrec[li++] = int32_t(lb);
+      const int32_t l = len_lds(o0 + __builtin_ctzll(x) + 64 * k);
+      wrec[li++] = lb;
       lb += l;
     }
   if (j == 0) {
-    wrec[tot] = int32_t(btot);
-    r.count = int32_t(tot);
-    r.bytes = int64_t(btot);
+    const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
+    wrec[nrec] = btot;
+    r.count = nrec;
+    r.bytes = btot;
     if (fb < kBlock) {
       r.bad = C.exitbad[fb];
       r.exit = C.exitv[fb];
@@ -336,6 +365,36 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
     }
     *res = r;
   }
+}
+
+// Window w > 0 guesses its entry (the first record start >= B_w) from the staged window itself:
+// wave 0 tests 64 positions per step for a plausible record (valid, followed by a valid one) and
+// takes the shortest of the first one and its next three positions (the last byte of a string
+// followed by a small length field reads as a record ~256x longer than the true one a byte later).
+// A wrong guess costs k_ba_wstitch a re-resolution, never a wrong result.
+__device__ __forceinline__ int32_t ba_guess_entry(const ChainLds& C, int32_t e0, int32_t wb, int32_t Bw) {
+  const int lane = threadIdx.x & 63;
+  const int32_t staged_end = wb + kChainWin;
+  for (int32_t x0 = Bw; x0 < Bw + 1024 && x0 < e0; x0 += 64) {
+    const int32_t x = x0 + lane;
+    int32_t nx, nx2, l = 0, l2;
+    bool ok = x < e0 && chain_step(C, wb, e0, x, nx, l) == PQH_OK && nx + 4 <= staged_end &&
+              (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
+    const uint64_t m = __ballot(ok);
+    if (m == 0) continue;
+    const int f = __builtin_ctzll(m);
+    int best = f;
+    int32_t bl = __shfl(l, f, 64);
+    for (int d = 1; d <= 3 && f + d < 64; d++) {
+      const int32_t ld = __shfl(l, f + d, 64);
+      if (((m >> (f + d)) & 1) && ld < bl) {
+        best = f + d;
+        bl = ld;
+      }
+    }
+    return x0 + best;
+  }
+  return Bw;
 }
 
 __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, int32_t* wrec) {
@@ -349,15 +408,14 @@ __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, 
     if (threadIdx.x == 0) *r = BaWin{-1, -1, 0, 0, 0, -1, 0, 0};
     return;
   }
+  const int64_t wb = ba_wbase(c, pw.y);
+  ba_stage(C, c, wb);
+  __syncthreads();
   int64_t entry = c.entry;
-  if (pw.y > 0) {  // guess the first record start >= B_w from the 2 KiB at B_w
-    constexpr int kGuess = 2048;
-    const int64_t wb = Bw - int64_t((reinterpret_cast<uintptr_t>(c.img) + uintptr_t(Bw)) & 15);
-    stage_copy(reinterpret_cast<uint4*>(C.win), c.img + wb, kGuess / 16, c.e0 - wb);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int64_t g = chain_guess(C, wb, c.e0, Bw, wb + kGuess - 1024, wb + kGuess);
-      C.guess = int32_t(g < 0 ? Bw : g);
+  if (pw.y > 0) {
+    if (threadIdx.x < 64) {
+      const int32_t g = ba_guess_entry(C, int32_t(c.e0), int32_t(wb), int32_t(Bw));
+      if (threadIdx.x == 0) C.guess = int32_t(g);
     }
     __syncthreads();
     entry = C.guess;
@@ -387,6 +445,10 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
     if (threadIdx.x == 0) cur = *r;
     __syncthreads();
     if (cur.entry != T) {  // the window's guess was not its true entry: resolve it again
+      if (T < c.entry + (w + 1) * kChainStride) {  // some record starts in it: stage it
+        ba_stage(C, c, ba_wbase(c, w));
+        __syncthreads();
+      }
       ba_window(C, c, w, T, r, wrec + int64_t(wr.x + w) * kChainRecs);
       __syncthreads();
       if (threadIdx.x == 0) cur = *r;
@@ -986,10 +1048,10 @@ __global__ __launch_bounds__(256) void k_ba_gather(DevBatch b, const Tile* tiles
 //   * a window whose last record runs past the stage (a string of more than ~1 KiB at its end)
 //     copies straight from the page: short records per thread, long ones by the workgroup.
 // ------------------------------------------------------------------------------------------------
-constexpr int kWStage = 33024;  // staged page bytes: a window plus ~1 KiB of overrun
-constexpr int kWV = (kWStage / 16 + kBlock - 1) / kBlock;  // 9 page vectors per thread
+constexpr int kWStage = kChainWin + 1280;  // staged page bytes: a window plus ~1 KiB of overrun
+constexpr int kWV = (kWStage / 16 + kBlock - 1) / kBlock;  // page vectors per thread
 constexpr int kWP = (kChainRecs / 2 + kBlock) / kBlock;    // 16 offset pairs per thread
-constexpr int kWGrid = 3 * 256;                             // resident workgroups (3 per CU)
+constexpr int kWGrid = (kChainSeg > 64 ? 3 : 6) * 256;       // resident workgroups (LDS-limited per CU)
 
 struct WcopyLds {
   uint32_t stage[kWStage / 4 + 4];

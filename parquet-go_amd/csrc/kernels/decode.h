@@ -169,7 +169,10 @@ enum TileKind : int32_t {
 constexpr int kBaTile = 2048;  // byte-array values per tile (one 256 x 8 block scan)
 
 // PLAIN byte-array chains (k_ba_wspec / k_ba_wstitch / k_ba_wemit): windows of 256 segments.
-constexpr int kChainSeg = 124;
+#ifndef PQH_CHAIN_SEG
+#define PQH_CHAIN_SEG 124
+#endif
+constexpr int kChainSeg = PQH_CHAIN_SEG;
 constexpr int kChainWin = kChainSeg * kBlock;      // 31744 bytes per window (4 workgroups per CU)
 constexpr int kChainWords = (kChainSeg + 63) / 64; // mask words per segment
 constexpr int kChainStride = kChainWin - 16;       // window bases: the window staged from a 16-aligned

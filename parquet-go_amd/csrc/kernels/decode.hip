@@ -107,15 +107,18 @@ struct WalkOut {
   int64_t fail_index;
 };
 
+// Every wave of the page's workgroup walks the same headers (wave-uniform, L2-hot after the first);
+// the value counting inside bit-packed runs is split over the nwv waves (wave wv takes every nwv-th
+// 64-lane slice) and count is this wave's share; wave 0 alone writes the checkpoints.
 __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, int64_t N, int phase, Ckpt* ck,
-                               int match, int lane) {
+                               int match, int lane, int wv = 0, int nwv = 1) {
   WalkOut o{kNoError, 0, N};
   if (N <= 0) return o;
   const int64_t T = kHybridTile;
   if (w == 0) {  // infinite zeros, no reads (hybrid_decoder.go:82-85)
-    if (ck)
+    if (ck && wv == 0)
       for (int64_t k = lane; k * T < N; k += 64) ck[k] = Ckpt{0, 0x7fffffff, 0, 0};
-    o.count = match == 0 ? N : 0;
+    o.count = match == 0 && wv == 0 ? N : 0;
     return o;
   }
   const uint8_t* end = img + e;
@@ -179,28 +182,39 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
       const int32_t nh = int32_t(next < 0x7fffffff ? next : 0x7fffffff) | (bp ? int32_t(0x80000000u) : 0);
       const int32_t rl = int32_t(cnt < 0x7fffffff ? cnt : 0x7fffffff);
       while (next_ck * T < N && next_ck * T < valid_end) {
-        if (lane == 0) ck[next_ck] = Ckpt{int32_t(produced), rl, data, nh};
+        if (lane == 0 && wv == 0) ck[next_ck] = Ckpt{int32_t(produced), rl, data, nh};
         next_ck++;
       }
     }
     if (match >= 0) {
       const int64_t lim = (valid_end < N ? valid_end : N) - produced;
       if (!bp) {
-        if (lane == 0 && data == match) cnt_lane += lim;
+        if (lane == 0 && wv == 0 && data == match) cnt_lane += lim;
       } else if (w == 1) {
         // one bit per value: popcount 128 values per lane-load (16-byte loads, many in flight)
         int64_t ones = 0;
-#pragma unroll 4
-        for (int64_t c = lane; c * 128 < lim; c += 64) {
-          const uint8_t* p = img + data + c * 16;
-          const uint64_t a = ld64_masked(p, end), b = ld64_masked(p + 8, end);
-          const int64_t nb = lim - c * 128;  // valid bits in this chunk
-          const uint64_t ma = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
-          const uint64_t mb = nb >= 128 ? ~0ull : nb <= 64 ? 0ull : ((1ull << (nb - 64)) - 1);
-          const int64_t valid = nb < 128 ? nb : 128;
-          const int64_t pc = __popcll(a & ma) + __popcll(b & mb);
-          ones += pc;
-          if (match == 0) cnt_lane += valid - pc;
+        for (int64_t c0 = int64_t(wv) * 64; c0 * 128 < lim; c0 += int64_t(64) * 8 * nwv) {  // 8 chunks per lane in flight
+          uint64_t a[8], bq[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int64_t c = c0 + int64_t(k) * 64 * nwv + lane;
+            const uint8_t* p = img + data + c * 16;
+            const bool in = c * 128 < lim;
+            a[k] = in ? ld64_masked(p, end) : 0;
+            bq[k] = in ? ld64_masked(p + 8, end) : 0;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int64_t c = c0 + int64_t(k) * 64 * nwv + lane;
+            const int64_t nb = lim - c * 128;  // valid bits in this chunk
+            if (nb <= 0) continue;
+            const uint64_t ma = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
+            const uint64_t mb = nb >= 128 ? ~0ull : nb <= 64 ? 0ull : ((1ull << (nb - 64)) - 1);
+            const int64_t valid = nb < 128 ? nb : 128;
+            const int64_t pc = __popcll(a[k] & ma) + __popcll(bq[k] & mb);
+            ones += pc;
+            if (match == 0) cnt_lane += valid - pc;
+          }
         }
         if (match == 1) cnt_lane += ones;
       } else if (w == 2 || w == 4 || w == 8) {
@@ -210,19 +224,29 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
         const uint64_t pat = lowm * uint64_t(uint32_t(match));
         const int per = 64 / w;
         const int64_t nw = (lim + per - 1) / per;
-#pragma unroll 4
-        for (int64_t c = lane; c < nw; c += 64) {
-          uint64_t t = ld64_masked(img + data + c * 8, end) ^ pat;
-          t |= t >> 1;
-          if (w >= 4) t |= t >> 2;
-          if (w == 8) t |= t >> 4;
-          const int64_t nv = lim - c * per;  // valid values in this word
-          const uint64_t valid = nv >= per ? lowm : (lowm & ((1ull << (nv * w)) - 1));
-          cnt_lane += __popcll(valid & ~t);
+        // 16 words per lane in flight (one wave walks a whole page: latency, not bandwidth, bound)
+        for (int64_t c0 = int64_t(wv) * 64; c0 < nw; c0 += int64_t(64) * 16 * nwv) {
+          uint64_t t[16];
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            const int64_t c = c0 + int64_t(k) * 64 * nwv + lane;
+            t[k] = c < nw ? ld64_masked(img + data + c * 8, end) : 0;
+          }
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            const int64_t c = c0 + int64_t(k) * 64 * nwv + lane;
+            uint64_t x = t[k] ^ pat;
+            x |= x >> 1;
+            if (w >= 4) x |= x >> 2;
+            if (w == 8) x |= x >> 4;
+            const int64_t nv = lim - c * per;  // valid values in this word
+            const uint64_t valid = nv >= per ? lowm : nv <= 0 ? 0ull : (lowm & ((1ull << (nv * w)) - 1));
+            cnt_lane += __popcll(valid & ~x);
+          }
         }
       } else {
 #pragma unroll 2
-        for (int64_t g = lane; g * 8 < lim; g += 64) {
+        for (int64_t g = int64_t(wv) * 64 + lane; g * 8 < lim; g += 64 * nwv) {
           const uint64_t q = ld64_masked(img + data + g * w, end);
           const uint64_t q2 = w > 8 ? ld64_masked(img + data + g * w + 8, end) : 0;
           for (int j = 0; j < 8; j++) {
@@ -249,12 +273,17 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_prologue: one wave64 per page.
+// k_prologue: kNwv waves per page.  kNwv = 1: four pages per workgroup (flat batches: short level
+// streams); kNwv = 4: one page per workgroup (batches with repeated columns: long level streams),
+// its four waves run the same (wave-uniform) framing and run walks and split the notNull count
+// over bit-packed definition levels.
 // ------------------------------------------------------------------------------------------------
+template <int kNwv>
 __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
+  __shared__ int64_t s_nn[4];
   const int lane = threadIdx.x & 63;
-  // one page per wave: make the page index provably wave-uniform so that its records live in SGPRs
-  const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
+  const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6) % kNwv);
+  const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * (4 / kNwv) + int(threadIdx.x >> 6) / kNwv);
   if (p >= b.num_pages) return;
   const DevPage P = b.pages[p];
   const DevChunk C = b.chunks[P.chunk];
@@ -366,7 +395,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
         if (rep_s < 0) {
           err = err_key(1, 0, PQH_ERR_READER_NOT_INITIALIZED);
         } else {
-          WalkOut r = walk_hybrid(img, rep_s, rep_e, rw, n, 1, P.ck_rep >= 0 ? b.ckpts + P.ck_rep : nullptr, -1, lane);
+          WalkOut r = walk_hybrid(img, rep_s, rep_e, rw, n, 1, P.ck_rep >= 0 ? b.ckpts + P.ck_rep : nullptr, -1, lane, wv, kNwv);
           err = r.err;
         }
       }
@@ -375,10 +404,15 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
         if (def_s < 0) {
           err = err_key(2, 0, PQH_ERR_READER_NOT_INITIALIZED);
         } else {
-          WalkOut r = walk_hybrid(img, def_s, def_e, dw, n, 2, P.ck_def >= 0 ? b.ckpts + P.ck_def : nullptr, C.max_def, lane);
+          WalkOut r = walk_hybrid(img, def_s, def_e, dw, n, 2, P.ck_def >= 0 ? b.ckpts + P.ck_def : nullptr, C.max_def, lane, wv, kNwv);
           err = r.err;
-          nn = r.count;
+          nn = r.count;  // this wave's share: summed below
         }
+      }
+      if (kNwv > 1 && dw > 0) {  // uniform over the workgroup (same page, same walk)
+        if (lane == 0) s_nn[wv] = nn;
+        __syncthreads();
+        nn = s_nn[0] + s_nn[1] + s_nn[2] + s_nn[3];
       }
       if (err == kNoError) {
         S.nn = int32_t(nn);
@@ -388,7 +422,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
           switch (P.kind) {
             case K_DICT:
             case K_RLE_BOOL: {
-              WalkOut r = walk_hybrid(img, hs, he, S.width, nn, 3, P.ck_val >= 0 ? b.ckpts + P.ck_val : nullptr, -1, lane);
+              WalkOut r = walk_hybrid(img, hs, he, S.width, nn, 3, P.ck_val >= 0 ? b.ckpts + P.ck_val : nullptr, -1, lane, wv, kNwv);
               err = r.err;
               limit = r.fail_index;
               break;
@@ -438,7 +472,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
     }
   }
   S.err = err;
-  if (lane == 0) b.states[p] = S;
+  if (lane == 0 && wv == 0) b.states[p] = S;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1033,9 +1067,10 @@ __global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* til
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_prologue(const DevBatch& b, hipStream_t s) {
+hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s) {
   if (b.num_pages <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prologue, dim3((b.num_pages + 3) / 4), dim3(256), 0, s, b);
+  if (wide) hipLaunchKernelGGL(k_prologue<4>, dim3(b.num_pages), dim3(256), 0, s, b);
+  else hipLaunchKernelGGL(k_prologue<1>, dim3((b.num_pages + 3) / 4), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

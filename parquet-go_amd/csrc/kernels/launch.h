@@ -27,7 +27,7 @@ struct DevBatch {
   int64_t* basums2;      // DELTA_BYTE_ARRAY: per tile suffix-byte sum, then its first suffix byte
 };
 
-hipError_t launch_prologue(const DevBatch& b, hipStream_t s);
+hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s);
 // Device codecs: one wave per page rebuilding its image from its (SNAPPY) source bytes.
 hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                          hipStream_t s);

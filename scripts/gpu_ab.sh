@@ -4,13 +4,13 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
 if [ "${TESTS:-0}" = 1 ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/ab/gpu_tests.log 2>&1
+  env ${TEST_ENV:-X=1} timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/ab/gpu_tests.log 2>&1
   rc=$?; echo "gpu_tests rc=$rc"; tail -3 gpurun_out/ab/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 for w in ${WORKLOADS:-c4}; do
   for v in ${VARIANTS:-X=1}; do
-    log=gpurun_out/ab/bench_${w}_${v//=/_}.log
-    env $v timeout -k 10 300 python -u bench.py --workload $w --steps ${STEPS:-10} --warmup 2 --no-cpu --no-e2e > $log 2>&1
+    log=gpurun_out/ab/bench_${w}_${v//[=,]/_}.log
+    env ${v//,/ } timeout -k 10 300 python -u bench.py --workload $w --steps ${STEPS:-10} --warmup 2 --no-cpu --no-e2e > $log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "bench $w $v rc=$rc"; tail -5 $log; exit $rc; }
     python - "$log" "$w $v" <<'P'
 import json, sys
