@@ -89,25 +89,36 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
   }
 }
 
+// Flags f and f + 1 of every thread packed in one dword (16 bits each: a tile counts at most
+// kNestTile < 2^16 of either), so one 32-bit DPP scan serves two flags.
+__device__ __forceinline__ uint32_t nest_pair(const uint32_t E[kNestFlags], int f, int L) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int g = 0; g < kNestFlags; g++) {
+    if (g == f) x |= uint32_t(__popc(E[g]));
+    if (g == f + 1 && g <= L) x |= uint32_t(__popc(E[g])) << 16;
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(256) void k_nest_count(DevBatch b, const Tile* tiles) {
-  __shared__ int32_t cnt[kNestFlags];
+  __shared__ int32_t cnt[kNestFlags + 1];
   const Tile t = tiles[blockIdx.x];
   const DevNest N = b.nests[t.page];
   const DevChunk C = b.chunks[N.chunk];
-  if (threadIdx.x < kNestFlags) cnt[threadIdx.x] = 0;
+  if (threadIdx.x < kNestFlags + 1) cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t s0 = int64_t(t.k) * kNestTile + int64_t(threadIdx.x) * kNestPer;
   const int m = s0 < N.n ? (N.n - s0 < kNestPer ? int(N.n - s0) : kNestPer) : 0;
+  const int L = N.levels;
   uint32_t E[kNestFlags], V[kMaxNest], LV;
   nest_masks(N, C, s0, m, E, V, LV);
-  int32_t c[kNestFlags];
-#pragma unroll
-  for (int f = 0; f < kNestFlags; f++) c[f] = __popc(E[f]);
-#pragma unroll
-  for (int f = 0; f < kNestFlags; f++) {
-    int32_t x = c[f];
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    if ((threadIdx.x & 63) == 0 && x) atomicAdd(&cnt[f], x);
+  for (int f = 0; f <= L; f += 2) {  // uniform: flags 0..L only
+    const uint32_t x = wave_incl_scan32(nest_pair(E, f, L));
+    if ((threadIdx.x & 63) == 63 && x) {
+      atomicAdd(&cnt[f], int32_t(x & 0xffffu));
+      atomicAdd(&cnt[f + 1], int32_t(x >> 16));
+    }
   }
   __syncthreads();
   if (threadIdx.x < kNestFlags) b.nsums[int64_t(N.tile_base + t.k) * kNestFlags + threadIdx.x] = cnt[threadIdx.x];
@@ -199,12 +210,27 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
   for (int f = 0; f < kNestFlags; f++) {
     lpos[f] = 0;
     tot[f] = 0;
-    gbase[f] = 0;
-    if (f <= L) {  // uniform
-      uint64_t tt;
-      lpos[f] = int32_t(block_exclusive_scan(uint64_t(__popc(E[f])), wsum, &tt));
-      tot[f] = int32_t(tt);
-      gbase[f] = base[f];
+    gbase[f] = f <= L ? base[f] : 0;
+  }
+#pragma unroll
+  for (int f = 0; f < kNestFlags; f += 2) {
+    if (f > L) break;  // uniform
+    // flags f and f + 1 in one block scan of packed 16-bit counts (DPP wave scans)
+    const uint32_t x = nest_pair(E, f, L);
+    const uint32_t incl = wave_incl_scan32(x);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* ws = reinterpret_cast<uint32_t*>(wsum);
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int k = 0; k < wv; k++) before += ws[k];
+    const uint32_t tt = ws[0] + ws[1] + ws[2] + ws[3], ex = before + incl - x;
+    __syncthreads();
+    lpos[f] = int32_t(ex & 0xffffu);
+    tot[f] = int32_t(tt & 0xffffu);
+    if (f + 1 < kNestFlags) {
+      lpos[f + 1] = int32_t(ex >> 16);
+      tot[f + 1] = int32_t(tt >> 16);
     }
   }
 #pragma unroll
