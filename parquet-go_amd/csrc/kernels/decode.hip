@@ -640,6 +640,19 @@ __device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, in
     // G values per thread and step (Sink::kGroup): 4 for 4-byte outputs, so that a wave's stores
     // are one contiguous kilobyte
     constexpr int G = Sink::kGroup;
+    if (w * G <= 32) {
+      // narrow values (levels, booleans, small dictionaries): a thread's G values fit one funnel
+      // shift of two LDS dwords
+      for (int64_t i0 = c0 + G * int64_t(threadIdx.x); i0 < c1; i0 += G * kBlock) {
+        uint32_t v[8];
+        const uint32_t bit0 = lead_bits + uint32_t(i0 - c0) * uint32_t(w);
+        const uint32_t x = __builtin_amdgcn_alignbit(stage[(bit0 >> 5) + 1], stage[bit0 >> 5], bit0 & 31);
+#pragma unroll
+        for (int j = 0; j < G; j++) v[j] = (x >> (uint32_t(j) * uint32_t(w))) & m;
+        sink(i0, v, int(c1 - i0 < G ? c1 - i0 : G));
+      }
+      continue;
+    }
     for (int64_t i0 = c0 + G * int64_t(threadIdx.x); i0 < c1; i0 += G * kBlock) {
       uint32_t v[8];
       const uint32_t bit0 = lead_bits + uint32_t(i0 - c0) * uint32_t(w);

@@ -265,12 +265,19 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
       gbaseL = gbase[f];
     }
   const int lead8 = int(gbaseL & 15);
-  int32_t k = lposL;
-  if (EL == ~0u) {  // every slot of the thread is an element: its 32 leaf flags in order
-#pragma unroll
-    for (int j = 0; j < kNestPer; j++) st8[lead8 + k + j] = uint8_t((LV >> j) & 1);
-  } else {
-    for (uint32_t x = EL; x; x &= x - 1) st8[lead8 + k++] = uint8_t((LV >> __builtin_ctz(x)) & 1);
+  {
+    // the thread's leaf flags compacted to its elements (the non-element slots, few, dropped from
+    // the top down), then stored as bytes up to a 4-aligned LDS position and nibble-expanded dwords
+    uint32_t c = LV;
+    for (uint32_t z = ~EL & (m >= kNestPer ? ~0u : (1u << m) - 1); z;) {
+      const int j = 31 - __clz(int(z));
+      z &= ~(1u << j);
+      c = (c & ((1u << j) - 1)) | (((c >> j) >> 1) << j);
+    }
+    int pos = lead8 + lposL, left = __popc(EL);
+    for (; left > 0 && (pos & 3); left--, c >>= 1) st8[pos++] = uint8_t(c & 1);
+    for (; left >= 4; left -= 4, c >>= 4, pos += 4) *reinterpret_cast<uint32_t*>(st8 + pos) = nibble_bytes(c & 15);
+    for (; left > 0; left--, c >>= 1) st8[pos++] = uint8_t(c & 1);
   }
   __syncthreads();
   nest_flush(N.leaf_valid + gbaseL, st8, lead8, totL);
