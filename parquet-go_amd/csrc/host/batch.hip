@@ -252,6 +252,7 @@ struct pqh_batch {
   int2* d_ba_wlist = nullptr;
   BaWin* d_ba_res = nullptr;
   int32_t* d_ba_wrec = nullptr;     // per window: its records' lengths / cumulative bytes
+  void* d_ba_wgeo = nullptr;        // per data-page window: its k_ba_wcopy geometry
   int32_t* d_ba_chunks = nullptr;
   int32_t* d_dcum = nullptr;
   int64_t* d_basums = nullptr;
@@ -687,6 +688,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wlist), sizeof(int2) * b->ba_wlist.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_res), sizeof(BaWin) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wrec), sizeof(int32_t) * size_t(kChainRecs) * b->ba_wins.size())) ||
+      (rc = dalloc(b, &b->d_ba_wgeo, size_t(kWGeoBytes) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
@@ -960,7 +962,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     const int32_t nwd = int32_t(b->ba_wlist.size()) - b->ba_wdict;
     if (e == hipSuccess && nwd)
       e = timed(23, nwd, s, [&](hipStream_t st) {
-        return launch_ba_wcopy(d, b->d_ba_wlist + b->ba_wdict, nwd, b->d_ba_res, b->d_ba_wrec, st);
+        return launch_ba_wcopy(d, b->d_ba_wlist + b->ba_wdict, nwd, b->d_ba_res, b->d_ba_wrec, b->d_ba_wgeo, st);
       });
     if (e == hipSuccess && b->has_dba)
       e = timed(15, nbt, s, [&](hipStream_t st) { return launch_dba_prefix(d, b->d_batiles, nbt, st); });

@@ -1098,36 +1098,51 @@ __device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const 
   return g;
 }
 
-__global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const int2* list, int32_t nlist, const BaWin* res,
-                                                   const int32_t* wrec) {
+// One thread per window: its geometry, so that k_ba_wcopy's workgroups load one record per window
+// instead of a chain of dependent loads (window -> page -> state -> chunk).
+__global__ __launch_bounds__(256) void k_ba_wgeo(DevBatch b, const int2* list, int32_t nlist, const BaWin* res,
+                                                  WGeo* geo) {
+  const int t = int(blockIdx.x) * kBlock + int(threadIdx.x);
+  if (t < nlist) geo[t] = wgeo(b, list, res, t);
+}
+
+// The window's page vectors and offset pairs into registers (every load unconditional, clamped
+// addresses), all in flight together.
+__device__ __forceinline__ void wcopy_issue(const WGeo& g, const int32_t* wrec, uint4 (&x)[kWV], int2 (&ov)[kWP]) {
+  const int tid = threadIdx.x;
+  const PQH_G uint8_t* wb = g.img + g.entry - g.in_lead;
+  const PQH_G int32_t* wo = (const PQH_G int32_t*)(wrec + int64_t(g.wi) * kChainRecs);
+#pragma unroll
+  for (int j = 0; j < kWV; j++) {
+    const int k = tid + j * kBlock;
+    x[j] = *reinterpret_cast<const PQH_G uint4*>(wb + (k < g.nvec ? 16 * k : 0));
+  }
+#pragma unroll
+  for (int j = 0; j < kWP; j++) {  // offsets 0 .. n (n + 1 entries; wrec holds the total at count)
+    const int k = tid + j * kBlock;
+    ov[j] = *reinterpret_cast<const PQH_G int2*>(wo + (2 * k <= g.n ? 2 * k : 0));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, int32_t nlist, const int32_t* wrec) {
   __shared__ WcopyLds L;
   const int tid = threadIdx.x;
+  const int grid = int(gridDim.x);
   int t = blockIdx.x;
   if (t >= nlist) return;
-  WGeo g = wgeo(b, list, res, t);
+  // the next window's geometry (one independent load) in flight during this window
+  WGeo g = geo[t];
+  uint4 x[kWV];
+  int2 ov[kWP];
   for (;;) {
-    const int tn = t + int(gridDim.x);
     WGeo gn{};
-    if (tn < nlist) gn = wgeo(b, list, res, tn);  // in flight during this window
+    if (t + grid < nlist) gn = geo[t + grid];
     const int n = g.n;
     const PQH_G int32_t* wo = (const PQH_G int32_t*)(wrec + int64_t(g.wi) * kChainRecs);
     typedef uint32_t u32u __attribute__((aligned(1)));
     if (n > 0 && g.nvec) {
-      // page vectors and offset pairs: every load unconditional (clamped addresses) and every LDS
-      // store too (out-of-range ones to spare slots), so all of them stay in flight together
-      const PQH_G uint8_t* wb = g.img + g.entry - g.in_lead;
-      uint4 x[kWV];
-      int2 ov[kWP];
-#pragma unroll
-      for (int j = 0; j < kWV; j++) {
-        const int k = tid + j * kBlock;
-        x[j] = *reinterpret_cast<const PQH_G uint4*>(wb + (k < g.nvec ? 16 * k : 0));
-      }
-#pragma unroll
-      for (int j = 0; j < kWP; j++) {  // offsets 0 .. n (n + 1 entries; wrec holds the total at count)
-        const int k = tid + j * kBlock;
-        ov[j] = *reinterpret_cast<const PQH_G int2*>(wo + (2 * k <= n ? 2 * k : 0));
-      }
+      wcopy_issue(g, wrec, x, ov);
+      // every LDS store unconditional too (out-of-range ones to spare slots)
       constexpr int kSpareVec = kWStage / 16;
       constexpr int kSpareRec = kChainRecs + 1;
 #pragma unroll
@@ -1202,8 +1217,8 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const int2* list, 
         if (cl > 0) block_copy(g.dst + o, src0 + 4 * (i + 1) + o, cl);
       }
     }
-    if (tn >= nlist) break;
+    if (t + grid >= nlist) break;
     g = gn;
-    t = tn;
+    t += grid;
   }
 }

@@ -177,7 +177,8 @@ constexpr int kChainWin = kChainSeg * kBlock;      // 31744 bytes per window (4 
 constexpr int kChainWords = (kChainSeg + 63) / 64; // mask words per segment
 constexpr int kChainStride = kChainWin - 16;       // window bases: the window staged from a 16-aligned
                                                    // entry >= B_w still covers [entry, B_w+1)
-constexpr int kChainRecs = kChainWin / 4 + 2;      // scratch entries per window (records >= 4 bytes)
+constexpr int kChainRecs = kChainWin / 4 + 2;
+constexpr int kWGeoBytes = 64;  // k_ba_wcopy: one window's geometry record      // scratch entries per window (records >= 4 bytes)
 
 // Scratch per window (k_ba_wspec -> k_ba_wstitch -> k_ba_wemit).
 struct BaWin {

@@ -1183,10 +1183,16 @@ hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const
   return hipGetLastError();
 }
 
+static_assert(sizeof(WGeo) <= kWGeoBytes, "window geometry record");
+
 hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
-                           hipStream_t s) {
+                           void* geo, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_wcopy, dim3(n < kWGrid ? n : kWGrid), dim3(256), 0, s, b, list, n, res, wrec);
+  WGeo* g = static_cast<WGeo*>(geo);
+  hipLaunchKernelGGL(k_ba_wgeo, dim3((n + kBlock - 1) / kBlock), dim3(256), 0, s, b, list, n, res, g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ba_wcopy, dim3(n < kWGrid ? n : kWGrid), dim3(256), 0, s, b, g, n, wrec);
   return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const i
 hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
                            hipStream_t s);
 hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
-                           hipStream_t s);
+                           void* geo, hipStream_t s);  // geo: kWGeoBytes per window
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n, bool dlba_pages,
                          hipStream_t s);
 hipError_t launch_ba_scan(const DevBatch& b, const int32_t* ba_chunks, int32_t n, const Tile* tiles, hipStream_t s);
