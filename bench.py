@@ -77,6 +77,7 @@ def cpu_baseline(data, seconds, threads=1, verify=None):
         if spent >= seconds:
             break
     rgs = len(sample)
+    cpu_baseline.row_groups = rgs
     res = {"value": round(out_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
            "sample": f"{rgs} of {len(fr.row_groups)} row groups ({out_bytes / 1e9:.3f} GB decoded) by oracle/refdecode.c "
                      f"(C restatement of the reference Go decoders), single thread, {spent:.1f} s"}
@@ -95,6 +96,31 @@ def cpu_baseline(data, seconds, threads=1, verify=None):
                  "sample": f"{rg} row groups ({len(flat)} chunks) decoded chunk-parallel on {threads} threads, "
                            f"{el:.2f} s"}
     return res, multi
+
+
+def cpu_comparator_pyarrow(data, rgs, bytes_per_row, threads):
+    """pyarrow's C++ Parquet reader (an industry CPU comparator, NOT the reference)
+    reading the oracle sample's row groups of the same in-memory file into Arrow tables on `threads`
+    host cores; best of 3.  Decoded bytes are counted with this bench's formula for the same rows."""
+    try:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        pa.set_cpu_count(threads)
+        pf = pq.ParquetFile(pa.BufferReader(pa.py_buffer(data)))
+        best, rows = None, 0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            t = pf.read_row_groups(list(range(rgs)), use_threads=threads > 1)
+            el = time.perf_counter() - t0
+            rows = t.num_rows
+            best = el if best is None else min(best, el)
+            del t
+        return {"value": round(bytes_per_row * rows / best / 1e9, 4), "unit": "GB/s", "cores": threads,
+                "kind": f"pyarrow {pa.__version__} C++ reader (comparator, not the reference)",
+                "sample": f"{rgs} row groups ({rows} rows) read into Arrow tables, best of 3: {best:.3f} s"}
+    except Exception as e:  # a file layout pyarrow refuses: reported, never fatal
+        return {"value": None, "error": f"{type(e).__name__}: {str(e)[:160]}"}
 
 
 def pmc_traffic(kernel, workload, rows):
@@ -303,7 +329,7 @@ def main():
                 "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
                 "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
     all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)  # kernel time of one profiled step
-    cpu = cpu_mt = None
+    cpu = cpu_mt = cpu_pa = None
     verified = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import numpy as np
@@ -318,6 +344,8 @@ def main():
         # the GPU box grants this job 16 host cores (os.cpu_count() reports the whole machine)
         cpu, cpu_mt = cpu_baseline(data, args.cpu_seconds, threads=min(16, os.cpu_count() or 1), verify=verify)
         verified = f"{nchk[0]} of {hb.num_chunks} chunks (the CPU sample) bit-exact vs the oracle"
+        cpu_pa = cpu_comparator_pyarrow(data, cpu_baseline.row_groups, bytes_written / max(1, my_rows),
+                                        min(16, os.cpu_count() or 1))
     batch.close()
 
     # End-to-end: one staged batch per row-group range holding its decompressed
@@ -435,6 +463,7 @@ def main():
             "e2e_device_snappy": e2e_dev,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
+            "cpu_comparator_pyarrow": cpu_pa,
             "verified": verified,
         }
         print(json.dumps(line), flush=True)

@@ -296,11 +296,16 @@ void free_batch(pqh_batch* b) {
 
 int32_t codec_fail_page(const pqh_batch* b, int32_t chunk);
 
+// Every planner buffer starts zeroed (once, at plan time, ordered before the batch's first run on
+// the context stream): no kernel can ever read stale memory from an earlier allocation, whichever
+// path it takes.
 int dalloc(pqh_batch* b, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   b->allocations.push_back(*p);
+  e = hipMemsetAsync(*p, 0, bytes, b->ctx->stream);
+  if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
   return PQH_OK;
 }
 
