@@ -258,6 +258,11 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       __syncthreads();  // the bulk bytes are visible to the next batches' reads
       continue;
     }
+#ifdef PQH_SNAPPY_PARSE_ONLY  // timing experiments: the element parse alone
+    d += T;
+    p = uni(E.p_next);
+    continue;
+#endif
     // ---- output byte -> element: start markers, then a max-scan (element ids rise with output)
     {  // every thread owns 32 consecutive entries (64 bytes: four 16-byte LDS accesses)
       uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
