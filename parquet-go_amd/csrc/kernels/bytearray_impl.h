@@ -187,7 +187,8 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
     int32_t l;
     plausible(x, l);
     int32_t start = x;
-    for (int d = 1; d <= 3 && x + d < s1; d++) {
+    // only a long record can be the false start (a string's last byte + a small length field)
+    for (int d = 1; d <= 3 && x + d < s1 && l >= 256; d++) {
       int32_t l2;
       if (plausible(x + d, l2) && l2 < l) {
         start = x + d;
@@ -332,24 +333,27 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   const int fb = C.first_bad;
   uint64_t m[kChainWords];
   const int cnt = chain_marks(C, j, wb, entry, fb, m);
-  const int32_t o0 = j * kChainSeg;  // the segment's first byte in the stage
-  auto len_lds = [&](int32_t o) {
-    return int32_t(__builtin_amdgcn_alignbit(C.win[(o >> 2) + 1], C.win[o >> 2], uint32_t(o & 3) * 8));
-  };
-  int32_t bytes = 0;
+  // The segment's records are consecutive on the chain, so their lengths need no LDS reads: record
+  // r's length is the next record's start - r's start - 4, and the last one ends at the segment's
+  // exit (the start of the next record, or of the invalid record that ended the chain).
+  const int32_t s0 = wb + j * kChainSeg, exj = C.exitv[j];
+  int32_t first = -1;
 #pragma unroll
-  for (int k = 0; k < kChainWords; k++)
-    for (uint64_t x = m[k]; x; x &= x - 1) bytes += len_lds(o0 + __builtin_ctzll(x) + 64 * k);
+  for (int k = kChainWords - 1; k >= 0; k--)
+    if (m[k]) first = 64 * k + __builtin_ctzll(m[k]);
+  const int32_t bytes = cnt > 0 ? exj - (s0 + first) - 4 * cnt : 0;
   // records and bytes of the window both fit 32 bits: one scan of the pair
   uint64_t tot;
   const uint64_t ex = block_exclusive_scan((uint64_t(uint32_t(cnt)) << 32) | uint32_t(bytes), C.wsum, &tot);
   int32_t li = int32_t(ex >> 32), lb = int32_t(uint32_t(ex));
+  int32_t prev = -1;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
     for (uint64_t x = m[k]; x; x &= x - 1) {
-      const int32_t l = len_lds(o0 + __builtin_ctzll(x) + 64 * k);
+      const int32_t pos = 64 * k + __builtin_ctzll(x);
+      if (prev >= 0) lb += pos - prev - 4;
       wrec[li++] = lb;
-      lb += l;
+      prev = pos;
     }
   if (j == 0) {
     const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
