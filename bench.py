@@ -357,11 +357,15 @@ def main():
         # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
         # >= 1/16 of the payload each
         nrg = rg1 - rg0
-        groups = min(nrg, 16)
+        # device SNAPPY: one batch, so that every page decompresses in the same k_snappy launch (a page
+        # is one workgroup's sequential walk: a launch takes a page's time however many pages it has)
+        groups = 1 if device_snappy else min(nrg, 16)
         cuts = [nrg * g // groups for g in range(groups + 1)]
-        staged, payload, images = [], 0, 0
+        staged, payload, images, walk = [], 0, 0, 0.0
         for g in range(groups):
+            t0 = time.perf_counter()
             hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)), device_snappy=device_snappy)
+            walk += time.perf_counter() - t0
             payload += hbr.payload_bytes
             images += hbr.image_bytes or hbr.payload_bytes
             staged.append(native.Batch.staged(ctx, hbr))
@@ -384,14 +388,18 @@ def main():
         barrier_sync()
         el = time.perf_counter() - t0
         el, total = pkg.shard.reduce_step(el, written, device=f"cuda:{local}" if world > 1 else None)
-        out = {"mode": ("pinned H2D of the COMPRESSED pages on a copy stream, k_snappy + decode on the compute "
-                        "stream, overlapped per row group" if device_snappy else
+        out = {"mode": ("pinned H2D of the COMPRESSED pages, then k_snappy + decode of all of them in one batch"
+                        if device_snappy else
                         "pinned H2D on a copy stream, overlapped per row group with decode; host decompression excluded"),
                "payload_bytes_per_gpu": payload, "image_bytes_per_gpu": images, "staged_batches": groups,
                "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
                "gbps": round(total * steps / el / 1e9, 2),
                "per_gpu_gbps": round(written * steps / el / 1e9, 2),
-               "payload_h2d_gbps_per_gpu": round(payload * steps / el / 1e9, 2)}
+               "payload_h2d_gbps_per_gpu": round(payload * steps / el / 1e9, 2),
+               # one pass over the file with the host's page walk (and, without device SNAPPY, its
+               # decompression on the host's chunk threads) counted too
+               "host_walk_s": round(walk, 3),
+               "per_gpu_gbps_incl_host_walk": round(written / (walk + el / steps) / 1e9, 2)}
         for sb in staged:
             sb.close()
         return out

@@ -76,35 +76,25 @@ __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
   return incl - x;
 }
 
-// The whole workgroup: the elements of one batch from block position p (the stage holds [a0, ...)),
-// output starting at d.  Results in E (nE, bend, p_next, bad, bulk_*).  Each step covers 256 input
-// bytes: thread t decodes the element that WOULD start at byte pos + t; every wave finds, by pointer
-// doubling over its 64 lanes, the path from each of its lanes to where it leaves the wave's 64 bytes;
-// the true chain is then followed across the four waves (four LDS look-ups) and a block scan places
-// its elements in the output.  Every position / count is uniform over the workgroup.
+// Wave 0: the elements of one batch from block position p (the stage holds [a0, ...)), output
+// starting at d.  Results in E (nE, bend, p_next, bad, bulk_*).
+// Every position / count here is wave-uniform; readfirstlane makes that visible to the compiler so
+// that the readlane chain steps take their lane index from an SGPR (a lane index it believes
+// divergent turns each readlane into a loop over the wave).
 __device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-struct SnapParseLds {
-  uint64_t R[kBlock];      // per thread: lanes of its wave on the path from it
-  int32_t ex[kBlock];      // per thread: where that path leaves the wave's bytes
-  uint64_t chain[4];       // per wave: its lanes on the true chain
-  int32_t wsum[4], wcnt[4];
-  int64_t wsum64[4];
-  int32_t exit;
-};
-
-__device__ __forceinline__ void snappy_parse(SnapLds& E, SnapParseLds& S, int32_t n_, int32_t p, int32_t a0_, int32_t d_,
-                                             int32_t total_) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+__device__ __forceinline__ void snappy_parse(SnapLds& E, int32_t n_, int32_t p, int32_t a0_, int32_t d_, int32_t total_) {
+  const int lane = threadIdx.x & 63;
   const int32_t n = uni(n_), a0 = uni(a0_), d = uni(d_), total = uni(total_);
   int32_t pos = uni(p), k = 0, T = 0, bulk_len = 0, bulk_src = 0;
   bool bad = false;
   for (;;) {
     pos = uni(pos);
-    if (pos >= n || pos - a0 > kSnapStage - kBlock) break;  // done, or the stage is used up
-    // ---- every thread: the element that would start at byte q
-    const int32_t q = pos + tid;
+    if (pos >= n || pos - a0 > kSnapStage - 64) break;  // done, or the stage is used up
+    // ---- every lane: the element that would start at byte q
+    const int32_t q = pos + lane;
     const int32_t o8 = int32_t(q - a0);
+    // bytes q..q+4 from two aligned LDS dwords
     const uint32_t* in32 = reinterpret_cast<const uint32_t*>(E.in);
     const uint64_t w = ((uint64_t(in32[(o8 >> 2) + 1]) << 32) | in32[o8 >> 2]) >> (8 * (o8 & 3));
     const uint32_t tag = uint32_t(w & 0xff);
@@ -138,12 +128,11 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, SnapParseLds& S, int32_
     const bool hdr_ok = int64_t(q) + hdr <= n;
     const int64_t nx64 = int64_t(q) + hdr + (lit ? len : 0);
     const int32_t nxt = nx64 > n ? int32_t(n) + 1 : int32_t(nx64);  // past the input: invalid below
-    // ---- pointer doubling inside the wave's 64 bytes: R = lanes on the path from this lane within
-    // 2^r steps, J = the lane 2^r steps on (64: the path left the wave's bytes)
-    const int32_t wbase = pos + 64 * wv;
+    // ---- the true chain from pos: pointer doubling over the window's lanes.  R = lanes on the path
+    // from this lane within 2^k steps, J = the lane 2^k steps on (64: the path left the window).
     const bool here = q < n;
     uint64_t R = here ? 1ull << lane : 0;
-    int32_t J = here ? (nxt - wbase < 64 ? nxt - wbase : 64) : 64;
+    int32_t J = here ? (nxt - pos < 64 ? nxt - pos : 64) : 64;
 #pragma unroll
     for (int r = 0; r < 6; r++) {
       const int32_t src_lane = J < 64 ? J : lane;
@@ -154,93 +143,41 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, SnapParseLds& S, int32_
         J = Jn;
       }
     }
-    const int32_t lex = __shfl(nxt, 63 - __builtin_clzll(R | 1), 64);  // every lane takes part
-    S.R[tid] = R;
-    S.ex[tid] = R ? lex : q;
-    __syncthreads();
-    if (tid == 0) {  // the true chain across the four waves
-      int32_t cur = pos;
-      for (int v = 0; v < 4; v++) {
-        const int32_t rel = cur - (pos + 64 * v);
-        uint64_t c = 0;
-        if (rel >= 0 && rel < 64 && pos + 64 * v + rel < n) {
-          c = S.R[64 * v + rel];
-          cur = S.ex[64 * v + rel];
-        }
-        S.chain[v] = c;
-      }
-      S.exit = cur;
-    }
-    __syncthreads();
-    const uint64_t chw = S.chain[wv];
-    const bool on = (chw >> lane) & 1;
-    const int32_t exitp = uni(S.exit);
-    if (__syncthreads_or(on && !hdr_ok)) {  // an element header past the input
+    const uint64_t chain = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(R >> 32)))) << 32) |
+                           uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(R)));  // lane 0's path
+    const bool on = (chain >> lane) & 1;
+    if (__ballot(on && !hdr_ok)) {  // an element header past the input
       bad = true;
       break;
     }
-    // element index and output position along the chain (thread order = chain order)
-    const int widx = __popcll(chw & ((1ull << lane) - 1));
-    const bool big = __syncthreads_or(on && len >= (1 << 24));
+    const int32_t exitp = uni(__builtin_amdgcn_readlane(nxt, 63 - __builtin_clzll(chain)));
+    const int idx = __popcll(chain & ((1ull << lane) - 1));
+    // output positions: a 32-bit DPP scan unless some element is 16 MiB or longer
     int64_t excl;
-    int idx;
-    if (lane == 63) S.wcnt[wv] = __popcll(chw);
-    if (!big) {
+    if (__ballot(on && len >= (1 << 24)) == 0) {
       const uint32_t x = on ? uint32_t(len) : 0u;
-      const uint32_t incl = wave_incl_scan32(x);
-      if (lane == 63) S.wsum[wv] = int32_t(incl);
-      __syncthreads();
-      uint32_t before = 0;
-      int cb = 0;
-      for (int v = 0; v < wv; v++) {
-        before += uint32_t(S.wsum[v]);
-        cb += S.wcnt[v];
-      }
-      excl = int64_t(before + incl - x);
-      idx = cb + widx;
+      excl = int64_t(wave_incl_scan32(x) - x);
     } else {
-      int64_t x = on ? len : 0, incl = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      if (lane == 63) S.wsum64[wv] = incl;
-      __syncthreads();
-      int64_t before = 0;
-      int cb = 0;
-      for (int v = 0; v < wv; v++) {
-        before += S.wsum64[v];
-        cb += S.wcnt[v];
-      }
-      excl = before + incl - x;
-      idx = cb + widx;
+      excl = wave_excl_scan64(on ? len : 0);
     }
-    const int nchain = S.wcnt[0] + S.wcnt[1] + S.wcnt[2] + S.wcnt[3];
     const int64_t eo = int64_t(d) + T + excl;  // stream output position
     bool ebad = false;
     if (on) {
       if (lit) ebad = nx64 > n || eo + len > total;
       else ebad = off == 0 || off > eo || eo + len > total;
     }
-    if (__syncthreads_or(ebad)) {
+    if (__ballot(ebad)) {
       bad = true;
       break;
     }
-    // every chain element now lies inside the output: lengths and positions fit 32 bits; the
-    // elements that fit the batch are a prefix of the chain
-    const bool fit = on && T + excl + len <= kSnapOut && k + idx < kSnapMaxE;
-    const int m = __syncthreads_count(fit);
+    // every chain element now lies inside the output: lengths and positions fit 32 bits
+    const uint64_t fit = __ballot(on && T + excl + len <= kSnapOut && k + idx < kSnapMaxE);
+    const int m = __popcll(fit);
     if (m == 0) {
-      if (k == 0) {  // a literal longer than a batch (the step's first element, thread 0): bulk copy
-        if (tid == 0) {
-          S.wsum[0] = int32_t(len);
-          S.wcnt[0] = pos + hdr;
-          S.exit = nxt;
-        }
-        __syncthreads();
-        bulk_len = uni(S.wsum[0]);
-        bulk_src = uni(S.wcnt[0]);
-        pos = uni(S.exit);
+      if (k == 0) {  // a literal longer than a batch (the window's first element, lane 0): bulk copy
+        bulk_len = __builtin_amdgcn_readfirstlane(int32_t(len));
+        bulk_src = pos + __builtin_amdgcn_readfirstlane(hdr);
+        pos = __builtin_amdgcn_readfirstlane(nxt);
       }
       break;
     }
@@ -250,20 +187,17 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, SnapParseLds& S, int32_
       E.elit[k + idx] = lit;
       E.esrc[k + idx] = lit ? q + hdr : off;
     }
-    if (on && idx == m - 1) S.wsum[0] = T + int32_t(excl + len);  // the last element taken: output so far
-    if (on && idx == m) S.wcnt[0] = q;  // the first element not taken
-    __syncthreads();
-    T = uni(S.wsum[0]);
+    const int last = uni(63 - __builtin_clzll(fit));  // lane of the last element taken
+    T = uni(T + __builtin_amdgcn_readlane(int32_t(excl + len), last));
     k = uni(k + m);
-    if (m < nchain) {  // batch full: the next batch starts at the first element not taken
-      pos = uni(S.wcnt[0]);
-      __syncthreads();  // S is reused by the next step
+    if (m < __popcll(chain)) {  // batch full: the next batch starts at the first element not taken
+      const uint64_t rest = chain & ~fit;
+      pos += __builtin_ctzll(rest);
       break;
     }
     pos = exitp;
-    __syncthreads();  // S is reused by the next step
   }
-  if (tid == 0) {
+  if (lane == 0) {
     E.nE = k;
     E.bend = T;
     E.eout[k] = T;
@@ -276,8 +210,7 @@ __device__ __forceinline__ void snappy_parse(SnapLds& E, SnapParseLds& S, int32_
 
 // Decode one snappy block src[0, n) into dst[0, expected).  Whole workgroup; returns PQH_OK or
 // PQH_ERR_DECOMPRESS (uniform).
-__device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expected, SnapLds& E,
-                            SnapParseLds& SP) {
+__device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expected, SnapLds& E) {
   const int tid = threadIdx.x;
   // decodedLen: binary.Uvarint, at most 10 bytes; > 0xffffffff is ErrCorrupt
   uint64_t v = 0;
@@ -311,7 +244,7 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       for (int u = tid; u < nu; u += kBlock) lp[u] = sp[u];
     }
     __syncthreads();
-    snappy_parse(E, SP, n32, p, a0, d, total);
+    if (tid < 64) snappy_parse(E, n32, p, a0, d, total);
     __syncthreads();
     if (uni(E.bad)) return PQH_ERR_DECOMPRESS;
     const int32_t nE = uni(E.nE), T = uni(E.bend);
@@ -491,7 +424,6 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
 __global__ __launch_bounds__(256) void k_snappy(const pqh_codec_page* cps, const uint8_t* src_all, uint8_t* dst_all,
                                                 int32_t* status) {
   __shared__ SnapLds E;
-  __shared__ SnapParseLds SP;
   const pqh_codec_page cp = cps[blockIdx.x];
   const uint8_t* src = src_all + cp.src_offset;
   uint8_t* dst = dst_all + cp.image_offset;
@@ -503,7 +435,7 @@ __global__ __launch_bounds__(256) void k_snappy(const pqh_codec_page* cps, const
     const int32_t raw = cp.raw_len < cp.src_len ? cp.raw_len : cp.src_len;
     snap_copy(dst, src, raw < cp.image_len ? raw : cp.image_len);  // DataPageV2 levels: never compressed
     if (raw > cp.image_len) rc = PQH_ERR_DECOMPRESS;
-    else rc = snappy_block(src + raw, cp.src_len - raw, dst + raw, int64_t(cp.image_len) - raw, E, SP);
+    else rc = snappy_block(src + raw, cp.src_len - raw, dst + raw, int64_t(cp.image_len) - raw, E);
   }
   if (threadIdx.x == 0) status[blockIdx.x] = rc;
 }
