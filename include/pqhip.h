@@ -272,7 +272,10 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out);
 int pqh_ctx_set_flags(pqh_ctx* ctx, uint32_t flags);
 void pqh_ctx_destroy(pqh_ctx* ctx);
 const char* pqh_last_error(const pqh_ctx* ctx);
-/* The HIP stream all kernels of this context are enqueued on (a hipStream_t). */
+/* The HIP stream every decode of this context is ordered on (a hipStream_t): a run is enqueued on
+ * it, and branches of the run that the context puts on its own side stream (the byte-array chain,
+ * the nesting kernels) fork from and rejoin it inside the run, so work a caller orders on this
+ * stream before / after pqh_batch_run sees the whole decode before / after it. */
 void* pqh_ctx_stream(pqh_ctx* ctx);
 
 int pqh_malloc(pqh_ctx* ctx, void** dptr, size_t bytes);
