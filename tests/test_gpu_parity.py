@@ -732,3 +732,31 @@ def test_delta_byte_array_pages(pq, ctx, delta_mode):
             cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, geom=(96, 3)))))
     compared, errors = _run_cases(pq, ctx, cases)
     assert compared == len(cases) and errors > 15
+
+
+@pytest.mark.parametrize("mode", ["graph", "direct", "one_stream", "profiled"])
+def test_launch_modes(pq, mode, monkeypatch):
+    """Every launch mode decodes the same bytes: graph replay and direct launches with the side-stream
+    branches (PLAIN byte-array chain beside k_scan / k_expand, nesting beside the byte-array copies),
+    everything on one stream (PQH_FORK=0), and profiled runs (per-kernel events, one stream).  The
+    flat file joins the chain branch before k_expand (byte-array dictionary keys need the dictionary
+    sizes); the nested one joins it before the byte sums."""
+    W = pq.writer
+    if mode == "direct":
+        monkeypatch.setenv("PQH_GRAPH", "0")
+    if mode == "one_stream":
+        monkeypatch.setenv("PQH_FORK", "0")
+    c = pq.native.Context(0, profile=(mode == "profiled"))
+    rng = np.random.default_rng(7)
+    n = 30000
+    words = [b"w%05d" % (i % 700) + b"x" * (i % 11) for i in rng.integers(0, 10**6, n)]
+    plain = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(0, 40, n)]
+    flat = W.flat([("d", W.Column(W.BYTE_ARRAY, words), W.REQUIRED),
+                   ("p", W.Column(W.BYTE_ARRAY, plain, use_dict=False), W.REQUIRED),
+                   ("i", W.Column(W.INT64, rng.integers(-2**40, 2**40, n), use_dict=False), W.REQUIRED)],
+                  12000, max_page_size=48 * 1024)
+    for data in (flat, pq.datasets.c4(rows=40_000, row_groups=2)):
+        for _ in range(2):  # a re-run of the same batch (graph replay) too
+            checked, skipped = _run_file(pq, c, data, allow_not_implemented=False)
+            assert checked > 0 and skipped == 0
+    c.close()
