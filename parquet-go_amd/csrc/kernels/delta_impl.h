@@ -1790,7 +1790,31 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
   } else {
     nxt = __builtin_amdgcn_readlane(p, last);
   }
-  n_out = total < nmax ? total : nmax;
+  int n = total < nmax ? total : nmax;
+  // A chain cut short by a lane that synchronised on a false header (low-entropy packed data reads
+  // as plausible headers) ends on a true header: continue from it serially inside the same window
+  // (one LDS header parse per block) instead of restaging the window for the next few blocks.
+  while (!stop && n < nmax) {
+    int32_t d;
+    if (!lds_block(data, nxt, eloc, plim, dlim, is64, mbc, gbytes, d)) {
+      int32_t dat;
+      uint64_t md, wd;
+      const int32_t de = nxt < plim ? lds_hdr(data, nxt, is64, mbc, gbytes, dat, md, wd) : 0;
+      stop = nxt + 24 > eloc || (nxt < plim && (de < 0 || de > eloc));
+      break;
+    }
+    int32_t dat;
+    uint64_t md, wd;
+    lds_hdr(data, nxt, is64, mbc, gbytes, dat, md, wd);
+    if (lane == 0) {
+      blkbit[n] = dat * 8;
+      blkw[n] = wd;
+      mdt[n] = md;
+    }
+    n++;
+    nxt = d;
+  }
+  n_out = n;
   next_out = nxt;
   stop_out = stop;
 }
