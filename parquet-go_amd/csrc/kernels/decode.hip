@@ -635,7 +635,7 @@ __device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, in
         wq = vb >= 4 ? wq : vb <= 0 ? 0u : (wq & ((1u << (8 * vb)) - 1u));
       }
     }
-    if (threadIdx.x == 0) stage[nvec * 4] = 0;  // the word after the last one (alignbit reads k+1)
+    if (threadIdx.x < 2) stage[nvec * 4 + threadIdx.x] = 0;  // the words after the last one (funnel shifts read k+1, k+2)
     __syncthreads();
     // G values per thread and step (Sink::kGroup): 4 for 4-byte outputs, so that a wave's stores
     // are one contiguous kilobyte
@@ -649,6 +649,22 @@ __device__ void bp_staged(const uint8_t* img, int64_t e, int w, int64_t data, in
         const uint32_t x = __builtin_amdgcn_alignbit(stage[(bit0 >> 5) + 1], stage[bit0 >> 5], bit0 & 31);
 #pragma unroll
         for (int j = 0; j < G; j++) v[j] = (x >> (uint32_t(j) * uint32_t(w))) & m;
+        sink(i0, v, int(c1 - i0 < G ? c1 - i0 : G));
+      }
+      continue;
+    }
+    if (w * G <= 64) {
+      // up to 64 bits per group (dictionary indices up to 16 bits wide, 8-value groups up to 8):
+      // two funnel shifts of three LDS dwords (the stage keeps slack words after its last one)
+      for (int64_t i0 = c0 + G * int64_t(threadIdx.x); i0 < c1; i0 += G * kBlock) {
+        uint32_t v[8];
+        const uint32_t bit0 = lead_bits + uint32_t(i0 - c0) * uint32_t(w);
+        const uint32_t k0 = bit0 >> 5, sh = bit0 & 31;
+        const uint32_t s0 = stage[k0], s1 = stage[k0 + 1], s2 = stage[k0 + 2];
+        const uint64_t x = uint64_t(__builtin_amdgcn_alignbit(s1, s0, sh)) |
+                           (uint64_t(__builtin_amdgcn_alignbit(s2, s1, sh)) << 32);
+#pragma unroll
+        for (int j = 0; j < G; j++) v[j] = uint32_t(x >> (uint32_t(j) * uint32_t(w))) & m;
         sink(i0, v, int(c1 - i0 < G ? c1 - i0 : G));
       }
       continue;
