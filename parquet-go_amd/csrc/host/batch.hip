@@ -183,6 +183,12 @@ int32_t resolve_kind(int32_t type, int32_t type_length, int32_t enc, int32_t* vs
   }
 }
 
+// Chunks output as offsets + bytes: BYTE_ARRAY, and FIXED_LEN_BYTE_ARRAY without a fixed output
+// width (type_length <= 0, or DELTA_BYTE_ARRAY pages: the planner then sets value_size 0).
+bool is_ba_chunk(const DevChunk& D) {
+  return D.physical_type == PQH_BYTE_ARRAY || (D.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && D.value_size == 0);
+}
+
 }  // namespace pqhip
 
 struct pqh_batch {
@@ -453,8 +459,21 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       return set_err(ctx, PQH_ERR_ARG, "chunk page range out of bounds");
     }
     const uint64_t chunk_err = C.host_status != PQH_OK ? err_key(0, 0, C.host_status) : kNoError;
-    const bool ba_chunk = C.column.physical_type == PQH_BYTE_ARRAY ||
-                          (C.column.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && C.column.type_length == 0);
+    // FIXED_LEN_BYTE_ARRAY pages with DELTA_BYTE_ARRAY go to byteArrayDeltaDecoder, which yields
+    // variable-length []byte with no length check (chunk_reader.go:67-78, type_bytearray.go:189-240):
+    // such a chunk is output as offsets + bytes.  Its fixed-width pages (PLAIN, dictionary) decode
+    // into the values buffer (scratch) as usual, and k_ba_expand lays them out as byte arrays.
+    // (A FIXED_LEN_BYTE_ARRAY chunk whose type_length is <= 0 has no fixed width either.)
+    bool flba_var = false;
+    if (C.column.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && C.column.type_length > 0)
+      for (int32_t i = 0; i < C.num_pages && !flba_var; i++) {
+        const int64_t p = int64_t(C.first_page) + i;
+        if (p >= 0 && p < num_pages && pages[p].page_type != PQH_DICTIONARY_PAGE &&
+            pages[p].encoding == PQH_ENC_DELTA_BYTE_ARRAY)
+          flba_var = true;
+      }
+    if (flba_var) D.value_size = 0;
+    const bool ba_chunk = is_ba_chunk(D);
     D.batile_base = int32_t(b->ba_tiles.size());
     if (ba_chunk) b->ba_chunks.push_back(c);
     int64_t level_base = 0;
@@ -513,11 +532,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
            int64_t(Q.rep_levels_byte_length) + Q.def_levels_byte_length > Q.image_len))
         P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
       if (kind == K_UNSUPPORTED) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_UNSUPPORTED));
-      const bool device_ready = kind == K_PLAIN_FIXED || kind == K_PLAIN_INT96 || kind == K_PLAIN_BOOL ||
-                                kind == K_RLE_BOOL || kind == K_FLBA_NEGATIVE || kind == K_UNSUPPORTED ||
-                                kind == K_DELTA32 || kind == K_DELTA64 || kind == K_DICT || kind == K_PLAIN_BA ||
-                                kind == K_DLBA || (kind == K_DBA && C.column.physical_type == PQH_BYTE_ARRAY);
-      if (!device_ready) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_NOT_IMPLEMENTED));
       const int64_t n = Q.num_values > 0 ? Q.num_values : 0;
       P.level_base = level_base;
       level_base += n;
@@ -539,7 +553,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         }
         if (kind == K_DBA) b->has_dba = true;
       }
-      const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT || kind == K_DBA);
+      const bool ba_page = ba_chunk && (kind == K_PLAIN_BA || kind == K_DLBA || kind == K_DICT || kind == K_DBA ||
+                                        (flba_var && kind == K_PLAIN_FIXED));
       if (ba_page && P.host_err == kNoError && n > 0) {
         P.batile_base = int32_t(b->ba_tiles.size());
         P.batile_n = int32_t(ceil_div(n, kBaTile));
@@ -548,7 +563,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         // output bytes: at most the page (PLAIN / DELTA_LENGTH); dictionary gathers are estimated
         // from the dictionary page's mean entry and re-sized after the first run if short
         int64_t est = kind == K_DBA ? 4 * int64_t(Q.image_len) : Q.image_len;  // prefixes repeat bytes
-        if (kind == K_DICT && D.dict_page >= 0) {
+        if (pvs > 0) {  // fixed-width page of a FIXED_LEN_BYTE_ARRAY chunk with DELTA_BYTE_ARRAY pages
+          est = n * pvs;
+        } else if (kind == K_DICT && D.dict_page >= 0) {
           const pqh_page& DQ = pages[D.dict_page];
           const int64_t nv = std::max(1, DQ.num_values);
           const int64_t mean = std::max<int64_t>(0, DQ.image_len - 4 * nv) / nv;
@@ -653,12 +670,16 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
   }
 
-  for (size_t i = 0; i < b->ba_tiles.size(); i++)
-    if (b->hpages[size_t(b->ba_tiles[i].page)].kind == K_DLBA) b->ba_xlist.push_back(int32_t(i));
+  // k_ba_expand's contiguous copies: DELTA_LENGTH tiles and the fixed-width tiles of FIXED_LEN_BYTE_ARRAY
+  // chunks laid out as byte arrays (copied from the values buffer)
+  for (size_t i = 0; i < b->ba_tiles.size(); i++) {
+    const DevPage& P = b->hpages[size_t(b->ba_tiles[i].page)];
+    if (P.kind == K_DLBA || P.value_size > 0) b->ba_xlist.push_back(int32_t(i));
+  }
   b->ba_ncopy = int32_t(b->ba_xlist.size());
   for (size_t i = 0; i < b->ba_tiles.size(); i++) {  // dictionary tiles (PLAIN pages: k_ba_wcopy)
-    const int32_t k = b->hpages[size_t(b->ba_tiles[i].page)].kind;
-    if (k != K_DLBA && k != K_DBA && k != K_PLAIN_BA) b->ba_xlist.push_back(int32_t(i));
+    const DevPage& P = b->hpages[size_t(b->ba_tiles[i].page)];
+    if (P.kind != K_DLBA && P.kind != K_DBA && P.kind != K_PLAIN_BA && P.value_size == 0) b->ba_xlist.push_back(int32_t(i));
   }
   // k_ba_sum's work list (after the copy + gather lists): every tile, except that PLAIN pages (and in
   // page mode DELTA_LENGTH pages) are represented by their tile 0: their sums come from k_ba_wstitch
@@ -708,8 +729,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     const int64_t n = b->chunk_n[size_t(c)];
     D.values_cap = n;
     void* p = nullptr;
-    const bool ba_chunk = D.physical_type == PQH_BYTE_ARRAY || (D.physical_type == PQH_FIXED_LEN_BYTE_ARRAY && D.type_length == 0);
-    if ((rc = dalloc(b, &p, ba_chunk ? 64 : size_t(n) * size_t(std::max(D.value_size, 1)) + 64))) break;
+    const bool ba_chunk = is_ba_chunk(D);
+    // values: fixed width, or the fixed-width pages' scratch of a FIXED_LEN_BYTE_ARRAY chunk laid out as byte arrays
+    const int32_t vsz = D.value_size > 0 ? D.value_size : (ba_chunk && D.physical_type == PQH_FIXED_LEN_BYTE_ARRAY
+                                                                ? std::max(D.type_length, 0) : 0);
+    if ((rc = dalloc(b, &p, vsz == 0 && ba_chunk ? 64 : size_t(n) * size_t(std::max(vsz, 1)) + 64))) break;
     D.values = static_cast<uint8_t*>(p);
     if (ba_chunk) {
       if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int64_t)))) break;
@@ -1066,15 +1090,23 @@ int pqh_batch_sync(pqh_batch* b) {
   // Byte-array outputs sized from an estimate (dictionary gathers): grow the chunks that came out
   // short (and decoded without error), then decode again.  Contents are deterministic, so this
   // happens at most once per batch.
+  // A chunk with a failing page needs (and gets) the bytes of the pages before it: what NextRow reads
+  // before it meets the error (data_store.go:236-260); the sums at and after a failing page may be
+  // garbage, so they never size an allocation.
   bool regrow = false;
   for (int32_t c : b->ba_chunks) {
     DevChunk& D = b->hchunks[size_t(c)];
     if (b->chunk_bytes[size_t(c)] <= D.bytes_cap) continue;
-    bool ok = true;
-    for (int32_t i = 0; i < D.num_pages && ok; i++) ok = b->states[size_t(D.first_page + i)].err == kNoError;
-    if (!ok) continue;
+    int64_t cap = b->chunk_bytes[size_t(c)];
+    for (int32_t i = 0; i < D.num_pages; i++) {
+      const PageState& S = b->states[size_t(D.first_page + i)];
+      if (S.err == kNoError) continue;
+      cap = 0;  // offsets[value_base of the failing page] = the bytes before it
+      if (S.value_base > 0) HIP_TRY(ctx, bounce_d2h(ctx, &cap, D.offsets + S.value_base, sizeof(int64_t)));
+      break;
+    }
+    if (cap <= D.bytes_cap) continue;
     void* np = nullptr;
-    const int64_t cap = b->chunk_bytes[size_t(c)];
     HIP_TRY(ctx, hipMalloc(&np, size_t(cap) + 64));
     for (auto& a : b->allocations)
       if (a == D.bytes) {
@@ -1115,7 +1147,8 @@ int pqh_batch_sync(pqh_batch* b) {
     const double n = P.num_values > 0 ? P.num_values : 0;
     const double levels = (C.max_def > 0 ? n : 0) + (C.max_rep > 0 ? n : 0);
     const double vals = double(S.nn) * P.value_size;
-    wr += levels + vals;
+    // (fixed-width pages of a chunk laid out as byte arrays: their output is counted with the chunk's bytes)
+    wr += levels + (C.value_size > 0 ? vals : 0.0);
     // everything after the prologue is moved by k_expand (or k_dict_global for large dictionaries)
     const int kx = (P.kind == K_DICT && P.dict_page >= 0 &&
                     int64_t(std::max(0, b->pages[size_t(P.dict_page)].num_values)) * P.value_size > kDictLdsMax)
@@ -1206,11 +1239,17 @@ int pqh_batch_sync(pqh_batch* b) {
 
 int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num_pages) {
   if (!b || !b->synced) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "batch not synced");
+  std::vector<int32_t> codec_fail(b->chunks.size(), -2);  // per chunk, computed on first use
   for (int32_t p = 0; p < num_pages && size_t(p) < b->pages.size(); p++) {
     const PageState& S = b->states[size_t(p)];
     pqh_page_result& r = out[p];
     memset(&r, 0, sizeof(r));
-    if (S.err != kNoError) {
+    const int32_t c = b->hpages[size_t(p)].chunk;
+    if (codec_fail[size_t(c)] == -2) codec_fail[size_t(c)] = codec_fail_page(b, c);
+    if (codec_fail[size_t(c)] >= 0) {  // readChunk failed (as pqh_batch_chunk_out): no page of it is read
+      r.status = PQH_ERR_DECOMPRESS;
+      r.phase = PQH_PHASE_LOAD;
+    } else if (S.err != kNoError) {
       r.status = int32_t(S.err & 0xff);
       r.phase = int32_t(S.err >> 56);
       r.index = int64_t((S.err >> 8) & 0xffffffffffffull);
@@ -1255,14 +1294,11 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
     out->status = int32_t(S.err & 0xff);
     out->phase = phase;
     out->index = idx;
-    // the whole-page call (readNextPage, data_store.go:241) fails; a ranged call fails when its
-    // range reaches the failing level slot (load errors fail every call, value errors below)
-    if (phase == PQH_PHASE_LOAD || ((phase == PQH_PHASE_REP || phase == PQH_PHASE_DEF) && idx < s1)) return PQH_OK;
-    if (phase != PQH_PHASE_VALUES) {
-      out->status = PQH_OK;
-      out->phase = 0;
-      out->index = 0;
-    }
+    // The whole-page call (readNextPage, data_store.go:241) fails.  A ranged call of a page whose
+    // levels failed fails too, even when its range ends before the failing slot (where the
+    // reference would return that range): the device decodes no values of such a page, so there
+    // are none to return (documented divergence).  Value errors: below.
+    if (phase != PQH_PHASE_VALUES) return PQH_OK;
   }
   if (s1 == s0) return PQH_OK;
   // levels of the range, and the non-null values before / inside it
@@ -1469,9 +1505,9 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
   }
   pqh_batch* b = *out;
   b->owned_payload = img;
-  b->d_src = d_src;
   b->src_bytes = hb->payload.size();
   b->codec_n = int32_t(hb->codec_pages.size());
+  // d_src passes to the batch only once nothing can fail: on an error the caller still owns (and frees) it
   if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec), sizeof(pqh_codec_page) * size_t(b->codec_n))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec_status), sizeof(int32_t) * size_t(b->codec_n)))) {
     pqh_batch_destroy(b);
@@ -1484,6 +1520,7 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
     *out = nullptr;
     return set_err(ctx, PQH_ERR_HIP, std::string("codec pages: ") + hipGetErrorString(e));
   }
+  b->d_src = d_src;
   return PQH_OK;
 }
 }  // namespace

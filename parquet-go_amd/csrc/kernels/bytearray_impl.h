@@ -587,6 +587,13 @@ __device__ void ba_tile_sum(const DevBatch& b, int page, int32_t k, int64_t* wsu
     const int64_t lim = ba_limit(b, page, P, S);
     const int64_t v0 = int64_t(k) * kBaTile;
     const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
+    if (P.value_size > 0) {  // fixed-width page of a FIXED_LEN_BYTE_ARRAY chunk laid out as byte arrays
+      if (threadIdx.x == 0) {
+        b.basums[P.batile_base + k] = v1 > v0 ? (v1 - v0) * P.value_size : 0;
+        b.basums2[P.batile_base + k] = 0;
+      }
+      return;
+    }
     const bool is_dict = P.kind == K_DICT;
     const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
     const int32_t* aux = C.aux + S.value_base;
@@ -871,6 +878,18 @@ __device__ __forceinline__ void ba_expand_tile(const DevBatch& b, const Tile& t,
   const int64_t v0 = int64_t(t.k) * kBaTile;
   const int64_t v1 = v0 + kBaTile < lim ? v0 + kBaTile : lim;
   if (v0 >= v1) return;
+  if (P.value_size > 0) {  // fixed-width page of a FIXED_LEN_BYTE_ARRAY chunk laid out as byte arrays:
+    if constexpr (!kGather) {  // its values (already decoded into the values buffer) are contiguous
+      const int64_t vs = P.value_size, n = v1 - v0;
+      const int64_t base = b.basums[P.batile_base + t.k];
+      PQH_G int64_t* offs = C.offsets + S.value_base + 1 + v0;
+      for (int64_t i = threadIdx.x; i < n; i += kBlock) offs[i] = base + (i + 1) * vs;
+      int64_t len = n * vs;
+      if (len > C.bytes_cap - base) len = C.bytes_cap - base;
+      if (len > 0) block_copy(C.bytes + base, C.values + (S.value_base + v0) * vs, len);
+    }
+    return;
+  }
   const bool is_dict = P.kind == K_DICT, is_dlba = P.kind == K_DLBA, is_dba = P.kind == K_DBA;
   if (is_dba || is_dlba == kGather) return;  // k_dba_expand; the other kernel
   const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};

@@ -25,6 +25,8 @@ STATUS = {
 }
 OK = 0
 NOT_IMPLEMENTED = 33
+# error phases (pqh_phase): page load (readChunk), repetition levels, definition levels, values
+PHASE_LOAD, PHASE_REP, PHASE_DEF, PHASE_VALUES = range(4)
 CTX_PROFILE = 1
 PAYLOAD_PAD = 256
 

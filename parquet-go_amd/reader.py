@@ -9,8 +9,10 @@ Mirrors github.com/fraugster/parquet-go's FileReader (file_reader.go:32-351) for
       chunks are walked on the host (thrift + codecs) and decoded on the GPU in ONE batch
   FileReader.ReadColumns()          -> {path: ColumnData}: columnar results of readValues for
       every page of the chunk (values, dLevel, rLevel) — the "throughput path" of SURVEY.md §8(b)
-Errors follow the reference: any page error fails the read of that chunk and raises DecodeError
-carrying the status, phase, index and page of the FIRST error in decode order.
+Errors follow the reference: ReadColumns raises DecodeError (status, phase, index and page of the
+FIRST error in decode order) for any failing chunk; the row-group cursor fails a row group only on
+readChunk errors (walker, codecs, page load), and NextRow raises a readValues error at the row that
+reaches the failing page (records.py).
 """
 import numpy as np
 
@@ -44,7 +46,12 @@ class ColumnData:
         self.rep_levels = None
         self.offsets = None
         self.data = None
-        if out.status != native.OK:
+        self.nesting = None
+        # readChunk errors (host walker, codecs, page load / decoder init: phase 0) fail the whole row
+        # group (chunk_reader.go:394-400); otherwise the outputs of the pages before the first failing
+        # one stay readable, as the reference decodes page by page (data_store.go:236-260)
+        self.load_error = self._load_error(out, page_info or [])
+        if out.status != native.OK and self.load_error is not None:
             return
         if out.value_size > 0:
             raw = ctx.d2h_array(out.values, out.num_non_null * out.value_size)
@@ -59,7 +66,9 @@ class ColumnData:
             self.def_levels = ctx.d2h_array(out.def_levels, out.num_values)
         if out.rep_levels:
             self.rep_levels = ctx.d2h_array(out.rep_levels, out.num_values)
-        self.nesting = None  # [(offsets int32, validity u8) per repetition level], leaf validity u8
+        if out.status != native.OK:
+            return
+        # nesting: [(offsets int32, validity u8) per repetition level], leaf validity u8
         if nest is not None and nest.num_levels and nest.status == native.OK:
             levels = []
             for k in range(nest.num_levels):
@@ -70,6 +79,24 @@ class ColumnData:
             leaf = ctx.d2h_array(nest.leaf_validity, nest.num_leaf_slots) if nest.leaf_validity else \
                 np.zeros(0, np.uint8)
             self.nesting = (levels, leaf)
+
+    @staticmethod
+    def _load_error(out, page_info):
+        """(status, phase, index, page) of the chunk's readChunk failure, or None."""
+        if out.status == native.OK:
+            return None
+        if out.error_phase == native.PHASE_LOAD:
+            return (out.status, out.error_phase, out.error_index, out.error_page)
+        for k, (pt, n, res) in enumerate(page_info):
+            if res.status != native.OK and res.phase == native.PHASE_LOAD:
+                return (res.status, res.phase, res.index, k)
+        return None
+
+    def raise_for_load(self):
+        """readChunk (chunk_reader.go:299-362): only page-load / walker / codec errors fail here."""
+        if self.load_error is not None:
+            raise DecodeError(self.path, *self.load_error)
+        return self
 
     def raise_for_status(self):
         if self.status != native.OK:
@@ -174,15 +201,19 @@ class FileReader:
             raise EOFError("EOF")
         self.row_group_position += 1
         rg = self.row_group_position - 1
-        self._loaded = decode_chunks(self.ctx, self.file, rg, rg + 1, self.selected, self.validate_crc)
+        self._loaded = None
         self._rows = None
+        loaded = decode_chunks(self.ctx, self.file, rg, rg + 1, self.selected, self.validate_crc)
+        for c in loaded:  # readRowGroupData: the first column whose readChunk fails (chunk_reader.go:394-400)
+            c.raise_for_load()
+        self._loaded = loaded
 
     def _advance_if_needed(self):  # advanceIfNeeded (file_reader.go:226-238)
         if (self.row_group_position == 0 or self.skip_row_group
                 or self.current_record >= self.file.row_group_num_rows(self.row_group_position - 1)):
             try:
                 self._read_row_group()
-            except EOFError:
+            except Exception:  # io.EOF or a readRowGroup error: the next call moves on (file_reader.go:228-232)
                 self.skip_row_group = True
                 raise
             self.current_record = 0
@@ -221,8 +252,8 @@ class FileReader:
 
         self._advance_if_needed()
         if self._rows is None:
-            for c in self._loaded:  # readRowGroupData fails on any chunk error (chunk_reader.go:394-400)
-                c.raise_for_status()
+            # readValues errors surface page by page, when the assembly reaches the failing page
+            # (ColumnStore.get -> readNextPage, data_store.go:236-269); rows before it are returned
             if self._schema is None:
                 self._schema = self.file.schema()
             cols = {self.selected[i]: (c, c.physical_type, c.path) for i, c in enumerate(self._loaded)}

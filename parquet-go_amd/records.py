@@ -13,14 +13,24 @@ group a list of dicts, a group a dict; null / empty fields are absent, exactly a
 map[string]interface{} rows.  Level cursors are page-local as in the reference (readNextPage resets
 them), so the assembly sees the same page boundaries.
 """
+from collections import namedtuple
+
 import numpy as np
 
 REQUIRED, OPTIONAL, REPEATED = 0, 1, 2
+# readValues outcome of one page: status 0 or the first error's (status, phase, index)
+PageResult = namedtuple("PageResult", "status phase index")
+PAGE_OK = PageResult(0, 0, 0)
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
 
 
 class RecordError(RuntimeError):
-    pass
+    """An error of the row assembly; for a page that failed to decode, its (status, phase, index)
+    and the page's position in the chunk."""
+
+    def __init__(self, msg, status=0, phase=0, index=0, page=-1):
+        super().__init__(msg)
+        self.status, self.phase, self.index, self.page = status, phase, index, page
 
 
 def page_values(ptype, col, v0, nn):
@@ -49,7 +59,7 @@ class LeafStore:
         self.rep_typ = rep_typ
         self.max_d, self.max_r = max_d, max_r
         self.skipped = skipped
-        self.pages = pages or []  # [(status, n, def, rep, values())] of the chunk's data pages
+        self.pages = pages or []  # [(result, n, def, rep, values())] of the chunk's data pages
         self.page_idx = 0
         self.read_pos = 0
         self.d = self.r = np.zeros(0, np.uint8)
@@ -59,14 +69,14 @@ class LeafStore:
     def from_column(cls, col, ptype, path, rep_typ):
         """Pages of a GPU-decoded chunk (reader.ColumnData with its page results)."""
         pages = []
-        if col.status == 0:
+        if col.load_error is None:  # (a chunk whose readChunk failed never gets here: its row group fails)
             for pt, n, res in col.page_info:
                 if pt == 2:  # the dictionary page is consumed at chunk load
                     continue
                 lo = res.level_offset
                 d = col.def_levels[lo:lo + n] if col.def_levels is not None else np.zeros(n, np.uint8)
                 r = col.rep_levels[lo:lo + n] if col.rep_levels is not None else np.zeros(n, np.uint8)
-                pages.append((res.status, n, d, r,
+                pages.append((res, n, d, r,
                               lambda v0=res.value_offset, nn=res.num_non_null: page_values(ptype, col, v0, nn)))
         return cls(col, path, rep_typ, col.max_def, col.max_rep, pages)
 
@@ -74,9 +84,10 @@ class LeafStore:
         if self.page_idx >= len(self.pages):
             raise RecordError(f"{self.path}: out of range: requested page index = {self.page_idx} "
                               f"total number of pages = {len(self.pages)}")
-        status, n, d, r, vals = self.pages[self.page_idx]
-        if status:
-            raise RecordError(f"{self.path}: page {self.page_idx} failed to decode (status {status})")
+        res, n, d, r, vals = self.pages[self.page_idx]
+        if res.status:  # readValues fails: the error surfaces here, page_idx stays (every later call fails too)
+            raise RecordError(f"{self.path}: page {self.page_idx} failed to decode (status {res.status}, phase "
+                              f"{res.phase}, index {res.index})", res.status, res.phase, res.index, self.page_idx)
         self.page_idx += 1
         self.read_pos = 0
         self.d, self.r = d, r

@@ -34,6 +34,9 @@ def flat_all_types(n=30000, v2=False, codec=0, page=64 * 1024, rows_per_group=12
     d32 = rng.integers(-2**31, 2**31 - 1, n).astype(np.int32)
     s = _strings(rng, n)
     smask = rng.random(n) < 0.1
+    fl_sorted = fl[np.lexsort(fl.T[::-1])]
+    fl6 = rng.integers(97, 101, (n, 6), dtype=np.uint8)[np.minimum(rng.geometric(0.002, n), n - 1)]
+    fl6_mask = rng.random(n) < 0.05
     cols = [
         ("i32_dict", W.Column(W.INT32, i32), W.REQUIRED),
         ("i64_plain", W.Column(W.INT64, i64, use_dict=False), W.REQUIRED),
@@ -52,6 +55,13 @@ def flat_all_types(n=30000, v2=False, codec=0, page=64 * 1024, rows_per_group=12
         ("str_dict_opt", W.optional(W.BYTE_ARRAY, [s[k % 500] for k in range(n)], smask), W.OPTIONAL),
         ("str_dlba", W.Column(W.BYTE_ARRAY, s, encoding=W.DELTA_LENGTH_BYTE_ARRAY, use_dict=False), W.REQUIRED),
         ("str_dba", W.Column(W.BYTE_ARRAY, sorted(s), encoding=W.DELTA_BYTE_ARRAY, use_dict=False), W.REQUIRED),
+        # FIXED_LEN_BYTE_ARRAY + DELTA_BYTE_ARRAY (chunk_reader.go:71-72): sorted rows share prefixes
+        ("flba16_dba", W.Column(W.FIXED_LEN_BYTE_ARRAY, fl_sorted, type_length=16, encoding=W.DELTA_BYTE_ARRAY,
+                                use_dict=False), W.REQUIRED),
+        # dictionary pages until the dictionary page would pass 2 KiB, then DELTA_BYTE_ARRAY pages in
+        # the same chunk (fixed-width dictionary values and variable-length DBA values in one chunk)
+        ("flba6_dict_dba", W.optional(W.FIXED_LEN_BYTE_ARRAY, fl6, fl6_mask, type_length=6,
+                                      encoding=W.DELTA_BYTE_ARRAY, dict_page_limit=2048), W.OPTIONAL),
     ]
     data = W.flat(cols, rows_per_group, v2=v2, codec=codec, max_page_size=page, crc=crc)
     return data

@@ -3,6 +3,8 @@ import numpy as np
 
 from oracle import oracle as O
 
+DELTA_BYTE_ARRAY = 7  # parquet.thrift Encoding
+
 
 class Expected:
     def __init__(self):
@@ -32,7 +34,14 @@ def oracle_chunk(fr, rg, ci):
     res = O.decode_chunk(ch)
     vals, defs, reps, offs, data = [], [], [], [], []
     base = 0
+    # FIXED_LEN_BYTE_ARRAY pages with DELTA_BYTE_ARRAY yield variable-length []byte
+    # (type_bytearray.go:189-240): the product lays such a chunk out as offsets + bytes throughout
+    flba_var = col.physical_type == O.FIXED_LEN_BYTE_ARRAY and col.type_length > 0 and \
+        any(p.encoding == DELTA_BYTE_ARRAY for p in ch.pages)
     for i, r in enumerate(res):
+        if flba_var and r.offsets is None:
+            L = col.type_length
+            r.offsets = np.arange(len(r.values) // L + 1, dtype=np.int64) * L
         if r.status and e.status == 0:
             e.status, e.phase, e.index, e.page = r.status, r.phase, r.index, i
         e.n += r.num_values

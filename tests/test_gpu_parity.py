@@ -29,7 +29,7 @@ def delta_mode(request, monkeypatch):
     return request.param
 
 
-def _run_file(pq, ctx, data, allow_not_implemented=True):
+def _run_file(pq, ctx, data):
     f = pq.native.File(data)
     ncols = len(f.columns())
     cols = list(range(ncols))
@@ -38,9 +38,9 @@ def _run_file(pq, ctx, data, allow_not_implemented=True):
     checked = skipped = 0
     for k, col in enumerate(res):
         rg, ci = divmod(k, ncols)
-        if col.status == pq.native.NOT_IMPLEMENTED and allow_not_implemented:
-            skipped += 1
-            continue
+        # every (type, encoding) pair getValuesDecoder accepts (chunk_reader.go:106-159) decodes
+        # on the device: NOT_IMPLEMENTED is a failure, never a skip
+        assert col.status != pq.native.NOT_IMPLEMENTED, f"rg{rg} {col.path}: NOT_IMPLEMENTED"
         assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"rg{rg} {col.path}")
         checked += 1
     return checked, skipped
@@ -56,7 +56,7 @@ def test_all_types(pq, ctx, v2, codec):
 
 @pytest.mark.parametrize("v2", [False, True])
 def test_c2_schema(pq, ctx, v2):
-    checked, skipped = _run_file(pq, ctx, fixtures.flat_c2_like(n=40000, v2=v2), allow_not_implemented=False)
+    checked, skipped = _run_file(pq, ctx, fixtures.flat_c2_like(n=40000, v2=v2))
     assert checked == 4 * 6
 
 
@@ -106,7 +106,7 @@ def test_large_pages_single_run(pq, ctx):
     cols = [("d", W.Column(W.INT32, rng.integers(0, 4096, n).astype(np.int32)), W.REQUIRED),
             ("o", W.optional(W.INT64, rng.integers(0, 2**60, n), rng.random(n) < 0.3, use_dict=False), W.OPTIONAL),
             ("b", W.Column(W.BOOLEAN, (rng.random(n) < 0.5).astype(np.uint8)), W.REQUIRED)]
-    checked, _ = _run_file(pq, ctx, W.flat(cols, n), allow_not_implemented=False)
+    checked, _ = _run_file(pq, ctx, W.flat(cols, n))
     assert checked == 3
 
 
@@ -209,8 +209,7 @@ def _run_cases(pq, ctx, cases):
         compared = errors = 0
         for i, (col, dict_img, (ptype, nv, enc, dl, rl, img)) in enumerate(cases):
             o = b.chunk_out(i)
-            if o.status == N.NOT_IMPLEMENTED:
-                continue
+            assert o.status != N.NOT_IMPLEMENTED, f"case {i}: NOT_IMPLEMENTED"
             cd = pq.reader.ColumnData("fuzz", col, o, [], ctx)
             od = O.decode_dict_page(col, dict_img[0], dict_img[1], dict_img[2]) if dict_img else None
             if od is not None and od.status:  # the dictionary page itself fails
@@ -455,7 +454,7 @@ def test_delta_writer_pages(pq, ctx, delta_mode):
             ("c", W.optional(W.INT64, rng.integers(0, 2**40, n), rng.random(n) < 0.2, encoding=W.DELTA_BINARY_PACKED,
                              use_dict=False), W.OPTIONAL)]
     for v2 in (False, True):
-        checked, _ = _run_file(pq, ctx, W.flat(cols, n // 2, v2=v2), allow_not_implemented=False)
+        checked, _ = _run_file(pq, ctx, W.flat(cols, n // 2, v2=v2))
         assert checked == 6
 
 
@@ -531,7 +530,7 @@ def test_byte_array_files(pq, ctx):
             ("d", W.Column(W.BYTE_ARRAY, [s[k % 4000] for k in range(n)]), W.REQUIRED),
             ("o", W.optional(W.BYTE_ARRAY, [s[k % 300] for k in range(n)], mask), W.OPTIONAL)]
     for v2, codec in ((False, 0), (True, 1), (True, 2)):
-        checked, _ = _run_file(pq, ctx, W.flat(cols, 25000, v2=v2, codec=codec), allow_not_implemented=False)
+        checked, _ = _run_file(pq, ctx, W.flat(cols, 25000, v2=v2, codec=codec))
         assert checked == 3 * 4
 
 
@@ -540,7 +539,7 @@ def test_c5_dictionary_fallback(pq, ctx, delta_mode):
     from parquet_go_amd import datasets
 
     data = datasets.c5(rows=600_000, row_groups=2)
-    checked, _ = _run_file(pq, ctx, data, allow_not_implemented=False)
+    checked, _ = _run_file(pq, ctx, data)
     assert checked == 2
 
 
@@ -730,8 +729,123 @@ def test_delta_byte_array_pages(pq, ctx, delta_mode):
                                       _dba_page(strs, plens=pl, slens=[len(x) for x in strs]))))
             cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, total=n + 1))))
             cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs, geom=(96, 3)))))
+    # FIXED_LEN_BYTE_ARRAY + DELTA_BYTE_ARRAY (chunk_reader.go:67-78): byteArrayDeltaDecoder yields
+    # variable-length []byte whatever type_length says (no length check): values of the declared
+    # length, shorter, longer and empty ones all come out as offsets + bytes
+    for tl in (16, 4):
+        for n in (1, 300, 5000):
+            fixed = [bytes(rng.integers(97, 100, tl).astype(np.uint8)) for _ in range(n)]
+            ragged = [bytes(rng.integers(97, 100, int(rng.integers(0, 2 * tl))).astype(np.uint8)) for _ in range(n)]
+            for strs in (sorted(fixed), ragged):
+                img = _dba_page(strs)
+                col = (W.FIXED_LEN_BYTE_ARRAY, tl, 0, 0)
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, img)))
+                cases.append((col, None, (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, img[: int(rng.integers(0, len(img)))])))
     compared, errors = _run_cases(pq, ctx, cases)
     assert compared == len(cases) and errors > 15
+
+
+def test_flba_mixed_chunks(pq, ctx, delta_mode):
+    """FIXED_LEN_BYTE_ARRAY chunks that mix fixed-width pages (PLAIN, dictionary) with
+    DELTA_BYTE_ARRAY pages (the reference decodes each page with its own decoder,
+    chunk_reader.go:249-251): the whole chunk comes out as offsets + bytes, the fixed pages'
+    values at their declared length, in page order; plus optional V2 pages and failing pages."""
+    W = fixtures.W
+    N = pq.native
+    rng = np.random.default_rng(45)
+    L = 16
+    dict_vals = [bytes(rng.integers(0, 256, L).astype(np.uint8)) for _ in range(40)]
+    dimg = b"".join(dict_vals)
+
+    def plain_page(n):
+        return (O.DATA_PAGE, n, W.PLAIN, 0, 0, rng.integers(0, 256, n * L).astype(np.uint8).tobytes())
+
+    def dict_page(n, bad=False):
+        idx = rng.integers(0, len(dict_vals), n).astype(np.int32)
+        if bad:
+            idx[n // 2] = 63
+        return (O.DATA_PAGE, n, W.RLE_DICTIONARY, 0, 0, bytes([6]) + W.hybrid_encode(6, idx))
+
+    def dba_page(n, ragged=False):
+        strs = sorted(bytes(rng.integers(97, 99, int(rng.integers(0, 2 * L)) if ragged else L).astype(np.uint8))
+                      for _ in range(n))
+        return (O.DATA_PAGE, n, W.DELTA_BYTE_ARRAY, 0, 0, _dba_page(strs))
+
+    col = (W.FIXED_LEN_BYTE_ARRAY, L, 0, 0)
+    chunks = [
+        (col, (len(dict_vals), W.PLAIN, dimg), [dict_page(3000), dba_page(2500), dict_page(100), dba_page(7, True)]),
+        (col, None, [plain_page(5000), dba_page(3000, True), plain_page(1), plain_page(0), plain_page(2100)]),
+        (col, (len(dict_vals), W.PLAIN, dimg), [plain_page(900), dict_page(4000), dba_page(4100)]),
+        (col, (len(dict_vals), W.PLAIN, dimg), [dict_page(300), dba_page(600), dict_page(500, bad=True)]),
+        (col, None, [plain_page(50), dba_page(70)[:5] + (dba_page(70)[5][:40],), plain_page(10)]),
+    ]
+    # optional column, V2 pages: levels raw before the values
+    ocol = (W.FIXED_LEN_BYTE_ARRAY, L, 1, 0)
+    opages = []
+    for kind in ("plain", "dba", "plain"):
+        n = 3000
+        defs = (rng.random(n) < 0.9).astype(np.int32)
+        nn = int(defs.sum())
+        lv = W.hybrid_encode(1, defs)
+        body = plain_page(nn)[5] if kind == "plain" else dba_page(nn)[5]
+        opages.append((O.DATA_PAGE_V2, n, W.PLAIN if kind == "plain" else W.DELTA_BYTE_ARRAY, len(lv), 0, lv + body))
+    chunks.append((ocol, None, opages))
+    blobs, tchunks, tpages = [], [], []
+    off = 0
+
+    def add(img):
+        nonlocal off
+        base = (off + 63) & ~63
+        blobs.append(b"\0" * (base - off) + img)
+        off = base + len(img)
+        return base
+
+    for c, d, pgs in chunks:
+        first = len(tpages)
+        if d is not None:
+            o = add(d[2])
+            tpages.append(N.Page(o, len(d[2]), O.DICTIONARY_PAGE, d[0], d[1], 0, 0, len(tchunks), 0))
+        for (ptype, nv, enc, dl, rl, img) in pgs:
+            o = add(img)
+            tpages.append(N.Page(o, len(img), ptype, nv, enc, dl, rl, len(tchunks), 0))
+        tchunks.append(N.Chunk(N.Column(*c), first, len(tpages) - first, 0, 0))
+    arr = np.frombuffer(b"".join(blobs) + b"\0" * N.PAYLOAD_PAD, dtype=np.uint8).copy()
+    dptr = ctx.malloc(len(arr))
+    try:
+        ctx.h2d(dptr, arr.ctypes.data, len(arr))
+        ctx.sync()
+        b = N.Batch.from_tables(ctx, tchunks, tpages, dptr, off)
+        b.run()
+        b.sync()
+        from parity import Expected
+
+        failed = 0
+        for i, (c, d, pgs) in enumerate(chunks):
+            od = O.decode_dict_page(c, d[0], d[1], d[2]) if d else None
+            e = Expected()
+            offs, data, defs = [np.zeros(1, np.int64)], [], []
+            base = 0
+            for k, pg in enumerate(pgs):
+                r = O.decode_page(c, *pg, od)
+                if r.status and e.status == 0:
+                    e.status, e.phase, e.index = r.status, r.phase, r.index
+                e.nn += r.nn
+                o = r.offsets if r.offsets is not None else np.arange(len(r.values) // L + 1, dtype=np.int64) * L
+                offs.append(o[1:] + base)
+                base += len(r.values)
+                data.append(r.values)
+                if r.def_levels is not None:
+                    defs.append(r.def_levels)
+            e.offsets, e.data = np.concatenate(offs), b"".join(data)
+            e.def_levels = np.concatenate(defs) if defs else None
+            cd = pq.reader.ColumnData("flba", c, b.chunk_out(i), [], ctx)
+            assert cd.value_size == 0, f"chunk {i}: not laid out as byte arrays"
+            assert_chunk(cd, e, where=f"flba chunk {i}")
+            failed += e.status != 0
+        b.close()
+        assert 2 <= failed < len(chunks), failed
+    finally:
+        ctx.free(dptr)
 
 
 @pytest.mark.parametrize("mode", ["graph", "direct", "one_stream", "profiled"])
@@ -757,6 +871,6 @@ def test_launch_modes(pq, mode, monkeypatch):
                   12000, max_page_size=48 * 1024)
     for data in (flat, pq.datasets.c4(rows=40_000, row_groups=2)):
         for _ in range(2):  # a re-run of the same batch (graph replay) too
-            checked, skipped = _run_file(pq, c, data, allow_not_implemented=False)
+            checked, skipped = _run_file(pq, c, data)
             assert checked > 0 and skipped == 0
     c.close()

@@ -37,7 +37,7 @@ def _compare(col_phys, exp, vals):
         assert np.frombuffer(exp.values, np.uint8).tolist() == [int(b) for b in vals.to_pylist()]
     elif col_phys == O.FIXED_LEN_BYTE_ARRAY:
         want = b"".join(vals.to_pylist())
-        assert exp.values == want
+        assert exp.values + exp.data == want  # (data: chunks with DELTA_BYTE_ARRAY pages)
     elif col_phys == O.BYTE_ARRAY:
         want = [v if isinstance(v, bytes) else v.encode() for v in vals.to_pylist()]
         got = [exp.data[exp.offsets[i]:exp.offsets[i + 1]] for i in range(len(exp.offsets) - 1)]

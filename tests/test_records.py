@@ -133,7 +133,7 @@ def oracle_rows(data):
                 n = r.num_values
                 d = r.def_levels if r.def_levels is not None else np.zeros(n, np.uint8)
                 rp = r.rep_levels if r.rep_levels is not None else np.zeros(n, np.uint8)
-                pages.append((0, n, d, rp, lambda r=r, col=col: _go_values(r, col)))
+                pages.append((R.PAGE_OK, n, d, rp, lambda r=r, col=col: _go_values(r, col)))
             el = [e for _, e in schema if e.num_children == 0][ci]
             stores[ci] = R.LeafStore(None, col.path, el.repetition, col.max_def, col.max_rep, pages)
         asm = R.RowAssembler(schema, None, fr.row_group_num_rows(rg), stores=stores)
@@ -168,7 +168,7 @@ def test_assembly_matches_reference_records(kat):
     for ci, col in enumerate(fr.columns):
         lf = by_path[col.path]
         n = len(lf["def"])
-        page = (0, n, np.array(lf["def"], np.uint8), np.array(lf["rep"], np.uint8), lambda lf=lf: list(lf["values"]))
+        page = (R.PAGE_OK, n, np.array(lf["def"], np.uint8), np.array(lf["rep"], np.uint8), lambda lf=lf: list(lf["values"]))
         stores[ci] = R.LeafStore(None, col.path, reps[dict(kat["schema"])[col.path]], lf["max_def"], lf["max_rep"],
                                  [page])
     asm = R.RowAssembler(schema, None, len(kat["rows"]), stores=stores)
@@ -244,3 +244,154 @@ def test_next_row_selected_columns_and_cursor(pq, ctx):
         fr2.NextRow()
     fr.close()
     fr2.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# Error timing (chunk_reader.go:364-404, data_store.go:236-269): a row group fails only on
+# readChunk errors; a readValues error surfaces at the row that reaches the failing page
+# ---------------------------------------------------------------------------------------------
+def oracle_next_rows(data):
+    """Every NextRow outcome of a file (a row dict, or ("error", status)), from the oracle's pages:
+    readRowGroupData fails at the first column whose readChunk fails (walker / codec / page load,
+    phase 0) -- one failing NextRow, then the next row group; otherwise each NextRow assembles a row,
+    and a page whose readValues failed raises when the assembly reaches it (rows before it are
+    returned).  Page 0's first readValues error is swallowed at load (chunk_reader.go:368-370) and
+    raised by the first get; the reference re-runs readValues on the partly consumed decoders there,
+    the restatement raises the first attempt's error (documented divergence)."""
+    R = _pkg().records
+    fr = O.FileReader(data)
+    schema = _oracle_schema(fr)
+    out = []
+    for rg in range(len(fr.row_groups)):
+        stores, rg_err = {}, None
+        for ci, col in enumerate(fr.columns):
+            ch = fr.read_chunk(rg, ci)
+            if ch.status:
+                rg_err = ch.status
+                break
+            res = O.decode_chunk(ch)
+            load = [r for r in res if r.status and r.phase == O.PHASE_LOAD]
+            if load:
+                rg_err = load[0].status
+                break
+            pages = []
+            for r in res:
+                n = r.num_values
+                d = r.def_levels if r.def_levels is not None else np.zeros(n, np.uint8)
+                rp = r.rep_levels if r.rep_levels is not None else np.zeros(n, np.uint8)
+                pages.append((R.PageResult(r.status, r.phase, r.index), n, d, rp,
+                              lambda r=r, col=col: _go_values(r, col)))
+            el = [e for _, e in schema if e.num_children == 0][ci]
+            stores[ci] = R.LeafStore(None, col.path, el.repetition, col.max_def, col.max_rep, pages)
+        if rg_err is not None:
+            out.append(("error", rg_err))
+            continue
+        asm = R.RowAssembler(schema, None, fr.row_group_num_rows(rg), stores=stores)
+        for _ in range(fr.row_group_num_rows(rg)):
+            try:
+                out.append(asm.next_row())
+            except R.RecordError as e:
+                out.append(("error", e.status))
+    return out
+
+
+def _page_blocks(data, rg, ci):
+    """File offsets of a chunk's page blocks: [(page_type, start, length)] (the readPages walk)."""
+    fr = O.FileReader(data)
+    md = fr.row_groups[rg][1][ci][3]
+    pos = md.get(11, md.get(9))
+    end = pos + md[7]
+    out = []
+    while pos < end:
+        rd = O.CompactReader(fr.data, pos)
+        ph = rd.struct()
+        pos = rd.pos
+        out.append((ph[1], pos, ph[3]))
+        pos += ph[3]
+    return out
+
+
+def _error_file():
+    """3 row groups x (dictionary INT64, optional DOUBLE, dictionary strings), V1, small pages."""
+    W = _pkg().writer
+    rng = np.random.default_rng(71)
+    n = 9000
+    a = rng.integers(0, 100, n) * 1000
+    b = rng.normal(size=n)
+    bmask = rng.random(n) < 0.2
+    c = [b"s%03d" % k for k in rng.integers(0, 300, n)]
+    cols = [("a", W.Column(W.INT64, a), W.REQUIRED), ("b", W.optional(W.DOUBLE, b, bmask, use_dict=False), W.OPTIONAL),
+            ("c", W.Column(W.BYTE_ARRAY, c), W.REQUIRED)]
+    return W.flat(cols, 3000, max_page_size=4 * 1024)
+
+
+def _corrupt(data, edits):
+    """edits: [(rg, column, data page k, fn(bytearray block) -> None)]."""
+    buf = bytearray(data)
+    for rg, ci, k, fn in edits:
+        blocks = [b for b in _page_blocks(data, rg, ci) if b[0] != O.DICTIONARY_PAGE]
+        _, s, ln = blocks[k]
+        blk = bytearray(buf[s:s + ln])
+        fn(blk)
+        assert len(blk) == ln
+        buf[s:s + ln] = blk
+    return bytes(buf)
+
+
+def _bad_key(blk):  # dictionary indices (after the width byte): a run of all-ones keys, out of range
+    blk[len(blk) // 2: len(blk) // 2 + 4] = b"\xff" * 4
+
+
+def _short_levels(blk):  # V1 definition levels' length prefix cut to one byte: the level stream ends early
+    blk[0:4] = (1).to_bytes(4, "little")
+
+
+def _bad_width(blk):  # dictionary bit width 33: dictDecoder.init fails (type_dict.go:23-30), a load error
+    blk[0] = 33
+
+
+ERROR_CASES = {
+    "dict_index_page2": [(0, 0, 2, _bad_key)],
+    "def_levels_page0": [(1, 1, 0, _short_levels)],
+    "load_error_rg0": [(0, 2, 1, _bad_width)],
+    "mixed": [(0, 1, 3, _short_levels), (1, 2, 0, _bad_width), (2, 0, 1, _bad_key), (2, 2, 4, _bad_key)],
+}
+
+
+@pytest.mark.parametrize("case", sorted(ERROR_CASES))
+def test_oracle_error_timing(case):
+    """The restated error timing over the corrupted files: every case produces its errors, and the
+    rows before a failing page are still returned."""
+    data = _corrupt(_error_file(), ERROR_CASES[case])
+    out = oracle_next_rows(data)
+    errs = [o for o in out if isinstance(o, tuple)]
+    rows = [o for o in out if not isinstance(o, tuple)]
+    assert errs and rows
+    if case == "dict_index_page2":  # the first two pages of column a decode: their rows come first
+        assert not isinstance(out[0], tuple) and isinstance(out[2999], tuple)
+    if case == "load_error_rg0":  # row group 0 fails as a whole: one error, then row group 1
+        assert isinstance(out[0], tuple) and len(out) == 1 + 6000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(ERROR_CASES))
+def test_next_row_error_timing(pq, ctx, case):
+    """NextRow over the GPU decode of a file with corrupted pages: exactly the rows and errors (with
+    the same status) that the assembly over the oracle's pages produces, call by call; after a failed
+    row group the cursor moves on (skipRowGroup, file_reader.go:228-232)."""
+    data = _corrupt(_error_file(), ERROR_CASES[case])
+    want = oracle_next_rows(data)
+    fr = pq.reader.FileReader(data, ctx=ctx)
+    got = []
+    while True:
+        try:
+            got.append(fr.NextRow())
+        except EOFError:
+            break
+        except (pq.reader.DecodeError, pq.records.RecordError) as e:
+            got.append(("error", e.status))
+        assert len(got) <= len(want) + 1
+    fr.close()
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert _norm(g) == _norm(w), f"call {i}: {g} vs {w}"
