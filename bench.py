@@ -4,11 +4,18 @@
 A "step" is one full decode pass (every page of every chunk of the rank's row groups) over
 HBM-resident page images: k_prologue -> (delta / byte-array walks) -> k_scan -> k_expand (levels,
 PLAIN copies, booleans, dictionaries) / k_delta_* / k_ba_* / k_nest_*.
-Default workload = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16 row
-groups per GPU.  Multi-GPU: one process per GPU (torchrun), row groups sharded (each rank decodes
-its own 16 row groups, different seed), no data-path collective -> "scaling": "weak".
+Default workload at N=1 = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16
+row groups.  Default at N>1 = BASELINE.json configs[2] (C3): ONE 1B-row file of 128 row groups whose
+row groups are sharded in contiguous blocks over the N GPUs -> "scaling": "strong" (the other
+workloads at N>1 give every rank its own file -> "weak").  One process per GPU, no data-path
+collective: the only collectives are the measurement reductions and one all-gather of the blocks.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c4|c5] [--rows R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|c5z] [--rows R]
+
+--gpus N without a launcher (WORLD_SIZE unset): bench.py starts the N rank processes itself (before
+anything touches the GPU), rendezvous at 127.0.0.1; under torchrun it is one of the ranks.
+--dry-run (tests): no GPU -- each rank decodes its shard with the CPU oracle over gloo, to check the
+launcher, the shard plan and the reductions.
 """
 import argparse
 import json
@@ -189,21 +196,95 @@ def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
         ctx.L.pqh_host_free(ctx.h, h.value)
 
 
+def launch_ranks(n):
+    """`--gpus N` without a launcher: start N copies of this script as ranks 0..N-1 (one per GPU,
+    LOCAL_RANK = rank) with a 127.0.0.1 rendezvous, wait for all of them and return the worst exit
+    status.  Runs before anything in this process touches the GPU (children are started, never
+    exec'd into).  Rank 0's stdout carries the JSON line."""
+    import signal
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}")
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            r = p.poll()
+            if r is None:
+                continue
+            pending.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in pending:  # a failed rank: the others would wait at a barrier forever
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank, dist, pkg, builder, kw, seed, strong, desc):
+    """--dry-run: the rank plan and the reductions without a GPU (CPU oracle decode of the shard)."""
+    from oracle import oracle as O
+
+    data = builder(seed=seed, **kw)
+    fr = O.FileReader(data)
+    nrg = len(fr.row_groups)
+    rg0, rg1 = pkg.shard.row_group_block(nrg, world, rank) if strong else (0, nrg)
+    rows = sum(fr.row_group_num_rows(g) for g in range(rg0, rg1))
+    t0 = time.perf_counter()
+    written = 0
+    for rg in range(rg0, rg1):
+        for ci in range(len(fr.columns)):
+            for r in O.decode_chunk(fr.read_chunk(rg, ci)):
+                written += len(r.values) + (0 if r.def_levels is None else len(r.def_levels))
+    elapsed = time.perf_counter() - t0
+    el, total = pkg.shard.reduce_step(elapsed, written)
+    blocks = pkg.shard.gather_blocks(rg0, rg1, rows, written)
+    if strong:
+        pkg.shard.check_cover(blocks, nrg, fr.num_rows)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "metric": METRIC, "n_gpus": world, "scaling": "strong" if strong else "weak",
+                          "config": {"workload": desc, "rows_total": fr.num_rows if strong else fr.num_rows * world},
+                          "decoded_bytes_total": total, "max_rank_s": el,
+                          "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
+                                     for r, b in enumerate(blocks)]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5z"])
+    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "c5z"],
+                    help="default: c2 on one GPU, c3 (strong scaling) on several")
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} (launcher) overrides --gpus {args.gpus}")
+    if args.workload is None:
+        args.workload = "c2" if world == 1 else "c3"
     torch = dist = None
     try:
         import torch  # noqa: F811
@@ -211,8 +292,9 @@ def main():
     except Exception:
         torch = None
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if not args.dry_run:
+            torch.cuda.set_device(local)
+        dist.init_process_group("gloo" if args.dry_run else "nccl")
 
     pkg = package()
     from parquet_go_amd import datasets, native
@@ -226,6 +308,8 @@ def main():
     # (shard.row_group_block).  The other workloads give every rank its own file (weak scaling).
     strong = args.workload == "c3"
     seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40, "c5z": 41}[args.workload] + (0 if strong else 1000 * rank)
+    if args.dry_run:
+        return dry_run(args, world, rank, dist, pkg, builder, kw, seed_kw, strong, desc)
     t0 = time.perf_counter()
     path = None
     if strong and world > 1:
@@ -460,6 +544,7 @@ def main():
             "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
                        for r, b in enumerate(blocks)],
             "per_gpu_gbps": round(bytes_written * args.steps / elapsed / 1e9, 2),
+            "per_gpu_gbps_mean": round(total_written / world * args.steps / elapsed / 1e9, 2),
             "algo_read_bytes_per_step": bytes_read,
             "decoded_bytes_per_step": bytes_written,
             "algo_gbps_all_kernels": round((bytes_read + bytes_written) / (all_ms * 1e-3) / 1e9, 1) if all_ms else None,

@@ -55,7 +55,10 @@ def c3_values(rows=1_000_000_000, seed=20):
     return np.cumsum(1_000_000 + rng.integers(0, 4096, rows), dtype=np.int64) + 1_700_000_000_000_000_000
 
 
-def c3(rows=1_000_000_000, rows_per_group=7_812_500, seed=20):
+def c3(rows=1_000_000_000, rows_per_group=None, seed=20, row_groups=128):
+    """BASELINE configs[2]: 128 row groups (7,812,500 rows each at 1B rows) unless rows_per_group."""
+    if rows_per_group is None:
+        rows_per_group = -(-rows // row_groups)
     ts = c3_values(rows, seed)
     return W.flat([("ts", W.Column(W.INT64, ts, encoding=W.DELTA_BINARY_PACKED, use_dict=False), W.REQUIRED)],
                   rows_per_group, v2=False, as_array=True)
@@ -182,7 +185,7 @@ WORKLOADS = {
     "c1": ("C1: 10M rows, required INT32 dictionary K=4096 (width 13), UNCOMPRESSED, data page V1", c1),
     "c2": ("C2: 100M rows x 6 columns (int32 dict / int64 PLAIN / float dict / optional double PLAIN "
            "1% null / boolean PLAIN / FLBA(16) PLAIN), data page V2, 16 row groups", c2),
-    "c3": ("C3: INT64 timestamps DELTA_BINARY_PACKED 128/4, 7,812,500-row row groups", c3),
+    "c3": ("C3: INT64 timestamps DELTA_BINARY_PACKED 128/4, 128 row groups (7,812,500 rows each at 1B rows)", c3),
     "c4": ("C4: optional LIST<optional int64> + optional MAP<string, optional int32>, 20M rows, V1, "
            "UNCOMPRESSED", c4),
     "c5": ("C5: required BYTE_ARRAY strings U[8,40] ~half unique, RLE_DICTIONARY (dict page <= 1 MiB) "

@@ -105,3 +105,29 @@ def test_two_rank_gloo_shards(tmp_path):
     # the plan the bench uses (shard.row_group_block) for 9 row groups over 2 ranks
     assert [b[:3] for b in blocks] == [(0, 5, 5000), (5, 9, 4000)] and offsets == [0, 5000]
     assert sum(b[3] for b in blocks) == total
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` without a launcher starts its two rank processes itself; the default
+    workload at N > 1 is C3 (one file of 128 row groups, strong scaling).  --dry-run puts the CPU
+    oracle in place of the GPU decode and gloo in place of RCCL, so the plan (contiguous blocks that
+    tile the file) and the reductions (sum of bytes, max of time) are checked here."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    rows = 300_000
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--rows", str(rows)],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["workload"].startswith("C3") and d["config"]["rows_total"] == rows
+    sh = d["shards"]
+    assert [s["rank"] for s in sh] == [0, 1]
+    assert sh[0]["row_groups"] == [0, 64] and sh[1]["row_groups"] == [64, 128]
+    assert sum(s["rows"] for s in sh) == rows
+    assert d["decoded_bytes_total"] == 8 * rows == sum(s["decoded_bytes"] for s in sh)
+    assert d["max_rank_s"] > 0
