@@ -1386,7 +1386,8 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   out->values = D.value_size > 0 ? D.values : nullptr;
   out->offsets = D.offsets;
   out->bytes = D.bytes;
-  out->num_bytes = D.offsets ? b->chunk_bytes[size_t(chunk)] : 0;
+  // (a failing chunk's byte total past its first failing page may be garbage: never past the buffer)
+  out->num_bytes = D.offsets ? std::max<int64_t>(0, std::min(b->chunk_bytes[size_t(chunk)], D.bytes_cap)) : 0;
   out->def_levels = D.def_levels;
   out->rep_levels = D.rep_levels;
   out->status = PQH_OK;
