@@ -350,6 +350,17 @@ int32_t pqh_file_num_columns(const pqh_file* f);
 /* Leaf column metadata; path is the dot-joined schema path (Column.FlatName). */
 int pqh_file_column(const pqh_file* f, int32_t column, pqh_column* out, char* path,
                     int32_t path_capacity);
+/* The full path / schema element name as bytes (names may hold any bytes, NULs included): copies
+ * min(length, cap) bytes, returns the length (-1: no such column / element). */
+int32_t pqh_file_column_path(const pqh_file* f, int32_t column, char* buf, int32_t cap);
+int32_t pqh_file_schema_name(const pqh_file* f, int32_t i, char* buf, int32_t cap);
+
+/* readRowGroupData's checks of column `column` in row group `rg` before any of its pages is read
+ * (reference chunk_reader.go:381-393 and readChunk :299-324 when selected, skipChunk :271-297
+ * when not): PQH_OK, PQH_ERR_SCHEMA (no such chunk / no metadata / wrong type) or PQH_ERR_IO
+ * (file_path set, negative offset).  A row group fails at the first column (in schema order)
+ * that fails here or whose chunk fails to load. */
+int pqh_file_chunk_check(const pqh_file* f, int32_t rg, int32_t column, int32_t selected);
 
 /* The schema as a flat DFS list (FileMetaData.schema, root first), with the levels the reader
  * derives for every node (readGroupSchema / readColumnSchema, schema.go:893-990): what the record

@@ -21,6 +21,11 @@ import zlib
 
 import numpy as np
 
+try:
+    from .thrift_spec import SPEC
+except ImportError:  # imported as a top-level module (oracle/ on sys.path)
+    from thrift_spec import SPEC
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liborcl.so")
 
@@ -96,7 +101,10 @@ def lib():
                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
         L.orc_decode_dict_page.argtypes = [ctypes.POINTER(OrcColumn), ctypes.c_int32, ctypes.c_int32, u8p,
                                            ctypes.c_int64, ctypes.POINTER(OrcDict)]
+        L.orc_decode_dict_page_ex.argtypes = [ctypes.POINTER(OrcColumn), ctypes.c_int32, ctypes.c_int32, u8p,
+                                              ctypes.c_int64, ctypes.POINTER(OrcDict), ctypes.POINTER(ctypes.c_int64)]
         L.orc_dict_free.argtypes = [ctypes.POINTER(OrcDict)]
+        L.orc_select.argtypes = [ctypes.POINTER(OrcColumn), ctypes.c_int32]
         L.orc_decode_page.argtypes = [ctypes.POINTER(OrcColumn), ctypes.POINTER(OrcPage), u8p, ctypes.c_int64,
                                       ctypes.POINTER(OrcDict), ctypes.POINTER(OrcOut)]
         L.orc_out_free.argtypes = [ctypes.POINTER(OrcOut)]
@@ -155,8 +163,9 @@ def delta_decode(data, n, bits=64):
 
 
 class Dictionary:
-    def __init__(self, status, num_values=0, value_size=0, values=b"", offsets=None):
+    def __init__(self, status, num_values=0, value_size=0, values=b"", offsets=None, index=0):
         self.status = status
+        self.index = index  # the values read before the failing one
         self.num_values = num_values
         self.value_size = value_size
         self.values = values
@@ -167,9 +176,11 @@ def decode_dict_page(col, num_values, encoding, image):
     arr, p = _u8(image)
     c = OrcColumn(*col)
     d = OrcDict()
-    st = lib().orc_decode_dict_page(ctypes.byref(c), num_values, encoding, p, len(arr), ctypes.byref(d))
+    ei = ctypes.c_int64()
+    st = lib().orc_decode_dict_page_ex(ctypes.byref(c), num_values, encoding, p, len(arr), ctypes.byref(d),
+                                       ctypes.byref(ei))
     if st:
-        return Dictionary(st)
+        return Dictionary(st, index=ei.value)
     vals = ctypes.string_at(d.values, d.num_bytes) if d.num_bytes else b""
     offs = None
     if d.value_size == 0:
@@ -213,6 +224,12 @@ def _to_cdict(d):
     return cd, keep
 
 
+def select(col, encoding):
+    """getValuesDecoder (chunk_reader.go:106-159): OK or ERR_UNSUPPORTED."""
+    c = OrcColumn(*col)
+    return lib().orc_select(ctypes.byref(c), encoding)
+
+
 def decode_page(col, page_type, num_values, encoding, def_len, rep_len, image, dictionary=None):
     arr, p = _u8(image if len(image) else b"\0")
     c = OrcColumn(*col)
@@ -237,99 +254,215 @@ def decode_page(col, page_type, num_values, encoding, def_len, rep_len, image, d
 
 
 # ------------------------------------------------------------------------------------------------
-# Thrift compact protocol (generic reader: struct -> {field id: value})
+# Thrift compact protocol, restated from the reference's thrift library (vendored apache/thrift
+# v0.16.0: lib/go/thrift/compact_protocol.go ReadFieldBegin :429-468, ReadListBegin :505-529,
+# ReadMapBegin :475-497, ReadBool :546-553, ReadI16/I32/I64 :565-588, ReadString :601-622,
+# readVarint64 :747-762, getTType :802-830; protocol.go Skip :92-182; configuration.go
+# checkSizeForProtocol :305-319) and the generated struct readers (parquet/parquet.go, their field
+# ids / accepted wire types / required fields as the table oracle/thrift_spec.py).
 # ------------------------------------------------------------------------------------------------
 class ThriftError(Exception):
     pass
 
 
+MAX_SIZE = 100 * 1024 * 1024  # DEFAULT_MAX_MESSAGE_SIZE
+MAX_DEPTH = 64                # DEFAULT_RECURSION_DEPTH
+
+
+def _i32(u):
+    u &= 0xFFFFFFFF
+    return u - (1 << 32) if u >> 31 else u
+
+
+def _i64(u):
+    u &= (1 << 64) - 1
+    return u - (1 << 64) if u >> 63 else u
+
+
 class CompactReader:
-    def __init__(self, buf, pos=0):
+    """A TCompactProtocol over buf[pos:end] (StreamTransport: reads past `end` fail)."""
+
+    def __init__(self, buf, pos=0, end=None):
         self.buf = buf
         self.pos = pos
+        self.end = len(buf) if end is None else end
+        self.bool_pending = None
 
     def byte(self):
-        if self.pos >= len(self.buf):
+        if self.pos >= self.end:
             raise ThriftError("EOF")
         b = self.buf[self.pos]
         self.pos += 1
         return b
 
-    def uvarint(self):
-        x = 0
-        s = 0
+    def varint64(self):  # no length limit; bits past 63 vanish
+        x, s = 0, 0
         while True:
             b = self.byte()
-            x |= (b & 0x7F) << s
-            if b < 0x80:
-                return x
+            if s < 64:
+                x |= (b & 0x7F) << s
+            if not b & 0x80:
+                return _i64(x)
             s += 7
-            if s > 63:
-                raise ThriftError("varint overflow")
 
-    def zigzag(self):
-        u = self.uvarint()
-        return (u >> 1) ^ -(u & 1)
+    def varint32(self):
+        return _i32(self.varint64())
 
-    def binary(self):
-        n = self.uvarint()
-        if self.pos + n > len(self.buf):
+    def i32(self):
+        u = self.varint32() & 0xFFFFFFFF
+        return _i32((u >> 1) ^ -(u & 1))
+
+    def i16(self):
+        v = self.i32() & 0xFFFF
+        return v - 0x10000 if v >> 15 else v
+
+    def i64(self):
+        u = self.varint64() & ((1 << 64) - 1)
+        return _i64((u >> 1) ^ -(u & 1))
+
+    def double(self):
+        if self.end - self.pos < 8:
+            raise ThriftError("EOF in double")
+        v = struct.unpack_from("<d", self.buf, self.pos)[0]
+        self.pos += 8
+        return v
+
+    def string(self):
+        n = self.varint32()
+        if n < 0 or n > MAX_SIZE:
+            raise ThriftError("bad size")
+        if self.end - self.pos < n:
             raise ThriftError("EOF in binary")
         v = bytes(self.buf[self.pos:self.pos + n])
         self.pos += n
         return v
 
-    def value(self, t):
-        if t in (1, 2):
-            return t == 1
+    @staticmethod
+    def wire(nib):
+        """getTType: 0 STOP, 1 bool (compact 1 / 2), 3..12, None for 13..15."""
+        nib &= 0x0F
+        if nib == 2:
+            return 1
+        return nib if nib <= 12 else None
+
+    def field(self, last):
+        """(id, wire type) or None at STOP."""
+        h = self.byte()
+        if h & 0x0F == 0:
+            return None
+        d = h >> 4
+        fid = self.i16() if d == 0 else ((last + d + 0x8000) & 0xFFFF) - 0x8000
+        t = self.wire(h)
+        if t is None:
+            raise ThriftError(f"unknown type {h & 0x0F}")
+        if t == 1:
+            self.bool_pending = (h & 0x0F) == 1
+        return fid, t
+
+    def read_bool(self):
+        if self.bool_pending is not None:
+            v, self.bool_pending = self.bool_pending, None
+            return v
+        return self.byte() == 1
+
+    def list_begin(self):
+        h = self.byte()
+        n = h >> 4
+        if n == 15:
+            n = self.varint32()
+        et = self.wire(h)
+        if n < 0 or n > MAX_SIZE or et is None:
+            raise ThriftError("bad list header")
+        return et, n
+
+    def skip(self, t, depth=MAX_DEPTH):
+        if depth <= 0:
+            raise ThriftError("depth limit")
+        if t == 1:
+            self.read_bool()
+        elif t == 3:
+            self.byte()
+        elif t in (4, 5):
+            self.varint32()
+        elif t == 6:
+            self.varint64()
+        elif t == 7:
+            self.double()
+        elif t == 8:
+            self.string()
+        elif t in (9, 10):
+            et, n = self.list_begin()
+            for _ in range(n):
+                self.skip(et, depth - 1)
+        elif t == 11:
+            n = self.varint32()
+            if n < 0 or n > MAX_SIZE:
+                raise ThriftError("bad map size")
+            kv = self.byte() if n else 0
+            kt, vt = self.wire(kv >> 4) or 0, self.wire(kv & 0x0F) or 0
+            for _ in range(n):
+                self.skip(kt, depth - 1)
+                self.skip(vt, depth - 1)
+        elif t == 12:
+            last = 0
+            while True:
+                f = self.field(last)
+                if f is None:
+                    return
+                last = f[0]
+                self.skip(f[1], depth - 1)
+        else:
+            raise ThriftError(f"unknown data type {t}")
+
+    def _elem(self, t, sub):
+        if t == 1:
+            return self.read_bool()
         if t == 3:
             b = self.byte()
             return b - 256 if b > 127 else b
-        if t in (4, 5, 6):
-            return self.zigzag()
+        if t == 4:
+            return self.i16()
+        if t == 5:
+            return self.i32()
+        if t == 6:
+            return self.i64()
         if t == 7:
-            if self.pos + 8 > len(self.buf):
-                raise ThriftError("EOF in double")
-            v = struct.unpack_from("<d", self.buf, self.pos)[0]
-            self.pos += 8
-            return v
+            return self.double()
         if t == 8:
-            return self.binary()
-        if t in (9, 10):
-            h = self.byte()
-            n = h >> 4
-            et = h & 0x0F
-            if n == 15:
-                n = self.uvarint()
-            out = []
-            for _ in range(n):
-                if et in (1, 2):
-                    out.append(self.byte() == 1)
-                else:
-                    out.append(self.value(et))
-            return out
-        if t == 11:
-            n = self.uvarint()
-            if n == 0:
-                return {}
-            kv = self.byte()
-            return {self.value(kv >> 4): self.value(kv & 0x0F) for _ in range(n)}
+            return self.string()
         if t == 12:
-            return self.struct()
-        raise ThriftError(f"bad type {t}")
+            return self.read(sub)
+        raise ThriftError(f"bad element type {t}")
 
-    def struct(self):
+    def read(self, name):
+        """The generated Go reader of struct `name`: {field id: value} of the fields whose id and wire
+        type match (others skipped; a repeated field keeps its last value); required fields checked."""
+        spec = SPEC[name]
         out = {}
         last = 0
         while True:
-            h = self.byte()
-            if h == 0:
-                return out
-            t = h & 0x0F
-            d = h >> 4
-            fid = last + d if d else self.zigzag()
+            f = self.field(last)
+            if f is None:
+                break
+            fid, t = f
             last = fid
-            out[fid] = self.value(t)
+            sp = spec.get(fid)
+            if sp is None or sp[1] != t:
+                self.skip(t)
+                continue
+            _, wt, et, sub, _ = sp
+            if wt == 9:
+                _, n = self.list_begin()
+                out[fid] = [self._elem(et, sub) for _ in range(n)]
+            else:
+                out[fid] = self._elem(wt, sub)
+        for fid, sp in spec.items():
+            if sp[4] and fid not in out:
+                raise ThriftError(f"required field {name}.{sp[0]} is not set")
+        return out
+
+    def struct(self, name="PageHeader"):
+        return self.read(name)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -348,29 +481,73 @@ class Column:
         return (self.physical_type, self.type_length or 0, self.max_def, self.max_rep)
 
 
+class SchemaError(ValueError):
+    pass
+
+
+def _name(s):
+    return s.get(4, b"").decode("utf-8", "surrogateescape")
+
+
 def read_schema(schema):
-    """readSchema / readGroupSchema / readColumnSchema (schema.go:893-1015): leaves in DFS order."""
+    """makeSchema + readSchema (schema.go:1048-1079, :992-1015): the elements after the root are read
+    as top-level groups / columns until the list ends; readGroupSchema / readColumnSchema
+    (:893-990) and getValuesStore (data_store.go:328-362) checks.  Leaves in DFS order."""
+    if len(schema) < 1:
+        raise SchemaError("no schema element found")
+    els = schema[1:]
     leaves = []
 
-    def walk(idx, path, d, r, rd, is_root):
-        s = schema[idx]
+    def column(idx, path, d, r, rd):
+        s = els[idx]
+        if not s.get(4):
+            raise SchemaError("name in schema is empty")
         rep = s.get(3)
-        if not is_root and rep is not None and rep != 0:
+        if rep is None:
+            raise SchemaError("field RepetitionType is nil")
+        if rep != 0:
             d += 1
-        if not is_root and rep == 2:
+        if rep == 2:
             r += 1
             rd = rd + [d]
-        name = s.get(4, b"").decode()
-        p = path + ([name] if not is_root else [])
-        if s.get(1) is not None and not is_root:
-            leaves.append(Column(".".join(p), s, d, r, rd))
-            return idx + 1
+        t = s.get(1)
+        if t < 0 or t > FIXED_LEN_BYTE_ARRAY:
+            raise SchemaError("unsupported type")
+        if t == FIXED_LEN_BYTE_ARRAY and s.get(2) is None:
+            raise SchemaError("type with nil type length")
+        leaves.append(Column(".".join(path + [_name(s)]), s, d, r, rd))
+        return idx + 1
+
+    def group(idx, path, d, r, rd):
+        if len(els) <= idx:
+            raise SchemaError("schema index out of bound")
+        s = els[idx]
+        if s.get(1) is not None:
+            raise SchemaError("field Type is not nil")
+        n = s.get(5)
+        if n is None:
+            raise SchemaError("the field NumChildren is invalid")
+        if n <= 0:
+            raise SchemaError("the field NumChildren is zero")
+        if len(els) <= idx + n:
+            raise SchemaError("not enough element in the schema list")
+        rep = s.get(3)
+        if rep is not None and rep != 0:
+            d += 1
+        if rep is not None and rep == 2:
+            r += 1
+            rd = rd + [d]
+        p = path + [_name(s)]
         idx += 1
-        for _ in range(s.get(5, 0)):
-            idx = walk(idx, p, d, r, rd, False)
+        for _ in range(n):
+            if len(els) <= idx:
+                raise SchemaError("schema index is out of bounds")
+            idx = group(idx, p, d, r, rd) if els[idx].get(1) is None else column(idx, p, d, r, rd)
         return idx
 
-    walk(0, [], 0, 0, [], True)
+    idx = 0
+    while idx < len(els):
+        idx = group(idx, [], 0, 0, []) if els[idx].get(1) is None else column(idx, [], 0, 0, [])
     return leaves
 
 
@@ -472,123 +649,196 @@ class Page:
 class Chunk:
     def __init__(self, column):
         self.column = column
-        self.pages = []   # data pages (Page)
+        self.pages = []   # data pages (Page) read before the walk ended
         self.dict_page = None
-        self.status = OK
+        self.status = OK  # readChunk's error: (status, index) of the first page it could not load
+        self.index = 0
+        self.page = -1    # data pages read before that page
+
+
+class FileError(ValueError):
+    pass
+
+
+ERR_IO = 26
+PLAIN_ENC, PLAIN_DICTIONARY_ENC, RLE_ENC = 0, 2, 3
 
 
 class FileReader:
-    """The oracle's NewFileReader: footer + schema + page walker over a bytes object."""
+    """The oracle's NewFileReader over a bytes object: ReadFileMetaData(r, extraValidation = true)
+    (file_meta.go:23-73) + makeSchema (schema.go:1048-1079).  Raises FileError where the reference's
+    NewFileReader returns an error."""
 
     def __init__(self, data):
         self.data = data.tobytes() if hasattr(data, "tobytes") else bytes(data)
-        if len(self.data) < 12 or self.data[:4] != b"PAR1" or self.data[-4:] != b"PAR1":
-            raise ValueError("not a parquet file")
-        flen = struct.unpack_from("<I", self.data, len(self.data) - 8)[0]
-        meta = CompactReader(self.data, len(self.data) - 8 - flen).struct()
+        d = self.data
+        if len(d) < 4 or d[:4] != b"PAR1":
+            raise FileError("invalid parquet file header")
+        if d[-4:] != b"PAR1":
+            raise FileError("invalid parquet file footer")
+        if len(d) < 8:
+            raise FileError("seek for the footer len failed")
+        flen = struct.unpack_from("<i", d, len(d) - 8)[0]
+        if flen <= 0:
+            raise FileError(f"invalid footer len {flen}")
+        if flen > len(d) - 8:
+            raise FileError("seek file meta data failed")
+        try:
+            meta = CompactReader(d, len(d) - 8 - flen, len(d) - 8).read("FileMetaData")
+        except ThriftError as e:
+            raise FileError(f"read file meta failed: {e}")
         self.meta = meta
-        self.columns = read_schema(meta[2])
-        self.row_groups = meta.get(4, [])
-        self.num_rows = meta.get(3, 0)
+        try:
+            self.columns = read_schema(meta[2])
+        except SchemaError as e:
+            raise FileError(f"creating schema failed: {e}")
+        self.row_groups = meta[4]
+        self.num_rows = meta[3]
 
     def row_group_num_rows(self, rg):
-        return self.row_groups[rg].get(3, 0)
+        return self.row_groups[rg][3]
+
+    def chunk_check(self, rg, ci, selected=True):
+        """readRowGroupData's checks of column ci before its pages (chunk_reader.go:381-393; readChunk
+        :299-324 when selected, skipChunk :271-297 when not): OK / ERR_SCHEMA / ERR_IO."""
+        cols = self.row_groups[rg][1]
+        if len(cols) <= ci:
+            return ERR_SCHEMA
+        cc = cols[ci]
+        if 1 in cc:
+            return ERR_IO
+        md = cc.get(3)
+        if md is None:
+            return ERR_SCHEMA
+        if md[1] != self.columns[ci].physical_type:
+            return ERR_SCHEMA
+        off = md.get(11, md[9])
+        if (off if selected else off + md[7]) < 0:
+            return ERR_IO
+        return OK
 
     def read_chunk(self, rg, ci, validate_crc=False):
-        """readChunk + readPages (chunk_reader.go:182-362); decompressed page images."""
+        """readChunk + readPages (chunk_reader.go:182-362) in the reference's order of checks: every
+        page is read and its decoders initialised (pageReader.read) before the next header; the walk
+        stops at the first page that fails (ch.status, ch.index = the load step / values read).
+        Returns the decompressed page images of the pages before it."""
         col = self.columns[ci]
         ch = Chunk(col)
-        cc = self.row_groups[rg][1][ci]
-        md = cc.get(3)
-        if md is None or md.get(1) != col.physical_type:
-            ch.status = ERR_SCHEMA
+
+        def fail(status, index=0):
+            ch.status, ch.index, ch.page = status, index, len(ch.pages)
             return ch
-        offset = md.get(11, md.get(9))
-        total = md.get(7)
-        codec = md.get(4, 0)
-        pos = offset
+
+        st = self.chunk_check(rg, ci)
+        if st:
+            return fail(st)
+        md = self.row_groups[rg][1][ci][3]
+        desc = col.desc()
+        pos = md.get(11, md[9])
+        total, codec = md[7], md[4]
         count = 0
+        d = self.data
         while total - count > 0:
             try:
-                rd = CompactReader(self.data, pos)
-                ph = rd.struct()
+                rd = CompactReader(d, min(pos, len(d)))
+                ph = rd.read("PageHeader")
             except ThriftError:
-                ch.status = ERR_THRIFT
-                return ch
-            count += rd.pos - pos
+                return fail(ERR_THRIFT)
+            count += rd.pos - min(pos, len(d))
             pos = rd.pos
-            ptype = ph.get(1)
-            usize, csize = ph.get(2, 0), ph.get(3, 0)
-            if csize < 0 or usize < 0:
-                ch.status = ERR_PAGE_HEADER
-                return ch
-            block = self.data[pos:pos + csize]
-            pos += len(block)
-            count += len(block)
-            if validate_crc and 4 in ph and (zlib.crc32(block) & 0xFFFFFFFF) != (ph[4] & 0xFFFFFFFF):
-                ch.status = ERR_CRC
-                return ch
+            ptype = ph[1]
+            usize, csize = ph[2], ph[3]
+            block = None
+
+            def read_block():  # readPageBlock (:161-180)
+                nonlocal pos, count, block
+                if csize < 0 or usize < 0:
+                    return ERR_PAGE_HEADER
+                block = d[pos:pos + csize]
+                pos += len(block)
+                count += len(block)
+                if validate_crc and 4 in ph and (zlib.crc32(block) & 0xFFFFFFFF) != (ph[4] & 0xFFFFFFFF):
+                    return ERR_CRC
+                return OK
+
+            def inflate(blk, csz, usz):  # newBlockReader (compress.go:131-152)
+                if csz < 0 or usz < 0:
+                    return None, ERR_PAGE_HEADER
+                if len(blk) != csz:
+                    return None, ERR_DECOMPRESS
+                try:
+                    img = decompress(codec, blk, usz)
+                except Exception:
+                    return None, ERR_DECOMPRESS
+                return (img, OK) if len(img) == usz else (None, ERR_DECOMPRESS)
+
             if ptype == DICTIONARY_PAGE:
                 if ch.dict_page is not None:
-                    ch.status = ERR_DICT_PAGE
-                    return ch
-                dh = ph.get(7)
-                if dh is None:
-                    ch.status = ERR_PAGE_HEADER
-                    return ch
-                try:
-                    img = decompress(codec, block, usize)
-                except Exception:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                if len(block) != csize or len(img) != usize:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                d = decode_dict_page(col.desc(), dh.get(1, 0), dh.get(2, 0), img)
-                if d.status != OK:
-                    ch.status = d.status
-                    return ch
-                ch.dict_page = d
-                if 11 in md and md[11] != pos:
+                    return fail(ERR_DICT_PAGE)
+                if col.physical_type == BOOLEAN:  # getDictValuesDecoder (:17-39)
+                    return fail(ERR_UNSUPPORTED)
+                dh = ph.get(7)  # dictPageReader.read (page_dict.go:35-72)
+                if dh is None or dh[1] < 0:
+                    return fail(ERR_PAGE_HEADER)
+                if dh[2] not in (PLAIN_ENC, PLAIN_DICTIONARY_ENC):
+                    return fail(ERR_DICT_PAGE)
+                st = read_block()
+                if st:
+                    return fail(st)
+                img, st = inflate(block, csize, usize)
+                if st:
+                    return fail(st)
+                dic = decode_dict_page(desc, dh[1], dh[2], img)
+                if dic.status != OK:
+                    return fail(dic.status, dic.index)
+                ch.dict_page = dic
+                if 11 in md and md[11] != pos:  # back to DataPageOffset
+                    if md[9] < 0:
+                        return fail(ERR_IO)
                     count += md[9] - pos
                     pos = md[9]
                 continue
             if ptype == DATA_PAGE:
-                h = ph.get(5)
+                h = ph.get(5)  # dataPageReaderV1.init (page_v1.go:65-85), then .read (:87-122)
                 if h is None:
-                    ch.status = ERR_PAGE_HEADER
-                    return ch
-                try:
-                    img = decompress(codec, block, usize)
-                except Exception:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                if len(block) != csize or len(img) != usize:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                ch.pages.append(Page(DATA_PAGE, h.get(1, 0), h.get(2, 0), 0, 0, img))
+                    return fail(ERR_PAGE_HEADER)
+                if (col.max_rep > 0 and h[4] != RLE_ENC) or (col.max_def > 0 and h[3] != RLE_ENC):
+                    return fail(ERR_UNSUPPORTED)
+                if h[1] < 0:
+                    return fail(ERR_PAGE_HEADER)
+                st = read_block()
+                if st:
+                    return fail(st)
+                img, st = inflate(block, csize, usize)
+                if st:
+                    return fail(st)
+                page = Page(DATA_PAGE, h[1], h[2], 0, 0, img)
             elif ptype == DATA_PAGE_V2:
-                h = ph.get(8)
+                h = ph.get(8)  # dataPageReaderV2.read (page_v2.go:79-131)
                 if h is None:
-                    ch.status = ERR_PAGE_HEADER
-                    return ch
-                dl, rl = h.get(5, 0), h.get(6, 0)
-                if dl < 0 or rl < 0 or h.get(1, 0) < 0 or dl + rl > len(block):
-                    ch.status = ERR_PAGE_HEADER
-                    return ch
-                lv = block[: rl + dl]
-                try:
-                    vals = decompress(codec, block[rl + dl:], usize - rl - dl)
-                except Exception:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                if len(vals) != usize - rl - dl:
-                    ch.status = ERR_DECOMPRESS
-                    return ch
-                ch.pages.append(Page(DATA_PAGE_V2, h.get(1, 0), h.get(4, 0), dl, rl, lv + vals))
+                    return fail(ERR_PAGE_HEADER)
+                dl, rl = h[5], h[6]
+                if h[1] < 0 or rl < 0 or dl < 0:
+                    return fail(ERR_PAGE_HEADER)
+                if select(desc, h[4]) != OK:  # getValuesDecoder before the block (:107-112)
+                    return fail(ERR_UNSUPPORTED)
+                st = read_block()
+                if st:
+                    return fail(st)
+                if rl + dl > len(block):  # the level slices: a runtime panic in the reference
+                    return fail(ERR_PAGE_HEADER)
+                vals, st = inflate(block[rl + dl:], csize - rl - dl, usize - rl - dl)
+                if st:
+                    return fail(st)
+                page = Page(DATA_PAGE_V2, h[1], h[4], dl, rl, block[: rl + dl] + vals)
             else:
-                ch.status = ERR_PAGE_HEADER
-                return ch
+                return fail(ERR_PAGE_HEADER)
+            # the page's decoders: getValuesDecoder, initSize / init (phase 0 of the page decode)
+            r = decode_page(desc, page.page_type, page.num_values, page.encoding, page.def_len, page.rep_len,
+                            page.image, ch.dict_page)
+            if r.status and r.phase == PHASE_LOAD:
+                return fail(r.status, r.index)
+            ch.pages.append(page)
         return ch
 
 

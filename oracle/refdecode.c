@@ -850,9 +850,24 @@ static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals,
  * Dictionary page: dictPageReader.read (page_dict.go:35-72) with getDictValuesDecoder
  * (chunk_reader.go:17-39).
  * ------------------------------------------------------------------------------------------- */
+/* getValuesDecoder (chunk_reader.go:106-159): PQH_OK or PQH_ERR_UNSUPPORTED for (type, encoding). */
+int orc_select(const orc_column *col, int32_t encoding) {
+  vdec_t v;
+  int st = vdec_select(col, encoding, &v);
+  vdec_free(&v);
+  return st;
+}
+
 int orc_decode_dict_page(const orc_column *col, int32_t num_values, int32_t encoding,
                          const uint8_t *img, int64_t img_len, orc_dict *out) {
+  int64_t ei;
+  return orc_decode_dict_page_ex(col, num_values, encoding, img, img_len, out, &ei);
+}
+
+int orc_decode_dict_page_ex(const orc_column *col, int32_t num_values, int32_t encoding,
+                            const uint8_t *img, int64_t img_len, orc_dict *out, int64_t *err_index) {
   memset(out, 0, sizeof(*out));
+  *err_index = 0;
   if (num_values < 0) return PQH_ERR_PAGE_HEADER;
   if (encoding != PQH_ENC_PLAIN && encoding != PQH_ENC_PLAIN_DICTIONARY) return PQH_ERR_DICT_PAGE;
   if (col->physical_type == PQH_BOOLEAN) return PQH_ERR_UNSUPPORTED;
@@ -864,6 +879,7 @@ int orc_decode_dict_page(const orc_column *col, int32_t num_values, int32_t enco
   int64_t ei;
   st = vdec_decode(&v, NULL, num_values, &vals, &offs, &ei);
   vdec_free(&v);
+  *err_index = st ? ei : 0;
   int is_ba = col->physical_type == PQH_BYTE_ARRAY ||
               (col->physical_type == PQH_FIXED_LEN_BYTE_ARRAY && col->type_length == 0);
   if (st) {

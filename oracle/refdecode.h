@@ -82,7 +82,13 @@ int orc_delta_decode64(const uint8_t *buf, int64_t len, int32_t n, int64_t *out,
 /* dictPageReader.read (page_dict.go:35-72) on a decompressed dictionary page image. */
 int orc_decode_dict_page(const orc_column *col, int32_t num_values, int32_t encoding,
                          const uint8_t *img, int64_t img_len, orc_dict *out);
+/* ... with the index of the first value that failed (the values read before it). */
+int orc_decode_dict_page_ex(const orc_column *col, int32_t num_values, int32_t encoding,
+                            const uint8_t *img, int64_t img_len, orc_dict *out, int64_t *err_index);
 void orc_dict_free(orc_dict *d);
+
+/* getValuesDecoder (chunk_reader.go:106-159): PQH_OK or PQH_ERR_UNSUPPORTED. */
+int orc_select(const orc_column *col, int32_t encoding);
 
 /* dataPageReaderV1/V2 .read + .readValues(numValues) (page_v1.go:33-122, page_v2.go:31-131) on a
  * page image (V1: decompressed block; V2: raw levels followed by the decompressed values). */

@@ -300,7 +300,11 @@ void free_batch(pqh_batch* b) {
   if (b->graph) hipGraphDestroy(b->graph);
 }
 
-int32_t codec_fail_page(const pqh_batch* b, int32_t chunk);
+struct ChunkErr {
+  int32_t status = PQH_OK, phase = 0, page = -1;
+  int64_t index = 0;
+};
+ChunkErr chunk_error(const pqh_batch* b, int32_t chunk);
 
 // Every planner buffer starts zeroed (once, at plan time, ordered before the batch's first run on
 // the context stream): no kernel can ever read stale memory from an earlier allocation, whichever
@@ -458,7 +462,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       delete b;
       return set_err(ctx, PQH_ERR_ARG, "chunk page range out of bounds");
     }
-    const uint64_t chunk_err = C.host_status != PQH_OK ? err_key(0, 0, C.host_status) : kNoError;
     // FIXED_LEN_BYTE_ARRAY pages with DELTA_BYTE_ARRAY go to byteArrayDeltaDecoder, which yields
     // variable-length []byte with no length check (chunk_reader.go:67-78, type_bytearray.go:189-240):
     // such a chunk is output as offsets + bytes.  Its fixed-width pages (PLAIN, dictionary) decode
@@ -493,7 +496,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       P.dict_page = -1;
       P.ck_rep = P.ck_def = P.ck_val = -1;
       P.dblk_base = -1;
-      P.host_err = chunk_err;
+      P.host_err = kNoError;  // (a walker error, host_status, lies after the listed pages: chunk_error)
       if (Q.image_offset < 0 || Q.image_len < 0 || Q.image_offset + Q.image_len > payload_bytes) {
         delete b;
         return set_err(ctx, PQH_ERR_ARG, "page image outside the payload");
@@ -504,7 +507,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         int32_t kind = resolve_kind(C.column.physical_type, C.column.type_length, PQH_ENC_PLAIN, &dvs);
         P.kind = kind;
         P.value_size = dvs;
-        if (i != 0 || D.dict_page >= 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
+        // "there should be only one dictionary" (chunk_reader.go:197-199); a dictionary page after data
+        // pages is read like any other: the pages before it decode without a dictionary
+        if (D.dict_page >= 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
         else if (Q.num_values < 0) P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_PAGE_HEADER));
         else if (Q.encoding != PQH_ENC_PLAIN && Q.encoding != PQH_ENC_PLAIN_DICTIONARY)
           P.host_err = std::min<uint64_t>(P.host_err, err_key(0, 0, PQH_ERR_DICT_PAGE));
@@ -515,7 +520,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
           dcum_cursor += int64_t(std::max(0, Q.num_values)) + 1;
           b->ba_pages.push_back(p);
         }
-        if (i == 0) D.dict_page = p;
+        if (D.dict_page < 0) D.dict_page = p;
         b->bytes_read += Q.image_len;
         continue;
       }
@@ -1239,15 +1244,12 @@ int pqh_batch_sync(pqh_batch* b) {
 
 int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num_pages) {
   if (!b || !b->synced) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "batch not synced");
-  std::vector<int32_t> codec_fail(b->chunks.size(), -2);  // per chunk, computed on first use
   for (int32_t p = 0; p < num_pages && size_t(p) < b->pages.size(); p++) {
     const PageState& S = b->states[size_t(p)];
     pqh_page_result& r = out[p];
     memset(&r, 0, sizeof(r));
-    const int32_t c = b->hpages[size_t(p)].chunk;
-    if (codec_fail[size_t(c)] == -2) codec_fail[size_t(c)] = codec_fail_page(b, c);
-    if (codec_fail[size_t(c)] >= 0) {  // readChunk failed (as pqh_batch_chunk_out): no page of it is read
-      r.status = PQH_ERR_DECOMPRESS;
+    if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) {
+      r.status = PQH_ERR_DECOMPRESS;  // the device could not decompress its image (readPageBlock)
       r.phase = PQH_PHASE_LOAD;
     } else if (S.err != kNoError) {
       r.status = int32_t(S.err & 0xff);
@@ -1279,9 +1281,11 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   const DevChunk& C = b->hchunks[size_t(P.chunk)];
   out->value_size = C.value_size;
   if (P.page_type == PQH_DICTIONARY_PAGE) return set_err(ctx, PQH_ERR_ARG, "dictionary pages have no readValues");
-  if (codec_fail_page(b, P.chunk) >= 0) {  // readChunk failed: no page of the chunk is ever read
-    out->status = PQH_ERR_DECOMPRESS;
+  const ChunkErr ce = chunk_error(b, P.chunk);
+  if (ce.status != PQH_OK && ce.phase == PQH_PHASE_LOAD) {  // readChunk failed: no page of it is ever read
+    out->status = ce.status;
     out->phase = PQH_PHASE_LOAD;
+    out->index = ce.index;
     return PQH_OK;
   }
   const int64_t n = std::max(0, P.num_values);
@@ -1356,21 +1360,48 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
 }  // extern "C"
 
 namespace {
-// Device codecs: the page of `chunk` whose image failed to decompress, if it decides the chunk's
-// result (-1 otherwise).  The reference walks a chunk's pages in order (readChunk) and decompresses
-// each one before looking at the next header, so the failing page wins over walker errors after it
-// (the host walker stopped there: host_status) and over every decode error; a page-level load error
-// found by the planner at or before it (P.host_err of a chunk the walker finished) wins instead.
-int32_t codec_fail_page(const pqh_batch* b, int32_t chunk) {
-  if (b->codec_status.empty()) return -1;
+// The first error of a chunk in the reference's order.  readChunk walks the pages and fails at the
+// first one it cannot load (chunk_reader.go:182-263): a page whose image the device could not
+// decompress (readPageBlock), a page-load error of the planner or the prologue (the decoders'
+// selection and init, phase 0), or -- after the listed pages -- the host walker's error
+// (host_status); any of these fails the whole row group (chunk_reader.go:394-400).  Otherwise
+// readValues errors surface page by page (data_store.go:236-260): the first in page order.
+ChunkErr chunk_error(const pqh_batch* b, int32_t chunk) {
   const DevChunk& D = b->hchunks[size_t(chunk)];
-  const bool walker_failed = b->chunks[size_t(chunk)].host_status != PQH_OK;
+  ChunkErr e;
+  auto key = [&](int32_t p, uint64_t k) {
+    e.status = int32_t(k & 0xff);
+    e.phase = int32_t(k >> 56);
+    e.index = int64_t((k >> 8) & 0xffffffffffffull);
+    e.page = p;
+  };
   for (int32_t i = 0; i < D.num_pages; i++) {
     const int32_t p = D.first_page + i;
-    if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) return p;
-    if (!walker_failed && b->hpages[size_t(p)].host_err != kNoError) return -1;
+    if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) {
+      e.status = PQH_ERR_DECOMPRESS;
+      e.phase = PQH_PHASE_LOAD;
+      e.page = p;
+      return e;
+    }
+    const uint64_t k = b->states[size_t(p)].err;
+    if (k != kNoError && (k >> 56) == PQH_PHASE_LOAD) {
+      key(p, k);
+      return e;
+    }
   }
-  return -1;
+  if (b->chunks[size_t(chunk)].host_status != PQH_OK) {
+    e.status = b->chunks[size_t(chunk)].host_status;
+    e.phase = PQH_PHASE_LOAD;
+    return e;  // (page -1: the page the walk stopped at is not in the batch)
+  }
+  for (int32_t i = 0; i < D.num_pages; i++) {
+    const int32_t p = D.first_page + i;
+    if (b->states[size_t(p)].err != kNoError) {
+      key(p, b->states[size_t(p)].err);
+      return e;
+    }
+  }
+  return e;
 }
 }  // namespace
 
@@ -1390,28 +1421,17 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   out->num_bytes = D.offsets ? std::max<int64_t>(0, std::min(b->chunk_bytes[size_t(chunk)], D.bytes_cap)) : 0;
   out->def_levels = D.def_levels;
   out->rep_levels = D.rep_levels;
-  out->status = PQH_OK;
-  out->error_page = -1;
+  const ChunkErr e = chunk_error(b, chunk);
+  out->status = e.status;
+  out->error_page = e.page;
+  out->error_phase = e.phase;
+  out->error_index = e.index;
   int64_t nn = 0;
   for (int32_t i = 0; i < D.num_pages; i++) {
     const int32_t p = D.first_page + i;
-    const PageState& S = b->states[size_t(p)];
-    if (S.err != kNoError && out->status == PQH_OK) {
-      out->status = int32_t(S.err & 0xff);
-      out->error_page = p;
-      out->error_phase = int32_t(S.err >> 56);
-      out->error_index = int64_t((S.err >> 8) & 0xffffffffffffull);
-    }
-    if (b->hpages[size_t(p)].page_type != PQH_DICTIONARY_PAGE) nn += S.nn;
+    if (b->hpages[size_t(p)].page_type != PQH_DICTIONARY_PAGE) nn += b->states[size_t(p)].nn;
   }
   out->num_non_null = nn;
-  const int32_t k = codec_fail_page(b, chunk);
-  if (k >= 0) {  // readPageBlock failed at page k: the chunk fails there, before any decode
-    out->status = PQH_ERR_DECOMPRESS;
-    out->error_page = k;
-    out->error_phase = PQH_PHASE_LOAD;
-    out->error_index = 0;
-  }
   return PQH_OK;
 }
 

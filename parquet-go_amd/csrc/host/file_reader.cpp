@@ -51,6 +51,7 @@ struct RowGroupMeta {
 struct SchemaEl {
   bool has_type = false;
   int32_t type = 0, type_length = 0;
+  bool has_type_length = false;
   bool has_rep = false;
   int32_t rep = 0;
   std::string name;
@@ -82,193 +83,155 @@ struct pqh_file {
 
 namespace {
 
-bool parse_schema_el(TReader& r, SchemaEl& e) {
-  int16_t last = 0, id;
-  uint8_t t;
-  while (r.field(last, id, t)) {
-    switch (id) {
-      case 1: e.has_type = true; e.type = int32_t(r.integer(t)); break;
-      case 2: e.type_length = int32_t(r.integer(t)); break;
-      case 3: e.has_rep = true; e.rep = int32_t(r.integer(t)); break;
-      case 4: e.name = r.binary(); break;
-      case 5: e.has_children = true; e.num_children = int32_t(r.integer(t)); break;
-      default: r.skip(t);
-    }
-  }
-  return r.ok();
+// The typed FileMetaData (generated readers of parquet/parquet.go, thrift_compact.h) -> the fields
+// the reader uses.
+void schema_el(const TNode& n, SchemaEl& e) {
+  if (const TNode* t = n.get(1)) e.has_type = true, e.type = int32_t(t->i);
+  if (const TNode* t = n.get(2)) e.has_type_length = true, e.type_length = int32_t(t->i);
+  if (const TNode* t = n.get(3)) e.has_rep = true, e.rep = int32_t(t->i);
+  if (const TNode* t = n.get(4)) e.name = t->s;
+  if (const TNode* t = n.get(5)) e.has_children = true, e.num_children = int32_t(t->i);
 }
 
-bool parse_column_meta(TReader& r, ChunkMeta& m) {
-  int16_t last = 0, id;
-  uint8_t t;
-  m.has_meta = true;
-  while (r.field(last, id, t)) {
-    switch (id) {
-      case 1: m.type = int32_t(r.integer(t)); break;
-      case 4: m.codec = int32_t(r.integer(t)); break;
-      case 7: m.total_compressed = r.integer(t); break;
-      case 9: m.data_page_offset = r.integer(t); break;
-      case 11: m.has_dict_offset = true; m.dict_page_offset = r.integer(t); break;
-      default: r.skip(t);
-    }
-  }
-  return r.ok();
+void chunk_meta(const TNode& cc, ChunkMeta& m) {
+  m.has_file_path = cc.get(1) != nullptr;
+  const TNode* md = cc.get(3);
+  if (!md) return;
+  m.has_meta = true;  // (its required fields are present: the typed read checked them)
+  m.type = int32_t(md->get_i(1));
+  m.codec = int32_t(md->get_i(4));
+  m.total_compressed = md->get_i(7);
+  m.data_page_offset = md->get_i(9);
+  if (const TNode* t = md->get(11)) m.has_dict_offset = true, m.dict_page_offset = t->i;
 }
 
-bool parse_row_group(TReader& r, RowGroupMeta& g) {
-  int16_t last = 0, id;
-  uint8_t t;
-  while (r.field(last, id, t)) {
-    if (id == 1 && t == T_LIST) {
-      uint8_t et;
-      uint32_t n;
-      r.list(et, n);
-      for (uint32_t i = 0; i < n && r.ok(); i++) {
-        ChunkMeta cm;
-        int16_t l2 = 0, id2;
-        uint8_t t2;
-        while (r.field(l2, id2, t2)) {
-          if (id2 == 1) {
-            cm.has_file_path = true;
-            r.skip(t2);
-          } else if (id2 == 3 && t2 == T_STRUCT) {
-            parse_column_meta(r, cm);
-          } else {
-            r.skip(t2);
-          }
-        }
-        g.chunks.push_back(cm);
-      }
-    } else if (id == 3) {
-      g.num_rows = r.integer(t);
-    } else {
-      r.skip(t);
-    }
-  }
-  return r.ok();
-}
-
-// readSchema (schema.go:992-1015) and its group/column readers: levels and error rules.
-bool build_columns(pqh_file* f, const std::vector<SchemaEl>& s) {
-  if (s.empty()) {
-    f->err = "empty schema";
+// makeSchema + readSchema (schema.go:992-1015, 1048-1079): the elements after the root are read
+// as top-level groups / columns until the list ends (the root's num_children is not consulted);
+// readGroupSchema / readColumnSchema (:893-990) and getValuesStore (data_store.go:328-362) checks.
+struct SchemaBuilder {
+  pqh_file* f;
+  const std::vector<SchemaEl>& s;  // s[0] = the root
+  bool fail(const char* m) {
+    f->err = m;
     return false;
   }
-  struct Frame {
-    int32_t remaining;
-    int32_t d, r;
-    std::string path;
-    std::vector<int32_t> rep_def;  // definition level of each REPEATED node above
-  };
-  std::vector<Frame> st;
-  const SchemaEl& root = s[0];
-  if (root.has_type || !root.has_children || root.num_children <= 0) {
-    f->err = "invalid schema root";
-    return false;
+  // element i of the list after the root = s[i + 1]
+  bool column(int32_t& idx, const std::string& path, int32_t d, int32_t r, const std::vector<int32_t>& rd) {
+    const SchemaEl& e = s[size_t(idx) + 1];
+    if (e.name.empty()) return fail("name in schema is empty");
+    if (!e.has_rep) return fail("field RepetitionType is nil");
+    if (e.rep != 0) d++;
+    std::vector<int32_t> rd2 = rd;
+    if (e.rep == 2) {
+      r++;
+      rd2.push_back(d);
+    }
+    if (e.type < 0 || e.type > PQH_FIXED_LEN_BYTE_ARRAY) return fail("unsupported type");
+    if (e.type == PQH_FIXED_LEN_BYTE_ARRAY && !e.has_type_length) return fail("type with nil type length");
+    ColumnMeta cm;
+    cm.col = pqh_column{e.type, e.type_length, d, r, {0, 0, 0, 0, 0, 0, 0, 0}};
+    for (size_t k = 0; k < rd2.size() && k < PQH_MAX_NEST; k++) cm.col.rep_def[k] = rd2[k];
+    cm.path = path.empty() ? e.name : path + "." + e.name;
+    f->schema[size_t(idx) + 1] = SchemaNode{e, int32_t(f->columns.size()), d, r};
+    f->columns.push_back(cm);
+    idx++;
+    return true;
   }
-  st.push_back({root.num_children, 0, 0, "", {}});
-  f->schema.assign(s.size(), SchemaNode{});
-  f->schema[0].el = root;
-  for (size_t i = 1; i < s.size(); i++) {
-    while (!st.empty() && st.back().remaining == 0) st.pop_back();
-    if (st.empty()) {
-      f->err = "schema has trailing elements";
-      return false;
+  bool group(int32_t& idx, const std::string& path, int32_t d, int32_t r, const std::vector<int32_t>& rd, int depth) {
+    const int32_t n = int32_t(s.size()) - 1;
+    if (depth > 10000) return fail("schema too deep");
+    if (n <= idx) return fail("schema index out of bound");
+    const SchemaEl& e = s[size_t(idx) + 1];
+    if (e.has_type) return fail("field Type is not nil");
+    if (!e.has_children) return fail("the field NumChildren is invalid");
+    if (e.num_children <= 0) return fail("the field NumChildren is zero");
+    const int32_t l = e.num_children;
+    if (int64_t(n) <= int64_t(idx) + l) return fail("not enough element in the schema list");
+    std::vector<int32_t> rd2 = rd;
+    if (e.has_rep && e.rep != 0) d++;
+    if (e.has_rep && e.rep == 2) {
+      r++;
+      rd2.push_back(d);
     }
-    Frame& parent = st.back();
-    parent.remaining--;
-    const SchemaEl& e = s[i];
-    if (e.name.empty()) {
-      f->err = "name in schema is empty";
-      return false;
-    }
-    const std::string path = parent.path.empty() ? e.name : parent.path + "." + e.name;
-    int32_t d = parent.d, r = parent.r;
-    std::vector<int32_t> rd = parent.rep_def;
-    if (e.has_type) {
-      if (!e.has_rep) {
-        f->err = "field RepetitionType is nil";
+    const std::string p = path.empty() ? e.name : path + "." + e.name;
+    f->schema[size_t(idx) + 1] = SchemaNode{e, -1, d, r};
+    idx++;
+    for (int32_t i = 0; i < l; i++) {
+      if (n <= idx) return fail("schema index is out of bounds");
+      if (!s[size_t(idx) + 1].has_type) {
+        if (!group(idx, p, d, r, rd2, depth + 1)) return false;
+      } else if (!column(idx, p, d, r, rd2)) {
         return false;
       }
-      if (e.rep != 0) d++;
-      if (e.rep == 2) {
-        r++;
-        rd.push_back(d);
-      }
-      ColumnMeta cm;
-      cm.col = pqh_column{e.type, e.type_length, d, r, {0, 0, 0, 0, 0, 0, 0, 0}};
-      for (size_t k = 0; k < rd.size() && k < PQH_MAX_NEST; k++) cm.col.rep_def[k] = rd[k];
-      cm.path = path;
-      f->schema[i] = SchemaNode{e, int32_t(f->columns.size()), d, r};
-      f->columns.push_back(cm);
-    } else {
-      if (!e.has_children || e.num_children <= 0) {
-        f->err = "group without children";
+    }
+    return true;
+  }
+  bool build() {
+    if (s.empty()) return fail("no schema element found");
+    f->schema.assign(s.size(), SchemaNode{});
+    f->schema[0].el = s[0];
+    const int32_t n = int32_t(s.size()) - 1;
+    for (int32_t idx = 0; idx < n;) {
+      if (!s[size_t(idx) + 1].has_type) {
+        if (!group(idx, "", 0, 0, {}, 0)) return false;
+      } else if (!column(idx, "", 0, 0, {})) {
         return false;
       }
-      if (e.has_rep && e.rep != 0) d++;
-      if (e.has_rep && e.rep == 2) {
-        r++;
-        rd.push_back(d);
-      }
-      f->schema[i] = SchemaNode{e, -1, d, r};
-      st.push_back({e.num_children, d, r, path, rd});
     }
+    return true;
   }
-  for (auto& fr : st)
-    if (fr.remaining > 0) {
-      f->err = "not enough element in the schema list";
-      return false;
-    }
-  return true;
-}
+};
 
+// ReadFileMetaData(r, extraValidation = true) (file_meta.go:23-73, as NewFileReaderWithOptions
+// calls it, file_reader.go:38-43): both magics, the footer length, the typed FileMetaData over
+// exactly the footer (io.LimitReader), then makeSchema.
 bool parse_footer(pqh_file* f) {
-  if (f->len < 12 || memcmp(f->data, "PAR1", 4) != 0 || memcmp(f->data + f->len - 4, "PAR1", 4) != 0) {
-    f->err = "invalid parquet file magic";
+  if (f->len < 4 || memcmp(f->data, "PAR1", 4) != 0) {
+    f->err = "invalid parquet file header";
     return false;
   }
-  uint32_t flen;
+  if (memcmp(f->data + f->len - 4, "PAR1", 4) != 0) {
+    f->err = "invalid parquet file footer";
+    return false;
+  }
+  if (f->len < 8) {
+    f->err = "seek for the footer len failed";
+    return false;
+  }
+  int32_t flen;
   memcpy(&flen, f->data + f->len - 8, 4);
-  if (int64_t(flen) > f->len - 12) {
-    f->err = "invalid footer length";
+  if (flen <= 0) {
+    f->err = "invalid footer len";
     return false;
   }
-  const uint8_t* p = f->data + f->len - 8 - flen;
-  TReader r(p, f->data + f->len - 8);
+  if (int64_t(flen) > f->len - 8) {
+    f->err = "seek file meta data failed";
+    return false;
+  }
+  TReader r(f->data + f->len - 8 - flen, f->data + f->len - 8);
+  TNode meta;
+  if (!read_typed(r, TS_FILE_META_DATA, meta)) {
+    f->err = "read file meta failed (thrift)";
+    return false;
+  }
   std::vector<SchemaEl> schema;
-  int16_t last = 0, id;
-  uint8_t t;
-  while (r.field(last, id, t)) {
-    if (id == 2 && t == T_LIST) {
-      uint8_t et;
-      uint32_t n;
-      r.list(et, n);
-      for (uint32_t i = 0; i < n && r.ok(); i++) {
-        SchemaEl e;
-        parse_schema_el(r, e);
-        schema.push_back(e);
-      }
-    } else if (id == 3) {
-      f->num_rows = r.integer(t);
-    } else if (id == 4 && t == T_LIST) {
-      uint8_t et;
-      uint32_t n;
-      r.list(et, n);
-      for (uint32_t i = 0; i < n && r.ok(); i++) {
-        RowGroupMeta g;
-        parse_row_group(r, g);
-        f->rgs.push_back(std::move(g));
-      }
-    } else {
-      r.skip(t);
+  for (const TNode& n : meta.get(2)->items) {
+    SchemaEl e;
+    schema_el(n, e);
+    schema.push_back(e);
+  }
+  f->num_rows = meta.get_i(3);
+  for (const TNode& g : meta.get(4)->items) {
+    RowGroupMeta rg;
+    rg.num_rows = g.get_i(3);
+    for (const TNode& cc : g.get(1)->items) {
+      ChunkMeta m;
+      chunk_meta(cc, m);
+      rg.chunks.push_back(m);
     }
+    f->rgs.push_back(std::move(rg));
   }
-  if (!r.ok()) {
-    f->err = "corrupt footer (thrift)";
-    return false;
-  }
-  return build_columns(f, schema);
+  return SchemaBuilder{f, schema}.build();
 }
 
 struct PageHdr {
@@ -277,45 +240,43 @@ struct PageHdr {
   int32_t crc = 0;
   bool has_dp = false, has_dict = false, has_v2 = false;
   int32_t num_values = 0, encoding = 0;
+  int32_t def_enc = 0, rep_enc = 0;  // DataPageHeader level encodings
   int32_t def_len = 0, rep_len = 0;
 };
 
 bool parse_page_header(TReader& r, PageHdr& h) {
-  int16_t last = 0, id;
-  uint8_t t;
-  while (r.field(last, id, t)) {
-    switch (id) {
-      case 1: h.type = int32_t(r.integer(t)); break;
-      case 2: h.usize = int32_t(r.integer(t)); break;
-      case 3: h.csize = int32_t(r.integer(t)); break;
-      case 4: h.has_crc = true; h.crc = int32_t(r.integer(t)); break;
-      case 5:
-      case 7:
-      case 8: {
-        if (t != T_STRUCT) {
-          r.skip(t);
-          break;
-        }
-        if (id == 5) h.has_dp = true;
-        if (id == 7) h.has_dict = true;
-        if (id == 8) h.has_v2 = true;
-        int16_t l2 = 0, i2;
-        uint8_t t2;
-        while (r.field(l2, i2, t2)) {
-          if (i2 == 1) h.num_values = int32_t(r.integer(t2));
-          else if (i2 == 2 && id != 8) h.encoding = int32_t(r.integer(t2));
-          else if (i2 == 4 && id == 8) h.encoding = int32_t(r.integer(t2));
-          else if (i2 == 5 && id == 8) h.def_len = int32_t(r.integer(t2));
-          else if (i2 == 6 && id == 8) h.rep_len = int32_t(r.integer(t2));
-          else r.skip(t2);
-        }
-        break;
-      }
-      default:
-        r.skip(t);
+  TNode n;
+  if (!read_typed(r, TS_PAGE_HEADER, n)) return false;
+  h.type = int32_t(n.get_i(1));
+  h.usize = int32_t(n.get_i(2));
+  h.csize = int32_t(n.get_i(3));
+  if (const TNode* c = n.get(4)) h.has_crc = true, h.crc = int32_t(c->i);
+  if (const TNode* d = n.get(5)) {
+    h.has_dp = true;
+    if (h.type == PQH_DATA_PAGE) {
+      h.num_values = int32_t(d->get_i(1));
+      h.encoding = int32_t(d->get_i(2));
+      h.def_enc = int32_t(d->get_i(3));
+      h.rep_enc = int32_t(d->get_i(4));
     }
   }
-  return r.ok();
+  if (const TNode* d = n.get(7)) {
+    h.has_dict = true;
+    if (h.type == PQH_DICTIONARY_PAGE) {
+      h.num_values = int32_t(d->get_i(1));
+      h.encoding = int32_t(d->get_i(2));
+    }
+  }
+  if (const TNode* d = n.get(8)) {
+    h.has_v2 = true;
+    if (h.type == PQH_DATA_PAGE_V2) {
+      h.num_values = int32_t(d->get_i(1));
+      h.encoding = int32_t(d->get_i(4));
+      h.def_len = int32_t(d->get_i(5));
+      h.rep_len = int32_t(d->get_i(6));
+    }
+  }
+  return true;
 }
 
 struct ChunkWork {
@@ -380,7 +341,11 @@ void append_image(ChunkWork& w, pqh_page& pg, const uint8_t* a, size_t na, const
   pg.image_len = int32_t(na + nb);
 }
 
-// readChunk + readPages for one chunk.
+// readChunk + readPages for one chunk (chunk_reader.go:182-362), page by page in the reference's
+// order of checks.  The walk stops at the first page it cannot read (host_status, with the pages
+// before it listed); the checks of each listed page that belong to the decoders (the values
+// decoder's selection and init, the level decoders' initSize) run on the device, and the batch
+// orders every error of the chunk as the reference's walk would meet them (pqh_batch_chunk_out).
 void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, int validate_crc, ChunkWork& w) {
   auto t0 = std::chrono::steady_clock::now();
   w.chunk.column = col.col;
@@ -389,26 +354,34 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
   w.chunk.host_status = PQH_OK;
   auto fail = [&](int code) { w.chunk.host_status = code; };
   if (m.has_file_path) return fail(PQH_ERR_IO);  // "nyi: data is in another file"
-  if (!m.has_meta) return fail(PQH_ERR_SCHEMA);
-  if (m.type != col.col.physical_type) return fail(PQH_ERR_SCHEMA);
+  if (!m.has_meta) return fail(PQH_ERR_SCHEMA);  // "missing meta data for Column"
+  if (m.type != col.col.physical_type) return fail(PQH_ERR_SCHEMA);  // "wrong type in Column chunk metadata"
   int64_t pos = m.has_dict_offset ? m.dict_page_offset : m.data_page_offset;
+  if (pos < 0) return fail(PQH_ERR_IO);  // Seek: negative position
   int64_t count = 0;
   bool have_dict = false;
   std::vector<uint8_t> out;
+  const int32_t max_def = col.col.max_def, max_rep = col.col.max_rep;
   while (m.total_compressed - count > 0) {
-    if (pos < 0 || pos > f->len) return fail(PQH_ERR_IO);
-    TReader r(f->data + pos, f->data + f->len);
+    // readThrift(PageHeader): reads past the end of the file fail like any short read
+    TReader r(f->data + std::min(pos, f->len), f->data + f->len);
     PageHdr h;
     if (!parse_page_header(r, h)) return fail(PQH_ERR_THRIFT);
     pos += int64_t(r.consumed());
     count += int64_t(r.consumed());
-    if (h.csize < 0 || h.usize < 0) return fail(PQH_ERR_PAGE_HEADER);  // readPageBlock
-    const int64_t avail = f->len - pos;
-    const int64_t got = h.csize < avail ? h.csize : avail;  // io.ReadAll(io.LimitReader)
-    const uint8_t* block = f->data + pos;
-    pos += got;
-    count += got;
-    if (validate_crc && h.has_crc && crc32_ieee(block, size_t(got)) != uint32_t(h.crc)) return fail(PQH_ERR_CRC);
+    // readPageBlock (:161-180): sizes, io.ReadAll(io.LimitReader), CRC
+    const uint8_t* block = nullptr;
+    int64_t got = 0;
+    auto read_block = [&]() -> int {
+      if (h.csize < 0 || h.usize < 0) return PQH_ERR_PAGE_HEADER;  // "invalid page data size"
+      const int64_t avail = std::max<int64_t>(0, f->len - pos);
+      got = h.csize < avail ? h.csize : avail;
+      block = f->data + std::min(pos, f->len);
+      pos += got;
+      count += got;
+      if (validate_crc && h.has_crc && crc32_ieee(block, size_t(got)) != uint32_t(h.crc)) return PQH_ERR_CRC;
+      return PQH_OK;
+    };
     pqh_page pg;
     memset(&pg, 0, sizeof(pg));
     pg.page_type = h.type;
@@ -416,8 +389,10 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
     pg.encoding = h.encoding;
     pg.chunk = 0;
     const bool dev = w.device_codecs && m.codec == PQH_CODEC_SNAPPY;
-    // whole-block pages (V1 data / dictionary): decompressed here, or left for the device
+    // newBlockReader (compress.go:131-152) of a whole block (V1 data / dictionary): decompressed
+    // here, or left for the device
     auto whole_block = [&]() -> bool {
+      if (got != h.csize) return false;
       if (dev) {
         if (!snappy_plausible(block, size_t(got), h.usize)) return false;
         append_source(w, pg, block, 0, block, size_t(got), h.usize, PQH_CODEC_SNAPPY);
@@ -430,28 +405,47 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       else append_image(w, pg, out.data(), out.size(), nullptr, 0);
       return true;
     };
+    int rc;
     if (h.type == PQH_DICTIONARY_PAGE) {
-      if (have_dict) return fail(PQH_ERR_DICT_PAGE);
+      if (have_dict) return fail(PQH_ERR_DICT_PAGE);  // "there should be only one dictionary"
+      // getDictValuesDecoder (:17-39): no BOOLEAN dictionaries
+      if (col.col.physical_type == PQH_BOOLEAN) return fail(PQH_ERR_UNSUPPORTED);
+      // dictPageReader.read (page_dict.go:35-72)
       if (!h.has_dict) return fail(PQH_ERR_PAGE_HEADER);
-      if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
+      if (h.num_values < 0) return fail(PQH_ERR_PAGE_HEADER);
+      if (h.encoding != PQH_ENC_PLAIN && h.encoding != PQH_ENC_PLAIN_DICTIONARY) return fail(PQH_ERR_DICT_PAGE);
+      if ((rc = read_block())) return fail(rc);
       if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
-      w.pages.push_back(pg);
+      w.pages.push_back(pg);  // its PLAIN values are decoded (and may fail) on the device
       have_dict = true;
       if (m.has_dict_offset && m.dict_page_offset != pos) {  // seek to DataPageOffset
+        if (m.data_page_offset < 0) return fail(PQH_ERR_IO);
         count += m.data_page_offset - pos;
         pos = m.data_page_offset;
       }
       continue;
     }
     if (h.type == PQH_DATA_PAGE) {
+      // dataPageReaderV1.init (page_v1.go:65-85): the level decoders need RLE when their level is used
       if (!h.has_dp) return fail(PQH_ERR_PAGE_HEADER);
-      if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
+      if (max_rep > 0 && h.rep_enc != PQH_ENC_RLE) return fail(PQH_ERR_UNSUPPORTED);
+      if (max_def > 0 && h.def_enc != PQH_ENC_RLE) return fail(PQH_ERR_UNSUPPORTED);
+      // .read (:87-122): NumValues, block, decompression (the values decoder: on the device)
+      if (h.num_values < 0) return fail(PQH_ERR_PAGE_HEADER);
+      if ((rc = read_block())) return fail(rc);
       if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
     } else if (h.type == PQH_DATA_PAGE_V2) {
+      // dataPageReaderV2.read (page_v2.go:79-131)
       if (!h.has_v2) return fail(PQH_ERR_PAGE_HEADER);
       if (h.num_values < 0 || h.rep_len < 0 || h.def_len < 0) return fail(PQH_ERR_PAGE_HEADER);
+      int32_t vs;  // getValuesDecoder runs before the block is read here (:107-112)
+      if (resolve_kind(col.col.physical_type, col.col.type_length, h.encoding, &vs) == 0) return fail(PQH_ERR_UNSUPPORTED);
+      if ((rc = read_block())) return fail(rc);
       const int64_t levels = int64_t(h.rep_len) + h.def_len;
-      if (levels > got) return fail(PQH_ERR_PAGE_HEADER);  // slice out of range in the reference
+      // the level slices of the block: out of range is a runtime panic in the reference (:117-123)
+      if (levels > got) return fail(PQH_ERR_PAGE_HEADER);
+      // newBlockReader(block[levels:], csize - levels, usize - levels)
+      if (int64_t(h.csize) - levels < 0 || int64_t(h.usize) - levels < 0) return fail(PQH_ERR_PAGE_HEADER);
       if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
       // the values section is decompressed regardless of is_compressed (page_v2.go:125)
       if (dev) {
@@ -658,6 +652,36 @@ int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_
   hb->payload_bytes = int64_t(hb->payload.size());
   hb->payload.resize(hb->payload.size() + PQH_PAYLOAD_PAD, 0);
   *out = hb;
+  return PQH_OK;
+}
+
+int32_t pqh_file_column_path(const pqh_file* f, int32_t column, char* buf, int32_t cap) {
+  if (!f || column < 0 || size_t(column) >= f->columns.size()) return -1;
+  const std::string& p = f->columns[size_t(column)].path;
+  if (buf && cap > 0) memcpy(buf, p.data(), std::min(p.size(), size_t(cap)));
+  return int32_t(p.size());
+}
+
+int32_t pqh_file_schema_name(const pqh_file* f, int32_t i, char* buf, int32_t cap) {
+  if (!f || i < 0 || size_t(i) >= f->schema.size()) return -1;
+  const std::string& n = f->schema[size_t(i)].el.name;
+  if (buf && cap > 0) memcpy(buf, n.data(), std::min(n.size(), size_t(cap)));
+  return int32_t(n.size());
+}
+
+int pqh_file_chunk_check(const pqh_file* f, int32_t rg, int32_t column, int32_t selected) {
+  // readRowGroupData's per-column checks before any page is read (chunk_reader.go:381-393), and
+  // skipChunk's (:271-297) for a column that is not selected
+  if (!f || rg < 0 || size_t(rg) >= f->rgs.size() || column < 0 || size_t(column) >= f->columns.size())
+    return PQH_ERR_ARG;
+  const RowGroupMeta& g = f->rgs[size_t(rg)];
+  if (size_t(column) >= g.chunks.size()) return PQH_ERR_SCHEMA;  // "column index %d is out of bounds"
+  const ChunkMeta& m = g.chunks[size_t(column)];
+  if (m.has_file_path) return PQH_ERR_IO;
+  if (!m.has_meta) return PQH_ERR_SCHEMA;
+  if (m.type != f->columns[size_t(column)].col.physical_type) return PQH_ERR_SCHEMA;
+  const int64_t off = m.has_dict_offset ? m.dict_page_offset : m.data_page_offset;
+  if ((selected ? off : off + m.total_compressed) < 0) return PQH_ERR_IO;  // Seek: negative position
   return PQH_OK;
 }
 

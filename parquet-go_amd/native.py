@@ -131,6 +131,9 @@ PROTOTYPES = [
     ("pqh_file_row_group_num_rows", i64, [vp, i32]),
     ("pqh_file_num_columns", i32, [vp]),
     ("pqh_file_column", ctypes.c_int, [vp, i32, ctypes.POINTER(Column), ctypes.c_char_p, i32]),
+    ("pqh_file_chunk_check", ctypes.c_int, [vp, i32, i32, i32]),
+    ("pqh_file_column_path", i32, [vp, i32, ctypes.c_char_p, i32]),
+    ("pqh_file_schema_name", i32, [vp, i32, ctypes.c_char_p, i32]),
     ("pqh_file_num_schema_elements", i32, [vp]),
     ("pqh_file_schema_element", ctypes.c_int, [vp, i32, ctypes.POINTER(SchemaElement), ctypes.c_char_p, i32]),
     ("pqh_file_load", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]),
@@ -342,22 +345,32 @@ class File:
 
     def columns(self):
         out = []
-        buf = ctypes.create_string_buffer(1024)
         for i in range(self.L.pqh_file_num_columns(self.h)):
             c = Column()
-            _check(self.L.pqh_file_column(self.h, i, ctypes.byref(c), buf, 1024))
-            out.append((buf.value.decode(), c.physical_type, c.type_length, c.max_def, c.max_rep))
+            _check(self.L.pqh_file_column(self.h, i, ctypes.byref(c), None, 0))
+            out.append((self._text(self.L.pqh_file_column_path, i), c.physical_type, c.type_length, c.max_def,
+                        c.max_rep))
         return out
 
     def schema(self):
         """[(name, SchemaElement)] in DFS order, root first."""
         out = []
-        buf = ctypes.create_string_buffer(1024)
         for i in range(self.L.pqh_file_num_schema_elements(self.h)):
             e = SchemaElement()
-            _check(self.L.pqh_file_schema_element(self.h, i, ctypes.byref(e), buf, 1024))
-            out.append((buf.value.decode(), e))
+            _check(self.L.pqh_file_schema_element(self.h, i, ctypes.byref(e), None, 0))
+            out.append((self._text(self.L.pqh_file_schema_name, i), e))
         return out
+
+    def _text(self, fn, i):
+        """A path / name of any bytes (Go strings), as str with undecodable bytes escaped."""
+        n = fn(self.h, i, None, 0)
+        buf = ctypes.create_string_buffer(max(n, 1))
+        fn(self.h, i, buf, n)
+        return buf.raw[:n].decode("utf-8", "surrogateescape")
+
+    def chunk_check(self, rg, column, selected=True):
+        """readRowGroupData's checks of a column before its pages (pqh_file_chunk_check): a status."""
+        return self.L.pqh_file_chunk_check(self.h, rg, column, int(selected))
 
     def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False):
         """Walk the pages of `columns` in row groups [rg_begin, rg_end).  device_snappy: SNAPPY

@@ -143,9 +143,7 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
         path, pt, tl, md, mr = cols[columns[i % len(columns)]]
         span = range(ch.first_page, ch.first_page + ch.num_pages)
         pr = [res[p] for p in span]
-        o = batch.chunk_out(i)
-        if ch.host_status != native.OK and o.status == native.OK:
-            o.status = ch.host_status
+        o = batch.chunk_out(i)  # (its status orders walker, load and readValues errors as the reference)
         info = [(pages[p].page_type, pages[p].num_values, res[p]) for p in span]
         out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None, info))
     if return_batch:
@@ -204,8 +202,15 @@ class FileReader:
         self._loaded = None
         self._rows = None
         loaded = decode_chunks(self.ctx, self.file, rg, rg + 1, self.selected, self.validate_crc)
-        for c in loaded:  # readRowGroupData: the first column whose readChunk fails (chunk_reader.go:394-400)
-            c.raise_for_load()
+        # readRowGroupData (chunk_reader.go:375-404): column by column in schema order, the column
+        # checks (skipChunk for the unselected ones), then readChunk; the first failure fails the group
+        by_col = dict(zip(self.selected, loaded))
+        for ci, path in enumerate(self._paths):
+            st = self.file.chunk_check(rg, ci, ci in by_col)
+            if st != native.OK:
+                raise DecodeError(path, st, native.PHASE_LOAD, 0, -1)
+            if ci in by_col:
+                by_col[ci].raise_for_load()
         self._loaded = loaded
 
     def _advance_if_needed(self):  # advanceIfNeeded (file_reader.go:226-238)

@@ -198,9 +198,11 @@ def build_tree(schema, stores):
             kids.append(node(j))
         return Node(name, e.repetition, e.max_def, e.max_rep, children=kids)
 
+    # readSchema (schema.go:992-1015): every element after the root is read as a top-level child
+    # until the list ends (the root's num_children is not consulted)
     root_name, root = schema[0]
     kids = []
-    for _ in range(root.num_children):
+    while pos[0] < len(schema):
         j = pos[0]
         pos[0] += 1
         kids.append(node(j))

@@ -26,9 +26,8 @@ def oracle_chunk(fr, rg, ci):
     """readChunk + readValues for every page (oracle)."""
     e = Expected()
     ch = fr.read_chunk(rg, ci)
-    if ch.status:
-        e.status = ch.status
-        e.host_error = True
+    if ch.status:  # readChunk failed (walker, codec or a page's load step): exact (status, phase 0, index)
+        e.status, e.phase, e.index = ch.status, O.PHASE_LOAD, ch.index
         return e
     col = ch.column
     res = O.decode_chunk(ch)

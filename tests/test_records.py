@@ -82,7 +82,7 @@ def _oracle_schema(fr):
         nr = r + (1 if rep == 2 else 0)
         n = e.get(5, 0)
         name = e.get(4, b"")
-        name = name.decode() if isinstance(name, bytes) else name
+        name = name.decode("utf-8", "surrogateescape") if isinstance(name, bytes) else name
         if n == 0:
             out.append((name, _El(leaf[0], nd, nr, rep, 0)))
             leaf[0] += 1
@@ -94,7 +94,7 @@ def _oracle_schema(fr):
     root = els[0]
     pos[0] = 1
     out.append((root.get(4, b"schema"), _El(-1, 0, 0, -1, root.get(5, 0))))
-    for _ in range(root.get(5, 0)):
+    while pos[0] < len(els):  # readSchema: top-level children until the list ends (schema.go:992-1015)
         walk(0, 0)
     return out
 
