@@ -425,6 +425,15 @@ int64_t pqh_host_batch_image_bytes(const pqh_host_batch* hb);
  * d_src / d_dst as described by `pages` (host array), status[i] = PQH_OK or PQH_ERR_DECOMPRESS. */
 int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_pages, const void* d_src,
                          void* d_dst, int32_t* status);
+
+/* The RLE / bit-packing hybrid decoder alone (reference hybridDecoder, hybrid_decoder.go:81-165, the
+ * levelDecoder of interfaces.go): n values of width `width` (0..32) from the stream at d_stream
+ * (device memory, len bytes, followed by PQH_PAYLOAD_PAD readable bytes) into d_out (device, n
+ * uint32), through the device's run walk and unpack (group = 8: the level path, 4: the dictionary
+ * path's 4-value groups).  *status = the first error (PQH_OK if none), *values = the values decoded
+ * before it (n if none).  Synchronous on the context stream. */
+int pqh_hybrid_decode(pqh_ctx* ctx, const void* d_stream, int64_t len, int32_t width, int64_t n, int32_t group,
+                      uint32_t* d_out, int32_t* status, int64_t* values);
 int pqh_batch_run_staged(pqh_batch* batch);
 
 #ifdef __cplusplus

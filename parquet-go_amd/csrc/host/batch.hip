@@ -1644,6 +1644,31 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   return PQH_OK;
 }
 
+int pqh_hybrid_decode(pqh_ctx* ctx, const void* d_stream, int64_t len, int32_t width, int64_t n, int32_t group,
+                      uint32_t* d_out, int32_t* status, int64_t* values) {
+  if (!ctx || len < 0 || n < 0 || width < 0 || width > 32 || (group != 4 && group != 8) || !status || !values ||
+      (n > 0 && !d_out) || (len > 0 && !d_stream) || n > (int64_t(1) << 40))
+    return set_err(ctx, PQH_ERR_ARG, "bad hybrid decode arguments");
+  hipSetDevice(ctx->device);
+  Ckpt* ck = nullptr;
+  uint64_t* res = nullptr;
+  uint64_t h[2] = {kNoError, 0};
+  const size_t nck = size_t((n + kHybridTile - 1) / kHybridTile) + 1;
+  hipError_t e = hipMalloc(&ck, sizeof(Ckpt) * nck);
+  if (e == hipSuccess) e = hipMalloc(&res, sizeof(h));
+  if (e == hipSuccess) e = hipMemsetAsync(ck, 0, sizeof(Ckpt) * nck, ctx->stream);
+  if (e == hipSuccess)
+    e = launch_hybrid_raw(static_cast<const uint8_t*>(d_stream), len, width, n, group, ck, res, d_out, ctx->stream);
+  if (e == hipSuccess) e = bounce_d2h(ctx, h, res, sizeof(h));
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (ck) hipFree(ck);
+  if (res) hipFree(res);
+  if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("pqh_hybrid_decode: ") + hipGetErrorString(e));
+  *status = h[0] == kNoError ? PQH_OK : int32_t(h[0] & 0xff);
+  *values = int64_t(h[1]);
+  return PQH_OK;
+}
+
 int pqh_batch_run_staged(pqh_batch* b) {
   if (!b) return set_err(nullptr, PQH_ERR_ARG, "null batch");
   pqh_ctx* ctx = b->ctx;

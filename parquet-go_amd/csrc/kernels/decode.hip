@@ -1094,8 +1094,62 @@ __global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* til
 }
 
 // ------------------------------------------------------------------------------------------------
+// The hybrid decoder alone (pqh_hybrid_decode, the reference's levelDecoder.next over a whole
+// stream, hybrid_decoder.go:81-165): one wave walks the run headers into tile checkpoints (the
+// prologue's walk), then one workgroup per kHybridTile tile unpacks its values through the same
+// expand_hybrid / bp_staged paths as k_expand, into uint32 values.
+// ------------------------------------------------------------------------------------------------
+template <int G>
+struct RawSink {
+  static constexpr int kGroup = G;
+  uint32_t* out;
+  __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (j < cnt) out[i0 + j] = v[j];
+  }
+};
+
+__global__ __launch_bounds__(64) void k_hybrid_walk(const uint8_t* s, int64_t len, int w, int64_t n, Ckpt* ck,
+                                                    uint64_t* res) {
+  const WalkOut o = walk_hybrid(s, 0, len, w, n, 3, ck, -1, int(threadIdx.x));
+  if (threadIdx.x == 0) {
+    res[0] = o.err;
+    res[1] = uint64_t(o.fail_index);
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_hybrid_raw(const uint8_t* s, int64_t len, int w, const Ckpt* ck,
+                                                    const uint64_t* res, uint32_t* out) {
+  __shared__ TileLds L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int64_t t0 = int64_t(blockIdx.x) * kHybridTile;
+  const int64_t lim = int64_t(res[1]);  // values before the first error
+  const int64_t t1 = t0 + kHybridTile < lim ? t0 + kHybridTile : lim;
+  if (t0 >= t1) return;
+  RawSink<G> sink{out};
+  expand_hybrid(s, len, w, ck[blockIdx.x], t0, t1, L, reinterpret_cast<uint32_t*>(lds), sink);
+}
+
+// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+hipError_t launch_hybrid_raw(const uint8_t* stream, int64_t len, int32_t width, int64_t n, int group, Ckpt* ck,
+                             uint64_t* res, uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_hybrid_walk, dim3(1), dim3(64), 0, s, stream, len, width, n, ck, res);
+  const int64_t tiles = (n + kHybridTile - 1) / kHybridTile;
+  if (tiles > 0) {
+    if (group == 4)
+      hipLaunchKernelGGL(k_hybrid_raw<4>, dim3(unsigned(tiles)), dim3(256), size_t(kStageBytes + 16), s, stream, len,
+                         width, ck, res, out);
+    else
+      hipLaunchKernelGGL(k_hybrid_raw<8>, dim3(unsigned(tiles)), dim3(256), size_t(kStageBytes + 16), s, stream, len,
+                         width, ck, res, out);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s) {
   if (b.num_pages <= 0) return hipSuccess;
   if (wide) hipLaunchKernelGGL(k_prologue<4>, dim3(b.num_pages), dim3(256), 0, s, b);

@@ -28,6 +28,9 @@ struct DevBatch {
 };
 
 hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s);
+// pqh_hybrid_decode: walk (res[0] = first error key, res[1] = values before it) + unpack (G = group)
+hipError_t launch_hybrid_raw(const uint8_t* stream, int64_t len, int32_t width, int64_t n, int group, Ckpt* ck,
+                             uint64_t* res, uint32_t* out, hipStream_t s);
 // Device codecs: one wave per page rebuilding its image from its (SNAPPY) source bytes.
 hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                          hipStream_t s);

@@ -143,6 +143,7 @@ PROTOTYPES = [
     ("pqh_host_batch_codec_pages", ctypes.POINTER(CodecPage), [vp]),
     ("pqh_host_batch_image_bytes", i64, [vp]),
     ("pqh_decompress_pages", ctypes.c_int, [vp, ctypes.POINTER(CodecPage), i32, vp, vp, ctypes.POINTER(i32)]),
+    ("pqh_hybrid_decode", ctypes.c_int, [vp, vp, i64, i32, i64, i32, vp, ctypes.POINTER(i32), ctypes.POINTER(i64)]),
     ("pqh_host_batch_num_chunks", i32, [vp]),
     ("pqh_host_batch_num_pages", i32, [vp]),
     ("pqh_host_batch_chunks", ctypes.POINTER(Chunk), [vp]),
@@ -233,6 +234,22 @@ class Context:
         st = (i32 * max(1, len(pages)))()
         self.check(self.L.pqh_decompress_pages(self.h, arr, len(pages), d_src, d_dst, st))
         return [st[i] for i in range(len(pages))]
+
+    def hybrid_decode(self, stream, width, n, group=8):
+        """The device's hybrid (RLE / bit-packing) decoder on one stream (host bytes): (status,
+        values decoded before the first error, uint32 values) (pqh_hybrid_decode)."""
+        arr = np.frombuffer(bytes(stream) + b"\0" * PAYLOAD_PAD, dtype=np.uint8).copy()
+        d = self.malloc(len(arr))
+        o = self.malloc(max(4 * n, 16))
+        try:
+            self.h2d(d, arr.ctypes.data, len(arr))
+            st, nv = i32(), i64()
+            self.check(self.L.pqh_hybrid_decode(self.h, d, len(stream), width, n, group, o, ctypes.byref(st),
+                                                ctypes.byref(nv)))
+            return st.value, nv.value, self.d2h_array(o, nv.value, np.uint32)
+        finally:
+            self.free(o)
+            self.free(d)
 
     def d2h_array(self, src, n, dtype=np.uint8):
         out = np.empty(n, dtype=dtype)
