@@ -1281,6 +1281,10 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   const DevChunk& C = b->hchunks[size_t(P.chunk)];
   out->value_size = C.value_size;
   if (P.page_type == PQH_DICTIONARY_PAGE) return set_err(ctx, PQH_ERR_ARG, "dictionary pages have no readValues");
+  const int64_t n = std::max(0, P.num_values);
+  // dataPageReaderV1/V2.readValues: size is clipped to the values left in the page
+  const int64_t s0 = std::min(first, n), s1 = std::min(n, s0 + count);
+  out->num_slots = s1 - s0;
   const ChunkErr ce = chunk_error(b, P.chunk);
   if (ce.status != PQH_OK && ce.phase == PQH_PHASE_LOAD) {  // readChunk failed: no page of it is ever read
     out->status = ce.status;
@@ -1288,10 +1292,6 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
     out->index = ce.index;
     return PQH_OK;
   }
-  const int64_t n = std::max(0, P.num_values);
-  // dataPageReaderV1/V2.readValues: size is clipped to the values left in the page
-  const int64_t s0 = std::min(first, n), s1 = std::min(n, s0 + count);
-  out->num_slots = s1 - s0;
   if (S.err != kNoError) {
     const int phase = int(S.err >> 56);
     const int64_t idx = int64_t((S.err >> 8) & 0xffffffffffffull);
