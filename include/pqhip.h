@@ -418,6 +418,14 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
 #define PQH_LOAD_DEVICE_SNAPPY 1u
 int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
                      int32_t validate_crc, uint32_t flags, pqh_host_batch** out);
+
+/* pqh_file_load_ex whose payload is written straight into pinned host memory from `ctx`'s pool
+ * (reused across loads): pqh_batch_create_staged adopts it without a copy, so the page bytes go
+ * file -> pinned payload (one decompression or copy, by the walker threads) -> HBM.  The block
+ * returns to the pool when the host batch and every staged batch made from it are freed; destroy
+ * the context last. */
+int pqh_file_load_pinned(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns,
+                         int32_t num_columns, int32_t validate_crc, uint32_t flags, pqh_host_batch** out);
 int32_t pqh_host_batch_num_codec_pages(const pqh_host_batch* hb);
 const pqh_codec_page* pqh_host_batch_codec_pages(const pqh_host_batch* hb);
 int64_t pqh_host_batch_image_bytes(const pqh_host_batch* hb);

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,7 +24,17 @@
 
 using namespace pqhip;
 
+// Reusable pinned host blocks of a context (pqh_file_load_pinned payloads): a block returns to the
+// pool when its last holder (host batch, staged batch) lets go, and is freed with the context (or
+// on release, once the context is gone).
+struct PinnedPool {
+  std::mutex m;
+  std::vector<std::pair<uint8_t*, size_t>> free_blocks;
+  bool closed = false;
+};
+
 struct pqh_ctx {
+  std::shared_ptr<PinnedPool> pool = std::make_shared<PinnedPool>();
   int32_t device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
@@ -132,6 +144,36 @@ hipError_t bounce_d2h(pqh_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 namespace pqhip {
 
+std::shared_ptr<uint8_t> pinned_acquire(pqh_ctx* ctx, size_t bytes) {
+  std::shared_ptr<PinnedPool> pool = ctx->pool;
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  {
+    std::lock_guard<std::mutex> g(pool->m);
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < pool->free_blocks.size(); i++)  // the smallest free block that fits
+      if (pool->free_blocks[i].second >= bytes && (best == SIZE_MAX || pool->free_blocks[i].second < pool->free_blocks[best].second))
+        best = i;
+    if (best != SIZE_MAX) {
+      p = pool->free_blocks[best].first;
+      cap = pool->free_blocks[best].second;
+      pool->free_blocks.erase(pool->free_blocks.begin() + long(best));
+    }
+  }
+  if (!p) {
+    cap = (std::max<size_t>(bytes, 1) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    hipSetDevice(ctx->device);
+    void* q = nullptr;
+    if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    p = static_cast<uint8_t*>(q);
+  }
+  return std::shared_ptr<uint8_t>(p, [pool, cap](uint8_t* q) {
+    std::lock_guard<std::mutex> g(pool->m);
+    if (pool->closed) hipHostFree(q);
+    else pool->free_blocks.emplace_back(q, cap);
+  });
+}
+
 int32_t resolve_kind(int32_t type, int32_t type_length, int32_t enc, int32_t* vs) {
   if (enc == PQH_ENC_PLAIN_DICTIONARY) enc = PQH_ENC_RLE_DICTIONARY;
   int32_t size = 0;
@@ -233,6 +275,7 @@ struct pqh_batch {
   std::vector<int32_t> codec_status;  // host copy after sync (per page)
   int64_t payload_bytes = 0;
   void* h_staged = nullptr;           // staged batches: pinned host page images
+  std::shared_ptr<uint8_t> h_pinned_ref;  // ... when they are a pinned host batch's payload (shared)
   size_t staged_bytes = 0;
   hipEvent_t ev_copied = nullptr, ev_done = nullptr;
   bool done_recorded = false;
@@ -291,7 +334,8 @@ void free_batch(pqh_batch* b) {
   for (void* p : b->allocations) hipFree(p);
   if (b->owned_payload) hipFree(b->owned_payload);
   if (b->d_src) hipFree(b->d_src);
-  if (b->h_staged) hipHostFree(b->h_staged);
+  if (b->h_staged && !b->h_pinned_ref) hipHostFree(b->h_staged);
+  b->h_pinned_ref.reset();
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
   if (b->ev_done) hipEventDestroy(b->ev_done);
   for (hipEvent_t e : b->ev_dep)
@@ -375,6 +419,12 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   for (hipEvent_t ev : ctx->bounce_ev)
     if (ev) hipEventDestroy(ev);
   if (ctx->bounce) hipHostFree(ctx->bounce);
+  {
+    std::lock_guard<std::mutex> g(ctx->pool->m);
+    ctx->pool->closed = true;
+    for (auto& fb : ctx->pool->free_blocks) hipHostFree(fb.first);
+    ctx->pool->free_blocks.clear();
+  }
   delete ctx;
 }
 
@@ -1526,7 +1576,7 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
   }
   pqh_batch* b = *out;
   b->owned_payload = img;
-  b->src_bytes = hb->payload.size();
+  b->src_bytes = hb->size();
   b->codec_n = int32_t(hb->codec_pages.size());
   // d_src passes to the batch only once nothing can fail: on an error the caller still owns (and frees) it
   if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec), sizeof(pqh_codec_page) * size_t(b->codec_n))) ||
@@ -1554,8 +1604,8 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
   hipSetDevice(ctx->device);
   if (!hb->codec_pages.empty()) {  // source payload to HBM; images rebuilt by every run
     void* src = nullptr;
-    HIP_TRY(ctx, hipMalloc(&src, hb->payload.size()));
-    hipError_t e = bounce_h2d(ctx, src, hb->payload.data(), hb->payload.size());
+    HIP_TRY(ctx, hipMalloc(&src, hb->size()));
+    hipError_t e = bounce_h2d(ctx, src, hb->data(), hb->size());
     if (e != hipSuccess) {
       hipFree(src);
       return set_err(ctx, PQH_ERR_HIP, std::string("source upload: ") + hipGetErrorString(e));
@@ -1565,9 +1615,10 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
     return rc;
   }
   void* d = nullptr;
-  const size_t bytes = hb->payload.size();
+  const size_t bytes = hb->size();
   HIP_TRY(ctx, hipMalloc(&d, bytes ? bytes : 16));
-  const hipError_t e = bounce_h2d(ctx, d, hb->payload.data(), bytes);
+  const hipError_t e = hb->pinned ? hipMemcpy(d, hb->data(), bytes, hipMemcpyHostToDevice)
+                                  : bounce_h2d(ctx, d, hb->data(), bytes);
   if (e != hipSuccess) {
     hipFree(d);
     return set_err(ctx, PQH_ERR_HIP, std::string("payload upload: ") + hipGetErrorString(e));
@@ -1587,10 +1638,18 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
   if (!ctx || !hb) return set_err(ctx, PQH_ERR_ARG, "null argument");
   hipSetDevice(ctx->device);
   if (!ctx->copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-  const size_t bytes = hb->payload.size();
+  const size_t bytes = hb->size();
   void* h = nullptr;
-  HIP_TRY(ctx, hipHostMalloc(&h, bytes ? bytes : 16, hipHostMallocDefault));
-  if (bytes) memcpy(h, hb->payload.data(), bytes);
+  std::shared_ptr<uint8_t> pinned = hb->pinned ? hb->buf : nullptr;  // a pinned payload is adopted, not copied
+  if (pinned) {
+    h = pinned.get();
+  } else {
+    HIP_TRY(ctx, hipHostMalloc(&h, bytes ? bytes : 16, hipHostMallocDefault));
+    if (bytes) memcpy(h, hb->data(), bytes);
+  }
+  auto free_h = [&]() {
+    if (!pinned) hipHostFree(h);
+  };
   void* d = nullptr;
   hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
   // the first upload happens here so that planning (which reads nothing from the payload) and the
@@ -1599,7 +1658,7 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     if (d) hipFree(d);
-    hipHostFree(h);
+    free_h();
     return set_err(ctx, PQH_ERR_HIP, std::string("staged payload: ") + hipGetErrorString(e));
   }
   int rc = hb->codec_pages.empty() ? pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()),
@@ -1608,12 +1667,13 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
                                     : create_codec_batch(ctx, hb, d, out);
   if (rc) {
     hipFree(d);
-    hipHostFree(h);
+    free_h();
     return rc;
   }
   pqh_batch* b = *out;
   if (hb->codec_pages.empty()) b->owned_payload = d;  // else: d is the source buffer (b->d_src)
   b->h_staged = h;
+  b->h_pinned_ref = pinned;
   b->staged_bytes = bytes;
   if (hipEventCreateWithFlags(&b->ev_copied, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming) != hipSuccess) {

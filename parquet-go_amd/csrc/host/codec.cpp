@@ -3,6 +3,7 @@
 
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstring>
 
 namespace pqhip {
@@ -192,6 +193,118 @@ bool gzip_compress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
   if (rc != Z_STREAM_END) return false;
   dst.resize(out);
   return true;
+}
+
+// Snappy block straight into dst[expected]: fails unless it decodes to exactly `expected` bytes.
+static bool snappy_into(const uint8_t* src, size_t n, uint8_t* out, size_t expected) {
+  const uint8_t* p = src;
+  const uint8_t* end = src + n;
+  uint64_t len;
+  if (!read_uvarint(p, end, len) || len > (uint64_t(1) << 32) - 1 || len != expected) return false;
+  size_t d = 0;
+  while (p < end) {
+    const uint8_t tag = *p++;
+    size_t length, offset;
+    switch (tag & 3) {
+      case 0: {
+        size_t x = tag >> 2;
+        if (x >= 60) {
+          const int k = int(x) - 59;
+          if (end - p < k) return false;
+          x = 0;
+          for (int i = 0; i < k; i++) x |= size_t(p[i]) << (8 * i);
+          p += k;
+        }
+        length = x + 1;
+        if (size_t(end - p) < length || len - d < length) return false;
+        memcpy(out + d, p, length);
+        p += length;
+        d += length;
+        continue;
+      }
+      case 1:
+        if (end - p < 1) return false;
+        length = 4 + ((tag >> 2) & 7);
+        offset = (size_t(tag >> 5) << 8) | p[0];
+        p += 1;
+        break;
+      case 2:
+        if (end - p < 2) return false;
+        length = 1 + (tag >> 2);
+        offset = size_t(p[0]) | (size_t(p[1]) << 8);
+        p += 2;
+        break;
+      default:
+        if (end - p < 4) return false;
+        length = 1 + (tag >> 2);
+        offset = size_t(p[0]) | (size_t(p[1]) << 8) | (size_t(p[2]) << 16) | (size_t(p[3]) << 24);
+        p += 4;
+        break;
+    }
+    if (offset == 0 || offset > d || len - d < length) return false;
+    if (offset >= length) {
+      memcpy(out + d, out + d - offset, length);
+    } else {
+      for (size_t i = 0; i < length; i++) out[d + i] = out[d + i - offset];  // overlapping: forward copy
+    }
+    d += length;
+  }
+  return d == len;
+}
+
+// Multistream gzip straight into dst[expected]: fails on corrupt input or any other output size.
+static bool gzip_into(const uint8_t* src, size_t n, uint8_t* dst, size_t expected) {
+  size_t pos = 0;
+  const uint8_t* in = src;
+  size_t left = n;
+  bool any = false;
+  while (left > 0) {
+    z_stream s;
+    memset(&s, 0, sizeof(s));
+    if (inflateInit2(&s, 16 + MAX_WBITS) != Z_OK) return false;
+    s.next_in = const_cast<Bytef*>(in);
+    s.avail_in = uInt(left);
+    for (;;) {
+      uint8_t scratch[64];
+      const bool full = pos == expected;  // more output past `expected` is a size mismatch
+      const size_t room = full ? sizeof(scratch) : std::min<size_t>(expected - pos, size_t(1) << 30);
+      s.next_out = full ? scratch : dst + pos;
+      s.avail_out = uInt(room);
+      const int rc = inflate(&s, Z_NO_FLUSH);
+      const size_t produced = room - s.avail_out;
+      if (full && produced > 0) {
+        inflateEnd(&s);
+        return false;
+      }
+      pos += full ? 0 : produced;
+      if (rc == Z_STREAM_END) break;
+      if (rc != Z_OK && !(rc == Z_BUF_ERROR && s.avail_out == 0)) {
+        inflateEnd(&s);
+        return false;
+      }
+    }
+    const size_t used = left - s.avail_in;
+    inflateEnd(&s);
+    in += used;
+    left -= used;
+    any = true;
+  }
+  return any && pos == expected;
+}
+
+bool decompress_into(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t expected) {
+  switch (codec) {
+    case 0:
+      if (n != expected) return false;
+      if (n) memcpy(dst, src, n);
+      return true;
+    case 1:
+      return snappy_into(src, n, dst, expected);
+    case 2:
+      return gzip_into(src, n, dst, expected);
+    default:
+      return false;
+  }
 }
 
 bool decompress_block(int codec, const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst) {

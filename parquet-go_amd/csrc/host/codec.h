@@ -15,6 +15,10 @@ namespace pqhip {
 // unsupported codec.  `expected` is the header's uncompressed size (a hint; the caller checks it).
 bool decompress_block(int codec, const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst);
 
+// Decompress `src` with `codec` straight into dst[0, expected): true iff the block is valid and
+// decodes to exactly `expected` bytes (readPageBlock + newBlockReader's size check).
+bool decompress_into(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t expected);
+
 bool snappy_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst);
 void snappy_compress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst);
 bool gzip_decompress(const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst);

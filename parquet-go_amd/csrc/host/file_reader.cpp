@@ -12,6 +12,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <new>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -279,38 +282,34 @@ bool parse_page_header(TReader& r, PageHdr& h) {
   return true;
 }
 
-struct ChunkWork {
-  pqh_chunk chunk;
-  std::vector<pqh_page> pages;  // image_offset relative to `bytes` (device codecs: to the image space)
-  std::vector<uint8_t> bytes;
-  double seconds = 0;
-  bool device_codecs = false;   // bytes = source bytes; images rebuilt on the device
-  std::vector<pqh_codec_page> cps;
-  int64_t image = 0;            // device codecs: image space used so far
+// ------------------------------------------------------------------------------------------------
+// The page walk in two passes, so that every page image is written once, straight to its place in
+// the batch payload (pinned host memory with pqh_file_load_pinned):
+//   plan (per chunk, parallel): readPages' header walk with every check that does not need the
+//     decompressed bytes, each page's image size (the header's uncompressed size) and place;
+//   materialise (per page, parallel): decompress (or copy) the page into its place; a page that
+//     fails ends its chunk there (pages after it are dropped, as readPages stops).
+// ------------------------------------------------------------------------------------------------
+struct PageOp {
+  pqh_page pg;            // image_offset: relative to the chunk's image area
+  const uint8_t* block;   // the page's bytes in the file (readPageBlock)
+  int64_t got = 0;        // bytes read
+  int64_t levels = 0;     // V2: raw level bytes in front of the (compressed) values
+  bool raw = false;       // device codecs: the page travels compressed (SNAPPY) and k_snappy rebuilds it
+  int64_t src_off = 0;    // device codecs: its source bytes in the chunk's source area
+  int64_t src_len = 0;
+  bool failed = false;    // materialise: decompression failed or the size differs
 };
 
-// Device codecs: the page's source bytes (raw prefix a, then b) go to `bytes`; its image (of
-// image_len bytes) gets a place in the image space.
-void append_source(ChunkWork& w, pqh_page& pg, const uint8_t* a, size_t na, const uint8_t* b, size_t nb,
-                   int64_t image_len, int32_t codec) {
-  const size_t off = (w.bytes.size() + 63) & ~size_t(63);
-  w.bytes.resize(off + na + nb);
-  if (na) memcpy(w.bytes.data() + off, a, na);
-  if (nb) memcpy(w.bytes.data() + off + na, b, nb);
-  const int64_t img = (w.image + 63) & ~int64_t(63);
-  w.image = img + image_len;
-  pg.image_offset = img;
-  pg.image_len = int32_t(image_len);
-  pqh_codec_page cp;
-  memset(&cp, 0, sizeof(cp));
-  cp.src_offset = int64_t(off);
-  cp.image_offset = img;
-  cp.src_len = int32_t(na + nb);
-  cp.image_len = int32_t(image_len);
-  cp.raw_len = codec == PQH_CODEC_SNAPPY ? int32_t(na) : 0;
-  cp.codec = codec;
-  w.cps.push_back(cp);
-}
+struct ChunkPlan {
+  pqh_chunk chunk;
+  std::vector<PageOp> ops;
+  int32_t codec = 0;
+  int64_t image = 0;      // image area bytes (64-aligned pages)
+  int64_t src = 0;        // device codecs: source area bytes
+  int64_t image_base = 0, src_base = 0;  // global offsets (assigned after planning)
+  double seconds = 0;
+};
 
 // The decoded length a snappy block announces (its uvarint header), -1 if malformed.
 int64_t snappy_announced(const uint8_t* p, size_t n) {
@@ -332,26 +331,21 @@ bool snappy_plausible(const uint8_t* p, size_t n, int64_t expected) {
   return v == expected && v <= 22 * int64_t(n) + 64;  // a 3-byte copy element yields <= 64 bytes
 }
 
-void append_image(ChunkWork& w, pqh_page& pg, const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
-  size_t off = (w.bytes.size() + 63) & ~size_t(63);
-  w.bytes.resize(off + na + nb);
-  if (na) memcpy(w.bytes.data() + off, a, na);
-  if (nb) memcpy(w.bytes.data() + off + na, b, nb);
-  pg.image_offset = int64_t(off);
-  pg.image_len = int32_t(na + nb);
-}
+int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
-// readChunk + readPages for one chunk (chunk_reader.go:182-362), page by page in the reference's
-// order of checks.  The walk stops at the first page it cannot read (host_status, with the pages
-// before it listed); the checks of each listed page that belong to the decoders (the values
-// decoder's selection and init, the level decoders' initSize) run on the device, and the batch
-// orders every error of the chunk as the reference's walk would meet them (pqh_batch_chunk_out).
-void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, int validate_crc, ChunkWork& w) {
+// Plan: readChunk + readPages for one chunk (chunk_reader.go:182-362), page by page in the
+// reference's order of checks.  The walk stops at the first page it cannot read (host_status, with
+// the pages before it listed); the checks of each listed page that belong to the decoders (the
+// values decoder's selection and init, the level decoders' initSize) run on the device, and the
+// batch orders every error of the chunk as the reference's walk would meet them (chunk_error).
+void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, int validate_crc, bool dev_codecs,
+                ChunkPlan& w) {
   auto t0 = std::chrono::steady_clock::now();
   w.chunk.column = col.col;
   w.chunk.first_page = 0;
   w.chunk.num_pages = 0;
   w.chunk.host_status = PQH_OK;
+  w.codec = m.codec;
   auto fail = [&](int code) { w.chunk.host_status = code; };
   if (m.has_file_path) return fail(PQH_ERR_IO);  // "nyi: data is in another file"
   if (!m.has_meta) return fail(PQH_ERR_SCHEMA);  // "missing meta data for Column"
@@ -360,8 +354,8 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
   if (pos < 0) return fail(PQH_ERR_IO);  // Seek: negative position
   int64_t count = 0;
   bool have_dict = false;
-  std::vector<uint8_t> out;
   const int32_t max_def = col.col.max_def, max_rep = col.col.max_rep;
+  const bool dev = dev_codecs && m.codec == PQH_CODEC_SNAPPY;
   while (m.total_compressed - count > 0) {
     // readThrift(PageHeader): reads past the end of the file fail like any short read
     TReader r(f->data + std::min(pos, f->len), f->data + f->len);
@@ -369,41 +363,44 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
     if (!parse_page_header(r, h)) return fail(PQH_ERR_THRIFT);
     pos += int64_t(r.consumed());
     count += int64_t(r.consumed());
+    PageOp op;
+    memset(&op.pg, 0, sizeof(op.pg));
+    op.pg.page_type = h.type;
+    op.pg.num_values = h.num_values;
+    op.pg.encoding = h.encoding;
     // readPageBlock (:161-180): sizes, io.ReadAll(io.LimitReader), CRC
-    const uint8_t* block = nullptr;
-    int64_t got = 0;
     auto read_block = [&]() -> int {
       if (h.csize < 0 || h.usize < 0) return PQH_ERR_PAGE_HEADER;  // "invalid page data size"
       const int64_t avail = std::max<int64_t>(0, f->len - pos);
-      got = h.csize < avail ? h.csize : avail;
-      block = f->data + std::min(pos, f->len);
-      pos += got;
-      count += got;
-      if (validate_crc && h.has_crc && crc32_ieee(block, size_t(got)) != uint32_t(h.crc)) return PQH_ERR_CRC;
+      op.got = h.csize < avail ? h.csize : avail;
+      op.block = f->data + std::min(pos, f->len);
+      pos += op.got;
+      count += op.got;
+      if (validate_crc && h.has_crc && crc32_ieee(op.block, size_t(op.got)) != uint32_t(h.crc)) return PQH_ERR_CRC;
       return PQH_OK;
     };
-    pqh_page pg;
-    memset(&pg, 0, sizeof(pg));
-    pg.page_type = h.type;
-    pg.num_values = h.num_values;
-    pg.encoding = h.encoding;
-    pg.chunk = 0;
-    const bool dev = w.device_codecs && m.codec == PQH_CODEC_SNAPPY;
-    // newBlockReader (compress.go:131-152) of a whole block (V1 data / dictionary): decompressed
-    // here, or left for the device
-    auto whole_block = [&]() -> bool {
-      if (got != h.csize) return false;
-      if (dev) {
-        if (!snappy_plausible(block, size_t(got), h.usize)) return false;
-        append_source(w, pg, block, 0, block, size_t(got), h.usize, PQH_CODEC_SNAPPY);
-        w.cps.back().raw_len = 0;
-        return true;
+    // newBlockReader (compress.go:131-152) of the (values) section [levels, got): what can be decided
+    // without decompressing; the rest is decided when the page is materialised
+    auto block_reader = [&](int64_t levels) -> int {
+      if (int64_t(h.csize) - levels < 0 || int64_t(h.usize) - levels < 0) return PQH_ERR_PAGE_HEADER;
+      if (op.got != h.csize) return PQH_ERR_DECOMPRESS;  // "compressed data must be %d byte"
+      if (m.codec == PQH_CODEC_UNCOMPRESSED && h.csize != h.usize) return PQH_ERR_DECOMPRESS;
+      if (dev && !snappy_plausible(op.block + levels, size_t(op.got - levels), int64_t(h.usize) - levels))
+        return PQH_ERR_DECOMPRESS;
+      op.levels = levels;
+      op.raw = dev;
+      op.src_len = dev ? op.got : h.usize;
+      op.pg.image_len = h.usize;
+      return PQH_OK;
+    };
+    auto place = [&]() {
+      op.pg.image_offset = align64(w.image);
+      w.image = op.pg.image_offset + op.pg.image_len;
+      if (dev_codecs) {
+        op.src_off = align64(w.src);
+        w.src = op.src_off + op.src_len;
       }
-      if (!decompress_block(m.codec, block, size_t(got), size_t(h.usize), out) || int64_t(out.size()) != h.usize)
-        return false;
-      if (w.device_codecs) append_source(w, pg, out.data(), out.size(), nullptr, 0, int64_t(out.size()), PQH_CODEC_UNCOMPRESSED);
-      else append_image(w, pg, out.data(), out.size(), nullptr, 0);
-      return true;
+      w.ops.push_back(op);
     };
     int rc;
     if (h.type == PQH_DICTIONARY_PAGE) {
@@ -414,9 +411,8 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if (!h.has_dict) return fail(PQH_ERR_PAGE_HEADER);
       if (h.num_values < 0) return fail(PQH_ERR_PAGE_HEADER);
       if (h.encoding != PQH_ENC_PLAIN && h.encoding != PQH_ENC_PLAIN_DICTIONARY) return fail(PQH_ERR_DICT_PAGE);
-      if ((rc = read_block())) return fail(rc);
-      if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
-      w.pages.push_back(pg);  // its PLAIN values are decoded (and may fail) on the device
+      if ((rc = read_block()) || (rc = block_reader(0))) return fail(rc);
+      place();  // its PLAIN values are decoded (and may fail) on the device
       have_dict = true;
       if (m.has_dict_offset && m.dict_page_offset != pos) {  // seek to DataPageOffset
         if (m.data_page_offset < 0) return fail(PQH_ERR_IO);
@@ -432,8 +428,7 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if (max_def > 0 && h.def_enc != PQH_ENC_RLE) return fail(PQH_ERR_UNSUPPORTED);
       // .read (:87-122): NumValues, block, decompression (the values decoder: on the device)
       if (h.num_values < 0) return fail(PQH_ERR_PAGE_HEADER);
-      if ((rc = read_block())) return fail(rc);
-      if (!whole_block()) return fail(PQH_ERR_DECOMPRESS);
+      if ((rc = read_block()) || (rc = block_reader(0))) return fail(rc);
     } else if (h.type == PQH_DATA_PAGE_V2) {
       // dataPageReaderV2.read (page_v2.go:79-131)
       if (!h.has_v2) return fail(PQH_ERR_PAGE_HEADER);
@@ -443,33 +438,30 @@ void walk_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if ((rc = read_block())) return fail(rc);
       const int64_t levels = int64_t(h.rep_len) + h.def_len;
       // the level slices of the block: out of range is a runtime panic in the reference (:117-123)
-      if (levels > got) return fail(PQH_ERR_PAGE_HEADER);
-      // newBlockReader(block[levels:], csize - levels, usize - levels)
-      if (int64_t(h.csize) - levels < 0 || int64_t(h.usize) - levels < 0) return fail(PQH_ERR_PAGE_HEADER);
-      if (got != h.csize) return fail(PQH_ERR_DECOMPRESS);
+      if (levels > op.got) return fail(PQH_ERR_PAGE_HEADER);
       // the values section is decompressed regardless of is_compressed (page_v2.go:125)
-      if (dev) {
-        if (!snappy_plausible(block + levels, size_t(got - levels), int64_t(h.usize) - levels))
-          return fail(PQH_ERR_DECOMPRESS);
-        append_source(w, pg, block, size_t(levels), block + levels, size_t(got - levels), h.usize, PQH_CODEC_SNAPPY);
-      } else {
-        if (!decompress_block(m.codec, block + levels, size_t(got - levels), size_t(h.usize - levels), out) ||
-            int64_t(out.size()) != int64_t(h.usize) - levels)
-          return fail(PQH_ERR_DECOMPRESS);
-        if (w.device_codecs)
-          append_source(w, pg, block, size_t(levels), out.data(), out.size(), int64_t(levels) + int64_t(out.size()),
-                        PQH_CODEC_UNCOMPRESSED);
-        else
-          append_image(w, pg, block, size_t(levels), out.data(), out.size());
-      }
-      pg.def_levels_byte_length = h.def_len;
-      pg.rep_levels_byte_length = h.rep_len;
+      if ((rc = block_reader(levels))) return fail(rc);
+      op.pg.def_levels_byte_length = h.def_len;
+      op.pg.rep_levels_byte_length = h.rep_len;
     } else {
       return fail(PQH_ERR_PAGE_HEADER);  // "DATA_PAGE or DATA_PAGE_V2 type supported"
     }
-    w.pages.push_back(pg);
+    place();
   }
   w.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Materialise one planned page: host codecs -> its image at `img`; device codecs -> its source
+// bytes at `src` (compressed SNAPPY, or the decompressed image of another codec) + its codec page.
+void materialise(const ChunkPlan& w, PageOp& op, uint8_t* img, uint8_t* src) {
+  if (op.raw) {  // SNAPPY for the device: raw levels + compressed values, as stored
+    memcpy(src + op.src_off, op.block, size_t(op.got));
+    return;
+  }
+  uint8_t* dst = src ? src + op.src_off : img + op.pg.image_offset;
+  if (op.levels) memcpy(dst, op.block, size_t(op.levels));
+  op.failed = !decompress_into(w.codec, op.block + op.levels, size_t(op.got - op.levels), dst + op.levels,
+                               size_t(op.pg.image_len - op.levels));
 }
 
 int file_error(pqh_file* f, int code, const std::string& m) {
@@ -572,8 +564,12 @@ int pqh_file_load(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* 
   return pqh_file_load_ex(f, rg_begin, rg_end, columns, num_columns, validate_crc, 0, out);
 }
 
-int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
-                     int32_t validate_crc, uint32_t flags, pqh_host_batch** out) {
+}  // extern "C"
+
+namespace {
+
+int file_load(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns,
+              int32_t num_columns, int32_t validate_crc, uint32_t flags, pqh_host_batch** out) {
   *out = nullptr;
   if (!f) return PQH_ERR_ARG;
   if (rg_begin < 0 || rg_end > int32_t(f->rgs.size()) || rg_begin > rg_end)
@@ -581,7 +577,15 @@ int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_
   for (int32_t i = 0; i < num_columns; i++)
     if (columns[i] < 0 || size_t(columns[i]) >= f->columns.size()) return file_error(f, PQH_ERR_ARG, "bad column");
   const int64_t nchunks = int64_t(rg_end - rg_begin) * num_columns;
-  std::vector<ChunkWork> work(static_cast<size_t>(nchunks));
+  std::vector<ChunkPlan> work(static_cast<size_t>(nchunks));
+  const bool timing = getenv("PQH_WALK_TIMING") != nullptr;
+  auto tw = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[walk] %s %.4f s\n", what, std::chrono::duration<double>(t - tw).count());
+    tw = t;
+  };
   // device codecs only when some selected chunk is SNAPPY (otherwise the plain layout)
   bool dev = false;
   if (flags & PQH_LOAD_DEVICE_SNAPPY)
@@ -591,68 +595,142 @@ int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_
         dev = size_t(columns[i]) < g.chunks.size() && g.chunks[size_t(columns[i])].has_meta &&
               g.chunks[size_t(columns[i])].codec == PQH_CODEC_SNAPPY;
       }
-  for (auto& w : work) w.device_codecs = dev;
-  std::atomic<int64_t> next{0};
-  auto worker = [&]() {
-    for (;;) {
-      int64_t k = next.fetch_add(1);
-      if (k >= nchunks) return;
-      const int32_t rg = rg_begin + int32_t(k / num_columns);
-      const int32_t ci = columns[k % num_columns];
-      const RowGroupMeta& g = f->rgs[size_t(rg)];
-      ChunkWork& w = work[size_t(k)];
-      if (size_t(ci) >= g.chunks.size()) {  // "column index %d is out of bounds"
-        w.chunk.column = f->columns[size_t(ci)].col;
-        w.chunk.host_status = PQH_ERR_SCHEMA;
-        continue;
-      }
-      walk_chunk(f, f->columns[size_t(ci)], g.chunks[size_t(ci)], validate_crc, w);
-    }
-  };
   int nt = int(std::thread::hardware_concurrency());
   if (nt > 16) nt = 16;
   if (nt < 1) nt = 1;
-  if (nt > nchunks) nt = int(nchunks > 0 ? nchunks : 1);
-  std::vector<std::thread> th;
-  for (int i = 0; i < nt; i++) th.emplace_back(worker);
-  for (auto& t : th) t.join();
-
+  auto parallel = [&](int64_t items, auto&& fn) {
+    std::atomic<int64_t> next{0};
+    const int k = int(std::min<int64_t>(nt, std::max<int64_t>(items, 1)));
+    std::vector<std::thread> th;
+    for (int i = 0; i < k; i++)
+      th.emplace_back([&]() {
+        for (int64_t j; (j = next.fetch_add(1)) < items;) fn(j);
+      });
+    for (auto& t : th) t.join();
+  };
+  // pass 1: plan every chunk
+  parallel(nchunks, [&](int64_t k) {
+    const int32_t rg = rg_begin + int32_t(k / num_columns);
+    const int32_t ci = columns[k % num_columns];
+    const RowGroupMeta& g = f->rgs[size_t(rg)];
+    ChunkPlan& w = work[size_t(k)];
+    if (size_t(ci) >= g.chunks.size()) {  // "column index %d is out of bounds"
+      w.chunk.column = f->columns[size_t(ci)].col;
+      w.chunk.host_status = PQH_ERR_SCHEMA;
+      return;
+    }
+    plan_chunk(f, f->columns[size_t(ci)], g.chunks[size_t(ci)], validate_crc, dev, w);
+  });
+  lap("plan");
+  // layout: chunk areas back to back (64-aligned); the payload is the images (host codecs) or the
+  // source bytes (device codecs)
+  int64_t images = 0, sources = 0;
+  std::vector<std::pair<size_t, size_t>> page_list;  // (chunk, op)
+  for (size_t k = 0; k < work.size(); k++) {
+    work[k].image_base = align64(images);
+    images = work[k].image_base + work[k].image;
+    work[k].src_base = align64(sources);
+    sources = work[k].src_base + work[k].src;
+    for (size_t i = 0; i < work[k].ops.size(); i++) page_list.emplace_back(k, i);
+  }
+  const int64_t payload_bytes = dev ? sources : images;
   pqh_host_batch* hb = new pqh_host_batch();
-  size_t total = 0;
-  for (auto& w : work) total = ((total + 63) & ~size_t(63)) + w.bytes.size();
-  hb->payload.reserve(total + PQH_PAYLOAD_PAD);
+  const size_t total = size_t(payload_bytes) + PQH_PAYLOAD_PAD;
+  uint8_t* base = nullptr;
+  if (ctx) {
+    hb->buf = pinned_acquire(ctx, total);
+    hb->pinned = true;
+  } else {  // uninitialised (the walker threads write every byte: images, gaps, pad)
+    hb->buf = std::shared_ptr<uint8_t>(new (std::nothrow) uint8_t[total], std::default_delete<uint8_t[]>());
+  }
+  if (!hb->buf) {
+    delete hb;
+    return file_error(f, PQH_ERR_NOMEM, "payload allocation failed");
+  }
+  hb->buf_size = total;
+  base = hb->buf.get();
+  lap("alloc");
+  // pass 2: every page to its place (pages of all chunks spread over the threads); alignment gaps
+  // and the pad are zeroed
+  parallel(int64_t(page_list.size()), [&](int64_t j) {
+    ChunkPlan& w = work[page_list[size_t(j)].first];
+    PageOp& op = w.ops[page_list[size_t(j)].second];
+    materialise(w, op, dev ? nullptr : base + w.image_base, dev ? base + w.src_base : nullptr);
+  });
+  lap("materialise");
+  {
+    int64_t end = 0;  // zero every gap between areas / pages
+    auto zero_to = [&](int64_t off) {
+      if (off > end) memset(base + end, 0, size_t(off - end));
+    };
+    for (auto& w : work) {
+      for (auto& op : w.ops) {
+        const int64_t o = dev ? w.src_base + op.src_off : w.image_base + op.pg.image_offset;
+        zero_to(o);
+        end = std::max(end, o + (dev ? op.src_len : int64_t(op.pg.image_len)));
+      }
+    }
+    zero_to(int64_t(total));
+  }
+  lap("gaps");
   int64_t image = 0;
   for (auto& w : work) {
-    size_t base = (hb->payload.size() + 63) & ~size_t(63);
-    hb->payload.resize(base);
-    hb->payload.insert(hb->payload.end(), w.bytes.begin(), w.bytes.end());
-    const int64_t ibase = dev ? (image + 63) & ~int64_t(63) : int64_t(base);
+    // a page that failed to decompress ends its chunk there (readPages returns the error)
+    size_t keep = w.ops.size();
+    for (size_t i = 0; i < w.ops.size(); i++)
+      if (w.ops[i].failed) {
+        keep = i;
+        w.chunk.host_status = PQH_ERR_DECOMPRESS;
+        break;
+      }
     pqh_chunk c = w.chunk;
     c.first_page = int32_t(hb->pages.size());
-    c.num_pages = int32_t(w.pages.size());
+    c.num_pages = int32_t(keep);
     const int32_t ci = int32_t(hb->chunks.size());
-    for (size_t i = 0; i < w.pages.size(); i++) {
-      pqh_page pg = w.pages[i];
-      pg.image_offset += ibase;
+    for (size_t i = 0; i < keep; i++) {
+      const PageOp& op = w.ops[i];
+      pqh_page pg = op.pg;
+      pg.image_offset += w.image_base;
       pg.chunk = ci;
       hb->pages.push_back(pg);
       if (dev) {
-        pqh_codec_page cp = w.cps[i];
-        cp.src_offset += int64_t(base);
-        cp.image_offset += ibase;
+        pqh_codec_page cp;
+        memset(&cp, 0, sizeof(cp));
+        cp.src_offset = w.src_base + op.src_off;
+        cp.image_offset = pg.image_offset;
+        cp.src_len = int32_t(op.src_len);
+        cp.image_len = pg.image_len;
+        cp.raw_len = op.raw ? int32_t(op.levels) : 0;
+        cp.codec = op.raw ? PQH_CODEC_SNAPPY : PQH_CODEC_UNCOMPRESSED;
         cp.chunk = ci;
         hb->codec_pages.push_back(cp);
       }
     }
-    if (dev) image = ibase + w.image;
     hb->chunks.push_back(c);
     hb->decompress_seconds += w.seconds;
+    image = std::max(image, w.image_base + w.image);
   }
-  hb->image_bytes = dev ? image : 0;
-  hb->payload_bytes = int64_t(hb->payload.size());
-  hb->payload.resize(hb->payload.size() + PQH_PAYLOAD_PAD, 0);
+  hb->image_bytes = dev ? images : 0;
+  hb->payload_bytes = payload_bytes;
+  lap("tables");
   *out = hb;
   return PQH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
+                     int32_t validate_crc, uint32_t flags, pqh_host_batch** out) {
+  return file_load(nullptr, f, rg_begin, rg_end, columns, num_columns, validate_crc, flags, out);
+}
+
+int pqh_file_load_pinned(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns,
+                         int32_t num_columns, int32_t validate_crc, uint32_t flags, pqh_host_batch** out) {
+  *out = nullptr;
+  if (!ctx) return file_error(f, PQH_ERR_ARG, "null context");
+  return file_load(ctx, f, rg_begin, rg_end, columns, num_columns, validate_crc, flags, out);
 }
 
 int32_t pqh_file_column_path(const pqh_file* f, int32_t column, char* buf, int32_t cap) {
@@ -692,7 +770,7 @@ int32_t pqh_host_batch_num_chunks(const pqh_host_batch* hb) { return int32_t(hb-
 int32_t pqh_host_batch_num_pages(const pqh_host_batch* hb) { return int32_t(hb->pages.size()); }
 const pqh_chunk* pqh_host_batch_chunks(const pqh_host_batch* hb) { return hb->chunks.data(); }
 const pqh_page* pqh_host_batch_pages(const pqh_host_batch* hb) { return hb->pages.data(); }
-const uint8_t* pqh_host_batch_payload(const pqh_host_batch* hb) { return hb->payload.data(); }
+const uint8_t* pqh_host_batch_payload(const pqh_host_batch* hb) { return hb->data(); }
 int64_t pqh_host_batch_payload_bytes(const pqh_host_batch* hb) { return hb->payload_bytes; }
 double pqh_host_batch_decompress_seconds(const pqh_host_batch* hb) { return hb->decompress_seconds; }
 void pqh_host_batch_free(pqh_host_batch* hb) { delete hb; }

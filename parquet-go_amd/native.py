@@ -139,6 +139,8 @@ PROTOTYPES = [
     ("pqh_file_load", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]),
     ("pqh_file_load_ex", ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.c_uint32,
                                         ctypes.POINTER(vp)]),
+    ("pqh_file_load_pinned", ctypes.c_int, [vp, vp, i32, i32, ctypes.POINTER(i32), i32, i32, ctypes.c_uint32,
+                                            ctypes.POINTER(vp)]),
     ("pqh_host_batch_num_codec_pages", i32, [vp]),
     ("pqh_host_batch_codec_pages", ctypes.POINTER(CodecPage), [vp]),
     ("pqh_host_batch_image_bytes", i64, [vp]),
@@ -389,13 +391,20 @@ class File:
         """readRowGroupData's checks of a column before its pages (pqh_file_chunk_check): a status."""
         return self.L.pqh_file_chunk_check(self.h, rg, column, int(selected))
 
-    def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False):
+    def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False, ctx=None):
         """Walk the pages of `columns` in row groups [rg_begin, rg_end).  device_snappy: SNAPPY
-        pages stay compressed (the batch decompresses them on the device, k_snappy)."""
+        pages stay compressed (the batch decompresses them on the device, k_snappy).  ctx: the
+        payload is written into pinned memory from the context's pool (pqh_file_load_pinned), which
+        Batch.staged adopts without a copy."""
         cols = (i32 * len(columns))(*columns)
         h = vp()
-        rc = self.L.pqh_file_load_ex(self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc),
-                                     LOAD_DEVICE_SNAPPY if device_snappy else 0, ctypes.byref(h))
+        flags = LOAD_DEVICE_SNAPPY if device_snappy else 0
+        if ctx is not None:
+            rc = self.L.pqh_file_load_pinned(ctx.h, self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc),
+                                             flags, ctypes.byref(h))
+        else:
+            rc = self.L.pqh_file_load_ex(self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc), flags,
+                                         ctypes.byref(h))
         if rc != OK:
             raise PqhError(rc, (self.L.pqh_file_error(self.h) or b"").decode())
         return HostBatch(self.L, h)
