@@ -334,7 +334,7 @@ def main():
     rg0, rg1 = pkg.shard.row_group_block(f.num_row_groups, world, rank) if strong else (0, f.num_row_groups)
     my_rows = sum(f.row_group_num_rows(rg) for rg in range(rg0, rg1))
     t0 = time.perf_counter()
-    hb = f.load(rg0, rg1, list(range(ncols)))
+    hb = f.load(rg0, rg1, list(range(ncols)), ctx=ctx)
     walk_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     batch = native.Batch.from_host(ctx, hb)
@@ -445,15 +445,27 @@ def main():
         # is one workgroup's sequential walk: a launch takes a page's time however many pages it has)
         groups = 1 if device_snappy else min(nrg, 16)
         cuts = [nrg * g // groups for g in range(groups + 1)]
-        staged, payload, images, walk = [], 0, 0, 0.0
-        for g in range(groups):
-            t0 = time.perf_counter()
-            hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)), device_snappy=device_snappy)
-            walk += time.perf_counter() - t0
-            payload += hbr.payload_bytes
-            images += hbr.image_bytes or hbr.payload_bytes
-            staged.append(native.Batch.staged(ctx, hbr))
-            hbr.close()
+
+        def load_all():
+            # the walker threads write every page image straight into pinned memory from the
+            # context's pool (pqh_file_load_pinned); the staged batches adopt it without a copy
+            staged, payload, images, walk = [], 0, 0, 0.0
+            for g in range(groups):
+                t0 = time.perf_counter()
+                hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)), device_snappy=device_snappy,
+                             ctx=ctx)
+                walk += time.perf_counter() - t0
+                payload += hbr.payload_bytes
+                images += hbr.image_bytes or hbr.payload_bytes
+                staged.append(native.Batch.staged(ctx, hbr))
+                hbr.close()
+            return staged, payload, images, walk
+
+        # a first load pins the pool's blocks (one-time cost per process), the second reuses them
+        staged, _, _, walk_cold = load_all()
+        for sb in staged:
+            sb.close()
+        staged, payload, images, walk = load_all()
         written = 0.0
         for sb in staged:
             sb.run_staged()
@@ -483,6 +495,8 @@ def main():
                # one pass over the file with the host's page walk (and, without device SNAPPY, its
                # decompression on the host's chunk threads) counted too
                "host_walk_s": round(walk, 3),
+               "host_walk_cold_s": round(walk_cold, 3),
+               "host_walk_gbps": round(images / walk / 1e9, 2) if walk > 0 else None,
                "per_gpu_gbps_incl_host_walk": round(written / (walk + el / steps) / 1e9, 2)}
         for sb in staged:
             sb.close()
