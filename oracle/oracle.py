@@ -27,7 +27,8 @@ except ImportError:  # imported as a top-level module (oracle/ on sys.path)
     from thrift_spec import SPEC
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liborcl.so")
+# ORC_LIB: another build of the oracle library (the sanitizer variant build/san/liborcl.so)
+LIB_PATH = os.environ.get("ORC_LIB") or os.path.join(HERE, "build", "liborcl.so")
 
 # parquet enums (parquet/parquet.thrift)
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)

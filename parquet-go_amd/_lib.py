@@ -7,7 +7,8 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIBDIR = os.path.join(PKG, "lib")
+# PQH_LIBDIR: another build of the same libraries (the sanitizer variants in lib/san)
+LIBDIR = os.environ.get("PQH_LIBDIR") or os.path.join(PKG, "lib")
 
 _gen = None
 _hip = None

@@ -23,6 +23,19 @@ HEADERS = sorted(os.path.relpath(os.path.join(d, f), CSRC) for d, _, fs in os.wa
                  if f.endswith(".h"))
 
 ARCH = os.environ.get("PQH_OFFLOAD_ARCH", "gfx950")
+# PQH_SANITIZE=1 (or --sanitize): ASan + UBSan variants of the host parsers -- codec.cpp and
+# file_reader.cpp inside libpqhip, and libpqgen -- into lib/san/ (load with PQH_LIBDIR=lib/san and
+# LD_PRELOAD of gcc's libasan + libubsan: scripts/run_sanitized.sh).  The kernels are not
+# instrumented (no GPU sanitizer on this pool); they are checked against the oracle instead.
+SANITIZE = os.environ.get("PQH_SANITIZE", "0") == "1" or "--sanitize" in sys.argv
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+if SANITIZE:
+    LIBDIR = os.path.join(LIBDIR, "san")
+
+
+def _san_link():
+    gcc_dir = os.path.dirname(subprocess.check_output(["gcc", "-print-file-name=libasan.so"], text=True).strip())
+    return ["-L" + gcc_dir, "-Wl,-rpath," + gcc_dir, "-lasan", "-lubsan"] if SANITIZE else []
 
 
 def _hipcc():
@@ -53,7 +66,7 @@ def build_gen(force=False):
     if force or _stale(out, GEN_SRCS):
         os.makedirs(LIBDIR, exist_ok=True)
         _run(["g++", "-O2", "-g", "-std=c++17", "-shared", "-fPIC", "-Wall", "-I", INCLUDE, "-o", out]
-             + [os.path.join(CSRC, s) for s in GEN_SRCS] + ["-lz", "-lpthread"])
+             + (SAN_FLAGS if SANITIZE else []) + [os.path.join(CSRC, s) for s in GEN_SRCS] + ["-lz", "-lpthread"])
     return out
 
 
@@ -64,7 +77,7 @@ def build_hip(force=False):
     if force or _stale(out, HOST_SRCS + HIP_SRCS):
         os.makedirs(LIBDIR, exist_ok=True)
         objs = []
-        bdir = os.path.join(PKG, "build", os.path.basename(out))
+        bdir = os.path.join(PKG, "build", ("san-" if SANITIZE else "") + os.path.basename(out))
         os.makedirs(bdir, exist_ok=True)
         for s in HIP_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")
@@ -75,9 +88,11 @@ def build_hip(force=False):
         for s in HOST_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")
             _run(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-Wall", "-I", INCLUDE,
-                  "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-c", os.path.join(CSRC, s), "-o", o])
+                  "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"] + (SAN_FLAGS if SANITIZE else [])
+                 + ["-c", os.path.join(CSRC, s), "-o", o])
             objs.append(o)
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lz", "-lpthread"])
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lz", "-lpthread"]
+             + _san_link())
     return out
 
 

@@ -476,7 +476,7 @@ int64_t pqg_hybrid_encode(int32_t width, const int32_t* values, int64_t n, uint8
   std::vector<uint32_t> v(values, values + n);
   hybrid_encode(width, v.data(), n, o);
   if (int64_t(o.size()) > cap) return -int64_t(o.size());
-  memcpy(out, o.data(), o.size());
+  if (!o.empty()) memcpy(out, o.data(), o.size());  // (an empty stream: memcpy needs non-null pointers)
   return int64_t(o.size());
 }
 
@@ -484,7 +484,7 @@ int64_t pqg_delta_encode32(const int32_t* values, int64_t n, uint8_t* out, int64
   std::vector<uint8_t> o;
   delta_encode<int32_t, uint32_t>(values, n, o);
   if (int64_t(o.size()) > cap) return -int64_t(o.size());
-  memcpy(out, o.data(), o.size());
+  if (!o.empty()) memcpy(out, o.data(), o.size());  // (an empty stream: memcpy needs non-null pointers)
   return int64_t(o.size());
 }
 
@@ -492,7 +492,7 @@ int64_t pqg_delta_encode64(const int64_t* values, int64_t n, uint8_t* out, int64
   std::vector<uint8_t> o;
   delta_encode<int64_t, uint64_t>(values, n, o);
   if (int64_t(o.size()) > cap) return -int64_t(o.size());
-  memcpy(out, o.data(), o.size());
+  if (!o.empty()) memcpy(out, o.data(), o.size());  // (an empty stream: memcpy needs non-null pointers)
   return int64_t(o.size());
 }
 
