@@ -77,7 +77,8 @@ class OrcOut(ctypes.Structure):
                 ("num_values", ctypes.c_int32), ("nn", ctypes.c_int32),
                 ("def_", ctypes.POINTER(ctypes.c_uint8)), ("rep", ctypes.POINTER(ctypes.c_uint8)),
                 ("value_size", ctypes.c_int32), ("values", ctypes.POINTER(ctypes.c_uint8)),
-                ("values_bytes", ctypes.c_int64), ("offsets", ctypes.POINTER(ctypes.c_int64))]
+                ("values_bytes", ctypes.c_int64), ("offsets", ctypes.POINTER(ctypes.c_int64)),
+                ("num_offsets", ctypes.c_int64)]
 
 
 _lib = None
@@ -248,8 +249,8 @@ def decode_page(col, page_type, num_values, encoding, def_len, rep_len, image, d
         r.rep_levels = np.ctypeslib.as_array(o.rep, shape=(o.num_values,)).copy()
     if o.values_bytes:
         r.values = ctypes.string_at(o.values, o.values_bytes)
-    if o.offsets:
-        r.offsets = np.ctypeslib.as_array(o.offsets, shape=(o.nn + 1,)).copy()
+    if o.offsets and o.num_offsets:
+        r.offsets = np.ctypeslib.as_array(o.offsets, shape=(o.num_offsets,)).copy()
     lib().orc_out_free(ctypes.byref(o))
     return r
 

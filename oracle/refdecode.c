@@ -1026,6 +1026,7 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
   out->values = vals.p;
   out->values_bytes = vals.len;
   out->offsets = (int64_t *)offs.p;
+  out->num_offsets = (int64_t)(offs.len / 8);
   int is_ba = col->physical_type == PQH_BYTE_ARRAY ||
               (col->physical_type == PQH_FIXED_LEN_BYTE_ARRAY && (col->type_length == 0 || pg->encoding == PQH_ENC_DELTA_BYTE_ARRAY));
   out->value_size = is_ba ? 0
@@ -1037,6 +1038,7 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
     int64_t z = 0;
     off_push(&offs, z);
     out->offsets = (int64_t *)offs.p;
+    out->num_offsets = 1;
   }
   if (st) set_err(out, st, PQH_PHASE_VALUES, ei);
   return out->status;

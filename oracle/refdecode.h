@@ -58,7 +58,8 @@ typedef struct orc_out {
   int32_t value_size;   /* bytes per value, 0 for byte arrays */
   uint8_t *values;      /* nn * value_size bytes (fixed), or byte array data */
   int64_t values_bytes;
-  int64_t *offsets;     /* byte arrays: nn + 1 */
+  int64_t *offsets;     /* byte arrays: num_offsets (nn + 1, fewer when the values fail) */
+  int64_t num_offsets;
 } orc_out;
 
 int orc_abi_version(void);
