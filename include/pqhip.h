@@ -416,6 +416,10 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
  * (readPageBlock / newBlockReader, compress.go:131-152): it fails the whole chunk unless a page
  * before it already failed on the host. */
 #define PQH_LOAD_DEVICE_SNAPPY 1u
+/* The same for GZIP chunks (gzipCompressor.DecompressBlock, compress.go:64-77): their pages travel
+ * compressed and k_gzip (one workgroup per page: Go's multistream gzip.Reader rules for members,
+ * headers and CRC-32 / ISIZE trailers; RFC 1951 inflate) rebuilds the images.  The flags combine. */
+#define PQH_LOAD_DEVICE_GZIP 2u
 int pqh_file_load_ex(pqh_file* f, int32_t rg_begin, int32_t rg_end, const int32_t* columns, int32_t num_columns,
                      int32_t validate_crc, uint32_t flags, pqh_host_batch** out);
 

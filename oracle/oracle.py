@@ -557,13 +557,92 @@ def decompress(codec, data, uncompressed_size):
     if codec == UNCOMPRESSED:
         return bytes(data)
     if codec == GZIP:
-        return gzip.decompress(bytes(data))
+        return gzip_decode(data)
+    if codec == SNAPPY:
+        return snappy_decode(data)
     import pyarrow as pa
 
-    name = {SNAPPY: "snappy", ZSTD: "zstd"}.get(codec)
+    name = {ZSTD: "zstd"}.get(codec)
     if name is None:
         raise ValueError(f"codec {codec} not supported")
     return pa.decompress(bytes(data), decompressed_size=uncompressed_size, codec=name, asbytes=True)
+
+
+class GzipCorrupt(Exception):
+    pass
+
+
+def gzip_decode(src):
+    """The reference's GZIP codec (gzipCompressor.DecompressBlock, compress.go:64-77):
+    gzip.NewReader + ioutil.ReadAll of Go's compress/gzip (gunzip.go, the standard library; not
+    vendored in /root/reference), restated member by member:
+      header  = 10 bytes (io.ReadFull: fewer is an error; none at all is io.EOF, an error for the
+                first member and the end of the stream after a later one), ID1 0x1f ID2 0x8b CM 8
+                (ErrHeader; reserved flag bits are ignored), FEXTRA (2-byte LE length + data, short
+                reads fail), FNAME / FCOMMENT (NUL-terminated within 512 bytes, else ErrHeader),
+                FHCRC (uint16 of the CRC-32 of the header bytes before it, else ErrHeader);
+      body    = one raw DEFLATE stream (RFC 1951) -> zlib raw inflate (identical to Go's
+                compress/flate on every valid stream; any error fails the block);
+      trailer = CRC-32 and ISIZE (output length mod 2^32) of the member, 8 bytes LE (short:
+                ErrUnexpectedEOF; mismatch: ErrChecksum);
+    then the next member (multistream, the Reader's default) until the input ends.  Python's
+    gzip.decompress differs (it skips zero padding after a member), so it is not used here.
+    Raises GzipCorrupt."""
+    data = bytes(src)
+    out = bytearray()
+    pos, first = 0, True
+    while True:
+        if pos == len(data) and not first:
+            break
+        if len(data) - pos < 10:
+            raise GzipCorrupt("header")
+        h = data[pos:pos + 10]
+        if h[0] != 0x1F or h[1] != 0x8B or h[2] != 8:
+            raise GzipCorrupt("ErrHeader")
+        flg, q = h[3], pos + 10
+        if flg & 4:  # FEXTRA
+            if len(data) - q < 2:
+                raise GzipCorrupt("extra length")
+            xlen = int.from_bytes(data[q:q + 2], "little")
+            q += 2
+            if len(data) - q < xlen:
+                raise GzipCorrupt("extra")
+            q += xlen
+        for bit in (8, 16):  # FNAME, FCOMMENT: readString
+            if flg & bit:
+                i = 0
+                while True:
+                    if i >= 512:
+                        raise GzipCorrupt("ErrHeader: string")
+                    if q + i >= len(data):
+                        raise GzipCorrupt("string EOF")
+                    if data[q + i] == 0:
+                        break
+                    i += 1
+                q += i + 1
+        if flg & 2:  # FHCRC
+            if len(data) - q < 2:
+                raise GzipCorrupt("header crc")
+            if (zlib.crc32(data[pos:q]) & 0xFFFF) != int.from_bytes(data[q:q + 2], "little"):
+                raise GzipCorrupt("ErrHeader: crc")
+            q += 2
+        d = zlib.decompressobj(-15)
+        try:
+            member = d.decompress(data[q:])
+        except zlib.error as e:
+            raise GzipCorrupt(f"flate: {e}") from None
+        if not d.eof:
+            raise GzipCorrupt("flate: unexpected EOF")
+        t = len(data) - len(d.unused_data)
+        if len(data) - t < 8:
+            raise GzipCorrupt("trailer")
+        crc = int.from_bytes(data[t:t + 4], "little")
+        isize = int.from_bytes(data[t + 4:t + 8], "little")
+        if crc != (zlib.crc32(member) & 0xFFFFFFFF) or isize != (len(member) & 0xFFFFFFFF):
+            raise GzipCorrupt("ErrChecksum")
+        out += member
+        pos, first = t + 8, False
+    return bytes(out)
 
 
 class SnappyCorrupt(Exception):

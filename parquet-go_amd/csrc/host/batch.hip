@@ -78,8 +78,8 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
-                              "k_ba_wcopy"};
-constexpr int kNumKernels = 24;
+                              "k_ba_wcopy",   "k_gzip"};
+constexpr int kNumKernels = 25;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -271,6 +271,7 @@ struct pqh_batch {
   size_t src_bytes = 0;
   pqh_codec_page* d_codec = nullptr;
   int32_t codec_n = 0;
+  int32_t codec_gzip = 0;  // GZIP pages among them (k_gzip)
   int32_t* d_codec_status = nullptr;
   std::vector<int32_t> codec_status;  // host copy after sync (per page)
   int64_t payload_bytes = 0;
@@ -950,6 +951,11 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
                            static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
     });
+  if (e == hipSuccess && b->codec_gzip)
+    e = timed(24, b->codec_gzip, s, [&](hipStream_t st) {
+      return launch_gzip(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
+                         static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
+    });
   // repeated columns carry long level streams: a workgroup per page splits their notNull count
   const bool wide = std::any_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& c) { return c.max_rep > 0; });
   if (e == hipSuccess)
@@ -1578,6 +1584,8 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
   b->owned_payload = img;
   b->src_bytes = hb->size();
   b->codec_n = int32_t(hb->codec_pages.size());
+  b->codec_gzip = int32_t(std::count_if(hb->codec_pages.begin(), hb->codec_pages.end(),
+                                        [](const pqh_codec_page& c) { return c.codec == PQH_CODEC_GZIP; }));
   // d_src passes to the batch only once nothing can fail: on an error the caller still owns (and frees) it
   if ((rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec), sizeof(pqh_codec_page) * size_t(b->codec_n))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_codec_status), sizeof(int32_t) * size_t(b->codec_n)))) {
@@ -1696,6 +1704,8 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   if (e == hipSuccess) e = bounce_h2d(ctx, dp, pages, sizeof(pqh_codec_page) * size_t(num_pages));
   if (e == hipSuccess)
     e = launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
+  if (e == hipSuccess && std::any_of(pages, pages + num_pages, [](const pqh_codec_page& c) { return c.codec == PQH_CODEC_GZIP; }))
+    e = launch_gzip(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
   if (e == hipSuccess) e = bounce_d2h(ctx, status, ds, sizeof(int32_t) * size_t(num_pages));
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (dp) hipFree(dp);

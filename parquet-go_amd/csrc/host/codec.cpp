@@ -140,39 +140,99 @@ void snappy_compress(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
   }
 }
 
-bool gzip_decompress(const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst) {
-  dst.clear();
-  dst.resize(expected > 0 ? expected : 64);
-  size_t pos = 0;
-  const uint8_t* in = src;
-  size_t left = n;
-  bool any = false;
-  // Go's gzip.Reader is multistream: concatenated members decode as one stream.
-  while (left > 0) {
+// Go's compress/gzip member header (gunzip.go readHeader), from src[pos]: sets *body to the first
+// DEFLATE byte.  False on ErrHeader or a short read.  Reserved flag bits are ignored, as in Go.
+static bool gzip_header(const uint8_t* src, size_t n, size_t pos, size_t* body) {
+  if (n - pos < 10) return false;
+  const uint8_t* h = src + pos;
+  if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8) return false;
+  const uint8_t flg = h[3];
+  size_t q = pos + 10;
+  if (flg & 4) {  // FEXTRA
+    if (n - q < 2) return false;
+    const size_t xlen = size_t(src[q]) | (size_t(src[q + 1]) << 8);
+    q += 2;
+    if (n - q < xlen) return false;
+    q += xlen;
+  }
+  for (int bit : {8, 16}) {  // FNAME, FCOMMENT: NUL-terminated within 512 bytes
+    if (!(flg & bit)) continue;
+    size_t i = 0;
+    for (;; i++) {
+      if (i >= 512 || q + i >= n) return false;
+      if (src[q + i] == 0) break;
+    }
+    q += i + 1;
+  }
+  if (flg & 2) {  // FHCRC: the low 16 bits of the CRC-32 of the header so far
+    if (n - q < 2) return false;
+    const uint32_t c = uint32_t(crc32(0L, src + pos, uInt(q - pos)));
+    if ((c & 0xffff) != (uint32_t(src[q]) | (uint32_t(src[q + 1]) << 8))) return false;
+    q += 2;
+  }
+  *body = q;
+  return true;
+}
+
+// Multistream gzip (gzip.NewReader + ReadAll, compress.go:64-77): header, raw DEFLATE (zlib), then
+// the CRC-32 / ISIZE trailer, member after member until the input ends.  Output goes to
+// out(pos, room) -> pointer with room bytes (nullptr: no more room is a failure).
+template <class Out>
+static bool gzip_members(const uint8_t* src, size_t n, size_t& pos, Out&& out) {
+  size_t in = 0;
+  bool first = true;
+  while (first || in < n) {
+    size_t body;
+    if (!gzip_header(src, n, in, &body)) return false;
     z_stream s;
     memset(&s, 0, sizeof(s));
-    if (inflateInit2(&s, 16 + MAX_WBITS) != Z_OK) return false;
-    s.next_in = const_cast<Bytef*>(in);
-    s.avail_in = uInt(left);
+    if (inflateInit2(&s, -MAX_WBITS) != Z_OK) return false;
+    s.next_in = const_cast<Bytef*>(src + body);
+    s.avail_in = uInt(n - body);
+    const size_t ms = pos;
+    uLong crc = crc32(0L, Z_NULL, 0);
     int rc;
     do {
-      if (pos == dst.size()) dst.resize(dst.size() * 2);
-      s.next_out = dst.data() + pos;
-      s.avail_out = uInt(dst.size() - pos);
+      size_t room = 0;
+      uint8_t* o = out(pos, room);
+      if (!o) {
+        inflateEnd(&s);
+        return false;
+      }
+      s.next_out = o;
+      s.avail_out = uInt(room);
       rc = inflate(&s, Z_NO_FLUSH);
-      pos = dst.size() - s.avail_out;
+      const size_t produced = room - s.avail_out;
+      crc = crc32(crc, o, uInt(produced));
+      pos += produced;
       if (rc != Z_OK && rc != Z_STREAM_END && !(rc == Z_BUF_ERROR && s.avail_out == 0)) {
         inflateEnd(&s);
         return false;
       }
     } while (rc != Z_STREAM_END);
-    size_t used = left - s.avail_in;
+    const size_t t = n - s.avail_in;
     inflateEnd(&s);
-    in += used;
-    left -= used;
-    any = true;
+    if (n - t < 8) return false;  // trailer: ErrUnexpectedEOF
+    const uint8_t* tr = src + t;
+    const uint32_t want_crc = uint32_t(tr[0]) | (uint32_t(tr[1]) << 8) | (uint32_t(tr[2]) << 16) | (uint32_t(tr[3]) << 24);
+    const uint32_t want_len = uint32_t(tr[4]) | (uint32_t(tr[5]) << 8) | (uint32_t(tr[6]) << 16) | (uint32_t(tr[7]) << 24);
+    if (uint32_t(crc) != want_crc || uint32_t(pos - ms) != want_len) return false;  // ErrChecksum
+    in = t + 8;
+    first = false;
   }
-  if (!any) return false;
+  return true;
+}
+
+bool gzip_decompress(const uint8_t* src, size_t n, size_t expected, std::vector<uint8_t>& dst) {
+  dst.clear();
+  dst.resize(expected > 0 ? expected : 64);
+  size_t pos = 0;
+  const bool ok = gzip_members(src, n, pos, [&](size_t at, size_t& room) -> uint8_t* {
+    if (at == dst.size()) dst.resize(dst.size() * 2);
+    room = std::min<size_t>(dst.size() - at, size_t(1) << 30);
+    return dst.data() + at;
+  });
+  if (!ok) return false;
   dst.resize(pos);
   return true;
 }
@@ -252,44 +312,21 @@ static bool snappy_into(const uint8_t* src, size_t n, uint8_t* out, size_t expec
   return d == len;
 }
 
-// Multistream gzip straight into dst[expected]: fails on corrupt input or any other output size.
+// Multistream gzip straight into dst[expected]: fails on corrupt input or any other output size
+// (more output than `expected` is decoded into a scratch buffer only to fail).
 static bool gzip_into(const uint8_t* src, size_t n, uint8_t* dst, size_t expected) {
   size_t pos = 0;
-  const uint8_t* in = src;
-  size_t left = n;
-  bool any = false;
-  while (left > 0) {
-    z_stream s;
-    memset(&s, 0, sizeof(s));
-    if (inflateInit2(&s, 16 + MAX_WBITS) != Z_OK) return false;
-    s.next_in = const_cast<Bytef*>(in);
-    s.avail_in = uInt(left);
-    for (;;) {
-      uint8_t scratch[64];
-      const bool full = pos == expected;  // more output past `expected` is a size mismatch
-      const size_t room = full ? sizeof(scratch) : std::min<size_t>(expected - pos, size_t(1) << 30);
-      s.next_out = full ? scratch : dst + pos;
-      s.avail_out = uInt(room);
-      const int rc = inflate(&s, Z_NO_FLUSH);
-      const size_t produced = room - s.avail_out;
-      if (full && produced > 0) {
-        inflateEnd(&s);
-        return false;
-      }
-      pos += full ? 0 : produced;
-      if (rc == Z_STREAM_END) break;
-      if (rc != Z_OK && !(rc == Z_BUF_ERROR && s.avail_out == 0)) {
-        inflateEnd(&s);
-        return false;
-      }
+  uint8_t scratch[64];
+  const bool ok = gzip_members(src, n, pos, [&](size_t at, size_t& room) -> uint8_t* {
+    if (at > expected) return nullptr;
+    if (at == expected) {
+      room = sizeof(scratch);
+      return scratch;
     }
-    const size_t used = left - s.avail_in;
-    inflateEnd(&s);
-    in += used;
-    left -= used;
-    any = true;
-  }
-  return any && pos == expected;
+    room = std::min<size_t>(expected - at, size_t(1) << 30);
+    return dst + at;
+  });
+  return ok && pos == expected;
 }
 
 bool decompress_into(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t expected) {

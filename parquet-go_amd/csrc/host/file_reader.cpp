@@ -339,7 +339,7 @@ int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 // values decoder's selection and init, the level decoders' initSize) run on the device, and the
 // batch orders every error of the chunk as the reference's walk would meet them (chunk_error).
 void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, int validate_crc, bool dev_codecs,
-                ChunkPlan& w) {
+                uint32_t flags, ChunkPlan& w) {
   auto t0 = std::chrono::steady_clock::now();
   w.chunk.column = col.col;
   w.chunk.first_page = 0;
@@ -355,7 +355,10 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
   int64_t count = 0;
   bool have_dict = false;
   const int32_t max_def = col.col.max_def, max_rep = col.col.max_rep;
-  const bool dev = dev_codecs && m.codec == PQH_CODEC_SNAPPY;
+  // this chunk's pages stay compressed for the device (the layout is the device-codec one whenever
+  // some selected chunk's codec is decoded on the device)
+  const bool dev = dev_codecs && ((m.codec == PQH_CODEC_SNAPPY && (flags & PQH_LOAD_DEVICE_SNAPPY)) ||
+                                  (m.codec == PQH_CODEC_GZIP && (flags & PQH_LOAD_DEVICE_GZIP)));
   while (m.total_compressed - count > 0) {
     // readThrift(PageHeader): reads past the end of the file fail like any short read
     TReader r(f->data + std::min(pos, f->len), f->data + f->len);
@@ -385,7 +388,7 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if (int64_t(h.csize) - levels < 0 || int64_t(h.usize) - levels < 0) return PQH_ERR_PAGE_HEADER;
       if (op.got != h.csize) return PQH_ERR_DECOMPRESS;  // "compressed data must be %d byte"
       if (m.codec == PQH_CODEC_UNCOMPRESSED && h.csize != h.usize) return PQH_ERR_DECOMPRESS;
-      if (dev && !snappy_plausible(op.block + levels, size_t(op.got - levels), int64_t(h.usize) - levels))
+      if (dev && m.codec == PQH_CODEC_SNAPPY && !snappy_plausible(op.block + levels, size_t(op.got - levels), int64_t(h.usize) - levels))
         return PQH_ERR_DECOMPRESS;
       op.levels = levels;
       op.raw = dev;
@@ -454,7 +457,7 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
 // Materialise one planned page: host codecs -> its image at `img`; device codecs -> its source
 // bytes at `src` (compressed SNAPPY, or the decompressed image of another codec) + its codec page.
 void materialise(const ChunkPlan& w, PageOp& op, uint8_t* img, uint8_t* src) {
-  if (op.raw) {  // SNAPPY for the device: raw levels + compressed values, as stored
+  if (op.raw) {  // SNAPPY / GZIP for the device: raw levels + compressed values, as stored
     memcpy(src + op.src_off, op.block, size_t(op.got));
     return;
   }
@@ -586,14 +589,17 @@ int file_load(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const
     fprintf(stderr, "[walk] %s %.4f s\n", what, std::chrono::duration<double>(t - tw).count());
     tw = t;
   };
-  // device codecs only when some selected chunk is SNAPPY (otherwise the plain layout)
+  // device codecs only when some selected chunk has a codec the flags put on the device
+  // (otherwise the plain layout)
   bool dev = false;
-  if (flags & PQH_LOAD_DEVICE_SNAPPY)
+  if (flags & (PQH_LOAD_DEVICE_SNAPPY | PQH_LOAD_DEVICE_GZIP))
     for (int32_t rg = rg_begin; rg < rg_end && !dev; rg++)
       for (int32_t i = 0; i < num_columns && !dev; i++) {
         const RowGroupMeta& g = f->rgs[size_t(rg)];
-        dev = size_t(columns[i]) < g.chunks.size() && g.chunks[size_t(columns[i])].has_meta &&
-              g.chunks[size_t(columns[i])].codec == PQH_CODEC_SNAPPY;
+        if (size_t(columns[i]) >= g.chunks.size() || !g.chunks[size_t(columns[i])].has_meta) continue;
+        const int32_t c = g.chunks[size_t(columns[i])].codec;
+        dev = (c == PQH_CODEC_SNAPPY && (flags & PQH_LOAD_DEVICE_SNAPPY)) ||
+              (c == PQH_CODEC_GZIP && (flags & PQH_LOAD_DEVICE_GZIP));
       }
   int nt = int(std::thread::hardware_concurrency());
   if (nt > 16) nt = 16;
@@ -619,7 +625,7 @@ int file_load(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const
       w.chunk.host_status = PQH_ERR_SCHEMA;
       return;
     }
-    plan_chunk(f, f->columns[size_t(ci)], g.chunks[size_t(ci)], validate_crc, dev, w);
+    plan_chunk(f, f->columns[size_t(ci)], g.chunks[size_t(ci)], validate_crc, dev, flags, w);
   });
   lap("plan");
   // layout: chunk areas back to back (64-aligned); the payload is the images (host codecs) or the
@@ -701,7 +707,7 @@ int file_load(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const
         cp.src_len = int32_t(op.src_len);
         cp.image_len = pg.image_len;
         cp.raw_len = op.raw ? int32_t(op.levels) : 0;
-        cp.codec = op.raw ? PQH_CODEC_SNAPPY : PQH_CODEC_UNCOMPRESSED;
+        cp.codec = op.raw ? w.codec : PQH_CODEC_UNCOMPRESSED;
         cp.chunk = ci;
         hb->codec_pages.push_back(cp);
       }

@@ -1069,6 +1069,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 #include "bytearray_impl.h"
 #include "nest_impl.h"
 #include "snappy_impl.h"
+#include "gzip_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
@@ -1173,6 +1174,13 @@ hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* 
                          hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_snappy, dim3(n), dim3(256), 0, s, pages, src, dst, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_gzip(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
+                       hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gzip, dim3(n), dim3(256), 0, s, pages, src, dst, status);
   return hipGetLastError();
 }
 

@@ -34,6 +34,9 @@ hipError_t launch_hybrid_raw(const uint8_t* stream, int64_t len, int32_t width, 
 // Device codecs: one wave per page rebuilding its image from its (SNAPPY) source bytes.
 hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                          hipStream_t s);
+// GZIP pages of the same table (one workgroup per page; the other pages' workgroups exit at once).
+hipError_t launch_gzip(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
+                       hipStream_t s);
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.

@@ -76,6 +76,128 @@ __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
   return incl - x;
 }
 
+// ---- Batch resolution shared by the device codecs (k_snappy, k_gzip).  A batch is up to kSnapOut
+// output bytes made of elements (eout[e] = start, batch-relative; eout[nE] = the batch size).
+constexpr int kPer = kSnapOut / kBlock;  // 32 output bytes per thread: b = i * kBlock + tid
+
+// Output byte -> element: start markers, then a max-scan (element ids rise with output).
+template <class L>
+__device__ __forceinline__ void batch_emap(L& E, int32_t nE) {
+  const int tid = threadIdx.x;
+  {  // every thread owns 32 consecutive entries (64 bytes: four 16-byte LDS accesses)
+    uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++) m4[k] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  for (int e = tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
+  __syncthreads();
+  {
+    uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
+    uint32_t wv[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 x = m4[k];
+      wv[4 * k] = x.x;
+      wv[4 * k + 1] = x.y;
+      wv[4 * k + 2] = x.z;
+      wv[4 * k + 3] = x.w;
+    }
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
+      mx = a > mx ? a : mx;
+      mx = c > mx ? c : mx;
+    }
+    int32_t incl = int32_t(mx);  // inclusive max over the threads before
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(incl, o, 64);
+      if ((tid & 63) >= o) incl = y > incl ? y : incl;
+    }
+    if ((tid & 63) == 63) E.wmax[tid >> 6] = incl;
+    __syncthreads();
+    int32_t runv = __shfl_up(incl, 1, 64);
+    if ((tid & 63) == 0) runv = 0;
+    for (int w8 = 0; w8 < (tid >> 6); w8++) runv = E.wmax[w8] > runv ? E.wmax[w8] : runv;
+    uint32_t run = uint32_t(runv);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
+      run = a > run ? a : run;
+      a = run;
+      run = c > run ? c : run;
+      c = run;
+      wv[k] = a | (c << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
+  }
+  __syncthreads();
+}
+
+// Pointer jumping over the batch (ptr[i] >= 0: byte b points at an earlier byte of the batch;
+// val[i]: the byte when known), then the batch to HBM at o: bytes until o is 16-byte aligned, then
+// 16-byte stores.
+template <class L>
+__device__ __forceinline__ void batch_jump_store(L& E, int32_t T, int16_t (&ptr)[kPer], uint8_t (&val)[kPer], uint8_t* o) {
+  const int tid = threadIdx.x;
+  __syncthreads();  // emap no longer read: it becomes the pointer array
+  int16_t* P = reinterpret_cast<int16_t*>(E.emap);
+#pragma unroll
+  for (int i = 0; i < kPer; i++) {
+    const int32_t b = i * kBlock + tid;
+    if (b < T) {
+      P[b] = ptr[i];
+      E.out[b] = val[i];
+    }
+  }
+  __syncthreads();
+  for (;;) {
+    // read half: a pointer to a resolved byte takes its value, otherwise jumps to its target's pointer
+    int pending = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      if (ptr[i] < 0) continue;
+      const int16_t q = P[ptr[i]];
+      if (q < 0) val[i] = E.out[ptr[i]];
+      else pending = 1;
+      ptr[i] = q;
+    }
+    const int more = __syncthreads_or(pending);
+    // write half
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const int32_t b = i * kBlock + tid;
+      if (b < T) {
+        P[b] = ptr[i];
+        E.out[b] = val[i];
+      }
+    }
+    __syncthreads();
+    if (!more) break;
+  }
+  // ---- the batch to HBM: bytes until dst is 16-byte aligned, then 16-byte stores
+  {
+    const int32_t head0 = int32_t((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
+    const int32_t head = head0 < T ? head0 : T;
+    if (tid < head) o[tid] = E.out[tid];
+    const int32_t units = (T - head) >> 4;
+    for (int32_t u = tid; u < units; u += kBlock) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int32_t x = head + 16 * u + 4 * q;
+        w[q] = uint32_t(E.out[x]) | (uint32_t(E.out[x + 1]) << 8) | (uint32_t(E.out[x + 2]) << 16) |
+               (uint32_t(E.out[x + 3]) << 24);
+      }
+      *reinterpret_cast<uint4*>(o + head + 16 * u) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    const int32_t done = head + units * 16;
+    if (tid < T - done) o[done + tid] = E.out[done + tid];
+  }
+}
+
 // Wave 0: the elements of one batch from block position p (the stage holds [a0, ...)), output
 // starting at d.  Results in E (nE, bend, p_next, bad, bulk_*).
 // Every position / count here is wave-uniform; readfirstlane makes that visible to the compiler so
@@ -263,61 +385,10 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
     p = uni(E.p_next);
     continue;
 #endif
-    // ---- output byte -> element: start markers, then a max-scan (element ids rise with output)
-    {  // every thread owns 32 consecutive entries (64 bytes: four 16-byte LDS accesses)
-      uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
-#pragma unroll
-      for (int k = 0; k < 4; k++) m4[k] = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    for (int e = tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
-    __syncthreads();
-    {
-      uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
-      uint32_t wv[16];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint4 x = m4[k];
-        wv[4 * k] = x.x;
-        wv[4 * k + 1] = x.y;
-        wv[4 * k + 2] = x.z;
-        wv[4 * k + 3] = x.w;
-      }
-      uint32_t mx = 0;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
-        mx = a > mx ? a : mx;
-        mx = c > mx ? c : mx;
-      }
-      int32_t incl = int32_t(mx);  // inclusive max over the threads before
-      for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(incl, o, 64);
-        if ((tid & 63) >= o) incl = y > incl ? y : incl;
-      }
-      if ((tid & 63) == 63) E.wmax[tid >> 6] = incl;
-      __syncthreads();
-      int32_t runv = __shfl_up(incl, 1, 64);
-      if ((tid & 63) == 0) runv = 0;
-      for (int w8 = 0; w8 < (tid >> 6); w8++) runv = E.wmax[w8] > runv ? E.wmax[w8] : runv;
-      uint32_t run = uint32_t(runv);
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
-        run = a > run ? a : run;
-        a = run;
-        run = c > run ? c : run;
-        c = run;
-        wv[k] = a | (c << 16);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
-    }
-    __syncthreads();
+    batch_emap(E, nE);
     // ---- the batch's bytes.  Each byte is either known at once (a literal byte: from the stage or
     // HBM; a copy byte whose source precedes the batch: read back from HBM) or points at an earlier
     // byte of the batch; pointer jumping then resolves every chain in O(log length) rounds.
-    constexpr int kPer = kSnapOut / kBlock;  // 32 bytes per thread: b = i * kBlock + tid
     const int32_t s_lo = a0, s_hi = a0 + kSnapStage + 96;
     int16_t ptr[kPer];
     uint8_t val[kPer];
@@ -358,61 +429,7 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
       for (int j = 0; j < 8; j++)  // the HBM reads of 8 bytes in flight together
         if (from[j]) val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
     }
-    __syncthreads();  // emap no longer read: it becomes the pointer array
-    int16_t* P = reinterpret_cast<int16_t*>(E.emap);
-#pragma unroll
-    for (int i = 0; i < kPer; i++) {
-      const int32_t b = i * kBlock + tid;
-      if (b < T) {
-        P[b] = ptr[i];
-        E.out[b] = val[i];
-      }
-    }
-    __syncthreads();
-    for (;;) {
-      // read half: a pointer to a resolved byte takes its value, otherwise jumps to its target's pointer
-      int pending = 0;
-#pragma unroll
-      for (int i = 0; i < kPer; i++) {
-        if (ptr[i] < 0) continue;
-        const int16_t q = P[ptr[i]];
-        if (q < 0) val[i] = E.out[ptr[i]];
-        else pending = 1;
-        ptr[i] = q;
-      }
-      const int more = __syncthreads_or(pending);
-      // write half
-#pragma unroll
-      for (int i = 0; i < kPer; i++) {
-        const int32_t b = i * kBlock + tid;
-        if (b < T) {
-          P[b] = ptr[i];
-          E.out[b] = val[i];
-        }
-      }
-      __syncthreads();
-      if (!more) break;
-    }
-    // ---- the batch to HBM: bytes until dst is 16-byte aligned, then 16-byte stores
-    {
-      uint8_t* o = dst + d;
-      const int32_t head0 = int32_t((16 - (reinterpret_cast<uintptr_t>(o) & 15)) & 15);
-      const int32_t head = head0 < T ? head0 : T;
-      if (tid < head) o[tid] = E.out[tid];
-      const int32_t units = (T - head) >> 4;
-      for (int32_t u = tid; u < units; u += kBlock) {
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int32_t x = head + 16 * u + 4 * q;
-          w[q] = uint32_t(E.out[x]) | (uint32_t(E.out[x + 1]) << 8) | (uint32_t(E.out[x + 2]) << 16) |
-                 (uint32_t(E.out[x + 3]) << 24);
-        }
-        *reinterpret_cast<uint4*>(o + head + 16 * u) = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      const int32_t done = head + units * 16;
-      if (tid < T - done) o[done + tid] = E.out[done + tid];
-    }
+    batch_jump_store(E, T, ptr, val, dst + d);
     __syncthreads();  // this batch's bytes are visible to the next batches' reads
     d += T;
     p = uni(E.p_next);
@@ -420,11 +437,13 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
   return d == total ? PQH_OK : PQH_ERR_DECOMPRESS;
 }
 
-// One workgroup per page: its image rebuilt at image_offset from its source bytes (codec 0: copied).
+// One workgroup per page: its image rebuilt at image_offset from its source bytes (codec 0: copied;
+// GZIP pages: k_gzip).
 __global__ __launch_bounds__(256) void k_snappy(const pqh_codec_page* cps, const uint8_t* src_all, uint8_t* dst_all,
                                                 int32_t* status) {
   __shared__ SnapLds E;
   const pqh_codec_page cp = cps[blockIdx.x];
+  if (cp.codec == PQH_CODEC_GZIP) return;  // k_gzip's
   const uint8_t* src = src_all + cp.src_offset;
   uint8_t* dst = dst_all + cp.image_offset;
   int rc = PQH_OK;

@@ -73,6 +73,7 @@ class CodecPage(ctypes.Structure):
 
 
 LOAD_DEVICE_SNAPPY = 1
+LOAD_DEVICE_GZIP = 2
 
 
 class SchemaElement(ctypes.Structure):
@@ -231,7 +232,8 @@ class Context:
         self.check(self.L.pqh_memcpy_h2d_pinned_async(self.h, dst, pinned_ptr, n))
 
     def decompress_pages(self, pages, d_src, d_dst):
-        """k_snappy on its own: rebuild `pages` (CodecPage list) from d_src into d_dst; statuses."""
+        """The device codecs on their own (k_snappy, k_gzip): rebuild `pages` (CodecPage list) from
+        d_src into d_dst; statuses."""
         arr = (CodecPage * max(1, len(pages)))(*pages)
         st = (i32 * max(1, len(pages)))()
         self.check(self.L.pqh_decompress_pages(self.h, arr, len(pages), d_src, d_dst, st))
@@ -391,14 +393,16 @@ class File:
         """readRowGroupData's checks of a column before its pages (pqh_file_chunk_check): a status."""
         return self.L.pqh_file_chunk_check(self.h, rg, column, int(selected))
 
-    def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False, ctx=None):
-        """Walk the pages of `columns` in row groups [rg_begin, rg_end).  device_snappy: SNAPPY
-        pages stay compressed (the batch decompresses them on the device, k_snappy).  ctx: the
+    def load(self, rg_begin, rg_end, columns, validate_crc=False, device_snappy=False, ctx=None,
+             device_gzip=False):
+        """Walk the pages of `columns` in row groups [rg_begin, rg_end).  device_snappy /
+        device_gzip: SNAPPY / GZIP pages stay compressed (the batch decompresses them on the
+        device, k_snappy / k_gzip).  ctx: the
         payload is written into pinned memory from the context's pool (pqh_file_load_pinned), which
         Batch.staged adopts without a copy."""
         cols = (i32 * len(columns))(*columns)
         h = vp()
-        flags = LOAD_DEVICE_SNAPPY if device_snappy else 0
+        flags = (LOAD_DEVICE_SNAPPY if device_snappy else 0) | (LOAD_DEVICE_GZIP if device_gzip else 0)
         if ctx is not None:
             rc = self.L.pqh_file_load_pinned(ctx.h, self.h, rg_begin, rg_end, cols, len(columns), int(validate_crc),
                                              flags, ctypes.byref(h))

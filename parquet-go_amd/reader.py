@@ -118,14 +118,15 @@ class ColumnData:
 
 
 def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, return_batch=False, staged_runs=0,
-                  device_snappy=False):
+                  device_snappy=False, device_gzip=False):
     """Walk (host) and decode (GPU) the chunks of `columns` in row groups [rg_begin, rg_end).
 
     staged_runs > 0: end-to-end mode -- the page images stay in pinned host memory and each of the
     `staged_runs` runs copies them to HBM on the copy stream ahead of the decode.
-    device_snappy: SNAPPY pages are decompressed on the device (k_snappy) instead of the host.
+    device_snappy / device_gzip: SNAPPY / GZIP pages are decompressed on the device (k_snappy /
+    k_gzip) instead of the host.
     Returns a list of ColumnData in (row group, column) order."""
-    hb = file.load(rg_begin, rg_end, columns, validate_crc, device_snappy=device_snappy)
+    hb = file.load(rg_begin, rg_end, columns, validate_crc, device_snappy=device_snappy, device_gzip=device_gzip)
     if staged_runs:
         batch = native.Batch.staged(ctx, hb)
         for _ in range(staged_runs):

@@ -88,7 +88,7 @@ def flat_c2_like(n=40000, v2=True, seed=11):
     return W.flat(cols, 10000, v2=v2, max_page_size=32 * 1024)
 
 
-def nested_list_map(n=5000, v2=False, seed=30):
+def nested_list_map(n=5000, v2=False, seed=30, codec=0):
     """optional LIST<optional int64> + optional MAP<string, optional int32> (C4 shape)."""
     rng = np.random.default_rng(seed)
     # LIST: levels for path l.list.element: maxD 3, maxR 1
@@ -140,7 +140,7 @@ def nested_list_map(n=5000, v2=False, seed=30):
         W.Column(W.INT32, np.array(mv, dtype=np.int32), def_levels=md_v, rep_levels=mr_k, use_dict=False),
     ]
     rg = [n // 2, n - n // 2]
-    return W.write(schema, cols, rg, v2=v2, max_page_size=16 * 1024)
+    return W.write(schema, cols, rg, v2=v2, codec=codec, max_page_size=16 * 1024)
 
 
 def pyarrow_file(n=20000, version="1.0", compression="NONE", seed=1, page=4096):

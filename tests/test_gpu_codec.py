@@ -1,4 +1,4 @@
-"""Device SNAPPY (k_snappy) against the oracle.
+"""Device SNAPPY and GZIP (k_snappy / k_gzip) against the oracle.
 
 * pqh_decompress_pages on its own: hand-built blocks covering every element kind, bulk literals,
   batch-cap boundaries and long chains of tiny overlapping copies; pyarrow-compressed data of
@@ -7,6 +7,10 @@
 * whole files decoded with the pages of SNAPPY chunks decompressed on the device (plain batches and
   staged end-to-end batches) must equal the oracle's decode chunk by chunk, bit for bit.
 * a chunk whose compressed page is corrupt reports PQH_ERR_DECOMPRESS, as the host walker does.
+* GZIP: every stream of tests/gzip_blocks.py (valid zlib streams of every level / strategy / flush,
+  multistream, header fields, hand-built blocks, each error class, seeded mutants) through k_gzip
+  against oracle.gzip_decode (Go's compress/gzip reader restated, compress.go:64-77), status and
+  bytes; whole GZIP files decoded with device_gzip against the oracle chunk by chunk.
 """
 import numpy as np
 import pyarrow as pa
@@ -27,7 +31,7 @@ def ctx(pq):
     return pq.native.Context(0)
 
 
-def _device_decompress(pq, ctx, blocks, sizes):
+def _device_decompress(pq, ctx, blocks, sizes, codec=O.SNAPPY):
     """Every block as one codec page; returns [(status, bytes)]."""
     N = pq.native
     src, pages, soff, ioff = [], [], 0, 0
@@ -36,7 +40,7 @@ def _device_decompress(pq, ctx, blocks, sizes):
         src.append(b"\0" * pad + blk)
         soff += pad
         ioff = (ioff + 63) & ~63
-        pages.append(N.CodecPage(soff, ioff, len(blk), size, 0, O.SNAPPY, 0, 0))
+        pages.append(N.CodecPage(soff, ioff, len(blk), size, 0, codec, 0, 0))
         soff += len(blk)
         ioff += size
     s = np.frombuffer(b"".join(src) + b"\0" * N.PAYLOAD_PAD, np.uint8).copy()
@@ -164,3 +168,98 @@ def test_device_snappy_corrupt_page_fails_its_chunk(pq, ctx):
         b.close()
         hb.close()
     assert failed >= 3, (failed, ok)
+
+
+def _gzip_check(pq, ctx, cases):
+    import test_gzip_codec as TG
+
+    got = _device_decompress(pq, ctx, [c[1] for c in cases], [c[2] for c in cases], codec=O.GZIP)
+    ok = bad = 0
+    for (name, s, size), (st, raw) in zip(cases, got):
+        est, eraw = TG.expected(s, size)
+        assert st == est, f"{name}: device status {st} vs oracle {est}"
+        if est == 0:
+            assert raw == eraw, f"{name}: bytes differ"
+        ok += est == 0
+        bad += est != 0
+    return ok, bad
+
+
+def test_gzip_valid_streams(pq, ctx):
+    import test_gzip_codec as TG
+
+    cases = [c for c in TG.all_cases() if "mut" not in c[0]]
+    ok, bad = _gzip_check(pq, ctx, cases)
+    assert ok > 60 and bad > 25, (ok, bad)
+
+
+def test_gzip_mutants(pq, ctx):
+    import gzip_blocks as G
+
+    valid = [(n, s, len(O.gzip_decode(s))) for n, s, _ in G.valid_cases()]
+    ok, bad = _gzip_check(pq, ctx, G.mutants(valid, seed=11, per=9))
+    assert bad > 100, (ok, bad)
+
+
+def _gzip_files():
+    yield "writer-v1", fixtures.flat_all_types(n=8000, v2=False, codec=O.GZIP, page=16 * 1024, rows_per_group=4000)
+    yield "writer-v2", fixtures.flat_all_types(n=8000, v2=True, codec=O.GZIP, page=16 * 1024, rows_per_group=4000)
+    yield "nested", fixtures.nested_list_map(n=3000, v2=True, codec=O.GZIP)
+    yield "pyarrow-v1", fixtures.pyarrow_file(n=20000, version="1.0", compression="GZIP")
+    yield "pyarrow-v2", fixtures.pyarrow_file(n=20000, version="2.0", compression="GZIP")
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_device_gzip_files(pq, ctx, staged):
+    checked = gz = 0
+    for name, data in _gzip_files():
+        f = pq.native.File(data)
+        ncols = len(f.columns())
+        hb = f.load(0, f.num_row_groups, list(range(ncols)), device_gzip=True)
+        gz += sum(c.codec == O.GZIP for c in hb.codec_pages())
+        hb.close()
+        res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(ncols)), device_gzip=True,
+                                      staged_runs=2 if staged else 0)
+        fr = O.FileReader(data)
+        for k, col in enumerate(res):
+            rg, ci = divmod(k, ncols)
+            assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"{name} rg{rg} {col.path}")
+            checked += 1
+    assert checked > 40 and gz > 50, (checked, gz)
+
+
+def test_device_gzip_corrupt_page_fails_its_chunk(pq, ctx):
+    """A corrupted GZIP page fails its chunk with DECOMPRESS on the device exactly when the
+    reference's reader rejects the block; the other chunk decodes."""
+    import test_gzip_codec as TG
+
+    W = pq.writer
+    rng = np.random.default_rng(4)
+    vals = np.repeat(rng.integers(0, 1 << 40, 3000), 8)
+    data = W.flat([("v", W.Column(W.INT64, vals, use_dict=False), W.REQUIRED),
+                   ("w", W.Column(W.INT64, vals[::-1].copy(), use_dict=False), W.REQUIRED)], len(vals),
+                  codec=O.GZIP, max_page_size=8 * 1024)
+    f = pq.native.File(data)
+    failed = ok = 0
+    for trial in range(12):
+        hb = f.load(0, 1, [0, 1], device_gzip=True)
+        cps = hb.codec_pages()
+        src = hb.payload()
+        victim = cps[int(rng.integers(0, len(cps)))]
+        i = int(rng.integers(victim.src_offset + 10, victim.src_offset + victim.src_len))
+        src[i] ^= 1 << int(rng.integers(0, 8))
+        blk = bytes(src[victim.src_offset:victim.src_offset + victim.src_len])
+        st, _ = TG.expected(blk, victim.image_len)
+        b = pq.native.Batch.from_host(ctx, hb)
+        b.run()
+        b.sync()
+        out = b.chunk_out(victim.chunk)
+        if st:
+            assert out.status == DECOMPRESS, f"trial {trial}: device status {out.status}"
+            failed += 1
+        else:
+            ok += 1
+        assert b.chunk_out(1 - victim.chunk).status == 0
+        b.close()
+        hb.close()
+    assert failed >= 6, (failed, ok)
