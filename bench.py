@@ -270,6 +270,8 @@ def main():
     ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "c5z"],
                     help="default: c2 on one GPU, c3 (strong scaling) on several")
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
+    ap.add_argument("--codec", default=None, choices=["snappy", "gzip"],
+                    help="c5 / c5z: the page codec (default SNAPPY, as configs[4] names)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
@@ -303,6 +305,11 @@ def main():
     kw = {}
     if args.rows:
         kw["rows"] = args.rows
+    if args.codec == "gzip" and args.workload in ("c5", "c5z"):
+        from parquet_go_amd import writer as W
+
+        kw["codec"] = W.GZIP
+        desc = desc.replace("SNAPPY", "GZIP") + " (--codec gzip)"
     # C3 (BASELINE configs[2]: 128 row groups of ONE file sharded across 1/2/4/8 GPUs) is strong
     # scaling: every rank opens the same file and decodes its contiguous block of row groups
     # (shard.row_group_block).  The other workloads give every rank its own file (weak scaling).
@@ -435,8 +442,8 @@ def main():
     # End-to-end: one staged batch per row-group range holding its decompressed
     # page images in pinned host memory; every pass copies each range to HBM on the copy stream
     # while the previous range decodes on the compute stream.  Host decompression excluded.
-    # device_snappy: the ranges hold the pages of SNAPPY chunks still compressed,
-    # so H2D moves compressed bytes and every decode starts with k_snappy.
+    # device codecs: the ranges hold the pages of SNAPPY / GZIP chunks still
+    # compressed, so H2D moves compressed bytes and every decode starts with k_snappy / k_gzip.
     def e2e_pass(device_snappy):
         # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
         # >= 1/16 of the payload each
@@ -453,7 +460,7 @@ def main():
             for g in range(groups):
                 t0 = time.perf_counter()
                 hbr = f.load(rg0 + cuts[g], rg0 + cuts[g + 1], list(range(ncols)), device_snappy=device_snappy,
-                             ctx=ctx)
+                             device_gzip=device_snappy, ctx=ctx)
                 walk += time.perf_counter() - t0
                 payload += hbr.payload_bytes
                 images += hbr.image_bytes or hbr.payload_bytes
@@ -484,7 +491,7 @@ def main():
         barrier_sync()
         el = time.perf_counter() - t0
         el, total = pkg.shard.reduce_step(el, written, device=f"cuda:{local}" if world > 1 else None)
-        out = {"mode": ("pinned H2D of the COMPRESSED pages, then k_snappy + decode of all of them in one batch"
+        out = {"mode": ("pinned H2D of the COMPRESSED pages, then k_snappy / k_gzip + decode of all of them in one batch"
                         if device_snappy else
                         "pinned H2D on a copy stream, overlapped per row group with decode; host decompression excluded"),
                "payload_bytes_per_gpu": payload, "image_bytes_per_gpu": images, "staged_batches": groups,
@@ -507,13 +514,14 @@ def main():
         e2e = e2e_pass(False)
         e2e["unstaged_h2d_s"] = round(h2d_s, 4)
         e2e["pinned_h2d_ceiling_gbps"] = pinned_h2d_rate(ctx, native)
-        probe = f.load(rg0, rg0 + 1, list(range(ncols)), device_snappy=True)
-        has_snappy = len(probe.codec_pages()) > 0
+        probe = f.load(rg0, rg0 + 1, list(range(ncols)), device_snappy=True, device_gzip=True)
+        dev_codecs = {c.codec for c in probe.codec_pages()} - {0}
         probe.close()
-        if has_snappy:
+        dev_kernel = "k_gzip" if 2 in dev_codecs else "k_snappy"
+        if dev_codecs:
             e2e_dev = e2e_pass(True)
-            # k_snappy alone: HBM-resident batch of the rank's row groups, profiled runs
-            hd = f.load(rg0, rg1, list(range(ncols)), device_snappy=True)
+            # the codec kernel alone: HBM-resident batch of the rank's row groups, profiled runs
+            hd = f.load(rg0, rg1, list(range(ncols)), device_snappy=True, device_gzip=True)
             bd = native.Batch.from_host(ctx, hd)
             bd.run()
             bd.sync()
@@ -522,11 +530,11 @@ def main():
             for _ in range(3):
                 bd.run()
             bd.sync()
-            ks = [s for s in bd.kernel_stats() if s.name.decode() == "k_snappy" and s.launches]
+            ks = [s for s in bd.kernel_stats() if s.name.decode() == dev_kernel and s.launches]
             ctx.set_profile(False)
             if ks:
                 ms = ks[0].total_ms / ks[0].launches
-                e2e_dev["k_snappy"] = {"avg_ms": round(ms, 4), "pages": ks[0].work_items,
+                e2e_dev[dev_kernel] = {"avg_ms": round(ms, 4), "pages": ks[0].work_items,
                                        "compressed_bytes": hd.payload_bytes, "image_bytes": hd.image_bytes,
                                        "decompressed_gbps": round(hd.image_bytes / (ms * 1e-3) / 1e9, 1)}
             bd.close()
@@ -567,7 +575,7 @@ def main():
             "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 3),
                      "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
             "e2e": e2e,
-            "e2e_device_snappy": e2e_dev,
+            ("e2e_device_gzip" if args.codec == "gzip" else "e2e_device_snappy"): e2e_dev,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
             "cpu_comparator_pyarrow": cpu_pa,

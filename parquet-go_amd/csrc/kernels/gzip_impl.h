@@ -64,13 +64,35 @@ struct __attribute__((aligned(16))) GzLds {
   uint16_t lens[320];             // code lengths of the current dynamic block
   uint16_t work[320];             // symbols sorted by code length (table construction)
   uint16_t cnt[16], offs[16];
+  int32_t tnext[16], toffs[17];   // canonical first code / sorted offset per length (gz_table_wave)
+  uint16_t gofs[320];             // long-code sub-tables (gz_table_wave): offset and index bits per group
+  uint8_t gbits[320];
+  int32_t nlen, ndist, tab_kind;
   int32_t wmax[4];
   // decoder state between batches (thread 0 writes, everyone reads after a barrier)
   int64_t pbit;                   // input bit position of the next symbol / header
   int32_t mode, final_blk, stored_left, members, lbits, dbits, ms, fixed_ready;
   uint32_t tcrc, tsize;
   int32_t nE, bend, bad, bulk_len, bulk_src, member_end, done, progress;
+  // Huffman stage (gz_huff_stage): per thread its entry / exit bit, output bytes, back-references,
+  // state (0 ok, 1 end of block, 2 invalid code); the first ended thread; the batch cut
+  int64_t hf[kBlock], hx[kBlock];
+  int32_t ho[kBlock], hk[kBlock];
+  uint8_t hst[kBlock];
+  int32_t wsum[8];
+  int32_t hend, hcut, hcut_out, hcut_tok;
+  int64_t hcut_pos;
+#ifdef PQH_GZIP_PROF  // timing experiments: clock64() per phase (wave 0), printed for page 0
+  uint64_t prof[12];
+#endif
 };
+#ifdef PQH_GZIP_PROF
+#define GZ_CLK(v) const uint64_t v = clock64()
+#define GZ_ADD(i, x) (E.prof[i] += (x))
+#else
+#define GZ_CLK(v)
+#define GZ_ADD(i, x)
+#endif
 
 __device__ __forceinline__ uint32_t gz_entry(uint32_t op, uint32_t bits, uint32_t val) {
   return op | (bits << 8) | (val << 16);
@@ -271,11 +293,12 @@ __device__ __forceinline__ uint32_t gz_decode(const uint32_t* tab, int32_t rbits
   return e;
 }
 
-// A dynamic block's header (RFC 1951 §3.2.7): the code-length code, then the literal/length and
-// distance code lengths, then both tables.  False where zlib reports "too many length or distance
-// symbols", "invalid code lengths set", "invalid bit length repeat", "missing end-of-block",
-// "invalid literal/lengths set" or "invalid distances set".
-__device__ bool gz_dynamic(GzLds& E, GzBits& R, int32_t a0) {
+// A dynamic block's header (RFC 1951 §3.2.7), lane 0: the code-length code, then the
+// literal/length and distance code lengths into E.lens (E.nlen, E.ndist); the wave then builds both
+// tables (gz_build_tables: "invalid literal/lengths set", "invalid distances set").  False where
+// zlib reports "too many length or distance symbols", "invalid code lengths set", "invalid bit
+// length repeat" or "missing end-of-block".
+__device__ __forceinline__ bool gz_dynamic(GzLds& E, GzBits& R, int32_t a0) {
   gz_refill(E, R, a0);
   const int nlen = int(R.hold & 31) + 257, ndist = int((R.hold >> 5) & 31) + 1, ncode = int((R.hold >> 10) & 15) + 4;
   gz_drop(R, 14);
@@ -322,245 +345,684 @@ __device__ bool gz_dynamic(GzLds& E, GzBits& R, int32_t a0) {
     while (rep--) E.lens[i++] = v;
   }
   if (E.lens[256] == 0) return false;
-  E.lbits = 9;
-  if (!gz_table(E, 1, E.lens, nlen, E.lcode, &E.lbits)) return false;
-  E.dbits = 6;
-  if (!gz_table(E, 2, E.lens + nlen, ndist, E.dcode, &E.dbits)) return false;
-  E.fixed_ready = 0;
+  E.nlen = nlen;
+  E.ndist = ndist;
   return true;
 }
 
-__device__ bool gz_fixed(GzLds& E) {
-  if (E.fixed_ready) return true;
-  for (int s = 0; s < 288; s++) E.lens[s] = uint16_t(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
-  E.lbits = 9;
-  if (!gz_table(E, 1, E.lens, 288, E.lcode, &E.lbits)) return false;
-  for (int s = 0; s < 32; s++) E.lens[s] = 5;
-  E.dbits = 5;
-  if (!gz_table(E, 2, E.lens, 32, E.dcode, &E.dbits)) return false;
-  E.fixed_ready = 1;
+__device__ __forceinline__ uint32_t gz_sym_entry(int type, int s, uint32_t bits) {
+  if (type == 0) return gz_entry(0, bits, uint32_t(s));
+  if (type == 1) {
+    if (s < 256) return gz_entry(0, bits, uint32_t(s));
+    if (s == 256) return gz_entry(96, bits, 0);
+    return gz_entry(kGzLOp[s - 257], bits, kGzLBase[s - 257]);
+  }
+  return gz_entry(kGzDOp[s], bits, kGzDBase[s]);
+}
+
+// A long code's canonical value, and its root-prefix key, from its sorted position i.
+__device__ __forceinline__ uint32_t gz_long_code(const GzLds& E, const uint16_t* lens, int i, int* len) {
+  const int l = lens[E.work[i]];
+  *len = l;
+  return uint32_t(E.tnext[l] + (i - E.toffs[l]));
+}
+
+__device__ __forceinline__ uint32_t gz_long_key(const GzLds& E, const uint16_t* lens, int i, int root) {
+  int l;
+  const uint32_t c = gz_long_code(E, lens, i, &l);
+  return c >> (l - root);
+}
+
+// gz_table's tables built by wave 0 in parallel: the same validity rules and the same decoding.  A
+// canonical code's long codes sharing a root prefix are contiguous in (length, symbol) order and
+// exactly fill a sub-table of (their longest length - root) index bits — the size zlib's
+// construction picks for a complete code.  Ranks by ballots; each short code replicated over the
+// root table by its own lane; sub-table offsets by a scan over the groups of long codes.
+__device__ bool gz_table_wave(GzLds& E, int type, const uint16_t* lens, int codes, uint32_t* table, int32_t root_req,
+                              int32_t* bits_out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1, upto = below | (1ull << lane);
+  const int nch = (codes + 63) >> 6;
+  int32_t cnt[16];
+#pragma unroll
+  for (int l = 0; l < 16; l++) cnt[l] = 0;
+  for (int c = 0; c < nch; c++) {
+    const int s = c * 64 + lane;
+    const int l = s < codes ? lens[s] : 0;
+#pragma unroll
+    for (int L = 1; L < 16; L++) cnt[L] += __popcll(__ballot(l == L));
+  }
+  int max = 15;
+  while (max >= 1 && cnt[max] == 0) max--;
+  int root = root_req > max ? max : root_req;
+  if (max == 0) {  // no codes: every entry invalid
+    if (lane == 0) {
+      table[0] = table[1] = gz_entry(64, 1, 0);
+      *bits_out = 1;
+    }
+    return true;
+  }
+  int min = 1;
+  while (min < max && cnt[min] == 0) min++;
+  if (root < min) root = min;
+  int left = 1;
+  for (int l = 1; l <= 15; l++) {
+    left = (left << 1) - cnt[l];
+    if (left < 0) return false;  // over-subscribed
+  }
+  if (left > 0 && (type == 0 || max != 1)) return false;  // incomplete
+  if (left > 0 && lane == 0) table[0] = table[1] = gz_entry(64, 1, 0);  // the single 1-bit code: one slot invalid
+  int32_t offs[17], next[16];
+  offs[0] = offs[1] = 0;
+  next[0] = 0;
+  int code = 0;
+#pragma unroll
+  for (int l = 1; l < 16; l++) {
+    offs[l + 1] = offs[l] + cnt[l];
+    code = (code + cnt[l - 1]) << 1;
+    next[l] = code;
+  }
+  if (lane < 16) {  // the same values for the dynamically indexed long-code passes
+    int32_t nv = 0, ov = 0;
+#pragma unroll
+    for (int l = 0; l < 16; l++)
+      if (lane == l) {
+        nv = next[l];
+        ov = offs[l];
+      }
+    E.tnext[lane] = nv;
+    E.toffs[lane] = ov;
+  }
+  // ranks, canonical codes, sorted order; short codes fill the root table
+  int32_t run[16];
+#pragma unroll
+  for (int l = 0; l < 16; l++) run[l] = 0;
+  const uint32_t rsize = 1u << root;
+  for (int c = 0; c < nch; c++) {
+    const int s = c * 64 + lane;
+    const int l = s < codes ? lens[s] : 0;
+    int rank = 0, nx = 0, of = 0;
+#pragma unroll
+    for (int L = 1; L < 16; L++) {
+      const uint64_t m = __ballot(l == L);
+      if (l == L) {
+        rank = run[L] + __popcll(m & below);
+        nx = next[L];
+        of = offs[L];
+      }
+      run[L] += __popcll(m);
+    }
+    if (l > 0) {
+      E.work[of + rank] = uint16_t(s);
+      if (l <= root) {
+        const uint32_t rev = __builtin_bitreverse32(uint32_t(nx + rank)) >> (32 - l);
+        const uint32_t ent = gz_sym_entry(type, s, uint32_t(l));
+        for (uint32_t j = rev; j < rsize; j += 1u << l) table[j] = ent;
+      }
+    }
+  }
+  if (max > root) {
+    // long codes: the sorted tail work[first, last); pass 1: groups' index bits and offsets
+    const int first = offs[root + 1], last = offs[16];
+    int gbase = 0, used = int(rsize);
+    for (int i0 = first; i0 < last; i0 += 64) {
+      const int i = i0 + lane;
+      const bool on = i < last;
+      bool start = false, end = false;
+      int l = 0;
+      if (on) {
+        const uint32_t key = gz_long_key(E, lens, i, root);
+        l = lens[E.work[i]];
+        start = i == first || gz_long_key(E, lens, i - 1, root) != key;
+        end = i == last - 1 || gz_long_key(E, lens, i + 1, root) != key;
+      }
+      const uint64_t sm = __ballot(start);
+      const int g = gbase + __popcll(sm & upto) - 1;
+      const uint32_t size = end ? (1u << (l - root)) : 0u;
+      const uint32_t incl = wave_incl_scan32(size);
+      if (end) {
+        E.gbits[g] = uint8_t(l - root);
+        E.gofs[g] = uint16_t(used + int(incl - size));
+      }
+      used += __builtin_amdgcn_readlane(int32_t(incl), 63);
+      gbase += __popcll(sm);
+    }
+    const int enough = type == 1 ? kGzEnoughL : kGzEnoughD;
+    if (type != 0 && used > enough) return false;
+    // pass 2: root links and sub-table entries
+    gbase = 0;
+    for (int i0 = first; i0 < last; i0 += 64) {
+      const int i = i0 + lane;
+      const bool on = i < last;
+      bool start = false;
+      int s = 0, l = 0;
+      uint32_t cv = 0;
+      if (on) {
+        s = E.work[i];
+        cv = gz_long_code(E, lens, i, &l);
+        start = i == first || gz_long_key(E, lens, i - 1, root) != (cv >> (l - root));
+      }
+      const uint64_t sm = __ballot(start);
+      const int g = gbase + __popcll(sm & upto) - 1;
+      gbase += __popcll(sm);
+      if (on) {
+        const uint32_t rev = __builtin_bitreverse32(cv) >> (32 - l);
+        const uint32_t sub = E.gbits[g], base = E.gofs[g];
+        if (start) table[rev & (rsize - 1)] = gz_entry(sub, uint32_t(root), base);
+        const uint32_t ent = gz_sym_entry(type, s, uint32_t(l - root));
+        for (uint32_t j = rev >> root; j < (1u << sub); j += 1u << (l - root)) table[base + j] = ent;
+      }
+    }
+  }
+  if (lane == 0) *bits_out = root;
   return true;
+}
+
+// Wave 0: the tables of the block whose header lane 0 just read (E.tab_kind 1 fixed, 2 dynamic).
+__device__ bool gz_build_tables(GzLds& E) {
+  const int lane = threadIdx.x & 63;
+  if (uni(E.tab_kind) == 1) {
+    if (uni(E.fixed_ready)) return true;
+    for (int s = lane; s < 320; s += 64) E.lens[s] = uint16_t(s >= 288 ? 5 : s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
+    const bool ok = gz_table_wave(E, 1, E.lens, 288, E.lcode, 9, &E.lbits) &&
+                    gz_table_wave(E, 2, E.lens + 288, 32, E.dcode, 6, &E.dbits);
+    if (lane == 0) E.fixed_ready = ok;
+    return ok;
+  }
+  const int32_t nlen = uni(E.nlen), ndist = uni(E.ndist);
+  if (lane == 0) E.fixed_ready = 0;
+  return gz_table_wave(E, 1, E.lens, nlen, E.lcode, 9, &E.lbits) &&
+         gz_table_wave(E, 2, E.lens + nlen, ndist, E.dcode, 6, &E.dbits);
 }
 
 enum : int32_t { kGzHeader = 0, kGzBlock = 1, kGzHuff = 2, kGzStored = 3, kGzTrailer = 4 };
 
-// Thread 0: the tokens of one batch from the state in E (input staged from a0), output from d.
-__device__ void gz_parse(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t d, int32_t total) {
+constexpr uint32_t kGzStop = 1, kGzBad = 2, kGzMemberEnd = 4, kGzDone = 8, kGzTables = 16;
+
+// Lane 0: one transition of the non-Huffman states (member header, block header, stored data,
+// trailer).  pos = the input bit position (byte aligned in the header / stored / trailer states);
+// T / k = the batch's output bytes / next token index (tokens start at 1).  Sets kGzStop to end the
+// batch here (restage, batch full, bulk copy), kGzBad on an error.
+__device__ void gz_serial(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t d, int32_t total, int32_t& mode,
+                          int64_t& pos, int32_t& T, int32_t& k, uint32_t& flags, int32_t& bulk_len, int32_t& bulk_src) {
   const int64_t nbits = int64_t(n) * 8;
-  const int32_t lim = a0 + kGzStage;  // the reader's next byte stays at or below this
-  int32_t mode = E.mode, k = 0, T = 0, bulk_len = 0, bulk_src = 0;
-  bool bad = false, member_end = false, done = false;
-  int64_t jump = -1;  // >= 0: the next batch starts at this bit (a position outside the stage)
-  const int64_t start = E.pbit;
-  GzBits R;
-  R.hold = 0;
-  R.nb = 0;
-  R.bp = 0;
-  bool live = false;  // R holds the position
+  const int32_t lim = a0 + kGzStage;
   if (mode == kGzHeader) {
-    jump = start;
-  } else {
-    gz_seek(E, R, start, a0);
-    live = true;
+    const int32_t p = int32_t(pos >> 3);
+    if (E.members > 0 && p == n) {
+      flags |= kGzDone;
+      return;
+    }
+    int32_t body;
+    if (!gz_header(E, src, n, p, &body)) {
+      flags |= kGzBad;
+      return;
+    }
+    E.ms = d + T;
+    mode = kGzBlock;
+    pos = int64_t(body) * 8;
+    if (body > lim - kGzHdrRoom) flags |= kGzStop;  // restage at the first block
+    return;
   }
-  int32_t run0 = -1;  // the open literal run's output start
-  auto close_run = [&]() {
-    if (run0 >= 0) {
-      E.eout[k] = run0;
-      E.elen[k] = T - run0;
-      E.etyp[k] = 0;
-      k++;
-      run0 = -1;
+  if (mode == kGzBlock) {
+    if ((pos >> 3) > lim - kGzHdrRoom) {  // restage: a dynamic header must fit the stage
+      flags |= kGzStop;
+      return;
     }
-  };
-  for (;;) {
-    if (mode == kGzHeader) {
-      const int32_t p = int32_t(jump >> 3);  // byte aligned
-      if (E.members > 0 && p == n) {
-        done = true;
-        break;
-      }
-      int32_t body;
-      if (!gz_header(E, src, n, p, &body)) {
-        bad = true;
-        break;
-      }
-      E.ms = d + T;
-      mode = kGzBlock;
-      jump = int64_t(body) * 8;
-      if (body > lim - kGzHdrRoom) break;  // restage at the first block
-      gz_seek(E, R, jump, a0);
-      live = true;
-      jump = -1;
-      continue;
-    }
-    if (mode == kGzBlock) {
-      if (R.bp > lim - kGzHdrRoom) break;  // restage: a dynamic header must fit the stage
+    GzBits R;
+    gz_seek(E, R, pos, a0);
+    gz_refill(E, R, a0);
+    E.final_blk = int32_t(R.hold & 1);
+    const int type = int((R.hold >> 1) & 3);
+    gz_drop(R, 3);
+    bool ok = true;
+    if (type == 0) {
+      gz_drop(R, R.nb & 7);  // to a byte boundary
       gz_refill(E, R, a0);
-      E.final_blk = int32_t(R.hold & 1);
-      const int type = int((R.hold >> 1) & 3);
-      gz_drop(R, 3);
-      if (type == 0) {
-        gz_drop(R, R.nb & 7);  // to a byte boundary
-        gz_refill(E, R, a0);
-        const uint32_t len = uint32_t(R.hold & 0xffff), nlen = uint32_t((R.hold >> 16) & 0xffff);
-        gz_drop(R, 32);
-        if (len != (~nlen & 0xffff)) bad = true;
-        E.stored_left = int32_t(len);
-        mode = kGzStored;
-      } else if (type == 1) {
-        if (!gz_fixed(E)) bad = true;
-        mode = kGzHuff;
-      } else if (type == 2) {
-        if (!gz_dynamic(E, R, a0)) bad = true;
-        mode = kGzHuff;
-      } else {
-        bad = true;
-      }
-      if (bad || gz_pos(R) > nbits) {
-        bad = true;
-        break;
-      }
-      continue;
+      const uint32_t len = uint32_t(R.hold & 0xffff), nlen = uint32_t((R.hold >> 16) & 0xffff);
+      gz_drop(R, 32);
+      ok = len == (~nlen & 0xffff);
+      E.stored_left = int32_t(len);
+      mode = kGzStored;
+    } else if (type == 1) {
+      E.tab_kind = 1;
+      flags |= kGzTables;
+      mode = kGzHuff;
+    } else if (type == 2) {
+      ok = gz_dynamic(E, R, a0);
+      E.tab_kind = 2;
+      flags |= kGzTables;
+      mode = kGzHuff;
+    } else {
+      ok = false;
     }
-    if (mode == kGzHuff) {
-      const uint32_t* lc = E.lcode;
-      const uint32_t* dc = E.dcode;
-      const int32_t lb = E.lbits, db = E.dbits;
-      const int32_t ms = E.ms;
-      bool eob = false;
-      for (;;) {
-        if (T > kSnapOut - 258 || k >= kGzMaxE - 2 || R.bp > lim) break;
-        gz_refill(E, R, a0);
-        int u;
-        const uint32_t e = gz_decode(lc, lb, R.hold, &u);
-        gz_drop(R, u);
-        const uint32_t op = e & 0xff;
-        if (op == 0) {  // literal
-          if (d + T >= total) {
-            bad = true;
-            break;
-          }
-          if (run0 < 0) run0 = T;
-          E.litb[T++] = uint8_t(e >> 16);
-        } else if (op & 16) {  // length, then a distance
-          const int32_t len = int32_t(e >> 16) + int32_t(uint32_t(R.hold) & ((1u << (op & 15)) - 1));
-          gz_drop(R, int(op & 15));
-          int v;
-          const uint32_t f = gz_decode(dc, db, R.hold, &v);
-          gz_drop(R, v);
-          const uint32_t dop = f & 0xff;
-          if (!(dop & 16)) {  // invalid distance code
-            bad = true;
-            break;
-          }
-          const int32_t dist = int32_t(f >> 16) + int32_t(uint32_t(R.hold) & ((1u << (dop & 15)) - 1));
-          gz_drop(R, int(dop & 15));
-          if (dist > d + T - ms || d + T + len > total) {  // too far back / past the page size
-            bad = true;
-            break;
-          }
-          close_run();
-          E.eout[k] = T;
-          E.elen[k] = len;
-          E.esrc[k] = dist;
-          E.etyp[k] = 1;
-          k++;
-          T += len;
-        } else if (op & 32) {  // end of block
-          eob = true;
-          break;
-        } else {  // invalid code
-          bad = true;
-          break;
-        }
-      }
-      if (!bad && gz_pos(R) > nbits) bad = true;  // the input ended inside a symbol
-      if (bad || !eob) break;
+    pos = gz_pos(R);
+    if (!ok || pos > nbits) flags |= kGzBad;
+    return;
+  }
+  if (mode == kGzStored) {
+    const int32_t q = int32_t(pos >> 3);
+    const int32_t left = E.stored_left;
+    if (left == 0) {
       mode = E.final_blk ? kGzTrailer : kGzBlock;
+      return;
+    }
+    if (T == 0 && k == 1 && left >= kSnapOut) {  // a batch or more: bulk copy
+      if (q + int64_t(left) > n || d + int64_t(left) > total) {
+        flags |= kGzBad;
+        return;
+      }
+      bulk_len = left;
+      bulk_src = q;
+      E.stored_left = 0;
+      mode = E.final_blk ? kGzTrailer : kGzBlock;
+      pos = int64_t(q + left) * 8;
+      flags |= kGzStop;
+      return;
+    }
+    const int32_t m = left < kSnapOut - T ? left : kSnapOut - T;
+    if (m == 0 || k >= kGzMaxE) {
+      flags |= kGzStop;
+      return;
+    }
+    if (q + int64_t(m) > n || d + T + int64_t(m) > total) {
+      flags |= kGzBad;
+      return;
+    }
+    E.eout[k] = T;
+    E.elen[k] = m;
+    E.esrc[k] = q;
+    E.etyp[k] = 2;
+    k++;
+    T += m;
+    E.stored_left = left - m;
+    pos = int64_t(q + m) * 8;
+    return;
+  }
+  // kGzTrailer: CRC-32 and ISIZE at the next byte boundary
+  const int32_t q = int32_t((pos + 7) >> 3);
+  if (int64_t(q) + 8 > n) {
+    flags |= kGzBad;
+    return;
+  }
+  E.tcrc = uint32_t(src[q]) | (uint32_t(src[q + 1]) << 8) | (uint32_t(src[q + 2]) << 16) | (uint32_t(src[q + 3]) << 24);
+  E.tsize = uint32_t(src[q + 4]) | (uint32_t(src[q + 5]) << 8) | (uint32_t(src[q + 6]) << 16) | (uint32_t(src[q + 7]) << 24);
+  E.members += 1;
+  mode = kGzHeader;
+  pos = int64_t(q + 8) * 8;
+  flags |= kGzMemberEnd;
+}
+
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(uint64_t(x) >> 32)))) << 32) |
+                 uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(x))));
+}
+
+// Wave 0: the non-Huffman states of one batch (lane 0's transitions, broadcast), until the stream
+// reaches Huffman-coded data (gz_huff_stage's), the batch ends, or the member / stream ends.
+__device__ void gz_parse(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t d, int32_t total) {
+  const int lane = threadIdx.x & 63;
+  int32_t mode = uni(E.mode);
+  const int32_t mode0 = mode;
+  int64_t pos = uni64(E.pbit);
+  const int64_t start = pos;
+  int32_t k = 1, T = 0, bulk_len = 0, bulk_src = 0;
+  uint32_t flags = 0;
+  while (mode != kGzHuff) {
+    int32_t s_mode = mode, s_T = T, s_k = k, s_bl = 0, s_bs = 0;
+    int64_t s_pos = pos;
+    uint32_t s_flags = 0;
+    if (lane == 0) gz_serial(E, src, n, a0, d, total, s_mode, s_pos, s_T, s_k, s_flags, s_bl, s_bs);
+    mode = uni(s_mode);
+    pos = uni64(s_pos);
+    T = uni(s_T);
+    k = uni(s_k);
+    flags = uint32_t(uni(int32_t(s_flags)));
+    bulk_len = uni(s_bl);
+    bulk_src = uni(s_bs);
+    if (flags & kGzTables) {  // a Huffman block's header was read: the wave builds its tables
+      flags &= ~kGzTables;
+      if (!(flags & kGzBad) && !gz_build_tables(E)) flags |= kGzBad;
+    }
+    if (flags) break;
+  }
+  if (lane == 0) {
+    E.pbit = pos;
+    E.mode = mode;
+    E.nE = k;
+    E.bend = T;
+    E.bad = (flags & kGzBad) != 0;
+    E.bulk_len = bulk_len;
+    E.bulk_src = bulk_src;
+    E.member_end = (flags & kGzMemberEnd) != 0;
+    E.done = (flags & kGzDone) != 0;
+    E.progress = T > 0 || bulk_len > 0 || (flags & (kGzMemberEnd | kGzDone)) || pos != start || mode != mode0;
+  }
+}
+
+// One Huffman-coded symbol at bit pos: kind 0 literal (x = byte), 1 length + distance (olen =
+// length, x = distance), 2 end of block, 3 invalid code; L = its bits.
+struct GzSym {
+  uint32_t kind, L, olen, x;
+};
+
+__device__ __forceinline__ GzSym gz_sym(const GzLds& E, int64_t pos, int32_t lb, int32_t db, int32_t a0) {
+  const uint64_t w = gz_load64(E, int32_t(pos >> 3) - a0) >> (pos & 7);  // >= 56 valid bits
+  int u;
+  const uint32_t e = gz_decode(E.lcode, lb, w, &u);
+  const uint32_t op = e & 0xff;
+  GzSym s;
+  s.kind = 3;
+  s.L = u > 0 ? uint32_t(u) : 1u;
+  s.olen = 0;
+  s.x = 0;
+  if (op == 0) {
+    s.kind = 0;
+    s.olen = 1;
+    s.x = e >> 16;
+  } else if (op & 16) {
+    const int ne = int(op & 15);
+    const uint32_t len = (e >> 16) + (uint32_t(w >> u) & ((1u << ne) - 1));
+    const uint64_t w2 = w >> (u + ne);
+    int v;
+    const uint32_t f = gz_decode(E.dcode, db, w2, &v);
+    const uint32_t dop = f & 0xff;
+    if (dop & 16) {
+      const int nd = int(dop & 15);
+      s.kind = 1;
+      s.olen = len;
+      s.x = (f >> 16) + (uint32_t(w2 >> v) & ((1u << nd) - 1));
+      s.L = uint32_t(u + ne + v + nd);
+    }
+  } else if (op & 32) {
+    s.kind = 2;
+  }
+  return s;
+}
+
+constexpr int64_t kGzWarm = 96;  // bits a speculative decode runs before its range to synchronise
+
+struct GzRun {
+  int64_t f, x;  // first symbol at or after count_from; the first symbol position at or after `end`
+  int32_t o, k, st;
+};
+
+// Decode from `start` while symbols start before `end`, counting (output bytes, back-references)
+// the symbols from count_from on.  An end-of-block or invalid code stops the walk (st 1 / 2; x = the
+// bit after the end of block).  Before count_from (the warm-up) such a symbol restarts the walk at
+// count_from.
+__device__ GzRun gz_run(const GzLds& E, int64_t start, int64_t count_from, int64_t end, int32_t lb, int32_t db,
+                        int32_t a0) {
+  GzRun R;
+  R.f = -1;
+  R.o = 0;
+  R.k = 0;
+  R.st = 0;
+  int64_t pos = start;
+  while (pos < end) {
+    const GzSym s = gz_sym(E, pos, lb, db, a0);
+    if (pos < count_from) {
+      pos = s.kind >= 2 ? count_from : pos + s.L;
       continue;
     }
-    if (mode == kGzStored) {
-      const int64_t here = live ? gz_pos(R) : jump;  // byte aligned
-      const int32_t q = int32_t(here >> 3);
-      const int32_t left = E.stored_left;
-      if (left == 0) {
-        mode = E.final_blk ? kGzTrailer : kGzBlock;
-        if (!live) {
-          if (q > lim - kGzHdrRoom) break;
-          gz_seek(E, R, here, a0);
-          live = true;
-          jump = -1;
-        }
-        continue;
-      }
-      close_run();
-      if (T == 0 && k == 0 && left >= kSnapOut) {  // a batch or more: bulk copy
-        if (q + int64_t(left) > n || d + int64_t(left) > total) {
-          bad = true;
-          break;
-        }
-        bulk_len = left;
-        bulk_src = q;
-        E.stored_left = 0;
-        mode = E.final_blk ? kGzTrailer : kGzBlock;
-        jump = int64_t(q + left) * 8;
-        live = false;
-        break;
-      }
-      const int32_t m = left < kSnapOut - T ? left : kSnapOut - T;
-      if (m == 0 || k >= kGzMaxE - 2) {
-        jump = here;
-        live = false;
-        break;
-      }
-      if (q + int64_t(m) > n || d + T + int64_t(m) > total) {
-        bad = true;
-        break;
-      }
-      E.eout[k] = T;
-      E.elen[k] = m;
-      E.esrc[k] = q;
-      E.etyp[k] = 2;
-      k++;
-      T += m;
-      E.stored_left = left - m;
-      jump = int64_t(q + m) * 8;
-      live = false;
-      continue;
+    if (R.f < 0) R.f = pos;
+    if (s.kind == 3) {
+      R.st = 2;
+      R.x = pos;
+      return R;
     }
-    // kGzTrailer: CRC-32 and ISIZE at the next byte boundary
-    {
-      const int64_t here = live ? gz_pos(R) : jump;
-      const int32_t q = int32_t((here + 7) >> 3);
-      if (int64_t(q) + 8 > n) {
-        bad = true;
-        break;
+    if (s.kind == 2) {
+      R.st = 1;
+      R.x = pos + s.L;
+      return R;
+    }
+    R.o += int32_t(s.olen);
+    R.k += s.kind == 1;
+    pos += s.L;
+  }
+  R.x = pos;
+  if (R.f < 0) R.f = pos;
+  return R;
+}
+
+enum : int { kGzEmitDone = 0, kGzEmitCut = 1, kGzEmitBad = 2 };
+
+// A thread's symbols from `pos` (stage output `out`, back-reference count `tok`) into the batch
+// [bo, lim_o) x token indices [1 + tok - bk ...]: literals to litb, back-references to the token
+// arrays, with the reference's checks; stops at the first symbol past the batch (the cut).
+__device__ int gz_emit(GzLds& E, int64_t pos, int64_t end, int32_t out, int32_t tok, int32_t bo, int32_t bk, int32_t lim_o,
+                       int32_t lim_k, int32_t dbase, int32_t ms, int32_t total, int64_t nbits, int32_t lb, int32_t db,
+                       int32_t a0, int64_t* cpos, int32_t* cout, int32_t* ctok) {
+  while (pos < end) {
+    const GzSym s = gz_sym(E, pos, lb, db, a0);
+    if (s.kind == 3 || pos + s.L > nbits) return kGzEmitBad;
+    if (s.kind == 2) return kGzEmitDone;
+    const bool copy = s.kind == 1;
+    if (out + int32_t(s.olen) > lim_o || (copy && tok >= lim_k)) {
+      *cpos = pos;
+      *cout = out;
+      *ctok = tok;
+      return kGzEmitCut;
+    }
+    if (int64_t(dbase) + out + s.olen > total) return kGzEmitBad;  // past the page's size
+    if (copy) {
+      if (int64_t(s.x) > int64_t(dbase) + out - ms) return kGzEmitBad;  // distance too far back
+      const int32_t i = 1 + tok - bk;
+      E.eout[i] = out - bo;
+      E.elen[i] = int32_t(s.olen);
+      E.esrc[i] = int32_t(s.x);
+      E.etyp[i] = 1;
+      tok++;
+    } else {
+      E.litb[out - bo] = uint8_t(s.x);
+    }
+    out += int32_t(s.olen);
+    pos += s.L;
+  }
+  return kGzEmitDone;
+}
+
+__device__ __forceinline__ int32_t block_excl_scan(GzLds& E, int32_t x, int32_t* total) {
+  const int tid = threadIdx.x;
+  const uint32_t incl = wave_incl_scan32(uint32_t(x));
+  if ((tid & 63) == 63) E.wsum[tid >> 6] = int32_t(incl);
+  __syncthreads();
+  int32_t base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; w++) {
+    const int32_t v = E.wsum[w];
+    if (w < (tid >> 6)) base += v;
+    all += v;
+  }
+  __syncthreads();  // wsum is reused
+  *total = all;
+  return base + int32_t(incl) - x;
+}
+
+// Resolve a batch of T output bytes (tokens 1..nE-1; literal bytes in litb) and store it at
+// dst + d.  Whole workgroup.
+__device__ void gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0, const uint8_t* src, uint8_t* dst) {
+  const int tid = threadIdx.x;
+  batch_emap(E, nE, 1);
+  const int32_t s_lo = a0, s_hi = a0 + kGzStage + 96;
+  int16_t ptr[kPer];
+  uint8_t val[kPer];
+#pragma unroll
+  for (int i0 = 0; i0 < kPer; i0 += 8) {
+    int32_t ga[8];
+    uint8_t from[8];  // 0 resolved / in-batch pointer, 1 dst (an earlier batch), 2 src (stored bytes outside the stage)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int32_t b = (i0 + j) * kBlock + tid;
+      from[j] = 0;
+      ga[j] = 0;
+      val[i0 + j] = 0;
+      ptr[i0 + j] = -1;
+      if (b >= T) continue;
+      const int e = E.emap[b];
+      const int32_t rel = b - E.eout[e];
+      if (e == 0 || rel >= E.elen[e]) {  // a literal
+        val[i0 + j] = E.litb[b];
+      } else if (E.etyp[e] == 2) {
+        const int32_t sp = E.esrc[e] + rel;
+        if (sp >= s_lo && sp < s_hi) {
+          val[i0 + j] = E.in[sp - s_lo];
+        } else {
+          from[j] = 2;
+          ga[j] = sp;
+        }
+      } else {
+        const int32_t o = E.esrc[e];
+        const int32_t sabs = d + E.eout[e] - o + (o < E.elen[e] ? rel % o : rel);  // overlapping copies repeat
+        if (sabs >= d) {
+          ptr[i0 + j] = int16_t(sabs - d);
+        } else {
+          from[j] = 1;
+          ga[j] = sabs;
+        }
       }
-      E.tcrc = uint32_t(src[q]) | (uint32_t(src[q + 1]) << 8) | (uint32_t(src[q + 2]) << 16) | (uint32_t(src[q + 3]) << 24);
-      E.tsize = uint32_t(src[q + 4]) | (uint32_t(src[q + 5]) << 8) | (uint32_t(src[q + 6]) << 16) |
-                (uint32_t(src[q + 7]) << 24);
-      E.members += 1;
-      member_end = true;
-      mode = kGzHeader;
-      jump = int64_t(q + 8) * 8;
-      live = false;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (from[j]) val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+  }
+  batch_jump_store(E, T, ptr, val, dst + d);
+}
+
+// The Huffman-coded data of the current block from E.pbit to the end of the stage (or the block's
+// end of block), by the whole workgroup.  The bit range is cut into kBlock equal parts; thread t
+// decodes its part speculatively, starting kGzWarm bits early so that its walk (almost always)
+// falls into step with the true symbol chain before its part begins (Huffman codes resynchronise
+// within a few symbols).  Rounds then re-decode every part whose first symbol differs from the
+// previous part's exit, from that exit, until nothing changes: thread 0 starts on the chain, so
+// after round r parts 0..r are exact and the fixpoint is the true decode.  A scan places the parts'
+// output; batches of at most kSnapOut bytes / kGzMaxE - 1 back-references are then emitted (each
+// part re-decoded from its true entry) and resolved with gz_batch.  Returns false on an error.
+__device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t& d, int32_t total,
+                              uint8_t* dst) {
+  const int tid = threadIdx.x;
+  const int64_t nbits = int64_t(n) * 8;
+  const int64_t P0 = uni64(E.pbit);
+  const int64_t stage_end = int64_t(a0 + kGzStage) * 8;
+  const int64_t Pend = stage_end < nbits ? stage_end : nbits;
+  if (P0 >= Pend) return false;  // the input ends inside the block
+  const int32_t lb = uni(E.lbits), db = uni(E.dbits), ms = uni(E.ms);
+  const int64_t S = (Pend - P0 + kBlock - 1) / kBlock;
+  const int64_t lo = P0 + S * tid < Pend ? P0 + S * tid : Pend;
+  const int64_t hi = P0 + S * (tid + 1) < Pend ? P0 + S * (tid + 1) : Pend;
+  GZ_CLK(h0);
+  {
+    const int64_t warm = tid == 0 ? P0 : (lo - kGzWarm > P0 ? lo - kGzWarm : P0);
+    const GzRun R = gz_run(E, warm, lo, hi, lb, db, a0);
+    E.hf[tid] = R.f;
+    E.hx[tid] = R.x;
+    E.ho[tid] = R.o;
+    E.hk[tid] = R.k;
+    E.hst[tid] = uint8_t(R.st);
+  }
+  bool converged = false;
+  for (int round = 0; round <= kBlock; round++) {
+    __syncthreads();
+    const bool redo = tid > 0 && E.hst[tid - 1] == 0 && E.hx[tid - 1] != E.hf[tid];
+    const int64_t entry = redo ? E.hx[tid - 1] : 0;
+    __syncthreads();  // every thread has read the previous round
+    if (redo) {
+      const GzRun R = gz_run(E, entry, entry, hi, lb, db, a0);
+      E.hf[tid] = R.f;
+      E.hx[tid] = R.x;
+      E.ho[tid] = R.o;
+      E.hk[tid] = R.k;
+      E.hst[tid] = uint8_t(R.st);
+    }
+#ifdef PQH_GZIP_PROF
+    if (tid == 0) GZ_ADD(1, 1);
+#endif
+    if (!__syncthreads_or(redo)) {
+      converged = true;
       break;
     }
   }
-  close_run();
-  E.eout[k] = T;
-  const int64_t next = live ? gz_pos(R) : jump;
-  E.pbit = next;
-  E.mode = mode;
-  E.nE = k;
-  E.bend = T;
-  E.bad = bad;
-  E.bulk_len = bulk_len;
-  E.bulk_src = bulk_src;
-  E.member_end = member_end;
-  E.done = done;
-  E.progress = T > 0 || bulk_len > 0 || member_end || done || next != start;
+  if (!converged) return false;  // (cannot happen: round r fixes part r)
+#ifdef PQH_GZIP_PROF
+  {
+    GZ_CLK(h1);
+    if (tid == 0) GZ_ADD(0, h1 - h0);
+  }
+#endif
+  // the first part that ended (end of block) or failed; the parts after it are not in this block
+  if (tid == 0) E.hend = kBlock;
+  __syncthreads();
+  if (E.hst[tid]) atomicMin(&E.hend, tid);
+  __syncthreads();
+  const int32_t e = uni(E.hend);
+  if (e < kBlock && E.hst[e] == 2) return false;  // an invalid code on the chain
+  const int32_t last = e < kBlock ? e : kBlock - 1;
+  const bool mine = tid <= last;
+  int32_t Ototal, Ktotal;
+  const int32_t O = block_excl_scan(E, mine ? E.ho[tid] : 0, &Ototal);
+  const int32_t K = block_excl_scan(E, mine ? E.hk[tid] : 0, &Ktotal);
+  const int64_t my_f = E.hf[tid];
+  // ---- batches
+  int32_t bt = 0, bo = 0, bk = 0;
+  int64_t bp = P0;
+  for (;;) {
+    const int32_t lim_o = bo + kSnapOut, lim_k = bk + kGzMaxE - 1;
+    if (tid == 0) E.hcut = -1;
+    __syncthreads();
+    int r = kGzEmitDone;
+    GZ_CLK(h2);
+    if (mine && tid >= bt) {
+      const int64_t p = tid == bt ? bp : my_f;
+      const int32_t out = tid == bt ? bo : O, tok = tid == bt ? bk : K;
+      if (out <= lim_o && tok <= lim_k) {
+        int64_t cp;
+        int32_t co, ck;
+        r = gz_emit(E, p, hi, out, tok, bo, bk, lim_o, lim_k, d, ms, total, nbits, lb, db, a0, &cp, &co, &ck);
+        if (r == kGzEmitCut) {  // exactly one part holds the first symbol past the batch
+          E.hcut = tid;
+          E.hcut_pos = cp;
+          E.hcut_out = co;
+          E.hcut_tok = ck;
+        }
+      }
+    }
+    if (__syncthreads_or(r == kGzEmitBad)) return false;
+    const int32_t cut = uni(E.hcut);
+    const int32_t end_o = cut >= 0 ? uni(E.hcut_out) : Ototal;
+    const int32_t end_k = cut >= 0 ? uni(E.hcut_tok) : Ktotal;
+    const int32_t T = end_o - bo;
+    GZ_CLK(h3);
+    if (T > 0) {
+      gz_batch(E, T, 1 + end_k - bk, d + bo, a0, src, dst);
+      __syncthreads();  // the batch's bytes are visible to later batches
+    }
+#ifdef PQH_GZIP_PROF
+    {
+      GZ_CLK(h4);
+      if (tid == 0) {
+        GZ_ADD(2, h3 - h2);
+        GZ_ADD(4, h4 - h3);
+        GZ_ADD(10, 1);
+      }
+    }
+#endif
+    if (cut < 0) break;
+    bt = cut;
+    bp = uni64(E.hcut_pos);
+    bo = end_o;
+    bk = end_k;
+  }
+  d += Ototal;
+  __syncthreads();
+  if (tid == 0) {
+    if (e < kBlock) {
+      E.pbit = E.hx[e];
+      E.mode = E.final_blk ? kGzTrailer : kGzBlock;
+    } else {
+      E.pbit = E.hx[kBlock - 1];
+    }
+  }
+  return true;
 }
 
 // Decode one gzip stream src[0, n) into dst[0, expected).  Whole workgroup; returns PQH_OK or
@@ -587,11 +1049,19 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
     E.final_blk = 0;
     E.stored_left = 0;
     E.ms = 0;
+    E.eout[0] = 0;  // token 0: the "literal" every byte before the first token maps to
+    E.elen[0] = 0;
+    E.etyp[0] = 0;
+    E.esrc[0] = 0;
+#ifdef PQH_GZIP_PROF
+    for (int i = 0; i < 12; i++) E.prof[i] = 0;
+#endif
   }
   const int32_t n = uni(int32_t(n64)), total = uni(int32_t(expected));
   int32_t d = 0;
   for (;;) {
     __syncthreads();  // the previous batch's readers of the stage and the state are done
+    GZ_CLK(t0);
     const int32_t p = uni(int32_t(E.pbit >> 3));
     const int32_t a0 = uni(p - int32_t((reinterpret_cast<uintptr_t>(src) + uintptr_t(p)) & 15));
     {  // up to the input's end rounded to 16 bytes (inside the payload pad)
@@ -602,65 +1072,45 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
       for (int u = tid; u < nu; u += kBlock) lp[u] = sp[u];
     }
     __syncthreads();
-    if (tid == 0) gz_parse(E, src, n, a0, d, total);
+    GZ_CLK(t1);
+#ifdef PQH_GZIP_PROF
+    if (tid == 0) GZ_ADD(6, t1 - t0);
+#endif
+    if (uni(E.mode) == kGzHuff) {
+      const bool ok = gz_huff_stage(E, src, n, a0, d, total, dst);
+#ifdef PQH_GZIP_PROF
+      GZ_CLK(t2);
+      if (tid == 0) {
+        GZ_ADD(7, t2 - t1);
+        GZ_ADD(3, 1);
+      }
+#endif
+      if (!ok) return PQH_ERR_DECOMPRESS;
+      continue;
+    }
+    if (tid < 64) gz_parse(E, src, n, a0, d, total);
     __syncthreads();
     if (uni(E.bad) || !uni(E.progress)) return PQH_ERR_DECOMPRESS;
     const int32_t nE = uni(E.nE), T = uni(E.bend);
-    if (nE == 0) {
-      const int32_t bl = uni(E.bulk_len);
-      if (bl > 0) {
-        snap_copy(dst + d, src + uni(E.bulk_src), bl);
-        d += bl;
-      }
-    } else {
-      batch_emap(E, nE);
-      const int32_t s_lo = a0, s_hi = a0 + kGzStage + 96;
-      int16_t ptr[kPer];
-      uint8_t val[kPer];
-#pragma unroll
-      for (int i0 = 0; i0 < kPer; i0 += 8) {
-        int32_t ga[8];
-        uint8_t from[8];  // 0 resolved / in-batch pointer, 1 dst (an earlier batch), 2 src (stored bytes outside the stage)
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int32_t b = (i0 + j) * kBlock + tid;
-          from[j] = 0;
-          ga[j] = 0;
-          val[i0 + j] = 0;
-          ptr[i0 + j] = -1;
-          if (b >= T) continue;
-          const int e = E.emap[b];
-          const int32_t rel = b - E.eout[e];
-          const int typ = E.etyp[e];
-          if (typ == 0) {
-            val[i0 + j] = E.litb[b];
-          } else if (typ == 2) {
-            const int32_t sp = E.esrc[e] + rel;
-            if (sp >= s_lo && sp < s_hi) {
-              val[i0 + j] = E.in[sp - s_lo];
-            } else {
-              from[j] = 2;
-              ga[j] = sp;
-            }
-          } else {
-            const int32_t o = E.esrc[e];
-            const int32_t sabs = d + E.eout[e] - o + (o < E.elen[e] ? rel % o : rel);  // overlapping copies repeat
-            if (sabs >= d) {
-              ptr[i0 + j] = int16_t(sabs - d);
-            } else {
-              from[j] = 1;
-              ga[j] = sabs;
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++)
-          if (from[j]) val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
-      }
-      batch_jump_store(E, T, ptr, val, dst + d);
+    const int32_t bl = uni(E.bulk_len);
+    if (bl > 0) {
+      snap_copy(dst + d, src + uni(E.bulk_src), bl);
+      d += bl;
+    } else if (T > 0) {
+      gz_batch(E, T, nE, d, a0, src, dst);
       d += T;
     }
     __syncthreads();  // this batch's bytes are visible to the next batches' reads and the CRC
+#ifdef PQH_GZIP_PROF
+    {
+      GZ_CLK(t3);
+      if (tid == 0) {
+        GZ_ADD(9, t3 - t1);
+        GZ_ADD(8, 1);
+      }
+    }
+#endif
+#ifndef PQH_GZIP_NO_CRC  // timing experiments: without the trailer check
     if (uni(E.member_end)) {
       // CRC-32 of the member's output [ms, d): a slice of whole words per thread, then a tree of
       // crc32_combine steps
@@ -689,8 +1139,15 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
           uint32_t(len) != uint32_t(uni(int32_t(E.tsize))))
         return PQH_ERR_DECOMPRESS;
     }
+#endif
     if (uni(E.done)) break;
   }
+#ifdef PQH_GZIP_PROF
+  if (tid == 0 && blockIdx.x == 0)
+    printf("gzprof huffman stages %lu (rounds %lu, batches %lu) serial batches %lu | cycles: stage loads %lu huffman %lu "
+           "(decode+rounds %lu emit %lu resolve %lu) serial+batches %lu\n",
+           E.prof[3], E.prof[1], E.prof[10], E.prof[8], E.prof[6], E.prof[7], E.prof[0], E.prof[2], E.prof[4], E.prof[9]);
+#endif
   return d == total ? PQH_OK : PQH_ERR_DECOMPRESS;
 }
 

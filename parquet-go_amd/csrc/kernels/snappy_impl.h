@@ -80,9 +80,10 @@ __device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
 // output bytes made of elements (eout[e] = start, batch-relative; eout[nE] = the batch size).
 constexpr int kPer = kSnapOut / kBlock;  // 32 output bytes per thread: b = i * kBlock + tid
 
-// Output byte -> element: start markers, then a max-scan (element ids rise with output).
+// Output byte -> element: start markers of elements e0..nE-1, then a max-scan (element ids rise
+// with output; bytes before the first marker map to 0).
 template <class L>
-__device__ __forceinline__ void batch_emap(L& E, int32_t nE) {
+__device__ __forceinline__ void batch_emap(L& E, int32_t nE, int32_t e0 = 0) {
   const int tid = threadIdx.x;
   {  // every thread owns 32 consecutive entries (64 bytes: four 16-byte LDS accesses)
     uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
@@ -90,7 +91,7 @@ __device__ __forceinline__ void batch_emap(L& E, int32_t nE) {
     for (int k = 0; k < 4; k++) m4[k] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  for (int e = tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
+  for (int e = e0 + tid; e < nE; e += kBlock) E.emap[E.eout[e]] = uint16_t(e);
   __syncthreads();
   {
     uint4* m4 = reinterpret_cast<uint4*>(E.emap) + tid * 4;
