@@ -94,6 +94,13 @@ bool sync_each_enabled() {
 }
 thread_local const char* g_fail_kernel = nullptr;
 
+// PQH_SNAPPY_PAGE=1 (A/B experiments): device SNAPPY by k_snappy, one workgroup per page, instead of
+// the multi-workgroup pipeline (k_snap_spec / stitch / emit / fixup).
+bool snappy_page_mode() {
+  const char* f = getenv("PQH_SNAPPY_PAGE");
+  return f && f[0] == '1';
+}
+
 constexpr size_t kBounceHalf = size_t(16) << 20;
 
 hipError_t bounce_init(pqh_ctx* ctx) {
@@ -274,6 +281,7 @@ struct pqh_batch {
   int32_t codec_gzip = 0;  // GZIP pages among them (k_gzip)
   int32_t* d_codec_status = nullptr;
   std::vector<int32_t> codec_status;  // host copy after sync (per page)
+  SnapPlan snap;                      // multi-workgroup SNAPPY tables and scratch (snappy_mw.h)
   int64_t payload_bytes = 0;
   void* h_staged = nullptr;           // staged batches: pinned host page images
   std::shared_ptr<uint8_t> h_pinned_ref;  // ... when they are a pinned host batch's payload (shared)
@@ -948,8 +956,11 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
   if (b->codec_n)  // device codecs: the page images first
     e = timed(22, b->codec_n, s, [&](hipStream_t st) {
-      return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
-                           static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
+      if (snappy_page_mode())
+        return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
+                             static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
+      return launch_snappy_mw(b->d_codec, b->snap, static_cast<const uint8_t*>(b->d_src),
+                              static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
     });
   if (e == hipSuccess && b->codec_gzip)
     e = timed(24, b->codec_gzip, s, [&](hipStream_t st) {
@@ -1561,6 +1572,27 @@ void pqh_batch_destroy(pqh_batch* b) {
 }  // extern "C"
 
 namespace {
+// The multi-workgroup SNAPPY plan of a codec page table: its tables in HBM and its scratch.
+int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
+  SnapPlan& P = b->snap;
+  P.n_pages = n;
+  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit);
+  int32_t* tab = nullptr;
+  int4* ws = nullptr;
+  int2* wt = nullptr;
+  int32_t* uf = nullptr;
+  int rc;
+  if ((rc = dalloc(b, reinterpret_cast<void**>(&tab), sizeof(int32_t) * t.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&ws), sizeof(int4) * size_t(P.n_win))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&wt), sizeof(int2) * size_t(P.n_win))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&uf), sizeof(int32_t) * size_t(P.n_unit))))
+    return rc;
+  const hipError_t e = bounce_h2d(b->ctx, tab, t.data(), sizeof(int32_t) * t.size());
+  if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_HIP, std::string("snappy plan: ") + hipGetErrorString(e));
+  snap_plan_bind(P, tab, ws, wt, uf);
+  return PQH_OK;
+}
+
 // Device codecs: the image buffer (zeroed, with its pad) the decode reads, planned over the host
 // batch's tables; the source payload at d_src (already in HBM or uploaded by the caller) is
 // decompressed into it at the start of every run.
@@ -1594,6 +1626,11 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
     return rc;
   }
   e = bounce_h2d(ctx, b->d_codec, hb->codec_pages.data(), sizeof(pqh_codec_page) * size_t(b->codec_n));
+  if (e == hipSuccess && (rc = snap_plan_alloc(b, hb->codec_pages.data(), b->codec_n))) {
+    pqh_batch_destroy(b);
+    *out = nullptr;
+    return rc;
+  }
   if (e != hipSuccess) {
     pqh_batch_destroy(b);
     *out = nullptr;
@@ -1702,14 +1739,31 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   hipError_t e = hipMalloc(&dp, sizeof(pqh_codec_page) * size_t(num_pages));
   if (e == hipSuccess) e = hipMalloc(&ds, sizeof(int32_t) * size_t(num_pages));
   if (e == hipSuccess) e = bounce_h2d(ctx, dp, pages, sizeof(pqh_codec_page) * size_t(num_pages));
-  if (e == hipSuccess)
-    e = launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
+  // the multi-workgroup SNAPPY plan (tables + scratch in one allocation)
+  SnapPlan P;
+  P.n_pages = num_pages;
+  const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit);
+  const size_t tb = (sizeof(int32_t) * tab.size() + 15) & ~size_t(15);
+  const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) + 16;
+  void* scratch = nullptr;
+  if (e == hipSuccess) e = hipMalloc(&scratch, sb);
+  if (e == hipSuccess) e = bounce_h2d(ctx, scratch, tab.data(), sizeof(int32_t) * tab.size());
+  if (e == hipSuccess) {
+    uint8_t* m = static_cast<uint8_t*>(scratch);
+    int4* ws = reinterpret_cast<int4*>(m + tb);
+    int2* wt = reinterpret_cast<int2*>(ws + P.n_win);
+    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, reinterpret_cast<int32_t*>(wt + P.n_win));
+    e = snappy_page_mode()
+            ? launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream)
+            : launch_snappy_mw(dp, P, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
+  }
   if (e == hipSuccess && std::any_of(pages, pages + num_pages, [](const pqh_codec_page& c) { return c.codec == PQH_CODEC_GZIP; }))
     e = launch_gzip(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);
   if (e == hipSuccess) e = bounce_d2h(ctx, status, ds, sizeof(int32_t) * size_t(num_pages));
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (dp) hipFree(dp);
   if (ds) hipFree(ds);
+  if (scratch) hipFree(scratch);
   if (e != hipSuccess) return set_err(ctx, PQH_ERR_HIP, std::string("pqh_decompress_pages: ") + hipGetErrorString(e));
   return PQH_OK;
 }

@@ -1069,6 +1069,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 #include "bytearray_impl.h"
 #include "nest_impl.h"
 #include "snappy_impl.h"
+#include "snappy_mw.h"
 #include "gzip_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
@@ -1174,6 +1175,63 @@ hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* 
                          hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_snappy, dim3(n), dim3(256), 0, s, pages, src, dst, status);
+  return hipGetLastError();
+}
+
+std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit) {
+  std::vector<int32_t> pw(size_t(n) + 1), pu(size_t(n) + 1), wp, up;
+  int32_t W = 0, U = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const pqh_codec_page& c = pages[i];
+    pw[size_t(i)] = W;
+    pu[size_t(i)] = U;
+    int64_t nw = 0, nu = 0;
+    if (c.codec == PQH_CODEC_SNAPPY) {
+      const int64_t raw = c.raw_len < c.src_len ? c.raw_len : c.src_len;
+      nw = (int64_t(c.src_len) - raw + kSnWin - 1) / kSnWin;
+      if (raw <= c.image_len) nu = (int64_t(c.image_len) - raw + kSnUnit - 1) / kSnUnit;
+    } else if (c.codec != PQH_CODEC_GZIP) {
+      nu = ((c.src_len < c.image_len ? c.src_len : c.image_len) + int64_t(kSnUnit) - 1) / kSnUnit;
+    }
+    for (int64_t j = 0; j < nw; j++) wp.push_back(i);
+    for (int64_t j = 0; j < nu; j++) up.push_back(i);
+    W += int32_t(nw);
+    U += int32_t(nu);
+  }
+  pw[size_t(n)] = W;
+  pu[size_t(n)] = U;
+  std::vector<int32_t> t;
+  t.reserve(pw.size() + pu.size() + wp.size() + up.size());
+  t.insert(t.end(), pw.begin(), pw.end());
+  t.insert(t.end(), pu.begin(), pu.end());
+  t.insert(t.end(), wp.begin(), wp.end());
+  t.insert(t.end(), up.begin(), up.end());
+  *n_win = W;
+  *n_unit = U;
+  return t;
+}
+
+void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag) {
+  P.page_win0 = tables;
+  P.page_unit0 = tables + P.n_pages + 1;
+  P.win_page = tables + 2 * (P.n_pages + 1);
+  P.unit_page = P.win_page + P.n_win;
+  P.wspec = wspec;
+  P.wtrue = wtrue;
+  P.uflag = uflag;
+}
+
+hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, const uint8_t* src, uint8_t* dst,
+                            int32_t* status, hipStream_t s) {
+  if (P.n_pages <= 0) return hipSuccess;
+  if (P.n_win > 0) hipLaunchKernelGGL(k_snap_spec, dim3(P.n_win), dim3(256), 0, s, pages, P.win_page, P.page_win0, src, P.wspec);
+  hipLaunchKernelGGL(k_snap_stitch, dim3(P.n_pages), dim3(256), 0, s, pages, P.page_win0, src, dst, P.wspec, P.wtrue, status);
+  if (P.n_unit > 0) {
+    hipLaunchKernelGGL(k_snap_emit, dim3(P.n_unit), dim3(kSnT), 0, s, pages, P.unit_page, P.page_unit0, P.page_win0, src,
+                       dst, P.wtrue, status, P.uflag);
+    hipLaunchKernelGGL(k_snap_fixup, dim3(P.n_pages), dim3(kSnT), 0, s, pages, P.page_unit0, P.page_win0, src, dst,
+                       P.wtrue, status, P.uflag);
+  }
   return hipGetLastError();
 }
 

@@ -841,8 +841,19 @@ __device__ __forceinline__ int32_t block_excl_scan(GzLds& E, int32_t x, int32_t*
 
 // Resolve a batch of T output bytes (tokens 1..nE-1; literal bytes in litb) and store it at
 // dst + d.  Whole workgroup.
-__device__ void gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0, const uint8_t* src, uint8_t* dst) {
+// Every HBM read is bounds-checked (a back-reference inside [0, d), a stored byte inside [0, n)) and
+// the batch must end inside the page (total): false, with nothing read or written out of bounds, when
+// the batch's tables are inconsistent (never for a well-formed decode).
+__device__ bool gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0, const uint8_t* src, uint8_t* dst,
+                         int32_t n, int32_t total) {
   const int tid = threadIdx.x;
+  if (T < 0 || T > kSnapOut || nE < 1 || nE > kGzMaxE || int64_t(d) + T > total) {
+#ifdef PQH_GZIP_DEBUG
+    if (tid == 0) printf("gz_batch guard: page %d T %d nE %d d %d total %d\n", int(blockIdx.x), T, nE, d, total);
+#endif
+    return false;
+  }
+  bool oob = false;
   batch_emap(E, nE, 1);
   const int32_t s_lo = a0, s_hi = a0 + kGzStage + 96;
   int16_t ptr[kPer];
@@ -883,10 +894,21 @@ __device__ void gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0,
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-      if (from[j]) val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+    for (int j = 0; j < 8; j++) {
+      if (!from[j]) continue;
+      if (ga[j] < 0 || ga[j] >= (from[j] == 1 ? d : n)) {
+#ifdef PQH_GZIP_DEBUG
+        printf("gz_batch guard: page %d from %d ga %d d %d n %d\n", int(blockIdx.x), int(from[j]), ga[j], d, n);
+#endif
+        oob = true;
+        continue;
+      }
+      val[i0 + j] = from[j] == 1 ? dst[ga[j]] : src[ga[j]];
+    }
   }
+  if (__syncthreads_or(oob)) return false;
   batch_jump_store(E, T, ptr, val, dst + d);
+  return true;
 }
 
 // The Huffman-coded data of the current block from E.pbit to the end of the stage (or the block's
@@ -993,7 +1015,7 @@ __device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a
     const int32_t T = end_o - bo;
     GZ_CLK(h3);
     if (T > 0) {
-      gz_batch(E, T, 1 + end_k - bk, d + bo, a0, src, dst);
+      if (!gz_batch(E, T, 1 + end_k - bk, d + bo, a0, src, dst, n, total)) return false;
       __syncthreads();  // the batch's bytes are visible to later batches
     }
 #ifdef PQH_GZIP_PROF
@@ -1094,10 +1116,12 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
     const int32_t nE = uni(E.nE), T = uni(E.bend);
     const int32_t bl = uni(E.bulk_len);
     if (bl > 0) {
-      snap_copy(dst + d, src + uni(E.bulk_src), bl);
+      const int32_t bs = uni(E.bulk_src);
+      if (int64_t(d) + bl > total || bs < 0 || int64_t(bs) + bl > n) return PQH_ERR_DECOMPRESS;  // (validated by gz_serial)
+      snap_copy(dst + d, src + bs, bl);
       d += bl;
     } else if (T > 0) {
-      gz_batch(E, T, nE, d, a0, src, dst);
+      if (!gz_batch(E, T, nE, d, a0, src, dst, n, total)) return PQH_ERR_DECOMPRESS;
       d += T;
     }
     __syncthreads();  // this batch's bytes are visible to the next batches' reads and the CRC

@@ -1,4 +1,4 @@
-"""k_snappy timing probe: one page vs many copies of it, per kind of block (bulk literals,
+"""Device SNAPPY timing probe (multi-workgroup pipeline "mw" and k_snappy "page"): one page vs many copies of it, per kind of block (bulk literals,
 copy-heavy runs, URL-like text, random letters).  Prints ms per launch and decompressed GB/s."""
 import os
 import sys
@@ -29,9 +29,14 @@ def main():
         "url_1MiB": url,
         "letters_1MiB": bytes(rng.integers(97, 123, 1 << 20, dtype=np.uint8)),
     }
+    modes = os.environ.get("PROBE_MODES", "mw,page").split(",")
+    sel = os.environ.get("PROBE_CASES")
     for name, raw in cases.items():
+        if sel and name not in sel.split(","):
+            continue
         blk = pa.compress(raw, codec="snappy", asbytes=True)
-        for copies in (1, 512):
+        for mode, copies in [(m, c) for m in modes for c in [int(x) for x in os.environ.get("PROBE_COPIES", "1,512").split(",")]]:
+            os.environ["PQH_SNAPPY_PAGE"] = "1" if mode == "page" else "0"  # k_snappy vs k_snap_* pipeline
             soff = (len(blk) + 63) & ~63
             ioff = (len(raw) + 63) & ~63
             pages = [N.CodecPage(i * soff, i * ioff, len(blk), len(raw), 0, 1, 0, 0) for i in range(copies)]
@@ -48,7 +53,7 @@ def main():
                 ctx.decompress_pages(pages, ds, dd)
             ms = (time.perf_counter() - t0) / reps * 1e3
             chk = ctx.d2h_array(dd, len(raw)).tobytes() == raw
-            print(f"{name:14s} ratio {len(raw) / len(blk):5.2f} pages {copies:4d}: {ms:8.3f} ms "
+            print(f"{mode:4s} {name:14s} ratio {len(raw) / len(blk):5.2f} pages {copies:4d}: {ms:8.3f} ms "
                   f"{len(raw) * copies / ms / 1e6:8.2f} GB/s ok={chk}", flush=True)
             ctx.free(ds)
             ctx.free(dd)

@@ -84,4 +84,79 @@ def edge_blocks():
     cases.append((block(n3, e3), O.snappy_decode(block(n3, e3))))
     cases.append((block(20, literal(b"ab") + copy2(18, 2)), b"ab" * 10))
     cases.append((block(0, b""), b""))
+    cases += multi_unit_blocks()
     return cases
+
+
+def _decode(blk):
+    from oracle import oracle as O
+
+    return O.snappy_decode(blk)
+
+
+def multi_unit_blocks():
+    """Blocks for the multi-workgroup decoder (k_snap_spec / stitch / emit / fixup): 4 KiB input
+    windows, 64 KiB output units.  Literals spanning many windows and straddling units, copies
+    straddling units, copies reaching into earlier units (each unit depending on the one before:
+    the in-order fixup), and a literal whose body is a run of valid-looking copy tags across a
+    window start (the window's guessed entry is wrong: the stitch parses it again)."""
+    rng = np.random.default_rng(21)
+    cases = []
+    # 1. one literal of 150 KiB (37 windows, three units)
+    lit = rng.bytes(150000)
+    cases.append(block(len(lit), literal(lit)))
+    # 2. short elements, then a literal and a copy straddling the 64 KiB unit boundary
+    e, n = literal(rng.bytes(1000)), 1000
+    while n < 65536 - 300:
+        e += copy2(64, 900)
+        n += 64
+    e += literal(rng.bytes(65536 - n + 200))
+    n = 65536 + 200
+    e += copy2(64, 3000) + literal(rng.bytes(5)) + copy1(11, 7)
+    cases.append(block(n + 64 + 5 + 11, e))
+    # 3. a copy straddling the unit boundary (starts 10 bytes before it)
+    e, n = literal(rng.bytes(2000)), 2000
+    while n + 64 <= 65536 - 10:
+        e += copy2(64, 1999)
+        n += 64
+    e += literal(rng.bytes(65536 - 10 - n))
+    n = 65536 - 10
+    e += copy2(40, 65000) + copy1(5, 3)
+    cases.append(block(n + 45, e))
+    # 4. copies 70000 back: every unit after the first reads the unit before it (fixup chain)
+    e, n = literal(rng.bytes(70000)), 70000
+    while n < 260000:
+        e += copy4(64, 70000) + literal(rng.bytes(3))
+        n += 67
+    cases.append(block(n, e))
+    # 5. a literal of copy1 tags across the window start at 4096 (the guessed entry is a false chain)
+    e = literal(rng.bytes(3700))
+    fake = bytes([1, 0]) * 300
+    e += literal(fake) + copy2(30, 100) + literal(rng.bytes(9000)) + copy2(64, 5000)
+    cases.append(block(3700 + 600 + 30 + 9000 + 64, e))
+    # 6. the same trick at every window start of a long block
+    e, n = b"", 0
+    for _ in range(40):
+        body = bytes([1, 0]) * 200 + rng.bytes(3000)
+        e += literal(body) + copy2(17, 333) + copy1(9, 1)
+        n += len(body) + 26
+    cases.append(block(n, e))
+    # 7. random short elements over 300 KiB of output (many units, many windows)
+    e, n = literal(rng.bytes(64)), 64
+    while n < 300000:
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            ln = int(rng.integers(1, 80))
+            e += literal(rng.bytes(ln))
+        elif k == 1:
+            ln = int(rng.integers(4, 12))
+            e += copy1(ln, int(rng.integers(1, min(n, 2047) + 1)))
+        elif k == 2:
+            ln = int(rng.integers(1, 65))
+            e += copy2(ln, int(rng.integers(1, min(n, 65535) + 1)))
+        else:
+            ln = int(rng.integers(1, 65))
+            e += copy4(ln, int(rng.integers(1, n + 1)))
+        n += ln
+    cases.append(block(n, e))
+    return [(b, _decode(b)) for b in cases]
