@@ -312,7 +312,8 @@ __device__ int4 sn_window(SnSpecLds& L, const uint8_t* src, int32_t n, int32_t h
 }
 
 __global__ __launch_bounds__(256) void k_snap_spec(const pqh_codec_page* cps, const int32_t* win_page,
-                                                   const int32_t* page_win0, const uint8_t* src_all, int4* wspec) {
+                                                   const int32_t* page_win0, const uint8_t* src_all, int4* wspec,
+                                                   int32_t* wseg) {
   __shared__ SnSpecLds L;
   const int32_t w = blockIdx.x;
   const int32_t p = win_page[w];
@@ -328,12 +329,13 @@ __global__ __launch_bounds__(256) void k_snap_spec(const pqh_codec_page* cps, co
   }
   const int4 r = sn_window(L, src, n, hl, w - page_win0[p], -1);
   if (threadIdx.x == 0) wspec[w] = r;
+  wseg[int64_t(w) * kBlock + threadIdx.x] = L.F.f[threadIdx.x];  // exact when the stitch accepts the guess
 }
 
 // Per page: status, true window entries / output bases, V2 level bytes.
 __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, const int32_t* page_win0,
                                                      const uint8_t* src_all, uint8_t* dst_all, const int4* wspec,
-                                                     int2* wtrue, int32_t* status) {
+                                                     int2* wtrue, int32_t* wseg, int32_t* status) {
   __shared__ SnSpecLds L;
   const int tid = threadIdx.x, lane = tid & 63;
   const int32_t p = blockIdx.x;
@@ -407,6 +409,7 @@ __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, 
     if (found == 1) {  // window c guessed its entry wrong: parse it from the true entry
       const int4 r = sn_window(L, src, n, hl, c, e);
       if (tid == 0) wtrue[w0 + c] = make_int2(e, O);
+      wseg[int64_t(w0 + c) * kBlock + tid] = L.F.f[tid];
       if (r.w) {
         bad = true;
         break;
