@@ -1581,15 +1581,17 @@ int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
   int4* ws = nullptr;
   int2* wt = nullptr;
   int32_t* uf = nullptr;
+  int32_t* seg = nullptr;
   int rc;
-  if ((rc = dalloc(b, reinterpret_cast<void**>(&tab), sizeof(int32_t) * t.size())) ||
+  if ((rc = dalloc(b, reinterpret_cast<void**>(&seg), sizeof(int32_t) * 256 * size_t(P.n_win))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&tab), sizeof(int32_t) * t.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&ws), sizeof(int4) * size_t(P.n_win))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&wt), sizeof(int2) * size_t(P.n_win))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&uf), sizeof(int32_t) * size_t(P.n_unit))))
     return rc;
   const hipError_t e = bounce_h2d(b->ctx, tab, t.data(), sizeof(int32_t) * t.size());
   if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_HIP, std::string("snappy plan: ") + hipGetErrorString(e));
-  snap_plan_bind(P, tab, ws, wt, uf);
+  snap_plan_bind(P, tab, ws, wt, uf, seg);
   return PQH_OK;
 }
 
@@ -1744,7 +1746,8 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   P.n_pages = num_pages;
   const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit);
   const size_t tb = (sizeof(int32_t) * tab.size() + 15) & ~size_t(15);
-  const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) + 16;
+  const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) +
+                    sizeof(int32_t) * 256 * size_t(P.n_win) + 16;
   void* scratch = nullptr;
   if (e == hipSuccess) e = hipMalloc(&scratch, sb);
   if (e == hipSuccess) e = bounce_h2d(ctx, scratch, tab.data(), sizeof(int32_t) * tab.size());
@@ -1752,7 +1755,8 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
     uint8_t* m = static_cast<uint8_t*>(scratch);
     int4* ws = reinterpret_cast<int4*>(m + tb);
     int2* wt = reinterpret_cast<int2*>(ws + P.n_win);
-    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, reinterpret_cast<int32_t*>(wt + P.n_win));
+    int32_t* uf = reinterpret_cast<int32_t*>(wt + P.n_win);
+    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, uf, uf + P.n_unit);
     e = snappy_page_mode()
             ? launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream)
             : launch_snappy_mw(dp, P, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);

@@ -1070,6 +1070,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 #include "nest_impl.h"
 #include "snappy_impl.h"
 #include "snappy_mw.h"
+#include "snappy_emit.h"
 #include "gzip_impl.h"
 
 __global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
@@ -1211,7 +1212,8 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
   return t;
 }
 
-void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag) {
+void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int32_t* wseg) {
+  P.wseg = wseg;
   P.page_win0 = tables;
   P.page_unit0 = tables + P.n_pages + 1;
   P.win_page = tables + 2 * (P.n_pages + 1);
@@ -1224,13 +1226,15 @@ void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int3
 hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, const uint8_t* src, uint8_t* dst,
                             int32_t* status, hipStream_t s) {
   if (P.n_pages <= 0) return hipSuccess;
-  if (P.n_win > 0) hipLaunchKernelGGL(k_snap_spec, dim3(P.n_win), dim3(256), 0, s, pages, P.win_page, P.page_win0, src, P.wspec);
-  hipLaunchKernelGGL(k_snap_stitch, dim3(P.n_pages), dim3(256), 0, s, pages, P.page_win0, src, dst, P.wspec, P.wtrue, status);
+  if (P.n_win > 0)
+    hipLaunchKernelGGL(k_snap_spec, dim3(P.n_win), dim3(256), 0, s, pages, P.win_page, P.page_win0, src, P.wspec, P.wseg);
+  hipLaunchKernelGGL(k_snap_stitch, dim3(P.n_pages), dim3(256), 0, s, pages, P.page_win0, src, dst, P.wspec, P.wtrue,
+                     P.wseg, status);
   if (P.n_unit > 0) {
     hipLaunchKernelGGL(k_snap_emit, dim3(P.n_unit), dim3(kSnT), 0, s, pages, P.unit_page, P.page_unit0, P.page_win0, src,
-                       dst, P.wtrue, status, P.uflag);
+                       dst, P.wtrue, P.wseg, status, P.uflag);
     hipLaunchKernelGGL(k_snap_fixup, dim3(P.n_pages), dim3(kSnT), 0, s, pages, P.page_unit0, P.page_win0, src, dst,
-                       P.wtrue, status, P.uflag);
+                       P.wtrue, P.wseg, status, P.uflag);
   }
   return hipGetLastError();
 }

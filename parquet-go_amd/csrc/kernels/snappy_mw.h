@@ -17,12 +17,13 @@
 //                 from the true entry by the workgroup), giving every window its true entry and its
 //                 output base; the header length, the element structure, the total and the input
 //                 end decide the page's status.  DataPageV2 level bytes are copied here.
-//   k_snap_emit   one 512-thread workgroup per 64 KiB of a page's output (a "unit"): from the last
-//                 window starting at or before the unit, its elements are parsed again stage by
-//                 stage (same thread-parallel parse from an exact entry), literal bytes go straight
-//                 into the unit's LDS image, copies are listed and resolved in spans of 16 KiB by
-//                 an output-byte -> copy map and pointer jumping over the span (sources before the
-//                 span are already final in LDS).  The unit is written to HBM once, 16-byte stores.
+//   k_snap_emit   one 512-thread workgroup per 64 KiB of a page's output (a "unit", snappy_emit.h):
+//                 from the last window whose output base is at or before the unit, window by
+//                 window, every thread walks its 16-byte segment from the exact entry the spec /
+//                 stitch kept for it (wseg), literal bytes go straight into the unit's LDS image,
+//                 copies are listed and resolved in spans of 16 KiB (each copy byte chases its source
+//                 through the span's copy map; pointer jumping finishes long chains).  The unit is
+//                 written to HBM once, with 16-byte stores.
 //                 golang/snappy and C++ snappy encode 64 KiB fragments independently
 //                 (snappy encode.go:22-32 maxBlockSize; snappy.cc kBlockSize), so their copies
 //                 never reach before a unit; a copy that does (any other encoder) marks the unit.
@@ -33,14 +34,12 @@
 constexpr int kSnWin = 4096;                 // compressed bytes per spec window
 constexpr int kSnWarm0 = 256;                // warm-up of a window's first thread (window > 0)
 constexpr int kSnWarm = 128;                 // warm-up of every other thread (spec windows, 16-byte segments)
-constexpr int kSnWarmE = 160;                // (emit stages, 8-byte segments)
 constexpr int kSnUnit = 65536;               // output bytes per emit unit
-constexpr int kSnStage = 4096;               // compressed bytes parsed per emit stage
 constexpr int kSnSpan = 16384;               // output bytes per copy-resolution span
 constexpr int kSnT = 512;                    // emit / fixup threads
 constexpr int kSnPer = kSnSpan / kSnT;       // span bytes per thread
-constexpr int kSnMaxC = kSnStage / 2 + 16;   // copies starting in one stage (a copy is >= 2 bytes)
-constexpr int kSnMaxL = kSnStage / 64 + 4;   // literals of > 64 unit bytes starting in one stage
+constexpr int kSnMaxC = kSnWin / 2 + 16;     // copies starting in one window (a copy is >= 2 bytes)
+constexpr int kSnMaxL = kSnWin / 64 + 4;     // literals of > 64 unit bytes starting in one window
 constexpr int kSnSpecStage = kSnWin + kSnWarm0 + 64;
 constexpr int kSnSpecRounds = 12;            // a speculative window that needs more rounds (inside a long
                                              // literal, usually) is left to the stitch
@@ -422,399 +421,4 @@ __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, 
   if (tid == 0) status[p] = (!bad && e == n && O == total) ? PQH_OK : PQH_ERR_DECOMPRESS;
 }
 
-struct __attribute__((aligned(16))) SnEmitLds {
-  uint8_t out[kSnUnit + 64];  // the unit's image
-  uint8_t in[kSnStage + 64];  // the stage: block bytes [a0, send + 16)
-  uint16_t emap[kSnSpan];     // span byte -> copy (1-based); then (as int16) the byte's pointer
-  int32_t cs[kSnMaxC];        // the stage's copies: output start (unit-relative), offset, unit bytes
-  int32_t co[kSnMaxC];
-  uint8_t cl[kSnMaxC];
-  int32_t l_out[kSnMaxL], l_src[kSnMaxL], l_len[kSnMaxL];  // literals of > 64 unit bytes
-  SnFix<kSnT> F;
-  int32_t nlong, bad, ext, cut, tmax, win;
-#ifdef PQH_SNAP_PROF  // timing experiments: clock64() per phase, printed for the first unit
-  uint64_t prof[12];
-#endif
-};
-
-// n bytes from src to dst (global, any alignment) by kSnT threads.
-__device__ __forceinline__ void sn_gcopy(uint8_t* dst, const uint8_t* src, int64_t n) {
-  const int tid = threadIdx.x;
-  const int64_t head0 = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15);
-  const int64_t head = head0 < n ? head0 : n;
-  if (tid < head) dst[tid] = src[tid];
-  typedef uint4 uint4_u __attribute__((aligned(1)));
-  const int64_t units = (n - head) >> 4;
-  const uint4_u* sp = reinterpret_cast<const uint4_u*>(src + head);
-  uint4* dp = reinterpret_cast<uint4*>(dst + head);
-  for (int64_t u = tid; u < units; u += kSnT) dp[u] = sp[u];
-  const int64_t done = head + units * 16;
-  if (tid < n - done) dst[done + tid] = src[done + tid];
-}
-
-// The stage's K copies (unit-relative output start cs, offset co, length cl, 0 when the copy has
-// no byte in the unit; in output order) resolved into L.out, span by span: each span byte is a literal / gap byte (final in L.out),
-// a copy byte whose source precedes the span (final in L.out, or before the unit: read from
-// dst_unit in ext mode, else the unit is marked) or a pointer to an earlier span byte; pointer
-// jumping then resolves every chain in O(log length) rounds.
-__device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, bool ext, const uint8_t* dst_unit) {
-  const int tid = threadIdx.x;
-  int32_t i = 0;
-  while (i < K) {
-    const int32_t c0 = L.cs[i];
-    const int32_t B0 = c0 < 0 ? 0 : (c0 > ulen ? ulen : c0);
-    __syncthreads();  // the previous span's readers are done
-    if (tid == 0) {
-      L.cut = K;
-      L.tmax = 0;
-    }
-    {
-      uint4* m4 = reinterpret_cast<uint4*>(L.emap) + tid * (kSnPer / 8);
-#pragma unroll
-      for (int k = 0; k < kSnPer / 8; k++) m4[k] = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    {
-      int32_t cut = K;
-      for (int32_t j = i + tid; j < K; j += kSnT) {
-        const int32_t e = L.cs[j] + L.cl[j] < ulen ? L.cs[j] + L.cl[j] : ulen;
-        if (e - B0 > kSnSpan) {
-          cut = j;
-          break;  // (starts rise with j)
-        }
-      }
-      cut = wave_min32(cut);
-      if ((tid & 63) == 0 && cut < K) atomicMin(&L.cut, cut);
-    }
-    __syncthreads();
-    const int32_t i1 = L.cut;
-    {
-      int32_t tm = 0;
-      for (int32_t j = i + tid; j < i1; j += kSnT) {
-        if (!L.cl[j]) continue;
-        const int32_t s = L.cs[j] > 0 ? L.cs[j] : 0;
-        const int32_t e = L.cs[j] + L.cl[j] < ulen ? L.cs[j] + L.cl[j] : ulen;
-        L.emap[s - B0] = uint16_t(j - i + 1);
-        tm = e - B0 > tm ? e - B0 : tm;
-      }
-      tm = wave_max32(tm);
-      if ((tid & 63) == 0 && tm > 0) atomicMax(&L.tmax, tm);
-    }
-    __syncthreads();
-    const int32_t T = L.tmax;
-    {  // max-scan: every thread owns kSnPer consecutive entries
-      uint4* m4 = reinterpret_cast<uint4*>(L.emap) + tid * (kSnPer / 8);
-      uint32_t wv[kSnPer / 2];
-#pragma unroll
-      for (int k = 0; k < kSnPer / 8; k++) {
-        const uint4 x = m4[k];
-        wv[4 * k] = x.x;
-        wv[4 * k + 1] = x.y;
-        wv[4 * k + 2] = x.z;
-        wv[4 * k + 3] = x.w;
-      }
-      uint32_t mx = 0;
-#pragma unroll
-      for (int k = 0; k < kSnPer / 2; k++) {
-        const uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
-        mx = a > mx ? a : mx;
-        mx = c > mx ? c : mx;
-      }
-      const int32_t run0 = sn_block_excl_max<kSnT>(L.F, int32_t(mx));
-      uint32_t run = run0 < 0 ? 0u : uint32_t(run0);
-#pragma unroll
-      for (int k = 0; k < kSnPer / 2; k++) {
-        uint32_t a = wv[k] & 0xffff, c = wv[k] >> 16;
-        run = a > run ? a : run;
-        a = run;
-        run = c > run ? c : run;
-        c = run;
-        wv[k] = a | (c << 16);
-      }
-#pragma unroll
-      for (int k = 0; k < kSnPer / 8; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
-    }
-    __syncthreads();
-    int16_t ptr[kSnPer];
-    uint8_t val[kSnPer];
-#pragma unroll
-    for (int q = 0; q < kSnPer; q++) {
-      const int32_t b = q * kSnT + tid;
-      ptr[q] = -1;
-      val[q] = 0;
-      if (b >= T) continue;
-      const int32_t pos = B0 + b;
-      const int e = L.emap[b];
-      const int32_t j = i + e - 1;
-      if (e == 0 || pos >= L.cs[j] + L.cl[j]) {
-        val[q] = L.out[pos];  // a literal byte (or a byte of an earlier copy of the stage's first span... final)
-        continue;
-      }
-      const int32_t cs = L.cs[j], o = L.co[j];
-      const int32_t rel = pos - cs;
-      if (o <= 0) continue;  // (a copy of offset 0 fails the unit that owns it)
-      const int32_t s = cs - o + (o < L.cl[j] ? rel % o : rel);  // overlapping copies repeat
-      if (s >= B0) {
-        ptr[q] = int16_t(s - B0);
-      } else if (s >= 0) {
-        val[q] = L.out[s];
-      } else if (ext) {
-        if (U0 + s >= 0) val[q] = dst_unit[s];  // (before the output start: its owner failed the page)
-      } else {
-        L.ext = 1;
-      }
-    }
-    __syncthreads();  // emap no longer read: it becomes the pointer array
-    int16_t* P = reinterpret_cast<int16_t*>(L.emap);
-#pragma unroll
-    for (int q = 0; q < kSnPer; q++) {
-      const int32_t b = q * kSnT + tid;
-      if (b < T) {
-        P[b] = ptr[q];
-        L.out[B0 + b] = val[q];
-      }
-    }
-    __syncthreads();
-    for (;;) {
-      int pending = 0;
-#pragma unroll
-      for (int q = 0; q < kSnPer; q++) {
-        if (ptr[q] < 0) continue;
-        const int16_t t = P[ptr[q]];
-        if (t < 0) val[q] = L.out[B0 + ptr[q]];
-        else pending = 1;
-        ptr[q] = t;
-      }
-      const int more = __syncthreads_or(pending);
-#ifdef PQH_SNAP_PROF
-      if (tid == 0) L.prof[10] += 1;
-#endif
-#pragma unroll
-      for (int q = 0; q < kSnPer; q++) {
-        const int32_t b = q * kSnT + tid;
-        if (b < T) {
-          P[b] = ptr[q];
-          L.out[B0 + b] = val[q];
-        }
-      }
-      __syncthreads();
-      if (!more) break;
-    }
-#ifdef PQH_SNAP_PROF
-    if (tid == 0) L.prof[11] += 1;
-#endif
-    i = i1;
-  }
-}
-
-// One unit [U0, U1) of a SNAPPY block's output: block src[0, n), output at dst (after the raw
-// prefix), true window entries / bases wt[0, nw).  Returns whether a copy reached before the unit
-// (not in ext mode, where such sources are read from dst); *bad: a copy of offset 0 or before the
-// output start (golang/snappy decode_other.go:104-106).
-__device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, uint8_t* dst, int32_t U0, int32_t U1,
-                        const int2* wt, int32_t nw, bool ext, bool* bad) {
-  const int tid = threadIdx.x;
-  const int32_t ulen = U1 - U0;
-  __syncthreads();  // an earlier unit's readers of L are done
-  if (tid == 0) {  // the last window whose true output base is at or before U0 (wt[0].y == 0)
-    int32_t lo = 0, hi = nw - 1;
-    while (lo < hi) {
-      const int32_t mid = (lo + hi + 1) >> 1;
-      if (wt[mid].y <= U0) lo = mid;
-      else hi = mid - 1;
-    }
-    L.win = lo;
-    L.bad = 0;
-    L.ext = 0;
-  }
-  __syncthreads();
-  const int2 w = wt[L.win];
-  int32_t pos = w.x, o = w.y;
-#ifdef PQH_SNAP_PROF
-  if (tid < 12) L.prof[tid] = 0;
-  uint64_t t0 = clock64();
-#define SN_T(i) do { __syncthreads(); const uint64_t t1 = clock64(); if (tid == 0) L.prof[i] += t1 - t0; t0 = t1; } while (0)
-#else
-#define SN_T(i) do {} while (0)
-#endif
-  while (pos < n && o < U1) {
-    const int32_t a0 = pos - int32_t((reinterpret_cast<uintptr_t>(src) + uintptr_t(pos)) & 15);
-    const int32_t send = a0 + kSnStage < n ? a0 + kSnStage : n;
-    __syncthreads();  // the previous stage's readers are done
-    {
-      const uint4* sp = reinterpret_cast<const uint4*>(src + a0);
-      uint4* lp = reinterpret_cast<uint4*>(L.in);
-      const int32_t nu = (send + 16 - a0 + 15) >> 4;
-      for (int u = tid; u < nu; u += kSnT) lp[u] = sp[u];
-    }
-    if (tid == 0) L.nlong = 0;
-    __syncthreads();
-    const int32_t span = send - pos;
-    const int32_t S = (span + kSnT - 1) / kSnT;
-    const int32_t lo = pos + (S * tid < span ? S * tid : span);
-    const int32_t hi = pos + (S * (tid + 1) < span ? S * (tid + 1) : span);
-    SN_T(0);
-    sn_chain<kSnT>(L.F, L.in, a0, n, lo, hi, pos, pos, pos, kSnWarmE);
-    SN_T(1);
-#ifdef PQH_SNAP_PROF
-    if (tid == 0) L.prof[9] += L.F.rounds;
-#endif
-    if (L.F.first_bad < kSnT) {  // (the stitch accepted this chain: cannot happen)
-      *bad = true;
-      return false;
-    }
-    int32_t Ot, Kt;
-    const int32_t ob = o + sn_block_excl_sum<kSnT>(L.F, L.F.o[tid], &Ot);
-    const int32_t kb = sn_block_excl_sum<kSnT>(L.F, L.F.k[tid], &Kt);
-    const int32_t stage_hi = send + 16;
-    {
-      int32_t q = L.F.f[tid], P = ob, k = kb;
-      while (q < hi && P < U1) {
-        const SnEl e = sn_el(L.in, q - a0);
-        const int32_t len = int32_t(e.len);
-        if (e.lit) {
-          const int32_t body = q + e.hdr;
-          const int32_t b0 = P > U0 ? P : U0, b1 = P + len < U1 ? P + len : U1;
-          if (b0 < b1) {
-            if (b1 - b0 <= 64) {
-              for (int32_t b = b0; b < b1; b++) {
-                const int32_t s = body + (b - P);
-                L.out[b - U0] = s < stage_hi ? L.in[s - a0] : src[s];
-              }
-            } else {
-              const int32_t li = atomicAdd(&L.nlong, 1);
-              L.l_out[li] = b0 - U0;
-              L.l_src[li] = body + (b0 - P);
-              L.l_len[li] = b1 - b0;
-            }
-          }
-          q = body + len;
-        } else {
-          if (P >= U0 && (e.off == 0 || e.off > P)) L.bad = 1;
-          L.cs[k] = P - U0;
-          L.co[k] = e.off;
-          L.cl[k] = P + len > U0 ? uint8_t(len) : 0;  // (P < U1 here)
-          k++;
-          q += e.hdr;
-        }
-        P += len;
-      }
-      for (; k < kb + L.F.k[tid]; k++) {  // copies past the unit
-        L.cs[k] = ulen;
-        L.co[k] = 1;
-        L.cl[k] = 0;
-      }
-    }
-    __syncthreads();
-    if (L.bad) {
-      *bad = true;
-      return false;
-    }
-    SN_T(2);
-    for (int32_t li = 0; li < L.nlong; li++) {
-      const int32_t lo2 = L.l_out[li], ls = L.l_src[li], ln = L.l_len[li];
-      for (int32_t j = tid; j < ln; j += kSnT) L.out[lo2 + j] = src[ls + j];
-    }
-    o += Ot;
-    pos = L.F.x[kSnT - 1];
-    SN_T(3);
-    sn_copies(L, Kt, U0, ulen, ext, dst + U0);
-    SN_T(4);
-#ifdef PQH_SNAP_PROF
-    if (tid == 0) L.prof[8] += 1;
-#endif
-  }
-  __syncthreads();
-  {  // the unit to HBM: bytes until the destination is 16-byte aligned, then 16-byte stores
-    uint8_t* g = dst + U0;
-    const int32_t head0 = int32_t((16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
-    const int32_t head = head0 < ulen ? head0 : ulen;
-    if (tid < head) g[tid] = L.out[tid];
-    const int32_t units = (ulen - head) >> 4;
-    const uint32_t* o32 = reinterpret_cast<const uint32_t*>(L.out);
-    const int32_t sh = 8 * (head & 3);
-    for (int32_t u = tid; u < units; u += kSnT) {
-      const int32_t wb = (head + 16 * u) >> 2;
-      uint32_t v[4];
-      if (sh == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) v[t] = o32[wb + t];
-      } else {
-        uint32_t x[5];
-#pragma unroll
-        for (int t = 0; t < 5; t++) x[t] = o32[wb + t];
-#pragma unroll
-        for (int t = 0; t < 4; t++) v[t] = __builtin_amdgcn_alignbit(x[t + 1], x[t], uint32_t(sh));
-      }
-      *reinterpret_cast<uint4*>(g + head + 16 * u) = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-    const int32_t done = head + units * 16;
-    if (tid < ulen - done) g[done + tid] = L.out[done + tid];
-  }
-  SN_T(5);
-#ifdef PQH_SNAP_PROF
-  if (tid == 0 && blockIdx.x < 2)
-    printf("snapprof unit %d stages %lu | cycles: load %lu chain %lu walk %lu long %lu copies %lu store %lu | rounds %lu jumps %lu spans %lu\n",
-           int(blockIdx.x), L.prof[8], L.prof[0], L.prof[1], L.prof[2], L.prof[3], L.prof[4], L.prof[5], L.prof[9], L.prof[10], L.prof[11]);
-#endif
-  return L.ext != 0;
-}
-
-__global__ __launch_bounds__(kSnT) void k_snap_emit(const pqh_codec_page* cps, const int32_t* unit_page,
-                                                    const int32_t* page_unit0, const int32_t* page_win0,
-                                                    const uint8_t* src_all, uint8_t* dst_all, const int2* wtrue,
-                                                    int32_t* status, int32_t* uflag) {
-  __shared__ SnEmitLds L;
-  const int32_t u = blockIdx.x;
-  const int32_t p = unit_page[u];
-  const int32_t k = u - page_unit0[p];
-  const pqh_codec_page cp = cps[p];
-  uint8_t* dst = dst_all + cp.image_offset;
-  if (cp.codec != PQH_CODEC_SNAPPY) {  // a plain copy, unit by unit
-    const int64_t len = cp.src_len < cp.image_len ? cp.src_len : cp.image_len;
-    const int64_t U0 = int64_t(k) * kSnUnit;
-    const int64_t m = len - U0 < kSnUnit ? len - U0 : kSnUnit;
-    if (m > 0) sn_gcopy(dst + U0, src_all + cp.src_offset + U0, m);
-    return;
-  }
-  if (status[p] != PQH_OK) {
-    if (threadIdx.x == 0) uflag[u] = 0;
-    return;
-  }
-  const int32_t raw = cp.raw_len < cp.src_len ? cp.raw_len : cp.src_len;
-  const int32_t total = cp.image_len - raw;
-  const int32_t U0 = k * kSnUnit, U1 = U0 + kSnUnit < total ? U0 + kSnUnit : total;
-  bool bad = false;
-  const bool ext = sn_unit(L, src_all + cp.src_offset + raw, cp.src_len - raw, dst + raw, U0, U1,
-                           wtrue + page_win0[p], page_win0[p + 1] - page_win0[p], false, &bad);
-  if (threadIdx.x == 0) {
-    uflag[u] = ext && !bad;
-    if (bad) status[p] = PQH_ERR_DECOMPRESS;
-  }
-}
-
-// The units a copy before the unit marked, again in order, their early sources read from HBM.
-__global__ __launch_bounds__(kSnT) void k_snap_fixup(const pqh_codec_page* cps, const int32_t* page_unit0,
-                                                     const int32_t* page_win0, const uint8_t* src_all,
-                                                     uint8_t* dst_all, const int2* wtrue, int32_t* status,
-                                                     const int32_t* uflag) {
-  __shared__ SnEmitLds L;
-  const int32_t p = blockIdx.x;
-  const pqh_codec_page cp = cps[p];
-  if (cp.codec != PQH_CODEC_SNAPPY || status[p] != PQH_OK) return;
-  const int32_t u0 = page_unit0[p], u1 = page_unit0[p + 1];
-  const int32_t raw = cp.raw_len < cp.src_len ? cp.raw_len : cp.src_len;
-  const int32_t total = cp.image_len - raw;
-  for (int32_t u = u0; u < u1; u++) {
-    if (!uflag[u]) continue;
-    const int32_t U0 = (u - u0) * kSnUnit, U1 = U0 + kSnUnit < total ? U0 + kSnUnit : total;
-    bool bad = false;
-    sn_unit(L, src_all + cp.src_offset + raw, cp.src_len - raw, dst_all + cp.image_offset + raw, U0, U1,
-            wtrue + page_win0[p], page_win0[p + 1] - page_win0[p], true, &bad);
-    __threadfence();
-    if (bad) {
-      if (threadIdx.x == 0) status[p] = PQH_ERR_DECOMPRESS;
-      return;
-    }
-  }
-}
+// The emit / fixup kernels: snappy_emit.h.
