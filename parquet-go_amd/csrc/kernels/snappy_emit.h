@@ -5,7 +5,8 @@
 struct __attribute__((aligned(16))) SnEmitLds {
   uint8_t out[kSnUnit + 64];  // the unit's image
   uint8_t in[kSnWin + 64];    // the stage: block bytes [a0, we + 16) of one window
-  uint16_t emap[kSnSpan];     // span byte -> copy (1-based); then (as int16) the byte's pointer
+  uint16_t emap[kSnSpan];     // span byte -> copy (1-based)
+  int16_t ptr[kSnSpan];       // span byte -> the span byte it copies (-1: final in out)
   int32_t cs[kSnMaxC];        // the window's copies: output start (unit-relative), offset, length
   int32_t co[kSnMaxC];
   uint8_t cl[kSnMaxC];
@@ -66,8 +67,6 @@ __device__ __forceinline__ void sn_gcopy(uint8_t* dst, const uint8_t* src, int64
   if (tid < n - done) dst[done + tid] = src[done + tid];
 }
 
-constexpr int kSnChase = 6;  // source hops followed per byte before pointer jumping takes over
-
 // The unit-relative source of byte pos of copy j (overlapping copies repeat their first period).
 __device__ __forceinline__ int32_t sn_csrc(const SnEmitLds& L, int32_t j, int32_t pos) {
   const int32_t cs = L.cs[j], o = L.co[j];
@@ -76,12 +75,10 @@ __device__ __forceinline__ int32_t sn_csrc(const SnEmitLds& L, int32_t j, int32_
 }
 
 // The window's K copies (unit-relative output start cs, offset co, length cl, 0 when the copy has
-// no byte in the unit; in output order) resolved into L.out, span by span.  A span byte is a
-// literal / gap byte (final in L.out) or a copy byte; a copy byte follows its source back up to
-// kSnChase hops (through the span's copy map) until it reaches a final byte: a literal byte of the
-// span, a byte before the span (final in L.out) or, before the unit, a byte of an earlier unit
-// (read from dst_unit in ext mode, else the unit is marked).  Bytes still on a copy after that
-// point at it, and pointer jumping over the span resolves them in O(log length) rounds.
+// no byte in the unit; in output order) resolved into L.out, span by span: an output-byte -> copy
+// map (start markers, max-scan) gives every copy byte its source; sources before the span (final
+// in L.out; before the unit: an earlier unit's bytes, read from dst_unit in ext mode, else the unit
+// is marked) and literal bytes resolve at once, the rest by pointer jumping over the span.
 __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, bool ext, const uint8_t* dst_unit) {
   const int tid = threadIdx.x;
   int32_t i = 0;
@@ -160,76 +157,63 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
       for (int k = 0; k < kSnPer / 8; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
     }
     __syncthreads();
-    // every copy byte chases its source; resolved bytes go to L.out at once (the chase reads only
-    // final bytes of L.out: literal bytes and bytes before the span)
-    int16_t ptr[kSnPer];
-    int pending = 0;
-#pragma unroll
+    // pass 1: every copy byte's source; a source before the span (final) or on a literal byte of
+    // the span resolves the byte at once (its value to L.out, then P = -1); any other byte points
+    // at its source's span byte (P >= 0)
+#pragma unroll 4
     for (int q = 0; q < kSnPer; q++) {
       const int32_t b = q * kSnT + tid;
-      ptr[q] = -1;
       if (b >= T) continue;
       const int32_t pos = B0 + b;
       int e = L.emap[b];
       int32_t j = i + e - 1;
-      if (e == 0 || pos >= L.cs[j] + L.cl[j] || L.co[j] <= 0) continue;  // a literal byte (or a failed page)
-      int32_t s = sn_csrc(L, j, pos);
-      int hop = 0;
-      for (;; hop++) {
-        if (s < B0) break;
-        e = L.emap[s - B0];
-        j = i + e - 1;
-        if (e == 0 || s >= L.cs[j] + L.cl[j] || L.co[j] <= 0 || hop == kSnChase) break;
-        s = sn_csrc(L, j, s);
+      int16_t ptr = -1;
+      if (e != 0 && pos < L.cs[j] + L.cl[j] && L.co[j] > 0) {
+        const int32_t s = sn_csrc(L, j, pos);
+        if (s >= B0) {
+          const int e2 = L.emap[s - B0];
+          const int32_t j2 = i + e2 - 1;
+          if (e2 != 0 && s < L.cs[j2] + L.cl[j2] && L.co[j2] > 0) ptr = int16_t(s - B0);
+          else L.out[pos] = L.out[s];  // a literal byte of the span
+        } else if (s >= 0) {
+          L.out[pos] = L.out[s];
+        } else if (ext) {
+          L.out[pos] = U0 + s >= 0 ? dst_unit[s] : 0;  // (before the output start: its owner failed the page)
+        } else {
+          L.ext = 1;
+        }
       }
-      if (s >= B0 && hop == kSnChase) {  // still on a copy: pointer jumping
-        ptr[q] = int16_t(s - B0);
-        pending = 1;
-        continue;
-      }
-      uint8_t v = 0;
-      if (s >= 0) {
-        v = L.out[s];
-      } else if (ext) {
-        if (U0 + s >= 0) v = dst_unit[s];  // (before the output start: its owner failed the page)
-      } else {
-        L.ext = 1;
-      }
-      L.out[pos] = v;
+      L.ptr[b] = ptr;
     }
-    if (__syncthreads_or(pending)) {
-      int16_t* P = reinterpret_cast<int16_t*>(L.emap);  // emap no longer read: the pointer array
-#pragma unroll
+    __syncthreads();
+    // pass 2: pointer jumping without barriers.  A byte whose pointer reaches a resolved byte takes
+    // its value (L.out written before P = -1: a wave's LDS writes land in order, so whoever sees
+    // P = -1 reads the final byte); otherwise it jumps to its target's pointer.  Any pointer a byte
+    // reads (old or already jumped) is a valid earlier byte of its chain, so the chains shorten
+    // until every byte is resolved.
+    for (;;) {
+      int pending = 0;
+#pragma unroll 4
       for (int q = 0; q < kSnPer; q++) {
         const int32_t b = q * kSnT + tid;
-        if (b < T) P[b] = ptr[q];
-      }
-      __syncthreads();
-      for (;;) {
-        int more = 0;
-        uint8_t val[kSnPer];
-#pragma unroll
-        for (int q = 0; q < kSnPer; q++) {
-          val[q] = 0;
-          if (ptr[q] < 0) continue;
-          const int16_t t = P[ptr[q]];
-          if (t < 0) val[q] = L.out[B0 + ptr[q]];
-          else more = 1;
-          ptr[q] = t;
+        if (b >= T) continue;
+        volatile int16_t* vp = L.ptr;
+        const int16_t p = vp[b];
+        if (p < 0) continue;
+        const int16_t t = vp[p];
+        if (t < 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // p's byte was written before its -1
+          L.out[B0 + b] = L.out[B0 + p];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          vp[b] = -1;
+        } else {
+          vp[b] = t;
+          pending = 1;
         }
-        more = __syncthreads_or(more);
-#pragma unroll
-        for (int q = 0; q < kSnPer; q++) {
-          const int32_t b = q * kSnT + tid;
-          if (b < T && P[b] >= 0) {  // (this thread's own entries: no other thread writes them)
-            P[b] = ptr[q];
-            if (ptr[q] < 0) L.out[B0 + b] = val[q];
-          }
-        }
-        __syncthreads();
-        if (!more) break;
       }
+      if (!pending) break;
     }
+    __syncthreads();
     i = i1;
   }
 }
