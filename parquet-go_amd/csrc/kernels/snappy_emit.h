@@ -7,6 +7,7 @@ struct __attribute__((aligned(16))) SnEmitLds {
   uint8_t in[kSnWin + 64];    // the stage: block bytes [a0, we + 16) of one window
   uint16_t emap[kSnSpan];     // span byte -> copy (1-based)
   int16_t ptr[kSnSpan];       // span byte -> the span byte it copies (-1: final in out)
+  uint32_t cbit[kSnSpan / 32];  // the span's copy bytes
   int32_t cs[kSnMaxC];        // the window's copies: output start (unit-relative), offset, length
   int32_t co[kSnMaxC];
   uint8_t cl[kSnMaxC];
@@ -94,6 +95,7 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
       uint4* m4 = reinterpret_cast<uint4*>(L.emap) + tid * (kSnPer / 8);
 #pragma unroll
       for (int k = 0; k < kSnPer / 8; k++) m4[k] = make_uint4(0, 0, 0, 0);
+      for (int k = tid; k < kSnSpan / 32; k += kSnT) L.cbit[k] = 0;
     }
     __syncthreads();
     {
@@ -118,6 +120,12 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
         const int32_t e = L.cs[j] + L.cl[j] < ulen ? L.cs[j] + L.cl[j] : ulen;
         L.emap[st - B0] = uint16_t(j - i + 1);
         tm = e - B0 > tm ? e - B0 : tm;
+        for (int32_t x = st - B0; x < e - B0;) {
+          const int32_t wq = x >> 5, b0 = x & 31;
+          const int32_t nb = e - B0 - x < 32 - b0 ? e - B0 - x : 32 - b0;
+          atomicOr(&L.cbit[wq], (nb == 32 ? ~0u : ((1u << nb) - 1)) << b0);
+          x += nb;
+        }
       }
       tm = wave_max32(tm);
       if ((tid & 63) == 0 && tm > 0) atomicMax(&L.tmax, tm);
@@ -158,32 +166,46 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     }
     __syncthreads();
     // pass 1: every copy byte's source; a source before the span (final) or on a literal byte of
-    // the span resolves the byte at once (its value to L.out, then P = -1); any other byte points
-    // at its source's span byte (P >= 0)
-#pragma unroll 4
-    for (int q = 0; q < kSnPer; q++) {
-      const int32_t b = q * kSnT + tid;
-      if (b >= T) continue;
-      const int32_t pos = B0 + b;
-      int e = L.emap[b];
-      int32_t j = i + e - 1;
-      int16_t ptr = -1;
-      if (e != 0 && pos < L.cs[j] + L.cl[j] && L.co[j] > 0) {
-        const int32_t s = sn_csrc(L, j, pos);
-        if (s >= B0) {
-          const int e2 = L.emap[s - B0];
-          const int32_t j2 = i + e2 - 1;
-          if (e2 != 0 && s < L.cs[j2] + L.cl[j2] && L.co[j2] > 0) ptr = int16_t(s - B0);
-          else L.out[pos] = L.out[s];  // a literal byte of the span
-        } else if (s >= 0) {
-          L.out[pos] = L.out[s];
-        } else if (ext) {
-          L.out[pos] = U0 + s >= 0 ? dst_unit[s] : 0;  // (before the output start: its owner failed the page)
-        } else {
-          L.ext = 1;
-        }
+    // the span (its bit clear) resolves the byte at once; any other byte points at its source's
+    // span byte (P >= 0).  Four bytes' lookups in flight before their stores.
+#pragma unroll
+    for (int q0 = 0; q0 < kSnPer; q0 += 4) {
+      int32_t pos[4], src[4];
+      int kind[4];  // 0 none, 1 value from L.out[src], 2 pointer, 3 before the unit
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t b = (q0 + k) * kSnT + tid;
+        pos[k] = B0 + b;
+        kind[k] = 0;
+        src[k] = 0;
+        if (b >= T) continue;
+        const int e = L.emap[b];
+        if (e == 0) continue;
+        const int32_t j = i + e - 1;
+        const int32_t cs = L.cs[j], o = L.co[j], len = L.cl[j];
+        if (pos[k] >= cs + len || o <= 0) continue;  // a literal byte (or a failed page)
+        const int32_t rel = pos[k] - cs;
+        const int32_t s2 = cs - o + (o < len ? rel % o : rel);  // overlapping copies repeat
+        src[k] = s2;
+        if (s2 < 0) kind[k] = 3;
+        else if (s2 < B0) kind[k] = 1;
+        else kind[k] = ((L.cbit[(s2 - B0) >> 5] >> ((s2 - B0) & 31)) & 1) ? 2 : 1;
       }
-      L.ptr[b] = ptr;
+      uint8_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        v[k] = 0;
+        if (kind[k] == 1) v[k] = L.out[src[k]];
+        else if (kind[k] == 3 && ext && U0 + src[k] >= 0) v[k] = dst_unit[src[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t b = (q0 + k) * kSnT + tid;
+        if (b >= T) continue;
+        if (kind[k] == 1 || (kind[k] == 3 && ext)) L.out[pos[k]] = v[k];
+        if (kind[k] == 3 && !ext) L.ext = 1;
+        L.ptr[b] = kind[k] == 2 ? int16_t(src[k] - B0) : int16_t(-1);
+      }
     }
     __syncthreads();
     // pass 2: pointer jumping without barriers.  A byte whose pointer reaches a resolved byte takes

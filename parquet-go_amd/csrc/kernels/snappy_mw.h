@@ -36,7 +36,7 @@ constexpr int kSnWarm0 = 256;                // warm-up of a window's first thre
 constexpr int kSnWarm = 128;                 // warm-up of every other thread (spec windows, 16-byte segments)
 constexpr int kSnUnit = 65536;               // output bytes per emit unit
 constexpr int kSnSpan = 16384;               // output bytes per copy-resolution span
-constexpr int kSnT = 512;                    // emit / fixup threads
+constexpr int kSnT = 1024;                   // emit / fixup threads
 constexpr int kSnPer = kSnSpan / kSnT;       // span bytes per thread
 constexpr int kSnMaxC = kSnWin / 2 + 16;     // copies starting in one window (a copy is >= 2 bytes)
 constexpr int kSnMaxL = kSnWin / 64 + 4;     // literals of > 64 unit bytes starting in one window
