@@ -83,6 +83,20 @@ __device__ __forceinline__ int32_t sn_csrc(const SnEmitLds& L, int32_t j, int32_
 __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, bool ext, const uint8_t* dst_unit) {
   const int tid = threadIdx.x;
   int32_t i = 0;
+#ifdef PQH_SNAP_PROF
+  uint64_t c0t = clock64();
+#define SC_T(k)                                     \
+  do {                                              \
+    __syncthreads();                                \
+    const uint64_t c1t = clock64();                 \
+    if (tid == 0) L.prof[k] += c1t - c0t;           \
+    c0t = c1t;                                      \
+  } while (0)
+#else
+#define SC_T(k) \
+  do {          \
+  } while (0)
+#endif
   while (i < K) {
     const int32_t c0 = L.cs[i];
     const int32_t B0 = c0 < 0 ? 0 : (c0 > ulen ? ulen : c0);
@@ -165,10 +179,11 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
       for (int k = 0; k < kSnPer / 8; k++) m4[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
     }
     __syncthreads();
+    SC_T(5);
     // pass 1: every copy byte's source; a source before the span (final) or on a literal byte of
     // the span (its bit clear) resolves the byte at once; any other byte points at its source's
     // span byte (P >= 0).  Four bytes' lookups in flight before their stores.
-#pragma unroll
+#pragma unroll 1
     for (int q0 = 0; q0 < kSnPer; q0 += 4) {
       int32_t pos[4], src[4];
       int kind[4];  // 0 none, 1 value from L.out[src], 2 pointer, 3 before the unit
@@ -213,38 +228,55 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     // P = -1 reads the final byte); otherwise it jumps to its target's pointer.  Any pointer a byte
     // reads (old or already jumped) is a valid earlier byte of its chain, so the chains shorten
     // until every byte is resolved.
+    SC_T(6);
     for (;;) {
+#ifdef PQH_SNAP_PROF
+      if (tid == 0) L.prof[10] += 1;
+#endif
       int pending = 0;
-#pragma unroll 4
-      for (int q = 0; q < kSnPer; q++) {
-        const int32_t b = q * kSnT + tid;
-        if (b >= T) continue;
-        volatile int16_t* vp = L.ptr;
-        const int16_t p = vp[b];
-        if (p < 0) continue;
-        const int16_t t = vp[p];
-        if (t < 0) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // p's byte was written before its -1
-          L.out[B0 + b] = L.out[B0 + p];
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          vp[b] = -1;
-        } else {
-          vp[b] = t;
-          pending = 1;
+#pragma unroll 1
+      for (int q0 = 0; q0 < kSnPer; q0 += 4) {  // four bytes' loads in flight together
+        int16_t p[4], t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int32_t b = (q0 + k) * kSnT + tid;
+          p[k] = b < T ? __atomic_load_n(&L.ptr[b], __ATOMIC_RELAXED) : int16_t(-1);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k] = p[k] >= 0 ? __atomic_load_n(&L.ptr[p[k]], __ATOMIC_RELAXED) : int16_t(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // a -1 read above: its byte is final
+        uint8_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = (p[k] >= 0 && t[k] < 0) ? L.out[B0 + p[k]] : uint8_t(0);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (p[k] >= 0 && t[k] < 0) L.out[B0 + (q0 + k) * kSnT + tid] = v[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the bytes before their -1
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (p[k] < 0) continue;
+          __atomic_store_n(&L.ptr[(q0 + k) * kSnT + tid], t[k] < 0 ? int16_t(-1) : t[k], __ATOMIC_RELAXED);
+          pending |= t[k] >= 0;
         }
       }
       if (!pending) break;
     }
     __syncthreads();
+    SC_T(7);
+#ifdef PQH_SNAP_PROF
+    if (tid == 0) L.prof[11] += 1;
+#endif
     i = i1;
   }
+#undef SC_T
 }
 
 // One unit [U0, U1) of a SNAPPY block's output: block src[0, n) (header length hl), output at dst
 // (after the raw prefix), true window entries / bases wt[0, nw) and per-thread segment entries
 // wseg (k_snap_spec / k_snap_stitch).  The unit's windows are walked in order from the last one
-// whose output base is at or before U0: every thread walks its 16-byte segment from its exact
-// entry, once to count (output bytes, copies), once to place literal bytes and list copies.
+// whose output base is at or before U0: every segment walker walks its 16-byte segment from its
+// exact entry, once to count (output bytes, copies, literals), once to list literals and copies;
+// waves then copy the literals (a lane per byte) and sn_copies resolves the copies.
 // Returns whether a copy reached before the unit (not in ext mode, where such sources are read
 // from dst); *bad: a copy of offset 0 or reaching before the output start (golang/snappy
 // decode_other.go:104-106).
@@ -302,42 +334,52 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
     if (tid == 0) L.nlong = 0;
     const int32_t span = we - ws;
     const int32_t S = (span + kBlock - 1) / kBlock;
-    const int32_t hi = tid < kBlock ? ws + (S * (tid + 1) < span ? S * (tid + 1) : span) : we;
-    const int32_t f = tid < kBlock ? wseg[int64_t(w) * kBlock + tid] : we;
+    // the 256 segment walkers are lanes 0..15 of every wave (walker = wave * 16 + lane), so that
+    // all 16 waves share the walks' latency; walker order is thread order for the scans
+    const int wk = (tid & 63) < 16 ? (tid >> 6) * 16 + (tid & 63) : -1;
+    const int32_t hi = wk >= 0 ? ws + (S * (wk + 1) < span ? S * (wk + 1) : span) : we;
+    const int32_t f = wk >= 0 ? wseg[int64_t(w) * kBlock + wk] : we;
     __syncthreads();
     SN_T(0);
-    int32_t ot = 0, kt = 0;
+    int32_t ot = 0, kt = 0, nlit = 0;
     for (int32_t q = f; q < hi && q < n;) {
       const SnEl e = sn_el(L.in, q - a0);
       ot += int32_t(e.len);
       kt += !e.lit;
+      nlit += e.lit;
       q += e.hdr + (e.lit ? int32_t(e.len) : 0);
     }
-    int32_t Ot, Kt;
+    int32_t Ot, Kt, Lt;
     const int32_t ob = tw.y + sn_excl_sum(L, ot, &Ot);
     const int32_t kb = sn_excl_sum(L, kt, &Kt);
+    const int32_t lb = sn_excl_sum(L, nlit, &Lt);
+    SN_T(9);
+    int32_t* lit_out = reinterpret_cast<int32_t*>(L.emap);  // the literal list (emap is free until sn_copies)
+    int32_t* lit_src = lit_out + kSnMaxC;
+    int32_t* lit_len = lit_src + kSnMaxC;
     const int32_t stage_hi = we + 16;
     {
-      int32_t q = f, P = ob, k = kb;
+      int32_t q = f, P = ob, k = kb, li = lb;
       while (q < hi && q < n && P < U1) {
         const SnEl e = sn_el(L.in, q - a0);
         const int32_t len = int32_t(e.len);
         if (e.lit) {
           const int32_t body = q + e.hdr;
           const int32_t b0 = P > U0 ? P : U0, b1 = P + len < U1 ? P + len : U1;
+          lit_out[li] = b0 - U0;
+          lit_src[li] = body + (b0 - P);
+          lit_len[li] = 0;
           if (b0 < b1) {
-            if (b1 - b0 <= 64) {
-              for (int32_t b = b0; b < b1; b++) {
-                const int32_t s = body + (b - P);
-                L.out[b - U0] = s < stage_hi ? L.in[s - a0] : src[s];
-              }
-            } else {
-              const int32_t li = atomicAdd(&L.nlong, 1);
-              L.l_out[li] = b0 - U0;
-              L.l_src[li] = body + (b0 - P);
-              L.l_len[li] = b1 - b0;
+            if (b1 - b0 <= kSnLongLit) {
+              lit_len[li] = b1 - b0;
+            } else {  // long: copied by the whole workgroup
+              const int32_t lg = atomicAdd(&L.nlong, 1);
+              L.l_out[lg] = b0 - U0;
+              L.l_src[lg] = body + (b0 - P);
+              L.l_len[lg] = b1 - b0;
             }
           }
+          li++;
           q = body + len;
         } else {
           if (P >= U0 && (e.off == 0 || e.off > P)) L.bad = 1;
@@ -354,12 +396,23 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
         L.co[k] = 1;
         L.cl[k] = 0;
       }
+      for (; li < lb + nlit; li++) lit_len[li] = 0;  // literals past the unit
     }
     __syncthreads();
     SN_T(1);
     if (L.bad) {
       *bad = true;
       return false;
+    }
+    {  // short literals: one wave each, a lane per byte (stage bytes, or HBM past the stage)
+      const int lane = tid & 63;
+      for (int32_t e = tid >> 6; e < Lt; e += kSnT / 64) {
+        const int32_t ln = lit_len[e], lo2 = lit_out[e], ls = lit_src[e];
+        for (int32_t x = lane; x < ln; x += 64) {
+          const int32_t sx = ls + x;
+          L.out[lo2 + x] = sx < stage_hi ? L.in[sx - a0] : src[sx];
+        }
+      }
     }
     for (int32_t li = 0; li < L.nlong; li++) {
       const int32_t lo2 = L.l_out[li], ls = L.l_src[li], ln = L.l_len[li];
@@ -403,8 +456,10 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
   SN_T(4);
 #ifdef PQH_SNAP_PROF
   if (tid == 0 && blockIdx.x < 2)
-    printf("snapprof unit %d windows %lu | cycles: load %lu walks %lu long %lu copies %lu store %lu\n", int(blockIdx.x),
-           L.prof[8], L.prof[0], L.prof[1], L.prof[2], L.prof[3], L.prof[4]);
+    printf("snapprof unit %d windows %lu | cycles: load %lu walks %lu lits %lu copies %lu (setup %lu pass1 %lu jump %lu; "
+           "spans %lu thread-rounds(t0) %lu) store %lu\n", int(blockIdx.x), L.prof[8], L.prof[0], L.prof[1], L.prof[2],
+           L.prof[3], L.prof[5], L.prof[6], L.prof[7], L.prof[11], L.prof[10], L.prof[4]);
+  if (tid == 0 && blockIdx.x < 2) printf("snapprof unit %d walk1+scans %lu walk2 %lu\n", int(blockIdx.x), L.prof[9], L.prof[1]);
 #endif
 #undef SN_T
   return L.ext != 0;

@@ -39,7 +39,8 @@ constexpr int kSnSpan = 16384;               // output bytes per copy-resolution
 constexpr int kSnT = 1024;                   // emit / fixup threads
 constexpr int kSnPer = kSnSpan / kSnT;       // span bytes per thread
 constexpr int kSnMaxC = kSnWin / 2 + 16;     // copies starting in one window (a copy is >= 2 bytes)
-constexpr int kSnMaxL = kSnWin / 64 + 4;     // literals of > 64 unit bytes starting in one window
+constexpr int kSnLongLit = 1024;             // literals of more unit bytes are copied by the whole workgroup
+constexpr int kSnMaxL = kSnWin / kSnLongLit + 4;  // (at most this many start in one window)
 constexpr int kSnSpecStage = kSnWin + kSnWarm0 + 64;
 constexpr int kSnSpecRounds = 12;            // a speculative window that needs more rounds (inside a long
                                              // literal, usually) is left to the stitch
