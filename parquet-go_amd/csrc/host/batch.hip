@@ -1581,9 +1581,9 @@ int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
   int4* ws = nullptr;
   int2* wt = nullptr;
   int32_t* uf = nullptr;
-  int32_t* seg = nullptr;
+  int16_t* seg = nullptr;
   int rc;
-  if ((rc = dalloc(b, reinterpret_cast<void**>(&seg), sizeof(int32_t) * 256 * size_t(P.n_win))) ||
+  if ((rc = dalloc(b, reinterpret_cast<void**>(&seg), sizeof(int16_t) * 1024 * size_t(P.n_win))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&tab), sizeof(int32_t) * t.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&ws), sizeof(int4) * size_t(P.n_win))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&wt), sizeof(int2) * size_t(P.n_win))) ||
@@ -1747,7 +1747,7 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit);
   const size_t tb = (sizeof(int32_t) * tab.size() + 15) & ~size_t(15);
   const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) +
-                    sizeof(int32_t) * 256 * size_t(P.n_win) + 16;
+                    sizeof(int16_t) * 1024 * size_t(P.n_win) + 16;
   void* scratch = nullptr;
   if (e == hipSuccess) e = hipMalloc(&scratch, sb);
   if (e == hipSuccess) e = bounce_h2d(ctx, scratch, tab.data(), sizeof(int32_t) * tab.size());
@@ -1756,7 +1756,7 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
     int4* ws = reinterpret_cast<int4*>(m + tb);
     int2* wt = reinterpret_cast<int2*>(ws + P.n_win);
     int32_t* uf = reinterpret_cast<int32_t*>(wt + P.n_win);
-    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, uf, uf + P.n_unit);
+    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, uf, reinterpret_cast<int16_t*>(uf + P.n_unit));
     e = snappy_page_mode()
             ? launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream)
             : launch_snappy_mw(dp, P, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);

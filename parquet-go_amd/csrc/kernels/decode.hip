@@ -1212,7 +1212,7 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
   return t;
 }
 
-void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int32_t* wseg) {
+void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int16_t* wseg) {
   P.wseg = wseg;
   P.page_win0 = tables;
   P.page_unit0 = tables + P.n_pages + 1;

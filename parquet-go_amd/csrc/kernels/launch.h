@@ -48,11 +48,11 @@ struct SnapPlan {
   int4* wspec = nullptr;          // [n_win] speculative window results (first element, exit, output, status)
   int2* wtrue = nullptr;          // [n_win] true entry, output base
   int32_t* uflag = nullptr;       // [n_unit] a copy reached before the unit (k_snap_fixup redoes it)
-  int32_t* wseg = nullptr;        // [n_win * 256] every window segment's exact first element
+  int16_t* wseg = nullptr;        // [n_win * 1024] every walker segment's exact first element (window-relative)
 };
 // Host tables page_win0 | page_unit0 | win_page | unit_page of a codec page list (device copy: bind).
 std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit);
-void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int32_t* wseg);
+void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int16_t* wseg);
 hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, const uint8_t* src, uint8_t* dst,
                             int32_t* status, hipStream_t s);
 // GZIP pages of the same table (one workgroup per page; the other pages' workgroups exit at once).

@@ -274,14 +274,14 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
 // One unit [U0, U1) of a SNAPPY block's output: block src[0, n) (header length hl), output at dst
 // (after the raw prefix), true window entries / bases wt[0, nw) and per-thread segment entries
 // wseg (k_snap_spec / k_snap_stitch).  The unit's windows are walked in order from the last one
-// whose output base is at or before U0: every segment walker walks its 16-byte segment from its
+// whose output base is at or before U0: every thread walks its 4-byte walker segment from its
 // exact entry, once to count (output bytes, copies, literals), once to list literals and copies;
 // waves then copy the literals (a lane per byte) and sn_copies resolves the copies.
 // Returns whether a copy reached before the unit (not in ext mode, where such sources are read
 // from dst); *bad: a copy of offset 0 or reaching before the output start (golang/snappy
 // decode_other.go:104-106).
 __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl, uint8_t* dst, int32_t U0, int32_t U1,
-                        const int2* wt, const int32_t* wseg, int32_t nw, bool ext, bool* bad) {
+                        const int2* wt, const int16_t* wseg, int32_t nw, bool ext, bool* bad) {
   const int tid = threadIdx.x;
   const int32_t ulen = U1 - U0;
   __syncthreads();  // an earlier unit's readers of L are done
@@ -333,12 +333,10 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
     }
     if (tid == 0) L.nlong = 0;
     const int32_t span = we - ws;
-    const int32_t S = (span + kBlock - 1) / kBlock;
-    // the 256 segment walkers are lanes 0..15 of every wave (walker = wave * 16 + lane), so that
-    // all 16 waves share the walks' latency; walker order is thread order for the scans
-    const int wk = (tid & 63) < 16 ? (tid >> 6) * 16 + (tid & 63) : -1;
-    const int32_t hi = wk >= 0 ? ws + (S * (wk + 1) < span ? S * (wk + 1) : span) : we;
-    const int32_t f = wk >= 0 ? wseg[int64_t(w) * kBlock + wk] : we;
+    const int32_t S4 = (span + kSnT - 1) / kSnT;
+    // one walker segment per thread, from the entry the spec / stitch left for it
+    const int32_t hi = ws + (S4 * (tid + 1) < span ? S4 * (tid + 1) : span);
+    const int32_t f = ws + wseg[int64_t(w) * kSnT + tid];
     __syncthreads();
     SN_T(0);
     int32_t ot = 0, kt = 0, nlit = 0;
@@ -468,7 +466,7 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
 __global__ __launch_bounds__(kSnT) void k_snap_emit(const pqh_codec_page* cps, const int32_t* unit_page,
                                                     const int32_t* page_unit0, const int32_t* page_win0,
                                                     const uint8_t* src_all, uint8_t* dst_all, const int2* wtrue,
-                                                    const int32_t* wseg, int32_t* status, int32_t* uflag) {
+                                                    const int16_t* wseg, int32_t* status, int32_t* uflag) {
   __shared__ SnEmitLds L;
   const int32_t u = blockIdx.x;
   const int32_t p = unit_page[u];
@@ -495,7 +493,7 @@ __global__ __launch_bounds__(kSnT) void k_snap_emit(const pqh_codec_page* cps, c
   const int32_t U0 = k * kSnUnit, U1 = U0 + kSnUnit < total ? U0 + kSnUnit : total;
   const int32_t w0 = page_win0[p];
   bool bad = false;
-  const bool ext = sn_unit(L, src, n, hl, dst + raw, U0, U1, wtrue + w0, wseg + int64_t(w0) * kBlock,
+  const bool ext = sn_unit(L, src, n, hl, dst + raw, U0, U1, wtrue + w0, wseg + int64_t(w0) * kSnT,
                            page_win0[p + 1] - w0, false, &bad);
   if (threadIdx.x == 0) {
     uflag[u] = ext && !bad;
@@ -506,7 +504,7 @@ __global__ __launch_bounds__(kSnT) void k_snap_emit(const pqh_codec_page* cps, c
 // The units a copy before the unit marked, again in order, their early sources read from HBM.
 __global__ __launch_bounds__(kSnT) void k_snap_fixup(const pqh_codec_page* cps, const int32_t* page_unit0,
                                                      const int32_t* page_win0, const uint8_t* src_all,
-                                                     uint8_t* dst_all, const int2* wtrue, const int32_t* wseg,
+                                                     uint8_t* dst_all, const int2* wtrue, const int16_t* wseg,
                                                      int32_t* status, const int32_t* uflag) {
   __shared__ SnEmitLds L;
   const int32_t p = blockIdx.x;
@@ -524,7 +522,7 @@ __global__ __launch_bounds__(kSnT) void k_snap_fixup(const pqh_codec_page* cps, 
     if (!uflag[u]) continue;
     const int32_t U0 = (u - u0) * kSnUnit, U1 = U0 + kSnUnit < total ? U0 + kSnUnit : total;
     bool bad = false;
-    sn_unit(L, src, n, hl, dst_all + cp.image_offset + raw, U0, U1, wtrue + w0, wseg + int64_t(w0) * kBlock,
+    sn_unit(L, src, n, hl, dst_all + cp.image_offset + raw, U0, U1, wtrue + w0, wseg + int64_t(w0) * kSnT,
             page_win0[p + 1] - w0, true, &bad);
     __threadfence();
     if (bad) {

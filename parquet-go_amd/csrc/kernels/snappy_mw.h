@@ -36,7 +36,8 @@ constexpr int kSnWarm0 = 256;                // warm-up of a window's first thre
 constexpr int kSnWarm = 128;                 // warm-up of every other thread (spec windows, 16-byte segments)
 constexpr int kSnUnit = 65536;               // output bytes per emit unit
 constexpr int kSnSpan = 16384;               // output bytes per copy-resolution span
-constexpr int kSnT = 1024;                   // emit / fixup threads
+constexpr int kSnT = 1024;                   // emit / fixup threads (= window walkers)
+constexpr int kSnSub = kSnT / kBlock;        // walker segments per spec thread
 constexpr int kSnPer = kSnSpan / kSnT;       // span bytes per thread
 constexpr int kSnMaxC = kSnWin / 2 + 16;     // copies starting in one window (a copy is >= 2 bytes)
 constexpr int kSnLongLit = 1024;             // literals of more unit bytes are copied by the whole workgroup
@@ -274,6 +275,7 @@ __device__ __forceinline__ int32_t sn_header(const uint8_t* src, int32_t n, uint
 struct __attribute__((aligned(16))) SnSpecLds {
   uint8_t in[kSnSpecStage];
   SnFix<kBlock> F;
+  int16_t sub[kSnSub * kBlock];  // walker segment entries (sn_window)
   int32_t c_mis, c_e, c_O, c_bad;
 };
 
@@ -295,7 +297,9 @@ __device__ int4 sn_window(SnSpecLds& L, const uint8_t* src, int32_t n, int32_t h
   }
   __syncthreads();
   const int32_t span = we > ws ? we - ws : 0;
-  const int32_t S = (span + kBlock - 1) / kBlock;
+  // thread segments of kSnSub walker segments each (the emit units walk the window with one
+  // walker per kSnT thread, from the entries this window leaves behind)
+  const int32_t S4 = (span + kSnT - 1) / kSnT, S = kSnSub * S4;
   const int32_t lo = ws + (S * tid < span ? S * tid : span);
   const int32_t hi = ws + (S * (tid + 1) < span ? S * (tid + 1) : span);
   const int32_t count0 = exact ? entry : ws;
@@ -308,12 +312,25 @@ __device__ int4 sn_window(SnSpecLds& L, const uint8_t* src, int32_t n, int32_t h
   r.y = fb < kBlock ? L.F.x[fb] : L.F.x[kBlock - 1];
   r.z = osum;
   r.w = L.F.unsettled ? 3 : (fb < kBlock ? 2 : 0);
+  {  // every walker segment's first element (window-relative; we - ws: none in the window)
+    int32_t q = L.F.f[tid];
+#pragma unroll
+    for (int k = 0; k < kSnSub; k++) {
+      const int32_t b = lo + k * S4 < hi ? lo + k * S4 : hi;
+      while (q < b && q < n && q < hi) {
+        const SnEl e = sn_el(L.in, q - a0);
+        const int64_t nx = int64_t(q) + e.hdr + (e.lit ? e.len : 0);
+        q = nx > n ? n : int32_t(nx);
+      }
+      L.sub[kSnSub * tid + k] = int16_t((q < we ? q : we) - ws);
+    }
+  }
   return r;
 }
 
 __global__ __launch_bounds__(256) void k_snap_spec(const pqh_codec_page* cps, const int32_t* win_page,
                                                    const int32_t* page_win0, const uint8_t* src_all, int4* wspec,
-                                                   int32_t* wseg) {
+                                                   int16_t* wseg) {
   __shared__ SnSpecLds L;
   const int32_t w = blockIdx.x;
   const int32_t p = win_page[w];
@@ -329,13 +346,14 @@ __global__ __launch_bounds__(256) void k_snap_spec(const pqh_codec_page* cps, co
   }
   const int4 r = sn_window(L, src, n, hl, w - page_win0[p], -1);
   if (threadIdx.x == 0) wspec[w] = r;
-  wseg[int64_t(w) * kBlock + threadIdx.x] = L.F.f[threadIdx.x];  // exact when the stitch accepts the guess
+  // exact when the stitch accepts the guess
+  reinterpret_cast<uint2*>(wseg + int64_t(w) * kSnT)[threadIdx.x] = reinterpret_cast<const uint2*>(L.sub)[threadIdx.x];
 }
 
 // Per page: status, true window entries / output bases, V2 level bytes.
 __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, const int32_t* page_win0,
                                                      const uint8_t* src_all, uint8_t* dst_all, const int4* wspec,
-                                                     int2* wtrue, int32_t* wseg, int32_t* status) {
+                                                     int2* wtrue, int16_t* wseg, int32_t* status) {
   __shared__ SnSpecLds L;
   const int tid = threadIdx.x, lane = tid & 63;
   const int32_t p = blockIdx.x;
@@ -409,7 +427,7 @@ __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, 
     if (found == 1) {  // window c guessed its entry wrong: parse it from the true entry
       const int4 r = sn_window(L, src, n, hl, c, e);
       if (tid == 0) wtrue[w0 + c] = make_int2(e, O);
-      wseg[int64_t(w0 + c) * kBlock + tid] = L.F.f[tid];
+      reinterpret_cast<uint2*>(wseg + int64_t(w0 + c) * kSnT)[tid] = reinterpret_cast<const uint2*>(L.sub)[tid];
       if (r.w) {
         bad = true;
         break;
