@@ -8,9 +8,8 @@ struct __attribute__((aligned(16))) SnEmitLds {
   uint16_t emap[kSnSpan];     // span byte -> copy (1-based)
   int16_t ptr[kSnSpan];       // span byte -> the span byte it copies (-1: final in out)
   uint32_t cbit[kSnSpan / 32];  // the span's copy bytes
-  int32_t cs[kSnMaxC];        // the window's copies: output start (unit-relative), offset, length
-  int32_t co[kSnMaxC];
-  uint8_t cl[kSnMaxC];
+  int2 cp[kSnMaxC];           // the window's copies: output start (unit-relative) | offset (clamped to
+                              // 2^24 - 1: any larger one reaches before the unit) + length << 24
   int32_t l_out[kSnMaxL], l_src[kSnMaxL], l_len[kSnMaxL];  // literals of > 64 unit bytes
   int32_t wred[kSnT / 64];
   int32_t nlong, bad, ext, cut, tmax, win;
@@ -68,13 +67,6 @@ __device__ __forceinline__ void sn_gcopy(uint8_t* dst, const uint8_t* src, int64
   if (tid < n - done) dst[done + tid] = src[done + tid];
 }
 
-// The unit-relative source of byte pos of copy j (overlapping copies repeat their first period).
-__device__ __forceinline__ int32_t sn_csrc(const SnEmitLds& L, int32_t j, int32_t pos) {
-  const int32_t cs = L.cs[j], o = L.co[j];
-  const int32_t rel = pos - cs;
-  return cs - o + (o < L.cl[j] ? rel % o : rel);
-}
-
 // The window's K copies (unit-relative output start cs, offset co, length cl, 0 when the copy has
 // no byte in the unit; in output order) resolved into L.out, span by span: an output-byte -> copy
 // map (start markers, max-scan) gives every copy byte its source; sources before the span (final
@@ -98,7 +90,7 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
   } while (0)
 #endif
   while (i < K) {
-    const int32_t c0 = L.cs[i];
+    const int32_t c0 = L.cp[i].x;
     const int32_t B0 = c0 < 0 ? 0 : (c0 > ulen ? ulen : c0);
     __syncthreads();  // the previous span's readers are done
     if (tid == 0) {
@@ -115,7 +107,9 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     {
       int32_t cut = K;
       for (int32_t j = i + tid; j < K; j += kSnT) {
-        const int32_t e = L.cs[j] + L.cl[j] < ulen ? L.cs[j] + L.cl[j] : ulen;
+        const int2 c = L.cp[j];
+        const int32_t ce = c.x + int32_t(uint32_t(c.y) >> 24);
+        const int32_t e = ce < ulen ? ce : ulen;
         if (e - B0 > kSnSpan) {
           cut = j;
           break;  // (starts rise with j)
@@ -129,9 +123,11 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     {
       int32_t tm = 0;
       for (int32_t j = i + tid; j < i1; j += kSnT) {
-        if (!L.cl[j]) continue;
-        const int32_t st = L.cs[j] > 0 ? L.cs[j] : 0;
-        const int32_t e = L.cs[j] + L.cl[j] < ulen ? L.cs[j] + L.cl[j] : ulen;
+        const int2 c = L.cp[j];
+        const int32_t len = int32_t(uint32_t(c.y) >> 24);
+        if (!len) continue;
+        const int32_t st = c.x > 0 ? c.x : 0;
+        const int32_t e = c.x + len < ulen ? c.x + len : ulen;
         L.emap[st - B0] = uint16_t(j - i + 1);
         tm = e - B0 > tm ? e - B0 : tm;
         for (int32_t x = st - B0; x < e - B0;) {
@@ -180,6 +176,7 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     }
     __syncthreads();
     SC_T(5);
+    uint32_t pmask = 0;  // this thread's bytes still pointing at a copy byte
     // pass 1: every copy byte's source; a source before the span (final) or on a literal byte of
     // the span (its bit clear) resolves the byte at once; any other byte points at its source's
     // span byte (P >= 0).  Four bytes' lookups in flight before their stores.
@@ -197,10 +194,15 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
         const int e = L.emap[b];
         if (e == 0) continue;
         const int32_t j = i + e - 1;
-        const int32_t cs = L.cs[j], o = L.co[j], len = L.cl[j];
+        const int2 c = L.cp[j];
+        const int32_t cs = c.x, o = c.y & 0xffffff, len = int32_t(uint32_t(c.y) >> 24);
         if (pos[k] >= cs + len || o <= 0) continue;  // a literal byte (or a failed page)
-        const int32_t rel = pos[k] - cs;
-        const int32_t s2 = cs - o + (o < len ? rel % o : rel);  // overlapping copies repeat
+        int32_t rel = pos[k] - cs;
+        if (o < len) {  // overlapping copies repeat their first period: rel % o (rel, o < 64: exact in f32)
+          const int32_t qq = int32_t(float(rel) * __builtin_amdgcn_rcpf(float(o)) + 1e-3f);
+          rel -= qq * o;
+        }
+        const int32_t s2 = cs - o + rel;
         src[k] = s2;
         if (s2 < 0) kind[k] = 3;
         else if (s2 < B0) kind[k] = 1;
@@ -220,6 +222,7 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
         if (kind[k] == 1 || (kind[k] == 3 && ext)) L.out[pos[k]] = v[k];
         if (kind[k] == 3 && !ext) L.ext = 1;
         L.ptr[b] = kind[k] == 2 ? int16_t(src[k] - B0) : int16_t(-1);
+        if (kind[k] == 2) pmask |= 1u << (q0 + k);
       }
     }
     __syncthreads();
@@ -229,19 +232,21 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
     // reads (old or already jumped) is a valid earlier byte of its chain, so the chains shorten
     // until every byte is resolved.
     SC_T(6);
-    for (;;) {
+    while (pmask) {
 #ifdef PQH_SNAP_PROF
       if (tid == 0) L.prof[10] += 1;
 #endif
-      int pending = 0;
-#pragma unroll 1
-      for (int q0 = 0; q0 < kSnPer; q0 += 4) {  // four bytes' loads in flight together
-        int16_t p[4], t[4];
+      uint32_t m = pmask;
+      while (m) {  // up to four pending bytes' loads in flight together
+        int q[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          const int32_t b = (q0 + k) * kSnT + tid;
-          p[k] = b < T ? __atomic_load_n(&L.ptr[b], __ATOMIC_RELAXED) : int16_t(-1);
+          q[k] = m ? __builtin_ctz(m) : -1;
+          m &= m ? m - 1 : 0u;
         }
+        int16_t p[4], t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) p[k] = q[k] >= 0 ? __atomic_load_n(&L.ptr[q[k] * kSnT + tid], __ATOMIC_RELAXED) : int16_t(-1);
 #pragma unroll
         for (int k = 0; k < 4; k++) t[k] = p[k] >= 0 ? __atomic_load_n(&L.ptr[p[k]], __ATOMIC_RELAXED) : int16_t(0);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // a -1 read above: its byte is final
@@ -250,16 +255,15 @@ __device__ void sn_copies(SnEmitLds& L, int32_t K, int32_t U0, int32_t ulen, boo
         for (int k = 0; k < 4; k++) v[k] = (p[k] >= 0 && t[k] < 0) ? L.out[B0 + p[k]] : uint8_t(0);
 #pragma unroll
         for (int k = 0; k < 4; k++)
-          if (p[k] >= 0 && t[k] < 0) L.out[B0 + (q0 + k) * kSnT + tid] = v[k];
+          if (p[k] >= 0 && t[k] < 0) L.out[B0 + q[k] * kSnT + tid] = v[k];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the bytes before their -1
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           if (p[k] < 0) continue;
-          __atomic_store_n(&L.ptr[(q0 + k) * kSnT + tid], t[k] < 0 ? int16_t(-1) : t[k], __ATOMIC_RELAXED);
-          pending |= t[k] >= 0;
+          __atomic_store_n(&L.ptr[q[k] * kSnT + tid], t[k] < 0 ? int16_t(-1) : t[k], __ATOMIC_RELAXED);
+          if (t[k] < 0) pmask &= ~(1u << q[k]);
         }
       }
-      if (!pending) break;
     }
     __syncthreads();
     SC_T(7);
@@ -381,18 +385,14 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
           q = body + len;
         } else {
           if (P >= U0 && (e.off == 0 || e.off > P)) L.bad = 1;
-          L.cs[k] = P - U0;
-          L.co[k] = e.off;
-          L.cl[k] = P + len > U0 ? uint8_t(len) : 0;  // (P < U1 here)
+          L.cp[k] = make_int2(P - U0, (e.off < 0xffffff ? e.off : 0xffffff) | ((P + len > U0 ? len : 0) << 24));  // (P < U1)
           k++;
           q += e.hdr;
         }
         P += len;
       }
       for (; k < kb + kt; k++) {  // copies past the unit
-        L.cs[k] = ulen;
-        L.co[k] = 1;
-        L.cl[k] = 0;
+        L.cp[k] = make_int2(ulen, 1);
       }
       for (; li < lb + nlit; li++) lit_len[li] = 0;  // literals past the unit
     }
