@@ -1576,7 +1576,7 @@ namespace {
 int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
   SnapPlan& P = b->snap;
   P.n_pages = n;
-  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit);
+  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit, &P.n_page_mode);
   int32_t* tab = nullptr;
   int4* ws = nullptr;
   int2* wt = nullptr;
@@ -1744,7 +1744,7 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   // the multi-workgroup SNAPPY plan (tables + scratch in one allocation)
   SnapPlan P;
   P.n_pages = num_pages;
-  const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit);
+  const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit, &P.n_page_mode);
   const size_t tb = (sizeof(int32_t) * tab.size() + 15) & ~size_t(15);
   const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) +
                     sizeof(int16_t) * 1024 * size_t(P.n_win) + 16;

@@ -1175,13 +1175,14 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
 hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                          hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_snappy, dim3(n), dim3(256), 0, s, pages, src, dst, status);
+  hipLaunchKernelGGL(k_snappy, dim3(n), dim3(256), 0, s, pages, src, dst, status, nullptr);
   return hipGetLastError();
 }
 
-std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit) {
-  std::vector<int32_t> pw(size_t(n) + 1), pu(size_t(n) + 1), wp, up;
-  int32_t W = 0, U = 0;
+std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit,
+                                      int32_t* n_page_mode) {
+  std::vector<int32_t> pw(size_t(n) + 1), pu(size_t(n) + 1), pm(size_t(n), 0), wp, up;
+  int32_t W = 0, U = 0, M = 0;
   for (int32_t i = 0; i < n; i++) {
     const pqh_codec_page& c = pages[i];
     pw[size_t(i)] = W;
@@ -1189,8 +1190,14 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
     int64_t nw = 0, nu = 0;
     if (c.codec == PQH_CODEC_SNAPPY) {
       const int64_t raw = c.raw_len < c.src_len ? c.raw_len : c.src_len;
-      nw = (int64_t(c.src_len) - raw + kSnWin - 1) / kSnWin;
-      if (raw <= c.image_len) nu = (int64_t(c.image_len) - raw + kSnUnit - 1) / kSnUnit;
+      const int64_t body = int64_t(c.src_len) - raw, out = int64_t(c.image_len) - raw;
+      if (5 * body >= 4 * out) {  // compresses by 1.25x or less: long literals, k_snappy's bulk copies
+        pm[size_t(i)] = 1;
+        M++;
+      } else {
+        nw = (body + kSnWin - 1) / kSnWin;
+        if (raw <= c.image_len) nu = (out + kSnUnit - 1) / kSnUnit;
+      }
     } else if (c.codec != PQH_CODEC_GZIP) {
       nu = ((c.src_len < c.image_len ? c.src_len : c.image_len) + int64_t(kSnUnit) - 1) / kSnUnit;
     }
@@ -1202,13 +1209,15 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
   pw[size_t(n)] = W;
   pu[size_t(n)] = U;
   std::vector<int32_t> t;
-  t.reserve(pw.size() + pu.size() + wp.size() + up.size());
+  t.reserve(pw.size() + pu.size() + pm.size() + wp.size() + up.size());
   t.insert(t.end(), pw.begin(), pw.end());
   t.insert(t.end(), pu.begin(), pu.end());
+  t.insert(t.end(), pm.begin(), pm.end());
   t.insert(t.end(), wp.begin(), wp.end());
   t.insert(t.end(), up.begin(), up.end());
   *n_win = W;
   *n_unit = U;
+  *n_page_mode = M;
   return t;
 }
 
@@ -1216,7 +1225,8 @@ void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int3
   P.wseg = wseg;
   P.page_win0 = tables;
   P.page_unit0 = tables + P.n_pages + 1;
-  P.win_page = tables + 2 * (P.n_pages + 1);
+  P.page_mode = tables + 2 * (P.n_pages + 1);
+  P.win_page = P.page_mode + P.n_pages;
   P.unit_page = P.win_page + P.n_win;
   P.wspec = wspec;
   P.wtrue = wtrue;
@@ -1226,10 +1236,12 @@ void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int3
 hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, const uint8_t* src, uint8_t* dst,
                             int32_t* status, hipStream_t s) {
   if (P.n_pages <= 0) return hipSuccess;
+  if (P.n_page_mode > 0)  // barely compressible pages: one workgroup each (bulk literal copies)
+    hipLaunchKernelGGL(k_snappy, dim3(P.n_pages), dim3(256), 0, s, pages, src, dst, status, P.page_mode);
   if (P.n_win > 0)
     hipLaunchKernelGGL(k_snap_spec, dim3(P.n_win), dim3(256), 0, s, pages, P.win_page, P.page_win0, src, P.wspec, P.wseg);
-  hipLaunchKernelGGL(k_snap_stitch, dim3(P.n_pages), dim3(256), 0, s, pages, P.page_win0, src, dst, P.wspec, P.wtrue,
-                     P.wseg, status);
+  hipLaunchKernelGGL(k_snap_stitch, dim3(P.n_pages), dim3(256), 0, s, pages, P.page_win0, P.page_mode, src, dst, P.wspec,
+                     P.wtrue, P.wseg, status);
   if (P.n_unit > 0) {
     hipLaunchKernelGGL(k_snap_emit, dim3(P.n_unit), dim3(kSnT), 0, s, pages, P.unit_page, P.page_unit0, P.page_win0, src,
                        dst, P.wtrue, P.wseg, status, P.uflag);

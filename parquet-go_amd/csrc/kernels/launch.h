@@ -40,9 +40,10 @@ hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* 
 // block) -> k_snap_stitch (per page) -> k_snap_emit (per 64 KiB of a page's output) -> k_snap_fixup
 // (per page).  Plain-copy pages (codec 0) are copied unit by unit; GZIP pages are k_gzip's.
 struct SnapPlan {
-  int32_t n_pages = 0, n_win = 0, n_unit = 0;
+  int32_t n_pages = 0, n_win = 0, n_unit = 0, n_page_mode = 0;
   int32_t* page_win0 = nullptr;   // [n_pages + 1] first window of each page
   int32_t* page_unit0 = nullptr;  // [n_pages + 1] first unit of each page
+  int32_t* page_mode = nullptr;   // [n_pages] 1: a barely compressible SNAPPY page, k_snappy's (one workgroup)
   int32_t* win_page = nullptr;    // [n_win]
   int32_t* unit_page = nullptr;   // [n_unit]
   int4* wspec = nullptr;          // [n_win] speculative window results (first element, exit, output, status)
@@ -50,8 +51,10 @@ struct SnapPlan {
   int32_t* uflag = nullptr;       // [n_unit] a copy reached before the unit (k_snap_fixup redoes it)
   int16_t* wseg = nullptr;        // [n_win * 1024] every walker segment's exact first element (window-relative)
 };
-// Host tables page_win0 | page_unit0 | win_page | unit_page of a codec page list (device copy: bind).
-std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit);
+// Host tables page_win0 | page_unit0 | page_mode | win_page | unit_page of a codec page list
+// (device copy: bind).
+std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit,
+                                      int32_t* n_page_mode);
 void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int16_t* wseg);
 hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, const uint8_t* src, uint8_t* dst,
                             int32_t* status, hipStream_t s);

@@ -404,11 +404,26 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
     }
     {  // short literals: one wave each, a lane per byte (stage bytes, or HBM past the stage)
       const int lane = tid & 63;
-      for (int32_t e = tid >> 6; e < Lt; e += kSnT / 64) {
-        const int32_t ln = lit_len[e], lo2 = lit_out[e], ls = lit_src[e];
-        for (int32_t x = lane; x < ln; x += 64) {
-          const int32_t sx = ls + x;
-          L.out[lo2 + x] = sx < stage_hi ? L.in[sx - a0] : src[sx];
+      for (int32_t e0 = 4 * (tid >> 6); e0 < Lt; e0 += 4 * (kSnT / 64)) {  // four literals per step
+        int32_t ln[4], lo2[4], ls[4], mx = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const bool on = e0 + k < Lt;
+          ln[k] = on ? lit_len[e0 + k] : 0;
+          lo2[k] = on ? lit_out[e0 + k] : 0;
+          ls[k] = on ? lit_src[e0 + k] : 0;
+          mx = ln[k] > mx ? ln[k] : mx;
+        }
+        for (int32_t x = lane; x < mx; x += 64) {
+          uint8_t v[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int32_t sx = ls[k] + x;
+            v[k] = x < ln[k] ? (sx < stage_hi ? L.in[sx - a0] : src[sx]) : uint8_t(0);
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (x < ln[k]) L.out[lo2[k] + x] = v[k];
         }
       }
     }

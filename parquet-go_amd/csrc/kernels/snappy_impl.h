@@ -441,8 +441,9 @@ __device__ int snappy_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t
 // One workgroup per page: its image rebuilt at image_offset from its source bytes (codec 0: copied;
 // GZIP pages: k_gzip).
 __global__ __launch_bounds__(256) void k_snappy(const pqh_codec_page* cps, const uint8_t* src_all, uint8_t* dst_all,
-                                                int32_t* status) {
+                                                int32_t* status, const int32_t* only) {
   __shared__ SnapLds E;
+  if (only && !only[blockIdx.x]) return;  // (the multi-workgroup pipeline's page)
   const pqh_codec_page cp = cps[blockIdx.x];
   if (cp.codec == PQH_CODEC_GZIP) return;  // k_gzip's
   const uint8_t* src = src_all + cp.src_offset;

@@ -352,13 +352,13 @@ __global__ __launch_bounds__(256) void k_snap_spec(const pqh_codec_page* cps, co
 
 // Per page: status, true window entries / output bases, V2 level bytes.
 __global__ __launch_bounds__(256) void k_snap_stitch(const pqh_codec_page* cps, const int32_t* page_win0,
-                                                     const uint8_t* src_all, uint8_t* dst_all, const int4* wspec,
+                                                     const int32_t* page_mode, const uint8_t* src_all, uint8_t* dst_all, const int4* wspec,
                                                      int2* wtrue, int16_t* wseg, int32_t* status) {
   __shared__ SnSpecLds L;
   const int tid = threadIdx.x, lane = tid & 63;
   const int32_t p = blockIdx.x;
   const pqh_codec_page cp = cps[p];
-  if (cp.codec == PQH_CODEC_GZIP) return;  // k_gzip's
+  if (cp.codec == PQH_CODEC_GZIP || page_mode[p]) return;  // k_gzip's / k_snappy's
   if (cp.codec != PQH_CODEC_SNAPPY) {       // a plain copy (k_snap_emit's units)
     if (tid == 0) status[p] = cp.src_len == cp.image_len ? PQH_OK : PQH_ERR_DECOMPRESS;
     return;
