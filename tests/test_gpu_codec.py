@@ -263,3 +263,37 @@ def test_device_gzip_corrupt_page_fails_its_chunk(pq, ctx):
         b.close()
         hb.close()
     assert failed >= 6, (failed, ok)
+
+
+@pytest.mark.parametrize("codec", ["snappy", "gzip"])
+def test_device_codec_url_pages_repeat(pq, ctx, codec):
+    """URL-like DELTA_LENGTH pages of ~1 MiB (many 64 KiB emit units per SNAPPY page, windows stitched
+    across long pages): decoded with device decompression in plain and staged batches, run several
+    times back to back; every run equals the oracle's decode bit for bit."""
+    from parquet_go_amd import datasets
+
+    W = pq.writer
+    data = datasets.c5z(rows=400_000, row_groups=2, seed=7, codec=W.GZIP if codec == "gzip" else W.SNAPPY).tobytes()
+    f = pq.native.File(data)
+    fr = O.FileReader(data)
+    expect = [oracle_chunk(fr, rg, 0) for rg in range(f.num_row_groups)]
+    dev = dict(device_snappy=codec == "snappy", device_gzip=codec == "gzip")
+    for staged in (False, True):
+        hb = f.load(0, f.num_row_groups, [0], ctx=ctx if staged else None, **dev)
+        units = sum(-(-(c.image_len - c.raw_len) // 65536) for c in hb.codec_pages())
+        assert units > 2 * len(hb.codec_pages())
+        b = pq.native.Batch.staged(ctx, hb) if staged else pq.native.Batch.from_host(ctx, hb)
+        for run in range(3):
+            for _ in range(2):  # back to back, no sync in between
+                b.run_staged() if staged else b.run()
+            b.sync()
+            res = b.page_results(hb.num_pages)
+            pages = hb.pages()
+            path, pt, tl, md, mr = f.columns()[0]
+            for rg, ch in enumerate(hb.chunks()):
+                span = range(ch.first_page, ch.first_page + ch.num_pages)
+                info = [(pages[p].page_type, pages[p].num_values, res[p]) for p in span]
+                col = pq.reader.ColumnData(path, (pt, tl, md, mr), b.chunk_out(rg), [res[p] for p in span], ctx, None, info)
+                assert_chunk(col, expect[rg], where=f"{codec} staged={staged} run {run} rg{rg}")
+        b.close()
+        hb.close()
