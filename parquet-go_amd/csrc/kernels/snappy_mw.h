@@ -31,9 +31,15 @@
 //                 sources before the unit read from the image in HBM (every earlier unit is final).
 #pragma once
 
+#ifndef PQH_SN_WARM  // (experiments: -DPQH_SN_WARM=..., -DPQH_SN_WARM0=...)
+#define PQH_SN_WARM 128
+#endif
+#ifndef PQH_SN_WARM0
+#define PQH_SN_WARM0 256
+#endif
 constexpr int kSnWin = 4096;                 // compressed bytes per spec window
-constexpr int kSnWarm0 = 256;                // warm-up of a window's first thread (window > 0)
-constexpr int kSnWarm = 128;                 // warm-up of every other thread (spec windows, 16-byte segments)
+constexpr int kSnWarm0 = PQH_SN_WARM0;       // warm-up of a window's first thread (window > 0)
+constexpr int kSnWarm = PQH_SN_WARM;         // warm-up of every other thread (spec windows, 16-byte segments)
 constexpr int kSnUnit = 65536;               // output bytes per emit unit
 constexpr int kSnSpan = 16384;               // output bytes per copy-resolution span
 constexpr int kSnT = 1024;                   // emit / fixup threads (= window walkers)
