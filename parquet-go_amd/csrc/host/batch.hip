@@ -309,7 +309,7 @@ struct pqh_batch {
   int2* d_ba_pwin = nullptr;        // per PLAIN page: (first window, windows)
   int2* d_ba_wlist = nullptr;
   BaWin* d_ba_res = nullptr;
-  int32_t* d_ba_wrec = nullptr;     // per window: its records' lengths / cumulative bytes
+  uint16_t* d_ba_wrec = nullptr;     // per window: its records' lengths / cumulative bytes
   void* d_ba_wgeo = nullptr;        // per data-page window: its k_ba_wcopy geometry
   int32_t* d_ba_chunks = nullptr;
   int32_t* d_dcum = nullptr;
@@ -777,7 +777,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pwin), sizeof(int2) * b->ba_pwin.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wlist), sizeof(int2) * b->ba_wlist.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_res), sizeof(BaWin) * b->ba_wins.size())) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wrec), sizeof(int32_t) * size_t(kChainRecs) * b->ba_wins.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_wrec), sizeof(uint16_t) * size_t(kChainRecs) * b->ba_wins.size())) ||
       (rc = dalloc(b, &b->d_ba_wgeo, size_t(kWGeoBytes) * b->ba_wins.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_chunks), sizeof(int32_t) * b->ba_chunks.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||

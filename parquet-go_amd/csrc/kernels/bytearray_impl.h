@@ -315,8 +315,9 @@ __device__ __forceinline__ void ba_stage(ChainLds& C, const BaPageCtx& c, int64_
 
 // Resolve and summarise one window (whole workgroup; C.win staged from ba_wbase(c, w)).  Its records
 // go to the window's scratch in order as the bytes of the records before each one within the window
-// (one more entry holds the window's total): record i's length is wrec[i + 1] - wrec[i].
-__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res, int32_t* wrec) {
+// (16 bits: a record starts inside the window, so fewer than kChainWin bytes precede it); the window's
+// total is res->bytes: record i's length is wrec[i + 1] - wrec[i], the last one's bytes - wrec[count - 1].
+__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res, uint16_t* wrec) {
   const int j = threadIdx.x;
   const int64_t wend64 = c.entry + (w + 1) * kChainStride;
   BaWin r{int32_t(entry64), int32_t(entry64), 0, 0, 0, -1, 0, 0};
@@ -352,12 +353,11 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
     for (uint64_t x = m[k]; x; x &= x - 1) {
       const int32_t pos = 64 * k + __builtin_ctzll(x);
       if (prev >= 0) lb += pos - prev - 4;
-      wrec[li++] = lb;
+      wrec[li++] = uint16_t(lb);
       prev = pos;
     }
   if (j == 0) {
     const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
-    wrec[nrec] = btot;
     r.count = nrec;
     r.bytes = btot;
     if (fb < kBlock) {
@@ -401,12 +401,12 @@ __device__ __forceinline__ int32_t ba_guess_entry(const ChainLds& C, int32_t e0,
   return Bw;
 }
 
-__global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, int32_t* wrec) {
+__global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, uint16_t* wrec) {
   __shared__ ChainLds C;
   const int2 pw = wins[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, pw.x);
   BaWin* r = res + blockIdx.x;
-  int32_t* mk = wrec + int64_t(blockIdx.x) * kChainRecs;
+  uint16_t* mk = wrec + int64_t(blockIdx.x) * kChainRecs;
   const int64_t Bw = c.entry + int64_t(pw.y) * kChainStride;
   if (!c.ok || Bw >= c.e0) {
     if (threadIdx.x == 0) *r = BaWin{-1, -1, 0, 0, 0, -1, 0, 0};
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, 
 }
 // One workgroup per PLAIN byte-array page: windows stitched in order (see above).
 __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* ba_pages, const int2* pwin, BaWin* res,
-                                                     int32_t* wrec) {
+                                                     uint16_t* wrec) {
   __shared__ ChainLds C;
   __shared__ BaWin cur;
   const int p = ba_pages[blockIdx.x];
@@ -508,20 +508,20 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
 // Dictionary pages, one workgroup per window (list: {window, page}): the window's records as
 // cumulative offsets (dcum) at its base.  Data-page windows go to k_ba_wcopy.
 __global__ __launch_bounds__(256) void k_ba_wemit(DevBatch b, const int2* list, const BaWin* res,
-                                                   const int32_t* wrec) {
+                                                   const uint16_t* wrec) {
   const int2 wl = list[blockIdx.x];
   const BaWin r = res[wl.x];
   if (r.base < 0 || r.entry < 0) return;
   const int p = wl.y;
   const BaPageCtx c = ba_page_ctx(b, p);
   if (!c.ok || !c.dict) return;
-  const int32_t* src = wrec + int64_t(wl.x) * kChainRecs;
+  const uint16_t* src = wrec + int64_t(wl.x) * kChainRecs;
   PQH_G int32_t* out = (PQH_G int32_t*)(b.dcum + b.pages[p].aux_base);
   for (int32_t i = threadIdx.x; i < r.count; i += kBlock) {
     const int64_t idx = r.base + i;
     if (idx >= c.count) break;
     out[idx] = int32_t(r.cbase + src[i]);
-    if (idx == c.count - 1) out[c.count] = int32_t(r.cbase + src[i + 1]);
+    if (idx == c.count - 1) out[c.count] = int32_t(r.cbase + (i + 1 < r.count ? int32_t(src[i + 1]) : r.bytes));
   }
 }
 
@@ -1086,7 +1086,8 @@ struct WGeo {
   int32_t wi, n;     // window, records to emit (0: nothing)
   int32_t in_lead;   // page bytes before the entry in its 16-byte vector
   int32_t nvec;      // staged 16-byte vectors (0: the window is not staged)
-  int64_t entry;
+  int32_t entry;     // page offset of the first record
+  int32_t endo;      // window bytes before record n (the end of the last record emitted)
   int64_t obase;     // chunk-relative first output byte of the window
   int64_t cap;       // output bytes the chunk can take from the window on
   const PQH_G uint8_t* img;
@@ -1094,7 +1095,8 @@ struct WGeo {
   PQH_G int64_t* offs_out;
 };
 
-__device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const BaWin* res, int t) {
+__device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const BaWin* res, const uint16_t* wrec,
+                                     int t) {
   WGeo g{};
   const int2 wl = list[t];
   const BaWin r = res[wl.x];
@@ -1108,6 +1110,7 @@ __device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const 
   if (n <= 0) return g;
   const DevChunk C = b.chunks[P.chunk];
   g.n = int32_t(n);
+  g.endo = n < r.count ? int32_t(wrec[int64_t(wl.x) * kChainRecs + n]) : r.bytes;
   g.img = b.payload + P.image_off;
   g.entry = r.entry;
   g.in_lead = int32_t(reinterpret_cast<uintptr_t>(g.img + r.entry) & 15);
@@ -1124,30 +1127,31 @@ __device__ __forceinline__ WGeo wgeo(const DevBatch& b, const int2* list, const 
 // One thread per window: its geometry, so that k_ba_wcopy's workgroups load one record per window
 // instead of a chain of dependent loads (window -> page -> state -> chunk).
 __global__ __launch_bounds__(256) void k_ba_wgeo(DevBatch b, const int2* list, int32_t nlist, const BaWin* res,
-                                                  WGeo* geo) {
+                                                  const uint16_t* wrec, WGeo* geo) {
   const int t = int(blockIdx.x) * kBlock + int(threadIdx.x);
-  if (t < nlist) geo[t] = wgeo(b, list, res, t);
+  if (t < nlist) geo[t] = wgeo(b, list, res, wrec, t);
 }
 
 // The window's page vectors and offset pairs into registers (every load unconditional, clamped
 // addresses), all in flight together.
-__device__ __forceinline__ void wcopy_issue(const WGeo& g, const int32_t* wrec, uint4 (&x)[kWV], int2 (&ov)[kWP]) {
+__device__ __forceinline__ void wcopy_issue(const WGeo& g, const uint16_t* wrec, uint4 (&x)[kWV], uint32_t (&ov)[kWP]) {
   const int tid = threadIdx.x;
   const PQH_G uint8_t* wb = g.img + g.entry - g.in_lead;
-  const PQH_G int32_t* wo = (const PQH_G int32_t*)(wrec + int64_t(g.wi) * kChainRecs);
+  // (kChainRecs is even: every window's entries start 4-byte aligned)
+  const PQH_G uint32_t* wo = (const PQH_G uint32_t*)(wrec + int64_t(g.wi) * kChainRecs);
 #pragma unroll
   for (int j = 0; j < kWV; j++) {
     const int k = tid + j * kBlock;
     x[j] = *reinterpret_cast<const PQH_G uint4*>(wb + (k < g.nvec ? 16 * k : 0));
   }
 #pragma unroll
-  for (int j = 0; j < kWP; j++) {  // offsets 0 .. n (n + 1 entries; wrec holds the total at count)
+  for (int j = 0; j < kWP; j++) {  // offsets 0 .. n - 1, two per dword (offset n is g.endo)
     const int k = tid + j * kBlock;
-    ov[j] = *reinterpret_cast<const PQH_G int2*>(wo + (2 * k <= g.n ? 2 * k : 0));
+    ov[j] = wo[2 * k < g.n ? k : 0];
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, int32_t nlist, const int32_t* wrec) {
+__global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, int32_t nlist, const uint16_t* wrec) {
   __shared__ WcopyLds L;
   const int tid = threadIdx.x;
   const int grid = int(gridDim.x);
@@ -1156,12 +1160,12 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
   // the next window's geometry (one independent load) in flight during this window
   WGeo g = geo[t];
   uint4 x[kWV];
-  int2 ov[kWP];
+  uint32_t ov[kWP];
   for (;;) {
     WGeo gn{};
     if (t + grid < nlist) gn = geo[t + grid];
     const int n = g.n;
-    const PQH_G int32_t* wo = (const PQH_G int32_t*)(wrec + int64_t(g.wi) * kChainRecs);
+    const PQH_G uint16_t* wo = (const PQH_G uint16_t*)(wrec + int64_t(g.wi) * kChainRecs);
     typedef uint32_t u32u __attribute__((aligned(1)));
     if (n > 0 && g.nvec) {
       wcopy_issue(g, wrec, x, ov);
@@ -1176,9 +1180,10 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
 #pragma unroll
       for (int j = 0; j < kWP; j++) {
         const int k = tid + j * kBlock;
-        L.offs[2 * k <= n ? 2 * k : kSpareRec] = uint16_t(ov[j].x);
-        L.offs[2 * k + 1 <= n ? 2 * k + 1 : kSpareRec] = uint16_t(ov[j].y);
+        L.offs[2 * k < n ? 2 * k : kSpareRec] = uint16_t(ov[j]);
+        L.offs[2 * k + 1 < n ? 2 * k + 1 : kSpareRec] = uint16_t(ov[j] >> 16);
       }
+      if (tid == 0) L.offs[n] = uint16_t(g.endo);  // < 2^16: the staged span holds the records' bytes
       __syncthreads();
       typedef uint64_t u64u __attribute__((aligned(1)));
       typedef uint16_t u16u __attribute__((aligned(1)));
@@ -1229,12 +1234,12 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
       const PQH_G uint8_t* src0 = g.img + g.entry;
       constexpr int kLong = 512;
       for (int i = tid; i < n; i += kBlock) {
-        const int64_t o = wo[i], l = wo[i + 1] - o;
+        const int64_t o = wo[i], l = (i + 1 < n ? int64_t(wo[i + 1]) : g.endo) - o;
         g.offs_out[i] = g.obase + o + l;
         if (l > 0 && l < kLong && o + l <= g.cap) copy_bytes(g.dst + o, src0 + 4 * (i + 1) + o, l);
       }
       for (int i = 0; i < n; i++) {  // uniform: the long records by the whole workgroup
-        const int64_t o = wo[i], l = wo[i + 1] - o;
+        const int64_t o = wo[i], l = (i + 1 < n ? int64_t(wo[i + 1]) : g.endo) - o;
         if (l < kLong && o + l <= g.cap) continue;
         const int64_t cl = o + l <= g.cap ? l : g.cap - o;
         if (cl > 0) block_copy(g.dst + o, src0 + 4 * (i + 1) + o, cl);

@@ -1314,7 +1314,7 @@ hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, in
   return hipGetLastError();
 }
 
-hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, int32_t* wrec,
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint16_t* wrec,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ba_wspec, dim3(n), dim3(256), 0, s, b, wins, res, wrec);
@@ -1322,13 +1322,13 @@ hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin
 }
 
 hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
-                             int32_t* wrec, hipStream_t s) {
+                             uint16_t* wrec, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ba_wstitch, dim3(n), dim3(256), 0, s, b, ba_pages, pwin, res, wrec);
   return hipGetLastError();
 }
 
-hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const uint16_t* wrec,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ba_wemit, dim3(n), dim3(256), 0, s, b, list, res, wrec);
@@ -1337,11 +1337,11 @@ hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const
 
 static_assert(sizeof(WGeo) <= kWGeoBytes, "window geometry record");
 
-hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
+hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const uint16_t* wrec,
                            void* geo, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   WGeo* g = static_cast<WGeo*>(geo);
-  hipLaunchKernelGGL(k_ba_wgeo, dim3((n + kBlock - 1) / kBlock), dim3(256), 0, s, b, list, n, res, g);
+  hipLaunchKernelGGL(k_ba_wgeo, dim3((n + kBlock - 1) / kBlock), dim3(256), 0, s, b, list, n, res, wrec, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_ba_wcopy, dim3(n < kWGrid ? n : kWGrid), dim3(256), 0, s, b, g, n, wrec);

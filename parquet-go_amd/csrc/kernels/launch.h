@@ -83,15 +83,15 @@ hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, 
 // per-chunk offset scan, offsets + byte copy.
 // PLAIN chains: every window of every PLAIN page resolved from a guessed entry, windows stitched
 // per page (wrong guesses resolved again), records emitted per window.
-hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, int32_t* wrec,
+hipError_t launch_ba_wspec(const DevBatch& b, const int2* wins, int32_t n, BaWin* res, uint16_t* wrec,
                            hipStream_t s);
 hipError_t launch_ba_wstitch(const DevBatch& b, const int32_t* ba_pages, const int2* pwin, int32_t n, BaWin* res,
-                             int32_t* wrec, hipStream_t s);
+                             uint16_t* wrec, hipStream_t s);
 // list: {window, page} of the dictionary pages' windows (k_ba_wemit: cumulative offsets) and of the
 // data pages' windows (k_ba_wcopy, after k_ba_scan: offsets + bytes of every record).
-hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
+hipError_t launch_ba_wemit(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const uint16_t* wrec,
                            hipStream_t s);
-hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const int32_t* wrec,
+hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const BaWin* res, const uint16_t* wrec,
                            void* geo, hipStream_t s);  // geo: kWGeoBytes per window
 hipError_t launch_ba_sum(const DevBatch& b, const Tile* tiles, const int32_t* list, int32_t n, bool dlba_pages,
                          hipStream_t s);
