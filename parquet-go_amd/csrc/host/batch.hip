@@ -856,9 +856,23 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     for (int32_t k = 0; k < N.tile_n; k++) b->nest_tiles.push_back(Tile{int32_t(b->nests.size()), k, 0, 1});
     b->nests.push_back(N);
   }
+  // Tiles in round-robin order over the chunks (tile k of every chunk, then tile k + 1): a chunk's
+  // tiles stay in order, as the one-pass write's look-back needs, and the tiles in flight at once
+  // spread over the chunks, so a look-back rarely reaches past its first window of 64 tiles.  (Every
+  // nesting kernel finds its slots from N.tile_base + t.k, not from the list position.)
+  if (!rc && b->nests.size() > 1) {
+    std::vector<Tile> rr;
+    rr.reserve(b->nest_tiles.size());
+    int32_t most = 0;
+    for (const DevNest& N : b->nests) most = std::max(most, N.tile_n);
+    for (int32_t k = 0; k < most; k++)
+      for (size_t i = 0; i < b->nests.size(); i++)
+        if (k < b->nests[i].tile_n) rr.push_back(Tile{int32_t(i), k, 0, 1});
+    b->nest_tiles.swap(rr);
+  }
   if (!rc && !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nests), sizeof(DevNest) * b->nests.size())) &&
       !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nest_tiles), sizeof(Tile) * b->nest_tiles.size())) &&
-      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nsums), sizeof(int64_t) * kNestFlags * b->nest_tiles.size())))
+      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nsums), sizeof(int64_t) * kNestFlags * (b->nest_tiles.size() + 1))))
     rc = dalloc(b, reinterpret_cast<void**>(&b->d_ntotals), sizeof(int64_t) * kNestFlags * b->nests.size());
   for (size_t i = 0; i < b->nests.size(); i++) b->nests[i].totals = b->d_ntotals + i * kNestFlags;
   if (rc || (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunks), sizeof(DevChunk) * size_t(std::max(num_chunks, 1))))) {
@@ -1043,10 +1057,18 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       ns = side;
       nest_open = true;
     }
-    if (e == hipSuccess) e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
-    if (e == hipSuccess) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    // count / scan / write passes; PQH_NEST_PASSES=1 reads the levels once (look-back bases in
+    // k_nest_write) when every chunk has a tile.  Measured on C4 (same box): one pass moves 0.39 GB
+    // less but its write takes 0.36 ms against 0.27 ms for the three kernels, and the graph step
+    // 1.60 ms against 1.35 ms (look-back waits hold workgroup slots the byte-array copies need)
+    const char* np = getenv("PQH_NEST_PASSES");
+    const bool one_pass = np && np[0] == '1' &&
+                          std::all_of(b->nests.begin(), b->nests.end(), [](const DevNest& N) { return N.tile_n > 0; });
+    if (e == hipSuccess && !one_pass)
+      e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
+    if (e == hipSuccess && !one_pass) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
     if (e == hipSuccess)
-      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, one_pass, st); });
   }
   if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
   if (e == hipSuccess && nbt) {

@@ -1380,9 +1380,15 @@ hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s)
   return hipGetLastError();
 }
 
-hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, bool one_pass, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_write, dim3(n), dim3(256), 0, s, b, tiles);
+  if (one_pass) {  // the look-back words and the ticket start at zero
+    const hipError_t e = hipMemsetAsync(b.nsums, 0, sizeof(int64_t) * kNestFlags * (size_t(n) + 1), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nest_write<true>, dim3(n), dim3(256), 0, s, b, tiles, n);
+  } else {
+    hipLaunchKernelGGL(k_nest_write<false>, dim3(n), dim3(256), 0, s, b, tiles, n);
+  }
   return hipGetLastError();
 }
 

@@ -103,7 +103,8 @@ hipError_t launch_dba_prefix(const DevBatch& b, const Tile* tiles, int32_t n, hi
 // Nesting (levels -> list offsets / presence / leaf validity): counts, per-chunk scan, write.
 hipError_t launch_nest_count(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s);
-hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
+// one_pass: flag bases by decoupled look-back (no k_nest_count / k_nest_scan before it)
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, bool one_pass, hipStream_t s);
 // Delta pages outside the fast-path geometry (exact sequential decode, one wave per delta page).
 hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.

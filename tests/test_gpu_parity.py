@@ -581,13 +581,20 @@ def test_nesting_list_map(pq, ctx, v2):
     assert _check_nesting(pq, ctx, fixtures.nested_list_map(n=6000, v2=v2)) == 6
 
 
-def test_nesting_c4_multi_tile(pq, ctx):
+@pytest.fixture(params=["one_pass", "three_passes"])
+def nest_passes(request, monkeypatch):
+    """The count / scan / write passes (default) and the one-pass write with look-back bases."""
+    monkeypatch.setenv("PQH_NEST_PASSES", "3" if request.param == "three_passes" else "1")
+    return request.param
+
+
+def test_nesting_c4_multi_tile(pq, ctx, nest_passes):
     from parquet_go_amd import datasets
 
     assert _check_nesting(pq, ctx, datasets.c4(rows=150_000, row_groups=2)) == 6
 
 
-def test_nesting_sparse_lists(pq, ctx):
+def test_nesting_sparse_lists(pq, ctx, nest_passes):
     """Mostly null / empty lists: nest tiles starting more than half a tile of lists (the list
     offsets are staged in parts), for one and two repetition levels."""
     import io
@@ -614,7 +621,7 @@ def test_nesting_sparse_lists(pq, ctx):
     assert _check_nesting(pq, ctx, buf.getvalue()) == 2
 
 
-def test_nesting_deep_lists(pq, ctx):
+def test_nesting_deep_lists(pq, ctx, nest_passes):
     """list<list<int32>> and list<struct<list<string>>> from pyarrow (max_rep 2)."""
     import io
 
