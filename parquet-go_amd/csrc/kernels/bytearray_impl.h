@@ -426,11 +426,28 @@ __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, 
   }
   ba_window(C, c, pw.y, entry, r, mk);
 }
-// One workgroup per PLAIN byte-array page: windows stitched in order (see above).
+// Wave-wide exclusive prefix sum (64-bit).
+__device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
+  const int lane = threadIdx.x & 63;
+  int64_t v = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(v, off, 64);
+    if (lane >= off) v += y;
+  }
+  return v - x;
+}
+
+// One workgroup per PLAIN byte-array page: windows stitched in order (see above).  Wave 0 takes 64
+// windows per step: a window whose guessed entry is its predecessor's exit (and before which the
+// chain neither ran out of bytes nor reached `count`) gets its bases from two wave scans; the first
+// other window (a wrong guess, an invalid record, or the end) is handled one at a time by the
+// workgroup exactly as the chain defines it.
 __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* ba_pages, const int2* pwin, BaWin* res,
                                                      uint16_t* wrec) {
   __shared__ ChainLds C;
   __shared__ BaWin cur;
+  __shared__ int64_t sh[6];  // done, cum, last_base, last_cbase, T, (w | last << 32 | stop << 63)
   const int p = ba_pages[blockIdx.x];
   const int2 wr = pwin[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, p);
@@ -439,13 +456,63 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
   int64_t last_base = 0, last_cbase = 0;  // the last window taken: records and bytes before it
   int code = PQH_OK;
   int w = 0, last = -1;
-  for (; w < wr.y && done < c.count; w++) {
-    BaWin* r = res + wr.x + w;
-    if (T >= c.e0) {  // no bytes left for the next length
-      code = PQH_ERR_EOF;
-      break;
+  for (;;) {
+    if (threadIdx.x < 64) {  // fast path over the windows whose guesses were right
+      const int lane = threadIdx.x;
+      bool stop = false;
+      for (;;) {
+        const int idx = w + lane;
+        BaWin x{-1, -1, 0, 0, 0, 0, 0, 0};
+        if (idx < wr.y) x = res[wr.x + idx];
+        const int64_t ec = done + wave_excl_scan64(x.count), eb = cum + wave_excl_scan64(x.bytes);
+        const int32_t pexit = __shfl_up(x.exit, 1, 64);
+        const int64_t Tl = lane == 0 ? T : pexit;
+        const bool before = idx >= wr.y || ec >= c.count || Tl >= c.e0;  // the loop ends before it
+        const uint64_t ev = __ballot(before || x.entry != Tl || x.bad);
+        const int f = ev ? __builtin_ctzll(ev) : 64;
+        if (lane < f) {
+          res[wr.x + idx].base = ec;
+          res[wr.x + idx].cbase = eb;
+        }
+        if (f > 0) {
+          last = w + f - 1;
+          last_base = __shfl(ec, f - 1, 64);
+          last_cbase = __shfl(eb, f - 1, 64);
+          done = last_base + __shfl(x.count, f - 1, 64);
+          cum = last_cbase + __shfl(x.bytes, f - 1, 64);
+          T = __shfl(x.exit, f - 1, 64);
+          w += f;
+        }
+        if (f < 64) {
+          stop = __shfl(int(before), f, 64) != 0;
+          break;
+        }
+      }
+      if (lane == 0) {
+        sh[0] = done;
+        sh[1] = cum;
+        sh[2] = last_base;
+        sh[3] = last_cbase;
+        sh[4] = T;
+        sh[5] = int64_t(uint32_t(w)) | (int64_t(uint32_t(last + 1)) << 32) | (int64_t(stop) << 62);
+      }
     }
     __syncthreads();
+    done = sh[0];
+    cum = sh[1];
+    last_base = sh[2];
+    last_cbase = sh[3];
+    T = sh[4];
+    w = int(uint32_t(sh[5]));
+    last = int((sh[5] >> 32) & 0x3fffffff) - 1;
+    const bool stop = (sh[5] >> 62) & 1;
+    __syncthreads();
+    if (stop || w >= wr.y || done >= c.count) {
+      if (w < wr.y && done < c.count && T >= c.e0) code = PQH_ERR_EOF;  // no bytes left for the next length
+      break;
+    }
+    // window w: a wrong guess (resolved again from the true entry) or an invalid record
+    BaWin* r = res + wr.x + w;
     if (threadIdx.x == 0) cur = *r;
     __syncthreads();
     if (cur.entry != T) {  // the window's guess was not its true entry: resolve it again
@@ -473,6 +540,8 @@ __global__ __launch_bounds__(256) void k_ba_wstitch(DevBatch b, const int32_t* b
       break;
     }
     T = cur.exit;
+    w++;
+    __syncthreads();  // cur is read again by the next window
   }
   if (!c.dict) {
     // the page's bytes before its value limit (min(count, records on the chain)) go to tile 0 of its

@@ -66,15 +66,7 @@ __device__ __forceinline__ void snap_copy(uint8_t* dst, const uint8_t* src, int6
   if (tid < n - done) dst[done + tid] = src[done + tid];
 }
 
-__device__ __forceinline__ int64_t wave_excl_scan64(int64_t x) {
-  const int lane = threadIdx.x & 63;
-  int64_t incl = x;
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  return incl - x;
-}
+// (wave_excl_scan64: bytearray_impl.h)
 
 // ---- Batch resolution shared by the device codecs (k_snappy, k_gzip).  A batch is up to kSnapOut
 // output bytes made of elements (eout[e] = start, batch-relative; eout[nE] = the batch size).
