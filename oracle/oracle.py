@@ -650,8 +650,11 @@ class SnappyCorrupt(Exception):
 
 
 def snappy_decode(src):
-    """github.com/golang/snappy v0.0.4 Decode (decode.go: decodedLen + decode), restated: the
-    reference's SNAPPY codec (compress.go:43-49).  Returns the block or raises SnappyCorrupt
+    """github.com/golang/snappy v0.0.4 Decode, restated from the copy vendored in the reference:
+    vendor/github.com/golang/snappy/decode.go:32-55 (decodedLen), :57-76 (Decode) and
+    decode_other.go:14-101 (decode: tagLiteral :18-58, tagCopy1/2/4 :60-83, the offset / length
+    check :85; the amd64 / arm64 assembly implements the same loop) — the reference's SNAPPY codec
+    (compress.go:43-49).  Returns the block or raises SnappyCorrupt
     (ErrCorrupt / ErrTooLarge).  Pinned against pyarrow's snappy on valid blocks
     (tests/test_codec_oracle.py)."""
     src = bytes(src)
