@@ -155,6 +155,7 @@ std::shared_ptr<uint8_t> pinned_acquire(pqh_ctx* ctx, size_t bytes) {
   std::shared_ptr<PinnedPool> pool = ctx->pool;
   uint8_t* p = nullptr;
   size_t cap = 0;
+  std::vector<uint8_t*> drop;
   {
     std::lock_guard<std::mutex> g(pool->m);
     size_t best = SIZE_MAX;
@@ -165,8 +166,15 @@ std::shared_ptr<uint8_t> pinned_acquire(pqh_ctx* ctx, size_t bytes) {
       p = pool->free_blocks[best].first;
       cap = pool->free_blocks[best].second;
       pool->free_blocks.erase(pool->free_blocks.begin() + long(best));
+    } else {
+      // a miss: the free blocks are all too small for this request; release them rather than keep
+      // them pinned for the context's life (payloads that keep growing would pile up otherwise)
+      for (auto& fb : pool->free_blocks) drop.push_back(fb.first);
+      pool->free_blocks.clear();
     }
   }
+  if (!drop.empty()) hipSetDevice(ctx->device);
+  for (uint8_t* q : drop) hipHostFree(q);
   if (!p) {
     cap = (std::max<size_t>(bytes, 1) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
     hipSetDevice(ctx->device);
@@ -1757,6 +1765,9 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
                          void* d_dst, int32_t* status) {
   if (!ctx || num_pages < 0 || (num_pages && (!pages || !status))) return set_err(ctx, PQH_ERR_ARG, "bad arguments");
   if (num_pages == 0) return PQH_OK;
+  // the stage loads round addresses down to 16 bytes from d_src (hipMalloc pointers are aligned)
+  if ((reinterpret_cast<uintptr_t>(d_src) | reinterpret_cast<uintptr_t>(d_dst)) & 15)
+    return set_err(ctx, PQH_ERR_ARG, "pqh_decompress_pages: d_src and d_dst must be 16-byte aligned");
   hipSetDevice(ctx->device);
   pqh_codec_page* dp = nullptr;
   int32_t* ds = nullptr;
@@ -1768,7 +1779,9 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
   P.n_pages = num_pages;
   const std::vector<int32_t> tab = snap_plan_tables(pages, num_pages, &P.n_win, &P.n_unit, &P.n_page_mode);
   const size_t tb = (sizeof(int32_t) * tab.size() + 15) & ~size_t(15);
-  const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + sizeof(int32_t) * size_t(P.n_unit) +
+  // the walker-segment entries (written as 8-byte stores) start 16-byte aligned after the unit flags
+  const size_t ub = (sizeof(int32_t) * size_t(P.n_unit) + 15) & ~size_t(15);
+  const size_t sb = tb + sizeof(int4) * size_t(P.n_win) + sizeof(int2) * size_t(P.n_win) + ub +
                     sizeof(int16_t) * 1024 * size_t(P.n_win) + 16;
   void* scratch = nullptr;
   if (e == hipSuccess) e = hipMalloc(&scratch, sb);
@@ -1778,7 +1791,7 @@ int pqh_decompress_pages(pqh_ctx* ctx, const pqh_codec_page* pages, int32_t num_
     int4* ws = reinterpret_cast<int4*>(m + tb);
     int2* wt = reinterpret_cast<int2*>(ws + P.n_win);
     int32_t* uf = reinterpret_cast<int32_t*>(wt + P.n_win);
-    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, uf, reinterpret_cast<int16_t*>(uf + P.n_unit));
+    snap_plan_bind(P, reinterpret_cast<int32_t*>(m), ws, wt, uf, reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(uf) + ub));
     e = snappy_page_mode()
             ? launch_snappy(dp, num_pages, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream)
             : launch_snappy_mw(dp, P, static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), ds, ctx->stream);

@@ -8,14 +8,21 @@
 
 namespace pqhip {
 
+// encoding/binary.Uvarint as golang/snappy's decodedLen calls it (vendor/github.com/golang/snappy/
+// decode.go:32-36): at most 10 bytes, and the 10th byte (bits 63..69) may only be 0 or 1 -- any
+// larger value overflows 64 bits and is an error (n < 0), never a silently truncated length.
 static bool read_uvarint(const uint8_t*& p, const uint8_t* end, uint64_t& v) {
   v = 0;
-  for (int s = 0; s < 64 && p < end; s += 7) {
-    uint8_t b = *p++;
-    v |= uint64_t(b & 0x7f) << s;
-    if (b < 0x80) return true;
+  for (int i = 0; i < 10 && p < end; i++) {
+    const uint8_t b = *p++;
+    if (b < 0x80) {
+      if (i == 9 && b > 1) return false;  // overflow
+      v |= uint64_t(b) << (7 * i);
+      return true;
+    }
+    v |= uint64_t(b & 0x7f) << (7 * i);
   }
-  return false;
+  return false;  // 10 continuation bytes (overflow) or the input ended (n == 0)
 }
 
 // Snappy block decoding (format of golang/snappy decode.go): uvarint length, then literal /

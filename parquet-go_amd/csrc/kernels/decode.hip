@@ -1191,7 +1191,11 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
     if (c.codec == PQH_CODEC_SNAPPY) {
       const int64_t raw = c.raw_len < c.src_len ? c.raw_len : c.src_len;
       const int64_t body = int64_t(c.src_len) - raw, out = int64_t(c.image_len) - raw;
-      if (5 * body >= 4 * out) {  // compresses by 1.25x or less: long literals, k_snappy's bulk copies
+      // compresses by 1.25x or less: long literals, k_snappy's bulk copies.  Also every block of
+      // more than 2^24 output bytes: k_snap_emit packs a copy's offset in 24 bits (an offset is at
+      // most the output position, so only such blocks can hold a copy4 reaching 2^24 or further;
+      // golang/snappy accepts offsets up to 2^32, decode_other.go:75-85), k_snappy keeps 31 bits.
+      if (5 * body >= 4 * out || out > (int64_t(1) << 24)) {
         pm[size_t(i)] = 1;
         M++;
       } else {

@@ -160,3 +160,48 @@ def multi_unit_blocks():
         n += ln
     cases.append(block(n, e))
     return [(b, _decode(b)) for b in cases]
+
+
+def uvarint_header_cases():
+    """(name, block, page size) around golang/snappy's decodedLen = encoding/binary.Uvarint
+    (vendor/github.com/golang/snappy/decode.go:32-36): non-minimal and 10-byte headers are valid
+    while their 10th byte is 0 or 1; a 10th byte > 1 overflows 64 bits and an 11th byte is never read
+    -- both ErrCorrupt, whatever the low bits say.  Body: one 8-byte literal."""
+    body = literal(b"abcdefgh")
+    cont = b"\x80"
+    return [
+        ("minimal", b"\x08" + body, 8),
+        ("3-byte", b"\x88\x80\x00" + body, 8),
+        ("10-byte, last 0", b"\x88" + cont * 8 + b"\x00" + body, 8),
+        ("10-byte, last 1 (> 2^32)", b"\x88" + cont * 8 + b"\x01" + body, 8),
+        ("10-byte, last 2 (overflow, low bits 8)", b"\x88" + cont * 8 + b"\x02" + body, 8),
+        ("10-byte, last 0x7f (overflow)", b"\x88" + cont * 8 + b"\x7f" + body, 8),
+        ("11-byte", b"\x88" + cont * 9 + b"\x00" + body, 8),
+        ("10 continuation bytes", b"\x88" + cont * 9 + b"\x80" + body, 8),
+        ("5-byte 2^32 - 1", b"\xff\xff\xff\xff\x0f" + body, 8),
+        ("5-byte 2^32", b"\x80\x80\x80\x80\x10" + body, 8),
+        ("truncated header", b"\x88\x80", 8),
+    ]
+
+
+def far_copy_block(far=(1 << 24) + 777, tail=200_000, seed=31):
+    """A valid block of more than 16 MiB whose copy4 elements reach 2^24 bytes back and further
+    (golang/snappy accepts any offset up to 2^32 within the output, decode_other.go:75-85; Go and C++
+    encoders never emit one, other encoders may).  Returns (block, raw)."""
+    rng = np.random.default_rng(seed)
+    head = rng.bytes(far + 64)
+    e = bytearray(literal(head))
+    raw = bytearray(head)
+    n = len(raw)
+    while n < far + 64 + tail:
+        for off in (far, far + 13, (1 << 24), (1 << 24) - 1, 5):
+            ln = int(rng.integers(1, 65))
+            e += copy4(ln, off)
+            for _ in range(ln):
+                raw.append(raw[-off])
+            n += ln
+        lit = rng.bytes(int(rng.integers(1, 300)))
+        e += literal(lit)
+        raw += lit
+        n += len(lit)
+    return block(len(raw), bytes(e)), bytes(raw)

@@ -92,3 +92,63 @@ def test_device_codec_walker_checks(pq):
         f2 = pq.native.File(bytes(data))
         hb2 = f2.load(0, 1, [0], device_snappy=dev)
         assert hb2.chunks()[0].host_status == {v: k for k, v in pq.native.STATUS.items()}["DECOMPRESS"]
+
+
+def test_snappy_uvarint_header_parity(pq):
+    """golang/snappy's decodedLen (binary.Uvarint, decode.go:32-36) on crafted page blocks: the host
+    walker (codec.cpp, both the host-decompressing and the device-codec layout) fails or decodes
+    every page exactly as the oracle does -- incl. the 10-byte header `88 80x8 02`, whose overflow
+    bit a plain 7-bit-shift loop drops (decoded length 8 instead of ErrCorrupt).  The device codecs
+    are checked against the same cases in test_gpu_codec.py."""
+    import pqcraft
+    from snappy_blocks import uvarint_header_cases
+
+    cases = uvarint_header_cases()
+    data = pqcraft.file_with_blocks([[(blk, size, size // 4)] for _, blk, size in cases], O.SNAPPY)
+    fr = O.FileReader(data)
+    f = pq.native.File(data)
+    host = f.load(0, f.num_row_groups, [0])
+    dev = f.load(0, f.num_row_groups, [0], device_snappy=True)
+    hch, hpages, hpay = host.chunks(), host.pages(), host.payload()
+    seen = set()
+    for i, (name, blk, size) in enumerate(cases):
+        och = fr.read_chunk(i, 0)
+        assert hch[i].host_status == och.status, f"{name}: host {hch[i].host_status} vs oracle {och.status}"
+        assert dev.chunks()[i].host_status == och.status, f"{name}: device-codec walker"
+        if och.status == 0:
+            p = hpages[hch[i].first_page]
+            assert hpay[p.image_offset:p.image_offset + p.image_len].tobytes() == och.pages[0].image, name
+        seen.add(och.status)
+    assert seen == {0, O.ERR_DECOMPRESS}
+    assert fr.read_chunk(4, 0).status == O.ERR_DECOMPRESS  # the 88 80x8 02 page
+
+
+def test_host_crc_mismatch_validated(pq):
+    """readPageBlock's CRC32 check (chunk_reader.go:173-177) under WithCRC32Validation
+    (file_reader.go:134-139): one flipped bit in a CRC'd page fails its chunk with PQH_ERR_CRC on the
+    host exactly when (and where) the oracle's walker does; without validation the flip only reaches
+    the decoders, and unflipped chunks stay OK."""
+    data = fixtures.flat_all_types(n=4000, v2=False, codec=O.UNCOMPRESSED, page=8 * 1024, rows_per_group=4000, crc=True)
+    fr = O.FileReader(data)
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    CRC = {v: k for k, v in pq.native.STATUS.items()}["CRC"]
+    assert CRC == O.ERR_CRC
+    rng = np.random.default_rng(8)
+    flipped = 0
+    for trial in range(8):
+        ci = trial % ncols
+        md = fr.row_groups[0][1][ci][3]
+        lo, span = md.get(11, md[9]), md[7]
+        buf = bytearray(data)
+        pos = lo + span // 2 + int(rng.integers(-span // 4, span // 4 + 1))
+        buf[pos] ^= 1 << int(rng.integers(0, 8))
+        fr2, f2 = O.FileReader(bytes(buf)), pq.native.File(bytes(buf))
+        hb = f2.load(0, 1, list(range(ncols)), validate_crc=True)
+        for c, ch in enumerate(hb.chunks()):
+            och = fr2.read_chunk(0, c, validate_crc=True)
+            assert ch.host_status == och.status, (trial, c, ch.host_status, och.status)
+            if c != ci:
+                assert och.status == 0
+        flipped += fr2.read_chunk(0, ci, validate_crc=True).status == O.ERR_CRC
+    assert flipped >= 4, flipped

@@ -19,7 +19,7 @@ import pytest
 import fixtures
 from oracle import oracle as O
 from parity import assert_chunk, oracle_chunk
-from snappy_blocks import edge_blocks, sample_blocks
+from snappy_blocks import edge_blocks, far_copy_block, sample_blocks, uvarint_header_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -78,6 +78,27 @@ def _check(pq, ctx, blocks, sizes):
 def test_snappy_edge_blocks(pq, ctx):
     cases = edge_blocks()
     assert _check(pq, ctx, [c[0] for c in cases], [len(c[1]) for c in cases]) == 0
+
+
+def test_snappy_uvarint_headers(pq, ctx):
+    """decodedLen = binary.Uvarint (golang/snappy decode.go:32-36) on the device: 10-byte headers
+    with a 10th byte > 1, 11-byte headers and lengths > 2^32 - 1 are ErrCorrupt, non-minimal ones
+    valid -- status and bytes equal to the oracle's (and the host walker's, test_codec_oracle.py)."""
+    cases = uvarint_header_cases()
+    bad = _check(pq, ctx, [c[1] for c in cases], [c[2] for c in cases])
+    assert bad == sum(1 for _, b, s in cases if _expect(b, s)[0]) and bad >= 6
+
+
+def test_snappy_far_copy_offsets(pq, ctx):
+    """A 16.2 MiB block whose copy4 offsets reach 2^24 and beyond (k_snap_emit packs
+    offsets in 24 bits; such blocks go to k_snappy, which keeps 31): bytes equal to the oracle's,
+    beside a small multi-workgroup block in the same launch."""
+    blk, raw = far_copy_block()
+    assert len(raw) > (1 << 24) + 64
+    small = edge_blocks()[1]
+    got = _device_decompress(pq, ctx, [blk, small[0]], [len(raw), len(small[1])])
+    assert got[0][0] == 0 and got[0][1] == raw
+    assert got[1][0] == 0 and got[1][1] == small[1]
 
 
 def test_snappy_pyarrow_blocks(pq, ctx):
