@@ -153,3 +153,28 @@ def test_page_read_matches_read_values(pq, ctx):
     finally:
         b.close()
         ctx.free(d)
+
+
+def test_shim_walk_device(pq, ctx):
+    """INTEGRATION.md's gpuPageReader inside the reference's readPages (tests/shim_adapter.py):
+    `read` consumes CompressedPageSize bytes and reports the batch's load error for its page,
+    readValues(size) is pqh_batch_page_read of the chunk's i-th data page -- every chunk of
+    multi-page V1 / V2 / dictionary / SNAPPY / nested / pyarrow files walks like the oracle's
+    dataPageReaderV1/V2, three readValues calls per page compared value for value, level for level."""
+    import test_shim_walk as TS
+
+    batches = []
+
+    def batch_for(hb):
+        b = pq.native.Batch.from_host(ctx, hb)
+        b.run()
+        b.sync()
+        batches.append(b)
+        return b
+
+    n = 0
+    for name, data in TS.files():
+        n += TS.walk_both(pq, data, backend="device", batch_for=batch_for)
+    for b in batches:
+        b.close()
+    assert n > 100
