@@ -116,7 +116,10 @@ typedef enum pqh_status {
   PQH_ERR_SCHEMA = 30,                /* schema / column metadata inconsistency (chunk_reader.go:303-312) */
   PQH_ERR_DICT_PAGE = 31,             /* second dictionary page / dictionary encoding not PLAIN (chunk_reader.go:197-199, page_dict.go:44-46) */
   PQH_ERR_NO_DEVICE = 32,             /* no HIP device present */
-  PQH_ERR_NOT_IMPLEMENTED = 33        /* decoder kind not (yet) available on the device */
+  PQH_ERR_NOT_IMPLEMENTED = 33,       /* decoder kind not (yet) available on the device */
+  PQH_ERR_INTERNAL = 34               /* a device consistency guard fired (an index outside its buffer,
+                                         a look-back that never completed): a bug, never a property of
+                                         the input -- the chunk's outputs are undefined */
 } pqh_status;
 
 /* Decode phases, in the order the reference runs them for one page (page_v1.go:33-122). */

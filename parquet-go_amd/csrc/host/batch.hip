@@ -1346,7 +1346,8 @@ int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num
     pqh_page_result& r = out[p];
     memset(&r, 0, sizeof(r));
     if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) {
-      r.status = PQH_ERR_DECOMPRESS;  // the device could not decompress its image (readPageBlock)
+      // the device could not decompress its image (readPageBlock), or a codec guard fired (INTERNAL)
+      r.status = b->codec_status[size_t(p)] == PQH_ERR_INTERNAL ? PQH_ERR_INTERNAL : PQH_ERR_DECOMPRESS;
       r.phase = PQH_PHASE_LOAD;
     } else if (S.err != kNoError) {
       r.status = int32_t(S.err & 0xff);
@@ -1475,7 +1476,7 @@ ChunkErr chunk_error(const pqh_batch* b, int32_t chunk) {
   for (int32_t i = 0; i < D.num_pages; i++) {
     const int32_t p = D.first_page + i;
     if (size_t(p) < b->codec_status.size() && b->codec_status[size_t(p)] != PQH_OK) {
-      e.status = PQH_ERR_DECOMPRESS;
+      e.status = b->codec_status[size_t(p)] == PQH_ERR_INTERNAL ? PQH_ERR_INTERNAL : PQH_ERR_DECOMPRESS;
       e.phase = PQH_PHASE_LOAD;
       e.page = p;
       return e;

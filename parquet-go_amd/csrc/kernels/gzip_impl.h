@@ -843,7 +843,9 @@ __device__ __forceinline__ int32_t block_excl_scan(GzLds& E, int32_t x, int32_t*
 // dst + d.  Whole workgroup.
 // Every HBM read is bounds-checked (a back-reference inside [0, d), a stored byte inside [0, n)) and
 // the batch must end inside the page (total): false, with nothing read or written out of bounds, when
-// the batch's tables are inconsistent (never for a well-formed decode).
+// the batch's tables are inconsistent.  gz_emit / gz_serial validate every token against the input
+// and the page before it is stored, so a failing guard is an internal inconsistency of the kernel,
+// never a corrupt page: the callers report PQH_ERR_INTERNAL (the r03 GZIP fault).
 __device__ bool gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0, const uint8_t* src, uint8_t* dst,
                          int32_t n, int32_t total) {
   const int tid = threadIdx.x;
@@ -919,15 +921,16 @@ __device__ bool gz_batch(GzLds& E, int32_t T, int32_t nE, int32_t d, int32_t a0,
 // previous part's exit, from that exit, until nothing changes: thread 0 starts on the chain, so
 // after round r parts 0..r are exact and the fixpoint is the true decode.  A scan places the parts'
 // output; batches of at most kSnapOut bytes / kGzMaxE - 1 back-references are then emitted (each
-// part re-decoded from its true entry) and resolved with gz_batch.  Returns false on an error.
-__device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t& d, int32_t total,
+// part re-decoded from its true entry) and resolved with gz_batch.  Returns PQH_OK,
+// PQH_ERR_DECOMPRESS (the stream is corrupt) or PQH_ERR_INTERNAL (a gz_batch guard fired); uniform.
+__device__ int gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t& d, int32_t total,
                               uint8_t* dst) {
   const int tid = threadIdx.x;
   const int64_t nbits = int64_t(n) * 8;
   const int64_t P0 = uni64(E.pbit);
   const int64_t stage_end = int64_t(a0 + kGzStage) * 8;
   const int64_t Pend = stage_end < nbits ? stage_end : nbits;
-  if (P0 >= Pend) return false;  // the input ends inside the block
+  if (P0 >= Pend) return PQH_ERR_DECOMPRESS;  // the input ends inside the block
   const int32_t lb = uni(E.lbits), db = uni(E.dbits), ms = uni(E.ms);
   const int64_t S = (Pend - P0 + kBlock - 1) / kBlock;
   const int64_t lo = P0 + S * tid < Pend ? P0 + S * tid : Pend;
@@ -964,7 +967,7 @@ __device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a
       break;
     }
   }
-  if (!converged) return false;  // (cannot happen: round r fixes part r)
+  if (!converged) return PQH_ERR_DECOMPRESS;  // (cannot happen: round r fixes part r)
 #ifdef PQH_GZIP_PROF
   {
     GZ_CLK(h1);
@@ -977,7 +980,7 @@ __device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a
   if (E.hst[tid]) atomicMin(&E.hend, tid);
   __syncthreads();
   const int32_t e = uni(E.hend);
-  if (e < kBlock && E.hst[e] == 2) return false;  // an invalid code on the chain
+  if (e < kBlock && E.hst[e] == 2) return PQH_ERR_DECOMPRESS;  // an invalid code on the chain
   const int32_t last = e < kBlock ? e : kBlock - 1;
   const bool mine = tid <= last;
   int32_t Ototal, Ktotal;
@@ -1008,14 +1011,14 @@ __device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a
         }
       }
     }
-    if (__syncthreads_or(r == kGzEmitBad)) return false;
+    if (__syncthreads_or(r == kGzEmitBad)) return PQH_ERR_DECOMPRESS;
     const int32_t cut = uni(E.hcut);
     const int32_t end_o = cut >= 0 ? uni(E.hcut_out) : Ototal;
     const int32_t end_k = cut >= 0 ? uni(E.hcut_tok) : Ktotal;
     const int32_t T = end_o - bo;
     GZ_CLK(h3);
     if (T > 0) {
-      if (!gz_batch(E, T, 1 + end_k - bk, d + bo, a0, src, dst, n, total)) return false;
+      if (!gz_batch(E, T, 1 + end_k - bk, d + bo, a0, src, dst, n, total)) return PQH_ERR_INTERNAL;
       __syncthreads();  // the batch's bytes are visible to later batches
     }
 #ifdef PQH_GZIP_PROF
@@ -1044,11 +1047,11 @@ __device__ bool gz_huff_stage(GzLds& E, const uint8_t* src, int32_t n, int32_t a
       E.pbit = E.hx[kBlock - 1];
     }
   }
-  return true;
+  return PQH_OK;
 }
 
-// Decode one gzip stream src[0, n) into dst[0, expected).  Whole workgroup; returns PQH_OK or
-// PQH_ERR_DECOMPRESS (uniform).
+// Decode one gzip stream src[0, n) into dst[0, expected).  Whole workgroup; returns PQH_OK,
+// PQH_ERR_DECOMPRESS or PQH_ERR_INTERNAL (uniform).
 __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_t expected, GzLds& E) {
   const int tid = threadIdx.x;
   if (n64 > 0x7fffffff - kGzStage || expected > 0x7fffffff) return PQH_ERR_DECOMPRESS;
@@ -1099,7 +1102,7 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
     if (tid == 0) GZ_ADD(6, t1 - t0);
 #endif
     if (uni(E.mode) == kGzHuff) {
-      const bool ok = gz_huff_stage(E, src, n, a0, d, total, dst);
+      const int hs = gz_huff_stage(E, src, n, a0, d, total, dst);
 #ifdef PQH_GZIP_PROF
       GZ_CLK(t2);
       if (tid == 0) {
@@ -1107,7 +1110,7 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
         GZ_ADD(3, 1);
       }
 #endif
-      if (!ok) return PQH_ERR_DECOMPRESS;
+      if (hs != PQH_OK) return hs;
       continue;
     }
     if (tid < 64) gz_parse(E, src, n, a0, d, total);
@@ -1117,11 +1120,11 @@ __device__ int gzip_stream(const uint8_t* src, int64_t n64, uint8_t* dst, int64_
     const int32_t bl = uni(E.bulk_len);
     if (bl > 0) {
       const int32_t bs = uni(E.bulk_src);
-      if (int64_t(d) + bl > total || bs < 0 || int64_t(bs) + bl > n) return PQH_ERR_DECOMPRESS;  // (validated by gz_serial)
+      if (int64_t(d) + bl > total || bs < 0 || int64_t(bs) + bl > n) return PQH_ERR_INTERNAL;  // (validated by gz_serial)
       snap_copy(dst + d, src + bs, bl);
       d += bl;
     } else if (T > 0) {
-      if (!gz_batch(E, T, nE, d, a0, src, dst, n, total)) return PQH_ERR_DECOMPRESS;
+      if (!gz_batch(E, T, nE, d, a0, src, dst, n, total)) return PQH_ERR_INTERNAL;
       d += T;
     }
     __syncthreads();  // this batch's bytes are visible to the next batches' reads and the CRC

@@ -205,7 +205,7 @@ __device__ __forceinline__ void nest_publish(int64_t* w, uint64_t v) {
 // reads 64 predecessors at once (lane i: tile k-1-i): the nearest inclusive word ends the walk,
 // otherwise the 64 counts are added and the window moves back; a window with an unpublished word
 // before the nearest inclusive one is read again.
-__device__ __forceinline__ int64_t nest_lookback(int64_t* words, int k, int f, int64_t count) {
+__device__ __forceinline__ int64_t nest_lookback(int64_t* words, int k, int f, int64_t count, bool* stuck) {
   const int lane = threadIdx.x & 63;
   uint64_t* mine = reinterpret_cast<uint64_t*>(words + int64_t(k) * kNestFlags + f);
   if (k == 0) {
@@ -223,7 +223,10 @@ __device__ __forceinline__ int64_t nest_lookback(int64_t* words, int k, int f, i
     const uint64_t notready = __ballot((w >> 62) == 0), incl = __ballot((w & kNestIncl) != 0);
     const uint64_t need = incl ? (incl & (0 - incl)) * 2 - 1 : ~0ull;  // lanes up to the nearest inclusive
     if (notready & need) {  // bounded: those workgroups are running (never expected to run out)
-      if (++spins > (1 << 20)) break;
+      if (++spins > (1 << 20)) {  // the base would be partial: the caller fails the chunk (INTERNAL)
+        *stuck = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -304,7 +307,11 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
     // wave v looks back for flags v, v + 4, ... (the counts were staged before the scans' barrier)
     for (int g = int(threadIdx.x >> 6); g <= L; g += kBlock / 64) {
       const int64_t cnt = sflag[1][g];
-      const int64_t excl = nest_lookback(b.nsums + int64_t(N.tile_base) * kNestFlags, t.k, g, cnt);
+      bool stuck = false;
+      const int64_t excl = nest_lookback(b.nsums + int64_t(N.tile_base) * kNestFlags, t.k, g, cnt, &stuck);
+      if (stuck && (threadIdx.x & 63) == 0)  // never a property of the input: PQH_ERR_INTERNAL
+        atomicMin(&b.states[b.chunks[N.chunk].first_page].err,
+                  (unsigned long long)err_key(PQH_PHASE_LOAD, 0, PQH_ERR_INTERNAL));
       if ((threadIdx.x & 63) == 0) {
         sflag[0][g] = excl;
         sflag[1][g] = excl + cnt;

@@ -21,10 +21,11 @@ STATUS = {
     14: "DELTA_BIT_WIDTH", 15: "DELTA_STREAM", 16: "NEGATIVE_LENGTH", 17: "NEGATIVE_DLBA_LENGTH",
     18: "DBA_PREFIX", 19: "DBA_COUNT", 20: "INT96_SHORT", 21: "UNSUPPORTED", 22: "PAGE_HEADER",
     23: "DECOMPRESS", 24: "CRC", 25: "THRIFT", 26: "IO", 27: "ARG", 28: "HIP", 29: "NOMEM", 30: "SCHEMA",
-    31: "DICT_PAGE", 32: "NO_DEVICE", 33: "NOT_IMPLEMENTED",
+    31: "DICT_PAGE", 32: "NO_DEVICE", 33: "NOT_IMPLEMENTED", 34: "INTERNAL",
 }
 OK = 0
 NOT_IMPLEMENTED = 33
+INTERNAL = 34
 # error phases (pqh_phase): page load (readChunk), repetition levels, definition levels, values
 PHASE_LOAD, PHASE_REP, PHASE_DEF, PHASE_VALUES = range(4)
 CTX_PROFILE = 1
