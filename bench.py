@@ -4,13 +4,17 @@
 A "step" is one full decode pass (every page of every chunk of the rank's row groups) over
 HBM-resident page images: k_prologue -> (delta / byte-array walks) -> k_scan -> k_expand (levels,
 PLAIN copies, booleans, dictionaries) / k_delta_* / k_ba_* / k_nest_*.
-Default workload at N=1 = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16
-row groups.  Default at N>1 = BASELINE.json configs[2] (C3): ONE 1B-row file of 128 row groups whose
-row groups are sharded in contiguous blocks over the N GPUs -> "scaling": "strong" (the other
-workloads at N>1 give every rank its own file -> "weak").  One process per GPU, no data-path
-collective: the only collectives are the measurement reductions and one all-gather of the blocks.
+Default workload = BASELINE.json configs[1] (C2): 100M rows x 6 columns, data page V2, 16 row
+groups, at EVERY N: each rank decodes its own C2 file ("scaling": "weak"), so the driver's N=1 and
+N>1 lines measure the same per-GPU work.  Every line also carries `c3_strong`, BASELINE.json
+configs[2] (C3: ONE 1B-row file of 128 row groups): at N>1 the row groups are sharded in contiguous
+blocks over the N GPUs and timed as strong scaling; at N=1 the whole file is timed, and so is rank
+0's share of it at N = 2, 4, 8 (shard.row_group_block) on the one GPU -- the single-GPU proxy of the
+1->8 curve, with its predicted efficiency.  (--workload c3 makes the strong-scaling C3 run the main
+line.)  One process per GPU, no data-path collective: the only collectives are the measurement
+reductions and one all-gather of the blocks.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|c5z] [--rows R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|c5z] [--rows R] [--no-c3]
 
 --gpus N without a launcher (WORLD_SIZE unset): bench.py starts the N rank processes itself (before
 anything touches the GPU), rendezvous at 127.0.0.1; under torchrun it is one of the ranks.
@@ -176,6 +180,104 @@ def check_chunk(ctx, batch, chunk, res, np):
         raise RuntimeError(f"chunk {chunk}: GPU output differs from the oracle")
 
 
+def check_statuses(batch, num_chunks, native, where):
+    """Every chunk of the batch's LAST run decoded without error (a guard that fired during the timed
+    passes -- PQH_ERR_INTERNAL, or any decode error -- fails the bench instead of passing unseen)."""
+    for c in range(num_chunks):
+        o = batch.chunk_out(c)
+        if o.status != native.OK:
+            raise RuntimeError(f"{where}: chunk {c} failed: {native.STATUS.get(o.status, o.status)} "
+                               f"page {o.error_page} phase {o.error_phase}")
+
+
+def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync):
+    """Load row groups [rg0, rg1) of f into one HBM-resident batch and time `steps` decode runs
+    (graph replays) between barriers; statuses checked before and after the timed runs.
+    Returns (seconds, decoded bytes per run, algorithmic bytes read per run, pages)."""
+    ncols = len(f.columns())
+    hb = f.load(rg0, rg1, list(range(ncols)), ctx=ctx)
+    b = native.Batch.from_host(ctx, hb)
+    try:
+        b.run()
+        b.sync()
+        check_statuses(b, hb.num_chunks, native, f"row groups [{rg0}, {rg1})")
+        rd, wr = b.traffic()
+        for _ in range(warmup):
+            b.run()
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            b.run()
+        barrier_sync()
+        el = time.perf_counter() - t0
+        b.sync()
+        check_statuses(b, hb.num_chunks, native, f"row groups [{rg0}, {rg1}) after the timed runs")
+        return el, wr, rd, hb.num_pages
+    finally:
+        b.close()
+        hb.close()
+
+
+def c3_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync, log):
+    """BASELINE.json configs[2] (C3, 128 row groups of one 1B-row file) as strong scaling.
+    N>1: every rank opens the SAME file (generated once into /dev/shm) and decodes its contiguous
+    block; whole-node GB/s = sum of decoded bytes / max rank time.  N=1: the whole file on the one
+    GPU, plus rank 0's block at N = 2, 4, 8 timed alone on the one GPU: the proxy of the 1->8 curve,
+    predicted efficiency(N) = T(128 row groups) / (N x T(rank 0's block))."""
+    desc, builder = datasets.WORKLOADS["c3"]
+    steps = max(3, min(args.steps, 10))
+    warm = max(1, min(args.warmup, 2))
+    t0 = time.perf_counter()
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    path = os.path.join(shm, f"pqh_bench_c3_20_{os.environ.get('MASTER_PORT', '0')}_{os.getpid() if world == 1 else 0}.parquet")
+    if rank == 0:
+        builder(seed=20, **({"rows": args.c3_rows} if args.c3_rows else {})).tofile(path + ".part")
+        os.replace(path + ".part", path)
+    if world > 1:
+        dist.barrier()
+    gen_s = time.perf_counter() - t0
+    f = native.File(path)
+    try:
+        nrg = f.num_row_groups
+        dev = f"cuda:{local}" if world > 1 else None
+        if world > 1:
+            rg0, rg1 = pkg.shard.row_group_block(nrg, world, rank)
+            el, wr, _, pages = timed_block(ctx, native, f, rg0, rg1, steps, warm, barrier_sync)
+            rows = sum(f.row_group_num_rows(g) for g in range(rg0, rg1))
+            el, total = pkg.shard.reduce_step(el, wr, device=dev)
+            blocks = pkg.shard.gather_blocks(rg0, rg1, rows, wr, device=dev)
+            pkg.shard.check_cover(blocks, nrg, f.num_rows)
+            rec = {"workload": desc, "scaling": "strong", "n_gpus": world, "rows_total": f.num_rows,
+                   "row_groups": nrg, "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
+                   "value": round(total * steps / el / 1e9, 2), "unit": "GB/s",
+                   "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
+                              for r, b in enumerate(blocks)]}
+        else:
+            el1, wr1, _, pages = timed_block(ctx, native, f, 0, nrg, steps, warm, barrier_sync)
+            t1 = el1 / steps
+            rec = {"workload": desc, "scaling": "strong", "n_gpus": 1, "rows_total": f.num_rows, "row_groups": nrg,
+                   "steps": steps, "ms_per_step": round(t1 * 1e3, 4), "value": round(wr1 / t1 / 1e9, 2), "unit": "GB/s",
+                   "proxy": []}
+            for n in (2, 4, 8):
+                a, b = pkg.shard.row_group_block(nrg, n, 0)
+                el, wr, _, _ = timed_block(ctx, native, f, a, b, steps, warm, barrier_sync)
+                tn = el / steps
+                rec["proxy"].append({"n_gpus": n, "rank0_row_groups": [a, b], "rank0_ms_per_step": round(tn * 1e3, 4),
+                                     "predicted_whole_node_gbps": round(wr1 / tn / 1e9, 2),
+                                     "predicted_efficiency": round(t1 / (n * tn), 4)})
+            rec["proxy_method"] = ("rank 0's block of shard.row_group_block(128, N, 0) decoded alone on this one GPU "
+                                   "(each rank owns a GPU, an HBM and a host link; no collective in the timed region): "
+                                   "predicted whole-node GB/s = the file's decoded bytes / that time")
+        rec["generate_s"] = round(gen_s, 2)
+        return rec
+    finally:
+        f.close()
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            os.unlink(path)
+
+
 def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
     """Plain pinned host -> HBM copy rate on this box (the PCIe bound of the end-to-end mode)."""
     import ctypes
@@ -231,32 +333,57 @@ def launch_ranks(n):
     return rc
 
 
-def dry_run(args, world, rank, dist, pkg, builder, kw, seed, strong, desc):
-    """--dry-run: the rank plan and the reductions without a GPU (CPU oracle decode of the shard)."""
+def dry_run(args, world, rank, dist, pkg, datasets, builder, kw, seed, strong, desc):
+    """--dry-run: the rank plan and the reductions without a GPU (CPU oracle decode of the shard) --
+    the main line's shape (weak: a file per rank; strong: blocks of one file) and the c3_strong
+    sub-record's (blocks of one C3 file at N > 1; at N = 1 the proxy blocks for N = 2, 4, 8)."""
     from oracle import oracle as O
 
-    data = builder(seed=seed, **kw)
-    fr = O.FileReader(data)
-    nrg = len(fr.row_groups)
-    rg0, rg1 = pkg.shard.row_group_block(nrg, world, rank) if strong else (0, nrg)
-    rows = sum(fr.row_group_num_rows(g) for g in range(rg0, rg1))
-    t0 = time.perf_counter()
-    written = 0
-    for rg in range(rg0, rg1):
-        for ci in range(len(fr.columns)):
-            for r in O.decode_chunk(fr.read_chunk(rg, ci)):
-                written += len(r.values) + (0 if r.def_levels is None else len(r.def_levels))
-    elapsed = time.perf_counter() - t0
-    el, total = pkg.shard.reduce_step(elapsed, written)
-    blocks = pkg.shard.gather_blocks(rg0, rg1, rows, written)
-    if strong:
-        pkg.shard.check_cover(blocks, nrg, fr.num_rows)
+    def decode(fr, rg0, rg1):
+        written = 0
+        for rg in range(rg0, rg1):
+            for ci in range(len(fr.columns)):
+                for r in O.decode_chunk(fr.read_chunk(rg, ci)):
+                    written += len(r.values) + (0 if r.def_levels is None else len(r.def_levels))
+        return written
+
+    def sharded(fr, strong_):
+        nrg = len(fr.row_groups)
+        rg0, rg1 = pkg.shard.row_group_block(nrg, world, rank) if strong_ else (0, nrg)
+        rows = sum(fr.row_group_num_rows(g) for g in range(rg0, rg1))
+        t0 = time.perf_counter()
+        written = decode(fr, rg0, rg1)
+        el, total = pkg.shard.reduce_step(time.perf_counter() - t0, written)
+        blocks = pkg.shard.gather_blocks(rg0, rg1, rows, written)
+        if strong_:
+            pkg.shard.check_cover(blocks, nrg, fr.num_rows)
+        return el, total, [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
+                           for r, b in enumerate(blocks)]
+
+    fr = O.FileReader(builder(seed=seed, **kw))
+    el, total, shards = sharded(fr, strong)
+    c3 = None
+    if not strong and not args.no_c3:
+        c3desc, c3b = datasets.WORKLOADS["c3"]
+        fr3 = O.FileReader(c3b(seed=20, **({"rows": args.c3_rows} if args.c3_rows else {})))
+        nrg = len(fr3.row_groups)
+        if world > 1:
+            el3, total3, shards3 = sharded(fr3, True)
+            c3 = {"workload": c3desc, "scaling": "strong", "n_gpus": world, "rows_total": fr3.num_rows,
+                  "row_groups": nrg, "decoded_bytes_total": total3, "max_rank_s": el3, "shards": shards3}
+        else:
+            full = decode(fr3, 0, nrg)
+            proxy = []
+            for n in (2, 4, 8):
+                a, b = pkg.shard.row_group_block(nrg, n, 0)
+                proxy.append({"n_gpus": n, "rank0_row_groups": [a, b], "rank0_decoded_bytes": decode(fr3, a, b)})
+            c3 = {"workload": c3desc, "scaling": "strong", "n_gpus": 1, "rows_total": fr3.num_rows, "row_groups": nrg,
+                  "decoded_bytes_total": full, "proxy": proxy}
     if rank == 0:
         print(json.dumps({"dry_run": True, "metric": METRIC, "n_gpus": world, "scaling": "strong" if strong else "weak",
                           "config": {"workload": desc, "rows_total": fr.num_rows if strong else fr.num_rows * world},
-                          "decoded_bytes_total": total, "max_rank_s": el,
-                          "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
-                                     for r, b in enumerate(blocks)]}), flush=True)
+                          "decoded_bytes_total": total, "max_rank_s": el, "shards": shards, "c3_strong": c3}),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -267,14 +394,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=None, choices=["c1", "c2", "c3", "c4", "c5", "c5z"],
-                    help="default: c2 on one GPU, c3 (strong scaling) on several")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5z"],
+                    help="default: c2 (weak scaling: a C2 file per GPU) at every N; c3 = strong scaling")
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--codec", default=None, choices=["snappy", "gzip"],
                     help="c5 / c5z: the page codec (default SNAPPY, as configs[4] names)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
+    ap.add_argument("--no-c3", action="store_true", help="skip the c3_strong sub-record")
+    ap.add_argument("--c3-rows", type=int, default=0, help=argparse.SUPPRESS)  # tests: a smaller C3 file
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -285,8 +414,6 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"WORLD_SIZE={world} (launcher) overrides --gpus {args.gpus}")
-    if args.workload is None:
-        args.workload = "c2" if world == 1 else "c3"
     torch = dist = None
     try:
         import torch  # noqa: F811
@@ -316,7 +443,7 @@ def main():
     strong = args.workload == "c3"
     seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40, "c5z": 41}[args.workload] + (0 if strong else 1000 * rank)
     if args.dry_run:
-        return dry_run(args, world, rank, dist, pkg, builder, kw, seed_kw, strong, desc)
+        return dry_run(args, world, rank, dist, pkg, datasets, builder, kw, seed_kw, strong, desc)
     t0 = time.perf_counter()
     path = None
     if strong and world > 1:
@@ -351,11 +478,9 @@ def main():
 
     batch.run()
     batch.sync()
-    for c in range(hb.num_chunks):
-        o = batch.chunk_out(c)
-        if o.status != native.OK:
-            raise RuntimeError(f"chunk {c} failed: {native.STATUS.get(o.status)} page {o.error_page}")
+    check_statuses(batch, hb.num_chunks, native, "first run")
     bytes_read, bytes_written = batch.traffic()
+    pages_per_gpu, payload_bytes = hb.num_pages, hb.payload_bytes
     for _ in range(args.warmup):
         batch.run()
     batch.sync()
@@ -374,6 +499,8 @@ def main():
         batch.run()
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    batch.sync()
+    check_statuses(batch, hb.num_chunks, native, "after the timed steps")
     # whole job: max step time over ranks, sum of decoded bytes (shard.py; RCCL for N > 1)
     dev = f"cuda:{local}" if world > 1 else None
     elapsed, total_written = pkg.shard.reduce_step(elapsed, bytes_written, device=dev)
@@ -390,6 +517,7 @@ def main():
         batch.run()
     batch.sync()
     prof_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    check_statuses(batch, hb.num_chunks, native, "after the profiled steps")
     stats = batch.kernel_stats()
     ctx.set_profile(False)
     ms_per_step = elapsed / args.steps * 1e3
@@ -490,6 +618,12 @@ def main():
                 sb.run_staged()
         barrier_sync()
         el = time.perf_counter() - t0
+        for g, sb in enumerate(staged):  # the last timed pass decoded every chunk without error
+            sb.sync()
+            for c in range(ncols * (cuts[g + 1] - cuts[g])):
+                if sb.chunk_out(c).status != native.OK:
+                    raise RuntimeError(f"staged decode failed after the timed passes: range {g} chunk {c} "
+                                       f"{native.STATUS.get(sb.chunk_out(c).status)}")
         el, total = pkg.shard.reduce_step(el, written, device=f"cuda:{local}" if world > 1 else None)
         out = {"mode": ("pinned H2D of the COMPRESSED pages, then k_snappy / k_gzip + decode of all of them in one batch"
                         if device_snappy else
@@ -530,6 +664,7 @@ def main():
             for _ in range(3):
                 bd.run()
             bd.sync()
+            check_statuses(bd, hd.num_chunks, native, f"{dev_kernel} profiled runs")
             ks = [s for s in bd.kernel_stats() if s.name.decode() == dev_kernel and s.launches]
             ctx.set_profile(False)
             if ks:
@@ -539,6 +674,11 @@ def main():
                                        "decompressed_gbps": round(hd.image_bytes / (ms * 1e-3) / 1e9, 1)}
             bd.close()
             hd.close()
+    c3 = None
+    if not args.no_c3 and args.workload != "c3":
+        hb.close()
+        hb = None
+        c3 = c3_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync, log)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -558,7 +698,7 @@ def main():
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
             "config": {"workload": desc, "rows_total": f.num_rows if strong else f.num_rows * world,
                        "rows_per_gpu": my_rows, "row_groups_per_gpu": rg1 - rg0,
-                       "pages_per_gpu": hb.num_pages,
+                       "pages_per_gpu": pages_per_gpu,
                        "parallelism": (f"row groups of one file sharded in contiguous blocks over {world} GPU(s)"
                                        if strong else f"one file of {f.num_row_groups} row groups per GPU x{world}")
                        + "; no data-path collective",
@@ -573,16 +713,18 @@ def main():
             "roofline": roof,
             "kernels": kernels,
             "host": {"generate_s": round(gen_s, 2), "walk_decompress_s": round(walk_s, 2), "h2d_s": round(h2d_s, 3),
-                     "h2d_gbps": round(hb.payload_bytes / h2d_s / 1e9, 2)},
+                     "h2d_gbps": round(payload_bytes / h2d_s / 1e9, 2)},
             "e2e": e2e,
             ("e2e_device_gzip" if args.codec == "gzip" else "e2e_device_snappy"): e2e_dev,
+            "c3_strong": c3,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
             "cpu_comparator_pyarrow": cpu_pa,
             "verified": verified,
         }
         print(json.dumps(line), flush=True)
-    hb.close()
+    if hb is not None:
+        hb.close()
     f.close()
     ctx.close()
     if world > 1:

@@ -107,27 +107,58 @@ def test_two_rank_gloo_shards(tmp_path):
     assert sum(b[3] for b in blocks) == total
 
 
-def test_bench_self_launch_two_ranks():
-    """`bench.py --gpus 2` without a launcher starts its two rank processes itself; the default
-    workload at N > 1 is C3 (one file of 128 row groups, strong scaling).  --dry-run puts the CPU
-    oracle in place of the GPU decode and gloo in place of RCCL, so the plan (contiguous blocks that
-    tile the file) and the reductions (sum of bytes, max of time) are checked here."""
+def _bench_dry(gpus, *extra):
     import json
     import subprocess
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    rows = 300_000
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--rows", str(rows)],
-                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run"] + list(extra),
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
-    d = json.loads(lines[0])
-    assert d["dry_run"] and d["n_gpus"] == 2 and d["scaling"] == "strong"
-    assert d["config"]["workload"].startswith("C3") and d["config"]["rows_total"] == rows
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` without a launcher starts its two rank processes itself.  The main line is
+    C2 at every N (weak scaling: a file per rank, the same per-GPU work as the N=1 line); the
+    c3_strong sub-record is C3 (one file of 128 row groups) sharded in contiguous blocks (strong
+    scaling).  --dry-run puts the CPU oracle in place of the GPU decode and gloo in place of RCCL, so
+    both plans (blocks that tile the file) and the reductions (sum of bytes, max of time) are checked
+    here."""
+    rows, c3rows = 20_000, 300_000
+    d = _bench_dry(2, "--rows", str(rows), "--c3-rows", str(c3rows))
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["workload"].startswith("C2") and d["config"]["rows_total"] == 2 * rows
     sh = d["shards"]
-    assert [s["rank"] for s in sh] == [0, 1]
+    assert [s["rank"] for s in sh] == [0, 1] and all(s["rows"] == rows for s in sh)
+    assert d["decoded_bytes_total"] == sum(s["decoded_bytes"] for s in sh) and d["max_rank_s"] > 0
+    c3 = d["c3_strong"]
+    assert c3["scaling"] == "strong" and c3["n_gpus"] == 2 and c3["workload"].startswith("C3")
+    assert c3["rows_total"] == c3rows and c3["row_groups"] == 128
+    sh = c3["shards"]
     assert sh[0]["row_groups"] == [0, 64] and sh[1]["row_groups"] == [64, 128]
-    assert sum(s["rows"] for s in sh) == rows
-    assert d["decoded_bytes_total"] == 8 * rows == sum(s["decoded_bytes"] for s in sh)
-    assert d["max_rank_s"] > 0
+    assert sum(s["rows"] for s in sh) == c3rows
+    assert c3["decoded_bytes_total"] == 8 * c3rows == sum(s["decoded_bytes"] for s in sh)
+
+
+def test_bench_single_gpu_scaling_proxy():
+    """At N=1 the c3_strong sub-record carries the single-GPU proxy of the 1->8 curve: the whole C3
+    file and rank 0's block of shard.row_group_block(128, N, 0) for N = 2, 4, 8."""
+    c3rows = 200_000
+    d = _bench_dry(1, "--rows", "10000", "--c3-rows", str(c3rows))
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak"
+    c3 = d["c3_strong"]
+    assert c3["n_gpus"] == 1 and c3["decoded_bytes_total"] == 8 * c3rows
+    assert [(p["n_gpus"], p["rank0_row_groups"]) for p in c3["proxy"]] == [(2, [0, 64]), (4, [0, 32]), (8, [0, 16])]
+    for p in c3["proxy"]:
+        assert abs(p["rank0_decoded_bytes"] * p["n_gpus"] - c3["decoded_bytes_total"]) <= 8 * p["n_gpus"] * 128
+
+
+def test_bench_strong_main_line():
+    """--workload c3 keeps the strong-scaling C3 run as the main line."""
+    rows = 300_000
+    d = _bench_dry(2, "--workload", "c3", "--rows", str(rows))
+    assert d["scaling"] == "strong" and d["config"]["rows_total"] == rows and d["c3_strong"] is None
+    assert [s["row_groups"] for s in d["shards"]] == [[0, 64], [64, 128]]
