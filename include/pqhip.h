@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 5
+#define PQH_ABI_VERSION 6
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -135,17 +135,20 @@ enum pqh_phase {
  * page_v2.go:31-131, page_dict.go:35-72) for every page of a set of column chunks.
  * ------------------------------------------------------------------------------------------- */
 
+/* Repetition levels the nesting outputs support (the schema walk records the repeated nodes'
+ * definition levels up to this depth).  Level bytes are uint8, so no column has more than 255. */
+#define PQH_MAX_NEST 32
+
 typedef struct pqh_column {
   int32_t physical_type; /* enum pqh_physical_type */
   int32_t type_length;   /* FIXED_LEN_BYTE_ARRAY length (SchemaElement.type_length) */
   int32_t max_def;       /* Column.MaxDefinitionLevel() (schema.go:904-914) */
   int32_t max_rep;       /* Column.MaxRepetitionLevel() */
-  int32_t rep_def[8];    /* definition level of the k-th REPEATED node on the path (k < max_rep), from
-                            readColumnSchema/readGroupSchema (schema.go:893-990); used by the nesting
-                            outputs (pqh_batch_nesting), which need max_rep <= PQH_MAX_NEST */
+  int32_t rep_def[PQH_MAX_NEST]; /* definition level of the k-th REPEATED node on the path
+                            (k < max_rep), from readColumnSchema/readGroupSchema (schema.go:893-990);
+                            used by the nesting outputs (pqh_batch_nesting), which need
+                            max_rep <= PQH_MAX_NEST */
 } pqh_column;
-
-#define PQH_MAX_NEST 8
 
 /* One page as the reference page walker sees it (parquet.PageHeader fields + the decompressed
  * page image).  For DATA_PAGE and DICTIONARY_PAGE the image is the decompressed block; for

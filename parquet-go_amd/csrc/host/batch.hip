@@ -836,33 +836,40 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   for (int32_t c = 0; c < num_chunks && !rc; c++) {
     const pqh_column& col = chunks[c].column;
     const int64_t n = b->chunk_n[size_t(c)];
-    if (col.max_rep <= 0 || col.max_rep > kMaxNest || n <= 0) continue;
+    if (col.max_rep <= 0 || col.max_rep > PQH_MAX_NEST || n <= 0) continue;
     bool ok = true;  // repeated-node definition levels must rise strictly within [1, max_def]
     for (int l = 0; l < col.max_rep; l++)
       ok = ok && col.rep_def[l] >= 1 && col.rep_def[l] <= col.max_def && (l == 0 || col.rep_def[l] > col.rep_def[l - 1]);
     if (!ok) continue;
-    DevNest N;
-    memset(&N, 0, sizeof(N));
-    N.chunk = c;
-    N.levels = col.max_rep;
-    N.max_def = col.max_def;
-    N.n = n;
-    N.tile_base = int32_t(b->nest_tiles.size());
-    N.tile_n = int32_t(ceil_div(n, kNestTile));
-    for (int l = 0; l < col.max_rep; l++) {
-      N.rep_def[l] = col.rep_def[l];
-      void* p = nullptr;
-      if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int32_t)))) break;
-      N.offsets[l] = static_cast<int32_t*>(p);
-      if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
-      N.validity[l] = static_cast<uint8_t*>(p);
-    }
-    void* p = nullptr;
-    if (rc || (rc = dalloc(b, &p, size_t(n) + 64))) break;
-    N.leaf_valid = static_cast<uint8_t*>(p);
+    // windows of kMaxNest levels: one DevNest each (the chunk's are consecutive in b->nests)
     b->chunk_nest[size_t(c)] = int32_t(b->nests.size());
-    for (int32_t k = 0; k < N.tile_n; k++) b->nest_tiles.push_back(Tile{int32_t(b->nests.size()), k, 0, 1});
-    b->nests.push_back(N);
+    void* leaf = nullptr;
+    if ((rc = dalloc(b, &leaf, size_t(n) + 64))) break;
+    for (int32_t l0 = 0; l0 < col.max_rep && !rc; l0 += kMaxNest) {
+      DevNest N;
+      memset(&N, 0, sizeof(N));
+      N.chunk = c;
+      N.levels = std::min<int32_t>(kMaxNest, col.max_rep - l0);
+      N.lbase = l0;
+      N.d0 = l0 > 0 ? col.rep_def[l0 - 1] : 0;
+      N.leaf = l0 + N.levels == col.max_rep;
+      N.max_def = col.max_def;
+      N.n = n;
+      N.tile_base = int32_t(b->nest_tiles.size());
+      N.tile_n = int32_t(ceil_div(n, kNestTile));
+      for (int l = 0; l < N.levels; l++) {
+        N.rep_def[l] = col.rep_def[l0 + l];
+        void* p = nullptr;
+        if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int32_t)))) break;
+        N.offsets[l] = static_cast<int32_t*>(p);
+        if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
+        N.validity[l] = static_cast<uint8_t*>(p);
+      }
+      N.leaf_valid = static_cast<uint8_t*>(leaf);
+      for (int32_t k = 0; k < N.tile_n; k++) b->nest_tiles.push_back(Tile{int32_t(b->nests.size()), k, 0, 1});
+      b->nests.push_back(N);
+    }
+    if (rc) break;
   }
   // Tiles in round-robin order over the chunks (tile k of every chunk, then tile k + 1): a chunk's
   // tiles stay in order, as the one-pass write's look-back needs, and the tiles in flight at once
@@ -1325,10 +1332,10 @@ int pqh_batch_sync(pqh_batch* b) {
     double w = 0;
     for (int l = 0; l < N.levels; l++) w += double(b->nest_totals[i * kNestFlags + size_t(l)] + 1) * 4 +
                                           double(b->nest_totals[i * kNestFlags + size_t(l)]);
-    w += double(b->nest_totals[i * kNestFlags + size_t(N.levels)]);
+    if (N.leaf) w += double(b->nest_totals[i * kNestFlags + size_t(N.levels)]);
     wr += w;
     b->k_written[13] += w;
-    b->k_read[13] += 2.0 * double(N.n);
+    if (N.lbase == 0) b->k_read[13] += 2.0 * double(N.n);  // (the algorithmic bytes read the levels once)
   }
   b->bytes_written = wr;
   for (int k = 0; k < kNumKernels; k++) {
@@ -1546,24 +1553,31 @@ int pqh_batch_nesting(const pqh_batch* b, int32_t chunk, pqh_nest_out* out) {
       out->num_levels = col.max_rep;
       return PQH_OK;
     }
-    return set_err(b->ctx, PQH_ERR_NOT_IMPLEMENTED, "nesting needs max_rep <= 8 and the repeated nodes' definition levels");
+    return set_err(b->ctx, PQH_ERR_NOT_IMPLEMENTED,
+                   "nesting needs max_rep <= PQH_MAX_NEST and the repeated nodes' definition levels");
   }
-  const DevNest& N = b->nests[size_t(ni)];
   const DevChunk& D = b->hchunks[size_t(chunk)];
   for (int32_t i = 0; i < D.num_pages; i++) {
     const PageState& S = b->states[size_t(D.first_page + i)];
     if (S.err != kNoError && out->status == PQH_OK) out->status = int32_t(S.err & 0xff);
   }
-  out->num_levels = N.levels;
-  const int64_t* tot = b->nest_totals.data() + size_t(ni) * kNestFlags;
-  for (int l = 0; l < N.levels; l++) {
-    out->levels[l].def_level = N.rep_def[l];
-    out->levels[l].num_lists = tot[l];
-    out->levels[l].offsets = N.offsets[l];
-    out->levels[l].validity = N.validity[l];
+  out->num_levels = col.max_rep;
+  // the chunk's windows (consecutive DevNests): window flag f counts E_{lbase + f}
+  for (int32_t w = ni; w < int32_t(b->nests.size()) && b->nests[size_t(w)].chunk == chunk; w++) {
+    const DevNest& N = b->nests[size_t(w)];
+    const int64_t* tot = b->nest_totals.data() + size_t(w) * kNestFlags;
+    for (int l = 0; l < N.levels; l++) {
+      pqh_nest_level& o = out->levels[N.lbase + l];
+      o.def_level = N.rep_def[l];
+      o.num_lists = tot[l];
+      o.offsets = N.offsets[l];
+      o.validity = N.validity[l];
+    }
+    if (N.leaf) {
+      out->num_leaf_slots = tot[N.levels];
+      out->leaf_validity = N.leaf_valid;
+    }
   }
-  out->num_leaf_slots = tot[N.levels];
-  out->leaf_validity = N.leaf_valid;
   return PQH_OK;
 }
 

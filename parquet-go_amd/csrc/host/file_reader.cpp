@@ -132,7 +132,7 @@ struct SchemaBuilder {
     if (e.type < 0 || e.type > PQH_FIXED_LEN_BYTE_ARRAY) return fail("unsupported type");
     if (e.type == PQH_FIXED_LEN_BYTE_ARRAY && !e.has_type_length) return fail("type with nil type length");
     ColumnMeta cm;
-    cm.col = pqh_column{e.type, e.type_length, d, r, {0, 0, 0, 0, 0, 0, 0, 0}};
+    cm.col = pqh_column{e.type, e.type_length, d, r, {}};
     for (size_t k = 0; k < rd2.size() && k < PQH_MAX_NEST; k++) cm.col.rep_def[k] = rd2[k];
     cm.path = path.empty() ? e.name : path + "." + e.name;
     f->schema[size_t(idx) + 1] = SchemaNode{e, int32_t(f->columns.size()), d, r};

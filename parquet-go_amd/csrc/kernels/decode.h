@@ -194,20 +194,24 @@ struct BaWin {
 
 
 // Nesting outputs of a repeated chunk (pqh_batch_nesting): list offsets / presence per repetition
-// level and leaf validity, from the chunk's decoded level bytes.
+// level and leaf validity, from the chunk's decoded level bytes.  A DevNest covers a window of at
+// most kMaxNest consecutive levels (lbase + 1 .. lbase + levels); a chunk nested deeper than that has
+// one DevNest per window (PQH_MAX_NEST levels in all), each reading the levels once more.
 constexpr int kMaxNest = 8;
 constexpr int kNestTile = 8192;  // level slots per tile (256 threads x 32)
 constexpr int kNestFlags = kMaxNest + 1;  // rows (r == 0) and element starts of levels 1..L
 
 struct DevNest {
   int32_t chunk;
-  int32_t levels;        // max_rep (1..kMaxNest)
+  int32_t levels;        // levels of this window (1..kMaxNest)
   int32_t max_def;
   int32_t tile_base;     // tiles [tile_base, tile_base + tile_n) of the k_nest_* work list
   int32_t tile_n;
-  int32_t pad;
+  int32_t lbase;         // the window's levels are lbase + 1 .. lbase + levels (0: from the rows)
   int64_t n;             // level slots of the chunk
-  int32_t rep_def[kMaxNest];
+  int32_t d0;            // definition level of level lbase's REPEATED node (0 when lbase == 0)
+  int32_t leaf;          // the window ends at max_rep: it writes the leaf validity
+  int32_t rep_def[kMaxNest];  // definition levels of levels lbase + 1 .. lbase + levels
   PQH_G int32_t* offsets[kMaxNest];
   PQH_G uint8_t* validity[kMaxNest];
   PQH_G uint8_t* leaf_valid;

@@ -8,7 +8,9 @@
 //   list of level l starts at slot i      <=>  row start (l == 1) or E_{l-1}(i)     (flag E_{l-1}, E_0 = r_i == 0)
 //   list present (possibly empty)         <=>  d_i >= D_l - 1 at its first slot
 //   leaf slots = E_L slots; non-null      <=>  d_i == max_def
-// so offsets_l[k] = #E_l before the k-th E_{l-1} slot.  Three passes over the level bytes: per-tile
+// so offsets_l[k] = #E_l before the k-th E_{l-1} slot.  With D_0 = 0, E_0 is E_l's formula at l = 0,
+// so a window of levels lbase + 1 .. lbase + L (DevNest) computes E_lbase .. E_{lbase+L} the same way
+// (flag f of the window = E_{lbase+f}).  Three passes over the level bytes: per-tile
 // flag counts (k_nest_count), per-chunk exclusive scans (k_nest_scan), and a write pass with block
 // scans (k_nest_write).  Pinned by oracle.nest_levels against the reference's KATs
 // (tests/golden/dremel_kat.json).
@@ -50,17 +52,17 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
 #pragma unroll
   for (int k = 0; k < 8; k++) hi |= dw[k] | rw[k];
   const uint32_t in = m >= kNestPer ? ~0u : (1u << m) - 1;
-  if ((hi & 0x80808080u) == 0 && N.max_def < 128) {
-    const uint32_t M = uint32_t(N.max_def);
+  if ((hi & 0x80808080u) == 0 && N.max_def < 128 && N.lbase + L < 128) {
+    const uint32_t M = uint32_t(N.max_def), lb = uint32_t(N.lbase), d0 = uint32_t(N.d0);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t d = dw[k], r = rw[k];
-      E[0] |= pack4(~ge8(r, 1) & 0x80808080u) << (4 * k);
+      E[0] |= pack4(~ge8(r, lb + 1) & ge8(d, d0)) << (4 * k);  // (lbase 0: r == 0)
 #pragma unroll
       for (int l = 1; l <= kMaxNest; l++) {
         if (l <= L) {
           const uint32_t D = uint32_t(N.rep_def[l - 1]);
-          E[l] |= pack4(~ge8(r, uint32_t(l) + 1) & ge8(d, D)) << (4 * k);
+          E[l] |= pack4(~ge8(r, lb + uint32_t(l) + 1) & ge8(d, D)) << (4 * k);
           V[l - 1] |= pack4(ge8(d, D - 1)) << (4 * k);
         }
       }
@@ -77,11 +79,11 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
   for (int j = 0; j < kNestPer; j++) {
     const uint32_t d = (dw[j >> 2] >> (8 * (j & 3))) & 0xff, r = (rw[j >> 2] >> (8 * (j & 3))) & 0xff;
     const uint32_t in = j < m ? 1u << j : 0u;
-    E[0] |= r == 0 ? in : 0u;
+    E[0] |= (r <= uint32_t(N.lbase) && d >= uint32_t(N.d0)) ? in : 0u;
 #pragma unroll
     for (int l = 1; l <= kMaxNest; l++) {
       if (l <= L) {
-        E[l] |= (r <= uint32_t(l) && d >= uint32_t(N.rep_def[l - 1])) ? in : 0u;
+        E[l] |= (r <= uint32_t(N.lbase + l) && d >= uint32_t(N.rep_def[l - 1])) ? in : 0u;
         V[l - 1] |= d + 1 >= uint32_t(N.rep_def[l - 1]) ? in : 0u;
       }
     }
@@ -345,6 +347,7 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
       __syncthreads();
     }
   }
+  if (!N.leaf) return;  // (a window above the innermost level)
   // leaf validity at the E_L slots
   uint32_t EL = 0;
   int32_t lposL = 0, totL = 0;

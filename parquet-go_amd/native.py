@@ -30,11 +30,12 @@ INTERNAL = 34
 PHASE_LOAD, PHASE_REP, PHASE_DEF, PHASE_VALUES = range(4)
 CTX_PROFILE = 1
 PAYLOAD_PAD = 256
+MAX_NEST = 32  # include/pqhip.h PQH_MAX_NEST
 
 
 class Column(ctypes.Structure):
     _fields_ = [("physical_type", i32), ("type_length", i32), ("max_def", i32), ("max_rep", i32),
-                ("rep_def", i32 * 8)]
+                ("rep_def", i32 * MAX_NEST)]
 
 
 class Page(ctypes.Structure):
@@ -60,7 +61,7 @@ class NestLevel(ctypes.Structure):
 
 class NestOut(ctypes.Structure):
     _fields_ = [("num_levels", i32), ("status", i32), ("num_leaf_slots", i64), ("leaf_validity", vp),
-                ("levels", NestLevel * 8)]
+                ("levels", NestLevel * MAX_NEST)]
 
 
 class PageResult(ctypes.Structure):
@@ -93,7 +94,7 @@ class KernelStat(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 5  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 6  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -373,6 +374,12 @@ class File:
             out.append((self._text(self.L.pqh_file_column_path, i), c.physical_type, c.type_length, c.max_def,
                         c.max_rep))
         return out
+
+    def rep_def(self, i):
+        """pqh_column.rep_def of column i: the definition level of each REPEATED node on its path."""
+        c = Column()
+        _check(self.L.pqh_file_column(self.h, i, ctypes.byref(c), None, 0))
+        return tuple(c.rep_def[k] for k in range(min(c.max_rep, MAX_NEST)))
 
     def schema(self):
         """[(name, SchemaElement)] in DFS order, root first."""

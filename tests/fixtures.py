@@ -165,3 +165,56 @@ def pyarrow_file(n=20000, version="1.0", compression="NONE", seed=1, page=4096):
     pqa.write_table(tbl, buf, data_page_version=version, compression=compression, row_group_size=n // 2 + 3,
                     data_page_size=page)
     return buf.getvalue()
+
+
+def deep_repeated(n=3000, depth=10, seed=5, wrap=None, v2=False):
+    """A chain of `depth` REPEATED groups (an OPTIONAL group before level l where wrap[l-1]) ending in
+    an OPTIONAL INT32 leaf: max_rep = depth, rep_def[l-1] = D_l.  Rows are random nested lists (null
+    wrappers, empty lists, null leaves), shredded with the Dremel rules the reference's writer follows
+    (data_store.go / schema.go): an element after the first of its list at level l has r = l; a
+    missing wrapper at level l has d = D_{l-1}, an empty list d = D_l - 1, a null leaf d = D_L."""
+    rng = np.random.default_rng(seed)
+    wrap = list(wrap) if wrap is not None else [l % 3 == 1 for l in range(depth)]
+    D, d = [], 0
+    for l in range(depth):
+        d += 2 if wrap[l] else 1
+        D.append(d)
+    dl, rl, vals = [], [], []
+
+    def shred(x, l, r):  # x = the content of level l (1-based)
+        base = D[l - 2] if l >= 2 else 0
+        if wrap[l - 1] and x is None:
+            dl.append(base); rl.append(r)
+            return
+        if not x:
+            dl.append(D[l - 1] - 1); rl.append(r)
+            return
+        for i, e in enumerate(x):
+            rr = r if i == 0 else l
+            if l == depth:
+                dl.append(D[-1] + (e is not None)); rl.append(rr)
+                if e is not None:
+                    vals.append(e)
+            else:
+                shred(e, l + 1, rr)
+
+    def gen(l):
+        if wrap[l - 1] and rng.random() < 0.08:
+            return None
+        k = int(rng.poisson(1.3 if l < depth else 2.0))
+        if l == depth:
+            return [None if rng.random() < 0.1 else int(rng.integers(-2**31, 2**31 - 1)) for _ in range(k)]
+        return [gen(l + 1) for _ in range(k)]
+
+    for _ in range(n):
+        shred(gen(1), 1, 0)
+    schema = [W.element("schema", repetition=-1, num_children=1)]
+    for l in range(depth):
+        if wrap[l]:
+            schema.append(W.element(f"o{l + 1}", repetition=W.OPTIONAL, num_children=1))
+        schema.append(W.element(f"r{l + 1}", repetition=W.REPEATED, num_children=1))
+    schema[-1] = W.element(f"r{depth}", repetition=W.REPEATED, num_children=1)
+    schema.append(W.element("v", W.INT32, W.OPTIONAL))
+    col = W.Column(W.INT32, np.array(vals, dtype=np.int32), def_levels=np.array(dl, np.uint8),
+                   rep_levels=np.array(rl, np.uint8), use_dict=False)
+    return W.write(schema, [col], [n // 2, n - n // 2], v2=v2, max_page_size=8 * 1024), D

@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(pq):
 
 def test_abi_version_and_devices(pq):
     L = pq._lib.hip()
-    assert L.pqh_abi_version() == pq.native.ABI_VERSION == 5
+    assert L.pqh_abi_version() == pq.native.ABI_VERSION == 6
     n = pq.native.device_count()
     assert n >= 0
 
@@ -115,3 +115,18 @@ def test_snappy_roundtrip_against_pyarrow(pq):
     assert fr.read_chunk(0, 0).status == 0  # pyarrow decompressed our snappy
     comp = pa.compress(blob, codec="snappy", asbytes=True)
     assert len(comp) < len(blob)
+
+
+@pytest.mark.parametrize("depth", [1, 9, 17, 32])
+def test_deep_schema_rep_def(pq, depth):
+    """readColumnSchema / readGroupSchema's levels (schema.go:893-990) for chains of repeated groups
+    up to PQH_MAX_NEST deep: max_def, max_rep and every repeated node's definition level (what the
+    nesting outputs need) equal the oracle's schema walk."""
+    data, D = fixtures.deep_repeated(n=40, depth=depth, seed=depth)
+    fr = O.FileReader(data)
+    f = pq.native.File(data)
+    c = fr.columns[0]
+    assert c.rep_def == tuple(D) and c.max_rep == depth
+    assert f.columns()[0][3:] == (c.max_def, c.max_rep)
+    assert f.rep_def(0) == tuple(D)
+    _walk_compare(pq, data)

@@ -646,6 +646,15 @@ def test_nesting_deep_lists(pq, ctx, nest_passes):
     assert _check_nesting(pq, ctx, buf.getvalue()) == 6
 
 
+@pytest.mark.parametrize("depth,rows", [(9, 3000), (10, 3000), (17, 600), (32, 40)])
+def test_nesting_deeper_than_a_window(pq, ctx, nest_passes, depth, rows):
+    """Chains of up to 32 repeated groups (schema.go:893-990 takes any depth): the nesting outputs
+    come in windows of 8 levels (one count / scan / write set per window, DevNest.lbase), every
+    level's offsets and presence and the leaf validity equal oracle.nest_levels."""
+    data, _ = fixtures.deep_repeated(n=rows, depth=depth, seed=depth)
+    assert _check_nesting(pq, ctx, data) == 2
+
+
 def test_plain_chain_layouts(pq, ctx):
     """PLAIN byte-array chains that stress the parallel chain resolution: runs of empty strings
     (every offset looks like a record start), zero bytes inside strings, strings longer than a
