@@ -28,7 +28,11 @@ def files():
     yield "pyarrow-2.0", fixtures.pyarrow_file(n=6000, version="2.0", compression="NONE", page=2048)
 
 
-SIZES = (7, 100, 1 << 30)  # readValues(size) calls per page: the page read in three calls
+SIZES = (7, 100, 1 << 30)
+
+
+def _raw(x):  # bytes as they are (np.asarray(b"") would be a one-byte S1 array), arrays by their bytes
+    return bytes(x) if isinstance(x, (bytes, bytearray)) else np.ascontiguousarray(x).tobytes()  # readValues(size) calls per page: the page read in three calls
 
 
 def walk_both(pq, data, backend="host", batch_for=None, crc=False):
@@ -64,7 +68,7 @@ def walk_both(pq, data, backend="host", batch_for=None, crc=False):
                     elif x is None or y is None:
                         assert x is None and y is None, f"{where} page {i}"
                     else:
-                        assert bytes(np.asarray(x).tobytes()) == bytes(np.asarray(y).tobytes()), f"{where} page {i}"
+                        assert _raw(x) == _raw(y), f"{where} page {i}"
             compared += 1
     hb.close()
     f.close()
