@@ -278,6 +278,72 @@ def c3_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist,
             os.unlink(path)
 
 
+def next_row_record(ctx, pkg, rows=100_000):
+    """FileReader.NextRow throughput on a C4-shaped file (LIST<optional int64> +
+    MAP<string, optional int32>, 2 row groups): records/s through the GPU decode + the columnar
+    assembly over the device's nesting outputs (NextBatch), the GPU decode + the value-by-value
+    restatement (records.RowAssembler), and the oracle's decode + the value-by-value assembly (the
+    CPU path the reference's algorithm implies).  Rows are compared across the three."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from parquet_go_amd import datasets, reader, records
+
+    data = datasets.c4(rows=rows, row_groups=2)
+    out = {"workload": f"C4 shape, {rows} rows, 2 row groups (NextRow records as dicts)"}
+
+    def gpu(columnar):
+        t0 = time.perf_counter()
+        fr = reader.FileReader(data, ctx=ctx, columnar=columnar)
+        got = []
+        while True:
+            b = fr.NextBatch(1 << 20)
+            if not b:
+                break
+            got.extend(b)
+        el = time.perf_counter() - t0
+        paths = dict(fr.assembled)
+        fr.close()
+        return got, el, paths
+
+    got_c, el_c, paths = gpu(True)
+    got_v, el_v, _ = gpu(False)
+    # the oracle's decode + value-by-value assembly
+    t0 = time.perf_counter()
+    fr = O.FileReader(data)
+    f = pkg.native.File(data)
+    schema = f.schema()
+    leaf_el = [e for _, e in schema if e.num_children == 0]
+    ref = []
+    for rg in range(len(fr.row_groups)):
+        stores = {}
+        for ci, col in enumerate(fr.columns):
+            pages = []
+            for r in O.decode_chunk(fr.read_chunk(rg, ci)):
+                if r.status:
+                    raise RuntimeError(f"oracle failed: {r.status}")
+                nv = r.num_values
+                if r.offsets is not None:
+                    vals = [r.values[a:b] for a, b in zip(r.offsets[:-1].tolist(), r.offsets[1:].tolist())]
+                else:
+                    vals = np.frombuffer(r.values, np.int64 if col.physical_type == 2 else np.int32).tolist()
+                pages.append((records.PAGE_OK, nv, r.def_levels, r.rep_levels, lambda v=vals: v))
+            stores[ci] = records.LeafStore(None, col.path, leaf_el[ci].repetition, col.max_def, col.max_rep, pages)
+        asm = records.RowAssembler(schema, None, fr.row_group_num_rows(rg), stores=stores)
+        ref.extend(asm.next_row() for _ in range(fr.row_group_num_rows(rg)))
+    el_o = time.perf_counter() - t0
+    f.close()
+    if not (got_c == got_v == ref):
+        raise RuntimeError("NextRow records differ between the assembly paths")
+    out.update({"rows": len(ref), "verified": "identical records from the three paths",
+                "gpu_columnar_rows_per_s": round(len(ref) / el_c), "gpu_columnar_s": round(el_c, 3),
+                "assembly_paths": paths,
+                "gpu_value_by_value_rows_per_s": round(len(ref) / el_v), "gpu_value_by_value_s": round(el_v, 3),
+                "oracle_value_by_value_rows_per_s": round(len(ref) / el_o), "oracle_value_by_value_s": round(el_o, 3),
+                "note": "each time covers the whole read: host page walk, decode, assembly into Python dicts"})
+    return out
+
+
 def pinned_h2d_rate(ctx, native, nbytes=256 << 20, reps=4):
     """Plain pinned host -> HBM copy rate on this box (the PCIe bound of the end-to-end mode)."""
     import ctypes
@@ -403,6 +469,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
     ap.add_argument("--no-c3", action="store_true", help="skip the c3_strong sub-record")
+    ap.add_argument("--no-next-row", action="store_true", help="skip the NextRow records/s sub-record")
+    ap.add_argument("--next-row-rows", type=int, default=100_000)
     ap.add_argument("--c3-rows", type=int, default=0, help=argparse.SUPPRESS)  # tests: a smaller C3 file
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -674,6 +742,9 @@ def main():
                                        "decompressed_gbps": round(hd.image_bytes / (ms * 1e-3) / 1e9, 1)}
             bd.close()
             hd.close()
+    next_row = None
+    if rank == 0 and world == 1 and not args.no_next_row:
+        next_row = next_row_record(ctx, pkg, rows=args.next_row_rows)
     c3 = None
     if not args.no_c3 and args.workload != "c3":
         hb.close()
@@ -717,6 +788,7 @@ def main():
             "e2e": e2e,
             ("e2e_device_gzip" if args.codec == "gzip" else "e2e_device_snappy"): e2e_dev,
             "c3_strong": c3,
+            "next_row": next_row,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
             "cpu_comparator_pyarrow": cpu_pa,

@@ -8,12 +8,12 @@ package mirrors the reference's reader interface on top of that ABI (see reader.
 """
 from . import _lib  # noqa: F401
 
-__all__ = ["reader", "records", "writer", "native"]
+__all__ = ["reader", "records", "assemble", "writer", "native"]
 
 
 def __getattr__(name):
     import importlib
 
-    if name in ("reader", "records", "writer", "native", "datasets", "build", "shard"):
+    if name in ("reader", "records", "assemble", "writer", "native", "datasets", "build", "shard"):
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

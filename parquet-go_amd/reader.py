@@ -9,6 +9,9 @@ Mirrors github.com/fraugster/parquet-go's FileReader (file_reader.go:32-351) for
       chunks are walked on the host (thrift + codecs) and decoded on the GPU in ONE batch
   FileReader.ReadColumns()          -> {path: ColumnData}: columnar results of readValues for
       every page of the chunk (values, dLevel, rLevel) — the "throughput path" of SURVEY.md §8(b)
+  FileReader.NextRow() / NextBatch(n)  (file_reader.go:258-272): records assembled columnar from
+      the device's nesting outputs (assemble.py), or value by value (records.py) for the row groups
+      where the reference's assembly quirks need it
 Errors follow the reference: ReadColumns raises DecodeError (status, phase, index and page of the
 FIRST error in decode order) for any failing chunk; the row-group cursor fails a row group only on
 readChunk errors (walker, codecs, page load), and NextRow raises a readValues error at the row that
@@ -66,10 +69,10 @@ class ColumnData:
             self.def_levels = ctx.d2h_array(out.def_levels, out.num_values)
         if out.rep_levels:
             self.rep_levels = ctx.d2h_array(out.rep_levels, out.num_values)
-        if out.status != native.OK:
-            return
-        # nesting: [(offsets int32, validity u8) per repetition level], leaf validity u8
-        if nest is not None and nest.num_levels and nest.status == native.OK:
+        # nesting: [(offsets int32, validity u8) per repetition level], leaf validity u8.  Also for a
+        # chunk whose pages fail in readValues: the lists before the failing page are exact (every
+        # offset counts only the slots before it), which is all the record assembly reads of them
+        if nest is not None and nest.num_levels:
             levels = []
             for k in range(nest.num_levels):
                 lv = nest.levels[k]
@@ -154,12 +157,18 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
     return out
 
 
+def records_error():
+    from . import records
+
+    return records.RecordError
+
+
 class FileReader:
     """FileReader (file_reader.go:32-351) over the GPU decode.  The row-group cursor follows the
     reference: rowGroupPosition is 1-based once a group is loaded, advanceIfNeeded loads the next
     group when the current one is exhausted or skipped, io.EOF past the last group (EOFError)."""
 
-    def __init__(self, source, *columns, device=0, validate_crc=False, ctx=None):
+    def __init__(self, source, *columns, device=0, validate_crc=False, ctx=None, columnar=True):
         self.file = native.File(source)
         self.ctx = ctx or native.Context(device)
         self.validate_crc = validate_crc
@@ -180,7 +189,10 @@ class FileReader:
         self.current_record = 0       # f.currentRecord
         self.skip_row_group = False   # f.skipRowGroup
         self._loaded = None           # decoded chunks of row group row_group_position - 1
-        self._rows = None             # records.RowAssembler over them
+        self._rows = None             # assemble.ColumnarAssembler or records.RowAssembler over them
+        self.columnar = columnar      # False: always the value-by-value records.RowAssembler
+        self._pending = None          # NextBatch: the error of the call it stopped at
+        self.assembled = {"columnar": 0, "value_by_value": 0}  # row groups per assembly path
 
     @classmethod
     def NewFileReader(cls, source, *columns, **kw):
@@ -251,22 +263,91 @@ class FileReader:
         self.PreLoad()
         return {c.path: c.raise_for_status() for c in self._loaded}
 
+    def _assembler(self):
+        """The current row group's record assembly: columnar over the device's nesting outputs
+        (assemble.ColumnarAssembler), else value by value (records.RowAssembler) when the row group
+        breaks one of its preconditions (the reference's page-local cursors / getFirstRDLevel
+        quirks)."""
+        from . import assemble, records
+
+        if self._schema is None:
+            self._schema = self.file.schema()
+        nrows = self.file.row_group_num_rows(self.row_group_position - 1)
+        if self.columnar:
+            leaves = {}
+            for ci, c in zip(self.selected, self._loaded):
+                pages = [(res.level_offset, res.status, res.phase, res.index)
+                         for pt, n, res in c.page_info if pt != 2]
+                levels, leaf = c.nesting if c.nesting is not None else (None, None)
+                if c.max_rep and c.nesting is None:
+                    break
+                leaves[ci] = assemble.Leaf(c.path, c.max_def, c.max_rep, self.file.rep_def(ci), c.def_levels,
+                                           c.rep_levels, levels, leaf,
+                                           lambda c=c: assemble.dense_values(c, c.physical_type), pages, c.num_values)
+            else:
+                try:
+                    a = assemble.ColumnarAssembler(self._schema, leaves, nrows)
+                    rows, errs = a.rows(), a.errors()
+                    self.assembled["columnar"] += 1
+                    return ("columnar", rows, errs)
+                except assemble.NotColumnar:
+                    pass
+        # readValues errors surface page by page, when the assembly reaches the failing page
+        # (ColumnStore.get -> readNextPage, data_store.go:236-269); rows before it are returned
+        cols = {self.selected[i]: (c, c.physical_type, c.path) for i, c in enumerate(self._loaded)}
+        self.assembled["value_by_value"] += 1
+        return ("value_by_value", records.RowAssembler(self._schema, cols, nrows))
+
     def NextRow(self):
-        """NextRow (file_reader.go:258-272): the next record as a dict (records.py), loading the
-        next row group when needed; EOFError after the last row."""
+        """NextRow (file_reader.go:258-272): the next record as a dict, loading the next row group
+        when needed; EOFError after the last row.  A readValues error surfaces at the row that
+        reaches the failing page (records.RecordError), as in the reference."""
         from . import records
 
+        if self._pending is not None:
+            e, self._pending = self._pending, None
+            raise e
         self._advance_if_needed()
         if self._rows is None:
-            # readValues errors surface page by page, when the assembly reaches the failing page
-            # (ColumnStore.get -> readNextPage, data_store.go:236-269); rows before it are returned
-            if self._schema is None:
-                self._schema = self.file.schema()
-            cols = {self.selected[i]: (c, c.physical_type, c.path) for i, c in enumerate(self._loaded)}
-            self._rows = records.RowAssembler(self._schema, cols,
-                                              self.file.row_group_num_rows(self.row_group_position - 1))
+            self._rows = self._assembler()
+        k = self.current_record
         self.current_record += 1
-        return self._rows.next_row()
+        if self._rows[0] == "value_by_value":
+            return self._rows[1].next_row()
+        _, rows, errs = self._rows
+        if k < len(rows):
+            return rows[k]
+        e = errs[k - len(rows)]
+        raise records.RecordError(f"{e[4]}: page failed to decode (status {e[1]}, phase {e[2]}, index {e[3]})",
+                                  e[1], e[2], e[3])
+
+    def NextBatch(self, n):
+        """Up to n records of the current row group (the next one when it is exhausted), stopping
+        before a row that fails -- that row's error is raised by the next NextRow / NextBatch call,
+        exactly as the same sequence of NextRow calls would; [] at the end of the file."""
+        if self._pending is not None:
+            e, self._pending = self._pending, None
+            raise e
+        out = []
+        try:
+            out.append(self.NextRow())
+        except EOFError:
+            return out
+        nrows = self.file.row_group_num_rows(self.row_group_position - 1)
+        if self._rows[0] == "columnar":  # the rest of the row group's ready rows at once
+            rows = self._rows[1]
+            k = self.current_record
+            take = rows[k:k + n - 1]
+            self.current_record += len(take)
+            out.extend(take)
+            return out
+        while len(out) < n and self.current_record < nrows:
+            try:
+                out.append(self.NextRow())
+            except records_error() as e:
+                self._pending = e
+                break
+        return out
 
     def close(self):
         self.file.close()

@@ -182,8 +182,8 @@ def test_oracle_file_records_match_reference(kat):
     assert oracle_rows(kat_file(kat)) == kat["rows"]
 
 
-def _read_all(pq, ctx, data, *columns):
-    fr = pq.reader.FileReader(data, *columns, ctx=ctx)
+def _read_all(pq, ctx, data, *columns, columnar=True, stats=None):
+    fr = pq.reader.FileReader(data, *columns, ctx=ctx, columnar=columnar)
     rows = []
     while True:
         try:
@@ -191,7 +191,28 @@ def _read_all(pq, ctx, data, *columns):
         except EOFError:
             break
     fr.close()
+    if stats is not None:
+        for k, v in fr.assembled.items():
+            stats[k] = stats.get(k, 0) + v
     return rows
+
+
+def _read_batches(pq, ctx, data, n):
+    """NextBatch(n) until the end, errors recorded as NextRow's are (("error", status))."""
+    fr = pq.reader.FileReader(data, ctx=ctx)
+    out = []
+    while True:
+        try:
+            b = fr.NextBatch(n)
+        except (pq.reader.DecodeError, pq.records.RecordError) as e:
+            out.append(("error", e.status))
+            continue
+        if not b:
+            break
+        assert len(b) <= n
+        out.extend(b)
+    fr.close()
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -203,9 +224,12 @@ def ctx():
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
 def test_next_row_matches_reference_records(pq, ctx, kat):
     """NextRow over the GPU decode of the KAT file returns exactly the reference's rows, then EOF."""
+    stats = {}
     for use_dict in (True, False):
         data = kat_file(kat, use_dict=use_dict)
-        assert _read_all(pq, ctx, data) == kat["rows"], f"use_dict={use_dict}"
+        assert _read_all(pq, ctx, data, stats=stats) == kat["rows"], f"use_dict={use_dict}"
+        assert _read_batches(pq, ctx, data, 3) == kat["rows"]
+    assert stats["columnar"] >= 1  # the device's nesting outputs assembled the rows
 
 
 @pytest.mark.gpu
@@ -215,10 +239,25 @@ def test_next_row_multi_page(pq, ctx, v2):
     NextRow (GPU) == assembly over the oracle's pages, row by row."""
     for data in (fixtures.nested_list_map(n=3000, v2=v2), fixtures.flat_all_types(n=4000, v2=v2)):
         want = oracle_rows(data)
-        got = _read_all(pq, ctx, data)
+        stats = {}
+        got = _read_all(pq, ctx, data, stats=stats)
+        assert stats == {"columnar": len(O.FileReader(data).row_groups), "value_by_value": 0}
         assert len(got) == len(want) == O.FileReader(data).num_rows
         for i, (g, w) in enumerate(zip(got, want)):
             assert _norm(g) == _norm(w), f"row {i}: {g} vs {w}"
+        assert [_norm(x) for x in _read_batches(pq, ctx, data, 700)] == [_norm(w) for w in want]
+
+
+@pytest.mark.gpu
+def test_next_row_columnar_vs_value_by_value(pq, ctx):
+    """Deep chains (value-by-value where getFirstRDLevel's quirk applies) and a columnar-only file:
+    FileReader's two assembly paths over the same GPU decode give identical rows."""
+    for data in (fixtures.deep_repeated(n=400, depth=10)[0], fixtures.deep_repeated(n=1500, depth=4, seed=2)[0],
+                 fixtures.nested_list_map(n=2000)):
+        want = oracle_rows(data)
+        for columnar in (True, False):
+            got = _read_all(pq, ctx, data, columnar=columnar)
+            assert [_norm(g) for g in got] == [_norm(w) for w in want], columnar
 
 
 @pytest.mark.gpu
@@ -381,6 +420,7 @@ def test_next_row_error_timing(pq, ctx, case):
     row group the cursor moves on (skipRowGroup, file_reader.go:228-232)."""
     data = _corrupt(_error_file(), ERROR_CASES[case])
     want = oracle_next_rows(data)
+    assert [_norm(x) for x in _read_batches(pq, ctx, data, 1000)] == [_norm(w) for w in want]
     fr = pq.reader.FileReader(data, ctx=ctx)
     got = []
     while True:
@@ -392,6 +432,7 @@ def test_next_row_error_timing(pq, ctx, case):
             got.append(("error", e.status))
         assert len(got) <= len(want) + 1
     fr.close()
+    assert fr.assembled["columnar"] >= 1
     assert len(got) == len(want)
     for i, (g, w) in enumerate(zip(got, want)):
         assert _norm(g) == _norm(w), f"call {i}: {g} vs {w}"
