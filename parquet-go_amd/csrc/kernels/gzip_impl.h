@@ -99,7 +99,14 @@ __device__ __forceinline__ uint32_t gz_entry(uint32_t op, uint32_t bits, uint32_
 }
 
 // The canonical Huffman decoding table for `codes` code lengths (RFC 1951 §3.2.2), built the way
-// zlib's inflate_table does: a root table of *bits index bits (lowered to the longest code,
+// zlib's inflate_table (inftrees.c) does -- a restatement of that routine; zlib is (C) 1995-2024
+// Jean-loup Gailly and Mark Adler under the zlib license ("This software is provided 'as-is' ...
+// Permission is granted to anyone to use this software for any purpose, including commercial
+// applications, and to alter it and redistribute it freely", with its three conditions: no
+// misrepresented origin, altered versions plainly marked, the notice kept).  gz_multmodp below
+// restates zlib's multmodp (crc32.c) under the same license.  The build's own wave-parallel
+// construction, gz_table_wave, builds the literal/length and distance tables; gz_table serves only
+// the 19-symbol code-length code.  zlib's inflate_table does: a root table of *bits index bits (lowered to the longest code,
 // raised to the shortest), codes longer than the root in sub-tables sized to what they need.
 // type 0 = code-length code, 1 = literal/length, 2 = distance.  False on an over-subscribed code,
 // or an incomplete one other than a single 1-bit code (code-length codes must be complete).  No
