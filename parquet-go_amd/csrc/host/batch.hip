@@ -1409,7 +1409,10 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
     // are none to return (documented divergence).  Value errors: below.
     if (phase != PQH_PHASE_VALUES) return PQH_OK;
   }
-  if (s1 == s0) return PQH_OK;
+  if (s1 == s0) {  // nothing left in the page: no values; a byte-array call still gets offsets[0] = 0
+    if (offsets && offsets_cap >= 1 && C.value_size == 0 && out->status == PQH_OK) offsets[0] = 0;
+    return PQH_OK;
+  }
   // levels of the range, and the non-null values before / inside it
   std::vector<uint8_t> defs;
   int64_t nn0 = s0, nn1 = s1 - s0;
