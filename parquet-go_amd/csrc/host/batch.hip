@@ -78,8 +78,9 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_nest_count", "k_nest_scan", "k_nest_write", "k_delta_serial",
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
-                              "k_ba_wcopy",   "k_gzip"};
-constexpr int kNumKernels = 25;
+                              "k_ba_wcopy",   "k_gzip",      "k_snap_spec",  "k_snap_stitch",
+                              "k_snap_emit",  "k_snap_fixup"};
+constexpr int kNumKernels = 29;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -983,14 +984,22 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     return r == hipSuccess ? hipStreamWaitEvent(to, b->ev_dep[k], 0) : r;
   };
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
-  if (b->codec_n)  // device codecs: the page images first
-    e = timed(22, b->codec_n, s, [&](hipStream_t st) {
-      if (snappy_page_mode())
+  if (b->codec_n) {  // device codecs: the page images first
+    if (snappy_page_mode()) {
+      e = timed(22, b->codec_n, s, [&](hipStream_t st) {
         return launch_snappy(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
                              static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
-      return launch_snappy_mw(b->d_codec, b->snap, static_cast<const uint8_t*>(b->d_src),
-                              static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st);
-    });
+      });
+    } else {
+      // the multi-workgroup pipeline kernel by kernel (k_snappy = its page-mode pages), each timed
+      const int32_t items[5] = {b->snap.n_page_mode, b->snap.n_win, b->codec_n, b->snap.n_unit, b->codec_n};
+      for (int part = 0; part < 5 && e == hipSuccess; part++)
+        e = timed(part == 0 ? 22 : 24 + part, items[part], s, [&](hipStream_t st) {
+          return launch_snappy_mw(b->d_codec, b->snap, static_cast<const uint8_t*>(b->d_src),
+                                  static_cast<uint8_t*>(b->owned_payload), b->d_codec_status, st, part);
+        });
+    }
+  }
   if (e == hipSuccess && b->codec_gzip)
     e = timed(24, b->codec_gzip, s, [&](hipStream_t st) {
       return launch_gzip(b->d_codec, b->codec_n, static_cast<const uint8_t*>(b->d_src),
@@ -1621,10 +1630,10 @@ void pqh_batch_destroy(pqh_batch* b) {
 
 namespace {
 // The multi-workgroup SNAPPY plan of a codec page table: its tables in HBM and its scratch.
-int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
+int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n, const uint8_t* host_src) {
   SnapPlan& P = b->snap;
   P.n_pages = n;
-  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit, &P.n_page_mode);
+  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit, &P.n_page_mode, host_src);
   int32_t* tab = nullptr;
   int4* ws = nullptr;
   int2* wt = nullptr;
@@ -1676,7 +1685,7 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
     return rc;
   }
   e = bounce_h2d(ctx, b->d_codec, hb->codec_pages.data(), sizeof(pqh_codec_page) * size_t(b->codec_n));
-  if (e == hipSuccess && (rc = snap_plan_alloc(b, hb->codec_pages.data(), b->codec_n))) {
+  if (e == hipSuccess && (rc = snap_plan_alloc(b, hb->codec_pages.data(), b->codec_n, hb->data()))) {
     pqh_batch_destroy(b);
     *out = nullptr;
     return rc;
