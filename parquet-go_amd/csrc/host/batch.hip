@@ -1630,10 +1630,10 @@ void pqh_batch_destroy(pqh_batch* b) {
 
 namespace {
 // The multi-workgroup SNAPPY plan of a codec page table: its tables in HBM and its scratch.
-int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n, const uint8_t* host_src) {
+int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
   SnapPlan& P = b->snap;
   P.n_pages = n;
-  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit, &P.n_page_mode, host_src);
+  const std::vector<int32_t> t = snap_plan_tables(pages, n, &P.n_win, &P.n_unit, &P.n_page_mode);
   int32_t* tab = nullptr;
   int4* ws = nullptr;
   int2* wt = nullptr;
@@ -1685,7 +1685,7 @@ int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_
     return rc;
   }
   e = bounce_h2d(ctx, b->d_codec, hb->codec_pages.data(), sizeof(pqh_codec_page) * size_t(b->codec_n));
-  if (e == hipSuccess && (rc = snap_plan_alloc(b, hb->codec_pages.data(), b->codec_n, hb->data()))) {
+  if (e == hipSuccess && (rc = snap_plan_alloc(b, hb->codec_pages.data(), b->codec_n))) {
     pqh_batch_destroy(b);
     *out = nullptr;
     return rc;

@@ -1179,43 +1179,8 @@ hipError_t launch_snappy(const pqh_codec_page* pages, int32_t n, const uint8_t* 
   return hipGetLastError();
 }
 
-// Mean output bytes per element over the first elements of a SNAPPY block (after its length
-// header), or -1 if the sample is malformed: long literals (a page of incompressible bytes stored as
-// a few literals of up to 64 KiB) give thousands, text of short literals and copies a few.
-static double snappy_sample_element_len(const uint8_t* p, int64_t n) {
-  int64_t q = 0;
-  while (q < n && q < 10 && (p[q] & 0x80)) q++;
-  q++;
-  int64_t out = 0, els = 0;
-  while (q < n && els < 256) {
-    const uint8_t t = p[q];
-    int64_t len;
-    switch (t & 3) {
-      case 0: {
-        int64_t x = t >> 2, h = 1;
-        if (x >= 60) {
-          const int k = int(x) - 59;
-          if (q + 1 + k > n) return -1;
-          x = 0;
-          for (int i = 0; i < k; i++) x |= int64_t(p[q + 1 + i]) << (8 * i);
-          h += k;
-        }
-        len = x + 1;
-        q += h + len;
-        break;
-      }
-      case 1: len = 4 + ((t >> 2) & 7); q += 2; break;
-      case 2: len = 1 + (t >> 2); q += 3; break;
-      default: len = 1 + (t >> 2); q += 5; break;
-    }
-    out += len;
-    els++;
-  }
-  return els ? double(out) / double(els) : -1;
-}
-
 std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit,
-                                      int32_t* n_page_mode, const uint8_t* host_src) {
+                                      int32_t* n_page_mode) {
   std::vector<int32_t> pw(size_t(n) + 1), pu(size_t(n) + 1), pm(size_t(n), 0), wp, up;
   int32_t W = 0, U = 0, M = 0;
   for (int32_t i = 0; i < n; i++) {
@@ -1230,14 +1195,11 @@ std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, in
       // more than 2^24 output bytes: k_snap_emit packs a copy's offset in 24 bits (an offset is at
       // most the output position, so only such blocks can hold a copy4 reaching 2^24 or further;
       // golang/snappy accepts offsets up to 2^32, decode_other.go:75-85), k_snappy keeps 31 bits.
-      // (With the host bytes at hand, a page counts as long-literal only when its first elements
-      // average >= 256 output bytes: text of short literals and copies that barely compresses -- C5's
-      // random letters -- is a long chain of short elements, the multi-workgroup pipeline's case.)
-      bool page_mode = 5 * body >= 4 * out || out > (int64_t(1) << 24);
-      if (page_mode && host_src && out <= (int64_t(1) << 24)) {
-        const double m = snappy_sample_element_len(host_src + c.src_offset + raw, body);
-        if (m >= 0 && m < 256) page_mode = false;
-      }
+      // (Pages that barely compress because they are short literals and copies of random text --
+      // C5 -- also stay here: r04 measured the pipeline at 57 vs 32 ms on C5, its speculative
+      // window entries almost never resynchronise inside such literals, so k_snap_stitch re-walks
+      // the windows one by one.)
+      const bool page_mode = 5 * body >= 4 * out || out > (int64_t(1) << 24);
       if (page_mode) {
         pm[size_t(i)] = 1;
         M++;

@@ -53,9 +53,8 @@ struct SnapPlan {
 };
 // Host tables page_win0 | page_unit0 | page_mode | win_page | unit_page of a codec page list
 // (device copy: bind).
-// host_src (optional): the host copy of the source bytes, for the long-literal test of each page
 std::vector<int32_t> snap_plan_tables(const pqh_codec_page* pages, int32_t n, int32_t* n_win, int32_t* n_unit,
-                                      int32_t* n_page_mode, const uint8_t* host_src = nullptr);
+                                      int32_t* n_page_mode);
 void snap_plan_bind(SnapPlan& P, int32_t* tables, int4* wspec, int2* wtrue, int32_t* uflag, int16_t* wseg);
 // part: -1 the whole pipeline, else one kernel of it (0 k_snappy for the page-mode pages, 1 k_snap_spec,
 // 2 k_snap_stitch, 3 k_snap_emit, 4 k_snap_fixup), launched in that order (profiled runs time each)
