@@ -35,6 +35,17 @@ def _raw(x):  # bytes as they are (np.asarray(b"") would be a one-byte S1 array)
     return bytes(x) if isinstance(x, (bytes, bytearray)) else np.ascontiguousarray(x).tobytes()  # readValues(size) calls per page: the page read in three calls
 
 
+def _as_arrays(v, desc):
+    """Byte-array values as (offsets, bytes).  A FIXED_LEN_BYTE_ARRAY chunk with DELTA_BYTE_ARRAY
+    pages comes off the device as offsets + bytes for all its pages (its dictionary pages too); the
+    oracle gives such a page's fixed-width values as they are -- the same []byte values either way."""
+    if isinstance(v, tuple):
+        return np.asarray(v[0], np.int64), _raw(v[1])
+    raw = _raw(v)
+    w = desc[1]  # type_length
+    return np.arange(0, len(raw) + 1, w, dtype=np.int64), raw
+
+
 def walk_both(pq, data, backend="host", batch_for=None, crc=False):
     """Returns the number of data pages compared."""
     fr = O.FileReader(data)
@@ -63,7 +74,8 @@ def walk_both(pq, data, backend="host", batch_for=None, crc=False):
                 if a[0]:
                     break
                 for x, y in zip(a[2:], b[2:]):
-                    if isinstance(x, tuple):
+                    if isinstance(x, tuple) or isinstance(y, tuple):
+                        x, y = _as_arrays(x, desc), _as_arrays(y, desc)
                         assert np.array_equal(x[0], y[0]) and bytes(x[1]) == bytes(y[1]), f"{where} page {i}"
                     elif x is None or y is None:
                         assert x is None and y is None, f"{where} page {i}"
