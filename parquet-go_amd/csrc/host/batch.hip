@@ -40,6 +40,7 @@ struct pqh_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // staged (end-to-end) runs: pinned -> HBM copies
   hipStream_t side = nullptr;         // unprofiled runs: branches beside the main launch sequence
+  hipStream_t side2 = nullptr;        //   (the fused PLAIN chains, beside both)
   std::string err;
   // Pinned bounce buffer for every copy between HBM and pageable host memory (two halves, so the
   // host-side memcpy of one overlaps the DMA of the other).  Pageable copies never reach the HIP
@@ -79,8 +80,8 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
                               "k_ba_wcopy",   "k_gzip",      "k_snap_spec",  "k_snap_stitch",
-                              "k_snap_emit",  "k_snap_fixup"};
-constexpr int kNumKernels = 29;
+                              "k_snap_emit",  "k_snap_fixup", "k_ba_chain"};
+constexpr int kNumKernels = 30;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -100,6 +101,13 @@ thread_local const char* g_fail_kernel = nullptr;
 bool snappy_page_mode() {
   const char* f = getenv("PQH_SNAPPY_PAGE");
   return f && f[0] == '1';
+}
+
+// PQH_BA_FUSE=0 (A/B experiments, tests): PLAIN-only byte-array chunks take the scratch path
+// (k_ba_wspec / wstitch / wcopy) instead of the fused k_ba_chain.
+bool fuse_enabled() {
+  const char* f = getenv("PQH_BA_FUSE");
+  return !(f && f[0] == '0');
 }
 
 constexpr size_t kBounceHalf = size_t(16) << 20;
@@ -273,6 +281,14 @@ struct pqh_batch {
   std::vector<int2> ba_wlist;       // {window, page}: dictionary pages' windows (k_ba_wemit), then data pages' (k_ba_wcopy)
   int32_t ba_wdict = 0;             // dictionary windows at the front of ba_wlist
   std::vector<int32_t> ba_chunks;   // k_ba_scan work list
+  // Fused PLAIN chains (k_ba_chain): chunks with DevChunk.ba_fused sort last in ba_pages / ba_wins /
+  // ba_chunks / the k_ba_sum list, so while ba_fuse_on the scratch path runs over the prefixes below
+  // and k_ba_chain over ba_wins[ba_wins_nf:]; a fallback (bafuse[1]) turns it off for good
+  bool ba_fuse_on = false;
+  int32_t ba_pages_nf = 0, ba_wins_nf = 0, ba_wlist_nf = 0, ba_chunks_nf = 0, ba_sum_nf = 0;
+  int32_t ba_fuse_fallbacks = 0;
+  uint32_t* d_bafuse = nullptr;
+  uint64_t* d_bawords = nullptr;
   std::vector<int64_t> chunk_bytes; // host copy after sync
   std::vector<DevNest> nests;       // repeated chunks with nesting outputs
   std::vector<int32_t> chunk_nest;  // chunk -> nests index, -1
@@ -297,7 +313,7 @@ struct pqh_batch {
   size_t staged_bytes = 0;
   hipEvent_t ev_copied = nullptr, ev_done = nullptr;
   bool done_recorded = false;
-  hipEvent_t ev_dep[4] = {nullptr, nullptr, nullptr, nullptr};  // fork / join points of the side branches
+  hipEvent_t ev_dep[6] = {};       // fork / join points of the side branches
   DevPage* d_pages = nullptr;
   DevChunk* d_chunks = nullptr;
   PageState* d_states = nullptr;
@@ -412,8 +428,10 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
   c->device = device;
   c->flags = flags;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) {
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->side) hipStreamDestroy(c->side);
     delete c;
     return set_err(nullptr, PQH_ERR_HIP, "stream creation failed");
   }
@@ -426,10 +444,11 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipStreamDestroy(ctx->stream);
-  if (ctx->side) {
-    hipStreamSynchronize(ctx->side);
-    hipStreamDestroy(ctx->side);
-  }
+  for (hipStream_t st : {ctx->side, ctx->side2})
+    if (st) {
+      hipStreamSynchronize(st);
+      hipStreamDestroy(st);
+    }
   if (ctx->copy_stream) {
     hipStreamSynchronize(ctx->copy_stream);
     hipStreamDestroy(ctx->copy_stream);
@@ -698,6 +717,26 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
     b->chunk_n[size_t(c)] = level_base;
     D.batile_n = int32_t(b->ba_tiles.size()) - D.batile_base;
+    // fused PLAIN chain: byte-array chunks of PLAIN data pages only (no dictionary page, nothing the
+    // planner already failed)
+    D.ba_fused = 0;
+    if (ba_chunk && fuse_enabled() && D.value_size == 0 && D.dict_page < 0 && C.num_pages > 0) {
+      bool all = true;
+      for (int32_t i = 0; i < C.num_pages && all; i++) {
+        const DevPage& P = b->hpages[size_t(C.first_page + i)];
+        all = P.page_type != PQH_DICTIONARY_PAGE && P.kind == K_PLAIN_BA && P.host_err == kNoError;
+      }
+      D.ba_fused = all ? 1 : 0;
+    }
+  }
+  {  // fused chunks last in the byte-array lists (their prefixes are the scratch path's while fused)
+    auto fused_page = [&](int32_t p) { return b->hchunks[size_t(b->hpages[size_t(p)].chunk)].ba_fused != 0; };
+    std::stable_partition(b->ba_pages.begin(), b->ba_pages.end(), [&](int32_t p) { return !fused_page(p); });
+    b->ba_pages_nf = int32_t(std::count_if(b->ba_pages.begin(), b->ba_pages.end(), [&](int32_t p) { return !fused_page(p); }));
+    std::stable_partition(b->ba_chunks.begin(), b->ba_chunks.end(), [&](int32_t c) { return !b->hchunks[size_t(c)].ba_fused; });
+    b->ba_chunks_nf = int32_t(std::count_if(b->ba_chunks.begin(), b->ba_chunks.end(),
+                                            [&](int32_t c) { return !b->hchunks[size_t(c)].ba_fused; }));
+    b->ba_fuse_on = b->ba_pages_nf < int32_t(b->ba_pages.size());
   }
   // Interleave the kinds proportionally along the dispatch order (k_expand's grid), so that every
   // CU sees a mix of byte-copy and bit-unpack tiles instead of one long phase per kind.
@@ -711,12 +750,15 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     for (auto& kv : keyed) b->expand_tiles.push_back(kv.second);
     b->global_tiles = by_kind[TK_DICT_GLOBAL];
     b->delta_tiles = by_kind[TK_DELTA];
-    for (int32_t p : b->ba_pages) {  // chain windows: enough to cover the whole page image
+    for (size_t i = 0; i < b->ba_pages.size(); i++) {  // chain windows: enough to cover the whole page image
+      const int32_t p = b->ba_pages[i];
+      if (int32_t(i) == b->ba_pages_nf) b->ba_wins_nf = int32_t(b->ba_wins.size());
       const int64_t len = std::max<int64_t>(b->hpages[size_t(p)].image_len, 1);
       const int32_t nw = int32_t((len + kChainStride - 1) / kChainStride);
       b->ba_pwin.push_back(make_int2(int32_t(b->ba_wins.size()), nw));
       for (int32_t w = 0; w < nw; w++) b->ba_wins.push_back(make_int2(p, w));
     }
+    if (b->ba_pages_nf == int32_t(b->ba_pages.size())) b->ba_wins_nf = int32_t(b->ba_wins.size());
     for (int dict = 1; dict >= 0; dict--) {
       for (size_t i = 0; i < b->ba_wins.size(); i++) {
         const int32_t p = b->ba_wins[i].x;
@@ -725,6 +767,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       }
       if (dict) b->ba_wdict = int32_t(b->ba_wlist.size());
     }
+    b->ba_wlist_nf = int32_t(std::count_if(b->ba_wlist.begin(), b->ba_wlist.end(),
+                                           [&](const int2& x) { return x.x < b->ba_wins_nf; }));
     b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
@@ -758,11 +802,14 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   // page mode DELTA_LENGTH pages) are represented by their tile 0: their sums come from k_ba_wstitch
   // (the delta kernels); the tile-0 workgroup checks that and otherwise sums the whole page
   b->ba_sum_off = int32_t(b->ba_xlist.size());
-  for (size_t i = 0; i < b->ba_tiles.size(); i++) {
-    const Tile& t = b->ba_tiles[i];
-    const int32_t kind = b->hpages[size_t(t.page)].kind;
-    if (t.k == 0 || !(kind == K_PLAIN_BA || (b->delta_page_mode && kind == K_DLBA))) b->ba_xlist.push_back(int32_t(i));
-  }
+  for (int fused = 0; fused < 2; fused++)  // (fused chunks' PLAIN tiles last)
+    for (size_t i = 0; i < b->ba_tiles.size(); i++) {
+      const Tile& t = b->ba_tiles[i];
+      const DevPage& P = b->hpages[size_t(t.page)];
+      if (int(b->hchunks[size_t(P.chunk)].ba_fused != 0) != fused) continue;
+      if (t.k == 0 || !(P.kind == K_PLAIN_BA || (b->delta_page_mode && P.kind == K_DLBA))) b->ba_xlist.push_back(int32_t(i));
+      if (!fused) b->ba_sum_nf = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
+    }
 
   // ---- device allocations ----
   int rc;
@@ -792,6 +839,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums2), sizeof(int64_t) * b->ba_tiles.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bafuse), sizeof(uint32_t) * 4)) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bawords), sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
@@ -949,7 +998,7 @@ namespace {
 hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
-             b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2};
+             b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2, b->d_bafuse, b->d_bawords};
   const bool sync_each = sync_each_enabled();
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1009,7 +1058,10 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   const bool wide = std::any_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& c) { return c.max_rep > 0; });
   if (e == hipSuccess)
     e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, wide, st); });
-  const int32_t nbp = int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()), nbc = int32_t(b->ba_chunks.size());
+  // (while the fused chains are on, the scratch path covers the lists' non-fused prefixes)
+  const bool fuse = b->ba_fuse_on;
+  const int32_t nbp = fuse ? b->ba_pages_nf : int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()),
+                nbc = fuse ? b->ba_chunks_nf : int32_t(b->ba_chunks.size());
   bool chain_open = false;  // the chain branch has not rejoined the main stream yet
   if (e == hipSuccess && nbp) {
     hipStream_t cs = s;
@@ -1018,7 +1070,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       cs = side;
       chain_open = true;
     }
-    const int32_t nw = int32_t(b->ba_wins.size());
+    const int32_t nw = fuse ? b->ba_wins_nf : int32_t(b->ba_wins.size());
     if (e == hipSuccess)
       e = timed(7, nw, cs, [&](hipStream_t st) { return launch_ba_wspec(d, b->d_ba_wins, nw, b->d_ba_res, b->d_ba_wrec, st); });
     if (e == hipSuccess)
@@ -1047,7 +1099,25 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     e = timed(16, ndp - ni, s, [&](hipStream_t st) { return launch_delta_spec(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess && ndp > ni)
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
+  const int32_t nfw = fuse ? int32_t(b->ba_wins.size()) - b->ba_wins_nf : 0;
+  if (e == hipSuccess && nfw) {  // fused chains: tickets, fallback flag, FINAL words
+    e = hipMemsetAsync(b->d_bafuse, 0, sizeof(uint32_t) * 2, s);
+    if (e == hipSuccess) e = hipMemsetAsync(b->d_bawords, 0, sizeof(uint64_t) * size_t(nfw), s);
+  }
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  // fused PLAIN chains: need the value and (guessed) byte bases only; latency bound, beside the rest
+  bool fuse_open = false;
+  if (e == hipSuccess && nfw) {
+    hipStream_t fs = s;
+    hipStream_t side2 = side ? b->ctx->side2 : nullptr;
+    if (side2) {
+      e = dep(s, side2, 4);
+      fs = side2;
+      fuse_open = true;
+    }
+    if (e == hipSuccess)
+      e = timed(29, nfw, fs, [&](hipStream_t st) { return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, nfw, st); });
+  }
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
@@ -1096,7 +1166,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   }
   if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
   if (e == hipSuccess && nbt) {
-    const int32_t nsum = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
+    const int32_t nsum = fuse ? b->ba_sum_nf : int32_t(b->ba_xlist.size()) - b->ba_sum_off;
     e = timed(8, nsum, s, [&](hipStream_t st) {
       return launch_ba_sum(d, b->d_batiles, b->d_ba_xlist + b->ba_sum_off, nsum, b->delta_page_mode, st);
     });
@@ -1106,7 +1176,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       e = timed(10, nbt, s, [&](hipStream_t st) {  // k_ba_expand + k_ba_gather
         return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, b->ba_sum_off - b->ba_ncopy, st);
       });
-    const int32_t nwd = int32_t(b->ba_wlist.size()) - b->ba_wdict;
+    const int32_t nwd = (fuse ? b->ba_wlist_nf : int32_t(b->ba_wlist.size())) - b->ba_wdict;
     if (e == hipSuccess && nwd)
       e = timed(23, nwd, s, [&](hipStream_t st) {
         return launch_ba_wcopy(d, b->d_ba_wlist + b->ba_wdict, nwd, b->d_ba_res, b->d_ba_wrec, b->d_ba_wgeo, st);
@@ -1121,6 +1191,10 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   }
   if (nest_open) {
     const hipError_t r = dep(side, s, 3);
+    if (e == hipSuccess) e = r;
+  }
+  if (fuse_open) {
+    const hipError_t r = dep(b->ctx->side2, s, 5);
     if (e == hipSuccess) e = r;
   }
   return e;
@@ -1205,6 +1279,27 @@ int pqh_batch_sync(pqh_batch* b) {
       return set_err(ctx, PQH_ERR_HIP, msg);
     }
   }
+  // Fused PLAIN chains that did not verify (an error, trailing bytes, a chain that ends early):
+  // decode the batch again on the scratch path, which gives the reference's errors and limits
+  if (b->ba_fuse_on) {
+    uint32_t flag = 0;
+    HIP_TRY(ctx, bounce_d2h(ctx, &flag, b->d_bafuse + 1, sizeof(uint32_t)));
+    if (flag) {
+      b->ba_fuse_on = false;
+      b->ba_fuse_fallbacks++;
+      for (DevChunk& D : b->hchunks) D.ba_fused = 0;
+      HIP_TRY(ctx, bounce_h2d(ctx, b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * b->hchunks.size()));
+      if (b->gexec) hipGraphExecDestroy(b->gexec);
+      if (b->graph) hipGraphDestroy(b->graph);
+      b->gexec = nullptr;
+      b->graph = nullptr;
+      b->pending.clear();
+      b->event_next = 0;
+      int rc = pqh_batch_run(b);
+      if (rc != PQH_OK) return rc;
+      return pqh_batch_sync(b);
+    }
+  }
   // Byte-array outputs sized from an estimate (dictionary gathers): grow the chunks that came out
   // short (and decoded without error), then decode again.  Contents are deterministic, so this
   // happens at most once per batch.
@@ -1255,6 +1350,7 @@ int pqh_batch_sync(pqh_batch* b) {
   // algorithmic bytes of one run: page bytes read once, dictionaries once per
   // chunk, decoded bytes written; attributed to the kernel that moves them.
   double wr = 0, plain_written = 0;
+  auto fused_chunk = [&](int32_t c) { return b->ba_fuse_on && b->hchunks[size_t(c)].ba_fused != 0; };
   std::fill(b->k_read.begin(), b->k_read.end(), 0.0);
   std::fill(b->k_written.begin(), b->k_written.end(), 0.0);
   for (size_t p = 0; p < b->pages.size(); p++) {
@@ -1303,14 +1399,17 @@ int pqh_batch_sync(pqh_batch* b) {
         b->k_written[kd] += vals;
         break;
       }
-      case K_PLAIN_BA:  // walked by k_ba_wspec / k_ba_wstitch; values read and offsets + bytes written by k_ba_wcopy
-        b->k_read[23] += S.val_e - S.val_s;
+      case K_PLAIN_BA: {  // walked by k_ba_wspec / k_ba_wstitch; values read and offsets + bytes written by
+                          // k_ba_wcopy -- or all of it by k_ba_chain
+        const int kx = fused_chunk(P.chunk) ? 29 : 23;
+        b->k_read[kx] += S.val_e - S.val_s;
         if (S.err == kNoError) {
           const double w = double(S.nn) * 8 + double(S.val_e - S.val_s - 4 * int64_t(S.nn));
-          b->k_written[23] += w;
-          plain_written += w;
+          b->k_written[kx] += w;
+          if (kx == 23) plain_written += w;
         }
         break;
+      }
       case K_DLBA:
       case K_DBA:
         b->k_read[10] += S.val_e - S.val_s;
@@ -1333,7 +1432,8 @@ int pqh_batch_sync(pqh_batch* b) {
       if (b->hpages[size_t(C.first_page + i)].page_type != PQH_DICTIONARY_PAGE) nn += b->states[size_t(C.first_page + i)].nn;
     const double w = double(nn + 1) * 8 + double(b->chunk_bytes[size_t(c)]);
     wr += w;
-    b->k_written[10] += w;
+    if (fused_chunk(c)) b->k_written[29] += 8;  // (its pages' offsets and bytes are counted above)
+    else b->k_written[10] += w;
   }
   b->k_written[10] -= plain_written;  // the PLAIN pages' share went to k_ba_wcopy
   for (size_t i = 0; i < b->nests.size(); i++) {  // list offsets (4 B) + presence (1 B) per list, leaf validity

@@ -1201,6 +1201,46 @@ __global__ __launch_bounds__(256) void k_ba_wgeo(DevBatch b, const int2* list, i
   if (t < nlist) geo[t] = wgeo(b, list, res, wrec, t);
 }
 
+// One string of l bytes from staged page bytes (dword array, the string at byte sx) to d.  Short
+// strings: five stage dwords, predicated stores, no per-byte loop.  The stage must hold 20 bytes
+// from sx's dword on for a short string, l + 4 for a long one.
+__device__ __forceinline__ void stage_string_out(const uint32_t* stage, int sx, int l, PQH_G uint8_t* d) {
+  typedef uint32_t u32u __attribute__((aligned(1)));
+  typedef uint64_t u64u __attribute__((aligned(1)));
+  typedef uint16_t u16u __attribute__((aligned(1)));
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  typedef v4u v4uu __attribute__((aligned(1)));
+  const int w0 = sx >> 2;
+  const uint32_t sh = uint32_t(sx & 3) * 8;
+  if (l <= 16) {
+    const uint32_t a0 = stage[w0], a1 = stage[w0 + 1], a2 = stage[w0 + 2], a3 = stage[w0 + 3], a4 = stage[w0 + 4];
+    const uint32_t v0 = __builtin_amdgcn_alignbit(a1, a0, sh), v1 = __builtin_amdgcn_alignbit(a2, a1, sh),
+                   v2 = __builtin_amdgcn_alignbit(a3, a2, sh), v3 = __builtin_amdgcn_alignbit(a4, a3, sh);
+    const int nw = l >> 2, tl = l & 3;
+    if (nw == 4) {
+      const v4u x4 = {v0, v1, v2, v3};
+      *reinterpret_cast<PQH_G v4uu*>(d) = x4;
+    } else {
+      if (nw >= 2) *reinterpret_cast<PQH_G u64u*>(d) = uint64_t(v0) | (uint64_t(v1) << 32);
+      if (nw & 1) *reinterpret_cast<PQH_G u32u*>(d + 4 * (nw & 2)) = (nw & 2) ? v2 : v0;
+      const uint32_t tv = nw == 0 ? v0 : nw == 1 ? v1 : nw == 2 ? v2 : v3;
+      PQH_G uint8_t* dt = d + 4 * nw;
+      if (tl & 2) *reinterpret_cast<PQH_G u16u*>(dt) = uint16_t(tv);
+      if (tl & 1) dt[tl & 2] = uint8_t(tv >> (8 * (tl & 2)));
+    }
+  } else {
+    int k = 0;
+    for (; k + 4 <= l; k += 4) {
+      const int q = sx + k;
+      *reinterpret_cast<PQH_G u32u*>(d + k) = __builtin_amdgcn_alignbit(stage[(q >> 2) + 1], stage[q >> 2], uint32_t(q & 3) * 8);
+    }
+    for (; k < l; k++) {
+      const int q = sx + k;
+      d[k] = uint8_t(stage[q >> 2] >> (8 * (q & 3)));
+    }
+  }
+}
+
 // The window's page vectors and offset pairs into registers (every load unconditional, clamped
 // addresses), all in flight together.
 __device__ __forceinline__ void wcopy_issue(const WGeo& g, const uint16_t* wrec, uint4 (&x)[kWV], uint32_t (&ov)[kWP]) {
@@ -1235,7 +1275,6 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
     if (t + grid < nlist) gn = geo[t + grid];
     const int n = g.n;
     const PQH_G uint16_t* wo = (const PQH_G uint16_t*)(wrec + int64_t(g.wi) * kChainRecs);
-    typedef uint32_t u32u __attribute__((aligned(1)));
     if (n > 0 && g.nvec) {
       wcopy_issue(g, wrec, x, ov);
       // every LDS store unconditional too (out-of-range ones to spare slots)
@@ -1254,48 +1293,12 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
       }
       if (tid == 0) L.offs[n] = uint16_t(g.endo);  // < 2^16: the staged span holds the records' bytes
       __syncthreads();
-      typedef uint64_t u64u __attribute__((aligned(1)));
-      typedef uint16_t u16u __attribute__((aligned(1)));
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      typedef v4u v4uu __attribute__((aligned(1)));
       for (int i = tid; i < n; i += kBlock) {
         const int o = L.offs[i], e = L.offs[i + 1];
         g.offs_out[i] = g.obase + e;
         int l = e - o;
         if (o + l > g.cap) l = g.cap > o ? int(g.cap - o) : 0;
-        const int sx = g.in_lead + 4 * (i + 1) + o;
-        const int w0 = sx >> 2;
-        const uint32_t sh = uint32_t(sx & 3) * 8;
-        PQH_G uint8_t* d = g.dst + o;
-        if (l <= 16) {  // short strings: five stage dwords, predicated stores, no per-byte loop
-          const uint32_t a0 = L.stage[w0], a1 = L.stage[w0 + 1], a2 = L.stage[w0 + 2], a3 = L.stage[w0 + 3],
-                         a4 = L.stage[w0 + 4];
-          const uint32_t v0 = __builtin_amdgcn_alignbit(a1, a0, sh), v1 = __builtin_amdgcn_alignbit(a2, a1, sh),
-                         v2 = __builtin_amdgcn_alignbit(a3, a2, sh), v3 = __builtin_amdgcn_alignbit(a4, a3, sh);
-          const int nw = l >> 2, tl = l & 3;
-          if (nw == 4) {
-            const v4u x4 = {v0, v1, v2, v3};
-            *reinterpret_cast<PQH_G v4uu*>(d) = x4;
-          } else {
-            if (nw >= 2) *reinterpret_cast<PQH_G u64u*>(d) = uint64_t(v0) | (uint64_t(v1) << 32);
-            if (nw & 1) *reinterpret_cast<PQH_G u32u*>(d + 4 * (nw & 2)) = (nw & 2) ? v2 : v0;
-            const uint32_t tv = nw == 0 ? v0 : nw == 1 ? v1 : nw == 2 ? v2 : v3;
-            PQH_G uint8_t* dt = d + 4 * nw;
-            if (tl & 2) *reinterpret_cast<PQH_G u16u*>(dt) = uint16_t(tv);
-            if (tl & 1) dt[tl & 2] = uint8_t(tv >> (8 * (tl & 2)));
-          }
-        } else {
-          int k = 0;
-          for (; k + 4 <= l; k += 4) {
-            const int q = sx + k;
-            *reinterpret_cast<PQH_G u32u*>(d + k) =
-                __builtin_amdgcn_alignbit(L.stage[(q >> 2) + 1], L.stage[q >> 2], uint32_t(q & 3) * 8);
-          }
-          for (; k < l; k++) {
-            const int q = sx + k;
-            d[k] = uint8_t(L.stage[q >> 2] >> (8 * (q & 3)));
-          }
-        }
+        stage_string_out(L.stage, g.in_lead + 4 * (i + 1) + o, l, g.dst + o);
       }
       __syncthreads();  // the stage is read before the next window's stores
     } else if (n > 0) {
@@ -1317,5 +1320,162 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
     if (t + grid >= nlist) break;
     g = gn;
     t += grid;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused PLAIN chains (k_ba_chain): chunks whose data pages are all PLAIN byte arrays and which have
+// no dictionary page (DevChunk.ba_fused) read their page bytes once.  One workgroup per window, in
+// ticket order (a window's predecessor in its page always holds an earlier ticket, so it is resident
+// or done):
+//   * the window is staged and resolved from its guessed entry as in k_ba_wspec, its records into
+//     LDS (no scratch);
+//   * its predecessor's FINAL word (records on the page's chain before this window's end, and the
+//     chain's position there) is read by a relaxed agent-scope spin -- one 64-bit word, so no fence;
+//     a wrong guess re-resolves the window from the true entry (LDS still holds the bytes);
+//   * the window publishes its own FINAL word at once, before its copies, so the page's chain moves
+//     on while it writes its offsets and strings straight from LDS.
+// Output byte bases come from k_scan: a page whose chain is exactly notNull records filling its
+// values section has val_e - val_s - 4 * notNull string bytes.  The window holding record notNull checks that record's end is
+// val_e; a chain that ends early, runs on, fails, or a page that failed earlier sets the batch's
+// fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again with the scratch path
+// (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and limits exactly.
+// ------------------------------------------------------------------------------------------------
+constexpr uint64_t kFinal = 1ull << 63, kEnded = 1ull << 62;
+constexpr int64_t kInclMax = (int64_t(1) << 30) - 1;
+
+__device__ __forceinline__ void fuse_fail(const DevBatch& b) {
+  __hip_atomic_store(b.bafuse + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, int32_t nwin) {
+  __shared__ ChainLds C;
+  __shared__ uint16_t recs[kChainRecs + 8];
+  __shared__ BaWin R;
+  __shared__ uint64_t sh[2];
+  const int tid = threadIdx.x;
+  if (tid == 0) sh[0] = atomicAdd(b.bafuse, 1u);
+  __syncthreads();
+  const int t = int(sh[0]);
+  if (t >= nwin) return;
+  const int2 pw = wins[t];
+  const int p = pw.x, w = pw.y;
+  const PageState S = b.states[p];
+  const DevPage P = b.pages[p];
+  const int64_t nn = S.nn;
+  BaPageCtx c;
+  c.ok = S.err == kNoError && nn > 0;
+  c.dict = false;
+  c.count = nn;
+  c.entry = S.val_s;
+  c.e0 = S.val_e;
+  c.img = b.payload + P.image_off;
+  const int64_t Bw = c.entry + int64_t(w) * kChainStride;
+  const int64_t wend = Bw + kChainStride;
+  const bool staged = c.ok && Bw < c.e0;
+  int64_t wb = 0, entry = c.entry;
+  if (staged) {
+    wb = ba_wbase(c, w);
+    ba_stage(C, c, wb);
+    __syncthreads();
+    if (w > 0) {
+      if (tid < 64) {
+        const int32_t g = ba_guess_entry(C, int32_t(c.e0), int32_t(wb), int32_t(Bw));
+        if (tid == 0) C.guess = g;
+      }
+      __syncthreads();
+      entry = C.guess;
+    }
+    ba_window(C, c, w, entry, &R, recs);
+  }
+  // the predecessor's chain position
+  int64_t pincl = 0, pexit = c.entry;
+  bool pended = false;
+  if (w > 0) {
+    if (tid == 0) {
+      uint64_t v = 0;
+      for (int spin = 0;; spin++) {
+        v = __hip_atomic_load(b.bawords + t - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v & kFinal) break;
+        if (spin > (1 << 22)) {  // (never: the predecessor is resident) -- give up on the fused path
+          fuse_fail(b);
+          v = kFinal | kEnded;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      sh[1] = v;
+    }
+    __syncthreads();
+    const uint64_t v = sh[1];
+    pended = (v & kEnded) != 0;
+    pincl = int64_t((v >> 32) & uint64_t(kInclMax));
+    pexit = int64_t(uint32_t(v));
+  }
+  if (!c.ok || pended || pexit >= c.e0 || pexit >= wend || !staged) {
+    // nothing of the chain starts here (a live chain reaches Bw before window w, so pexit < e0
+    // means Bw < e0: the window is staged)
+    if (tid == 0) {
+      const int bad = (c.ok && !pended && pexit >= c.e0 && pexit < wend) ? PQH_ERR_EOF : 0;
+      R = BaWin{int32_t(pexit), int32_t(pexit), 0, bad, 0, 0, 0, 0};
+    }
+    __syncthreads();
+  } else if (w > 0 && pexit != entry) {
+    // wrong guess: resolve again from the true entry
+    __syncthreads();
+    ba_window(C, c, w, pexit, &R, recs);
+    __syncthreads();
+  } else {
+    __syncthreads();
+  }
+  const BaWin r = R;
+  if (tid == 0) {
+    int64_t incl = pincl + r.count;
+    if (incl > kInclMax) incl = kInclMax;
+    const bool ended = pended || !c.ok || r.bad != 0;
+    __hip_atomic_store(b.bawords + t, kFinal | (ended ? kEnded : 0) | (uint64_t(incl) << 32) | uint64_t(uint32_t(r.exit)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the page's check: record nn ends at val_e, or the chain falls short of nn records
+    if (c.ok && !pended && pincl < nn) {
+      if (pincl + r.count >= nn) {
+        const int64_t k = nn - pincl;  // records of the page up to and including record nn, in this window
+        const int64_t end = int64_t(r.entry) + 4 * k + (k < r.count ? int64_t(recs[k]) : r.bytes);
+        if (end != c.e0) fuse_fail(b);
+      } else if (r.bad || r.exit >= c.e0) {
+        fuse_fail(b);
+      }
+    }
+  }
+  if (!c.ok || pended || pincl >= nn || r.count == 0) return;
+  // emit: the window's records before the page's notNull, at the page's guessed byte base
+  const int n = int(nn - pincl < r.count ? nn - pincl : r.count);
+  const DevChunk D = b.chunks[P.chunk];
+  const int64_t obase = S.byte_base + (int64_t(r.entry) - c.entry) - 4 * pincl;
+  const int64_t endo = n < r.count ? int64_t(recs[n]) : r.bytes;
+  if (obase < 0 || obase + endo > D.bytes_cap || S.value_base + pincl + n > D.values_cap) {
+    if (tid == 0) fuse_fail(b);  // a wrong guess somewhere: never written, the batch goes again
+    return;
+  }
+  PQH_G int64_t* offs = D.offsets + S.value_base + 1 + pincl;
+  PQH_G uint8_t* dst = D.bytes + obase;
+  const int lead = int(r.entry - wb);  // the entry in the stage
+  constexpr int kStaged = kChainWin + 64;
+  constexpr int kLong = 512;
+  for (int i = tid; i < n; i += kBlock) {
+    const int o = recs[i];
+    const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
+    offs[i] = obase + e;
+    const int l = e - o;
+    const int sx = lead + 4 * (i + 1) + o;
+    if (sx + l + 20 <= kStaged) stage_string_out(C.win, sx, l, dst + o);
+    else if (l > 0 && l < kLong) copy_bytes(dst + o, c.img + r.entry + 4 * (i + 1) + o, l);
+  }
+  // the strings past the stage (at most the last few of the window) by the whole workgroup
+  for (int i = n - 1; i >= 0; i--) {
+    const int o = recs[i];
+    const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
+    const int sx = lead + 4 * (i + 1) + o;
+    if (sx + (e - o) + 20 <= kStaged) break;
+    if (e - o >= kLong) block_copy(dst + o, (const PQH_G uint8_t*)(c.img + r.entry + 4 * (i + 1) + o), e - o);
   }
 }

@@ -93,6 +93,8 @@ struct DevChunk {
   PQH_G int32_t* aux2;   // DELTA_BYTE_ARRAY: per value slot, prefix length
   int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
   int32_t batile_n;
+  int32_t ba_fused;      // PLAIN byte-array data pages only: byte bases guessed by k_scan, k_ba_chain
+  int32_t pad2;
 };
 
 // Written by the prologue (one wave per page) and the scan kernel.  64 bytes.

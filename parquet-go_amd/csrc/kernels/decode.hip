@@ -511,6 +511,42 @@ __global__ __launch_bounds__(256) void k_scan(DevBatch b) {
     if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }
+  if (!C.ba_fused) return;
+  // fused PLAIN chains (k_ba_chain): each page's string bytes taken as val_e - val_s - 4 * notNull,
+  // which k_ba_chain verifies; any page error, or a page that cannot be so, sends the batch back to
+  // the scratch path (bafuse[1])
+  bool fail = false;
+  if (t == 0) {
+    carry = 0;
+    if (C.offsets) C.offsets[0] = 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < C.num_pages; base += 256) {
+    const int i = base + t;
+    const int p = C.first_page + i;
+    int64_t g = 0;
+    if (i < C.num_pages) {
+      const PageState s = b.states[p];
+      if (s.err != kNoError || s.nn > (1 << 30) - 1) fail = true;
+      if (s.nn > 0) g = int64_t(s.val_e) - s.val_s - 4 * int64_t(s.nn);
+      if (g < 0) fail = true;
+    }
+    int64_t x = g;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < wv; k++) before += wsum[k];
+    if (i < C.num_pages) b.states[p].byte_base = before + x - g;
+    __syncthreads();
+    if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (t == 0) b.chunk_bytes[blockIdx.x] = carry;
+  if (fail) __hip_atomic_store(b.bafuse + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -1356,6 +1392,12 @@ hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_ba_wcopy, dim3(n < kWGrid ? n : kWGrid), dim3(256), 0, s, b, g, n, wrec);
+  return hipGetLastError();
+}
+
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, n);
   return hipGetLastError();
 }
 

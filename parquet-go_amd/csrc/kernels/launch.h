@@ -27,6 +27,8 @@ struct DevBatch {
   const DevNest* nests;  // repeated chunks with nesting outputs
   int64_t* nsums;        // per nest tile: kNestFlags counts, then (after k_nest_scan) bases
   int64_t* basums2;      // DELTA_BYTE_ARRAY: per tile suffix-byte sum, then its first suffix byte
+  uint32_t* bafuse;      // fused PLAIN chains: [0] window tickets, [1] fallback flag (zeroed per run)
+  uint64_t* bawords;     // fused PLAIN chains: per window FINAL word (zeroed per run)
 };
 
 hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s);
@@ -64,6 +66,8 @@ hipError_t launch_snappy_mw(const pqh_codec_page* pages, const SnapPlan& P, cons
 hipError_t launch_gzip(const pqh_codec_page* pages, int32_t n, const uint8_t* src, uint8_t* dst, int32_t* status,
                        hipStream_t s);
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
+// Fused PLAIN byte-array chains (bytearray_impl.h k_ba_chain): one workgroup per window of wins.
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, int32_t n, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);

@@ -179,9 +179,10 @@ def _fuzz(pq, ctx, data, seed, per_page=3):
     return _run_cases(pq, ctx, cases)
 
 
-def _run_cases(pq, ctx, cases):
+def _run_cases(pq, ctx, cases, stats=None):
     """Decode `cases` = [(column, dictionary (num_values, encoding, image) or None, data page)] in ONE
-    batch (every case its own chunk) and compare each against the oracle's decode_page."""
+    batch (every case its own chunk) and compare each against the oracle's decode_page.  stats: a
+    dict that gets the batch's kernel launch counts by name (profiled contexts)."""
     N = pq.native
     # every case is its own chunk (dictionary page first when present)
     blobs, chunks, pages = [], [], []
@@ -233,6 +234,8 @@ def _run_cases(pq, ctx, cases):
             assert_chunk(cd, e, where=f"case {i} col {col} enc {enc} type {ptype}")
             compared += 1
             errors += r.status != 0
+        if stats is not None:
+            stats.update({k.name.decode(): k.launches for k in b.kernel_stats()})
         b.close()
         return compared, errors
     finally:
@@ -700,6 +703,71 @@ def test_plain_chain_layouts(pq, ctx):
                       (O.DATA_PAGE, 5000, W.RLE_DICTIONARY, 0, 0, bytes([w]) + W.hybrid_encode(w, idx))))
     compared, errors = _run_cases(pq, ctx, cases)
     assert compared == len(cases) and errors >= 10
+
+
+def test_fused_plain_chains(pq):
+    """Chunks of PLAIN byte-array pages only take the fused k_ba_chain (one read of the page bytes,
+    byte bases from the page sizes, look-back between windows): the layouts of
+    test_plain_chain_layouts, several pages per chunk, in one batch that decodes without the scratch
+    path.  Then each defect alone in an otherwise clean batch -- a page whose chain has records past
+    notNull (trailing bytes), one that ends early, an invalid length, a page with fewer bytes than
+    4 * notNull -- sends the batch back to the scratch path, with the reference's results."""
+    W = fixtures.W
+    rng = np.random.default_rng(47)
+    col = (W.BYTE_ARRAY, 0, 0, 0)
+    ctx = pq.native.Context(0, profile=True)
+
+    def strings(n, kind):
+        out = []
+        for _ in range(n):
+            u = rng.random()
+            if kind == "empty_runs":
+                out.append(b"" if u < 0.7 else bytes(int(rng.integers(0, 3))))
+            elif kind == "long":
+                out.append(rng.bytes(int(rng.integers(200, 3000))) if u < 0.8 else b"")
+            elif kind == "huge":
+                out.append(rng.bytes(int(rng.integers(60000, 140000))) if u < 0.3 else rng.bytes(5))
+            elif kind == "lookalike":
+                k = int(rng.integers(0, 6))
+                out.append(b"".join(int(rng.integers(0, 24)).to_bytes(4, "little") for _ in range(k)))
+            else:
+                out.append(bytes(rng.integers(97, 123, int(rng.integers(0, 41))).astype(np.uint8)))
+        return out
+
+    clean = []
+    for kind, n in (("empty_runs", 40000), ("long", 400), ("huge", 12), ("ascii", 60000), ("lookalike", 50000),
+                    ("ascii", 1), ("ascii", 0)):
+        s = strings(n, kind)
+        clean.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, _plain_chain(s))))
+    stats = {}
+    compared, errors = _run_cases(pq, ctx, clean, stats)
+    assert compared == len(clean) and errors == 0
+    assert stats.get("k_ba_chain", 0) == 1 and stats.get("k_ba_wspec", 0) == 0 and stats.get("k_ba_wcopy", 0) == 0
+
+    # multi-page chunks through the file path (value / byte bases across pages, pages of many windows)
+    words = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(0, 60, 200000)]
+    data = W.flat([("p", W.Column(W.BYTE_ARRAY, words, use_dict=False), W.REQUIRED),
+                   ("q", W.optional(W.BYTE_ARRAY, words[::-1], rng.random(200000) < 0.2, use_dict=False), W.OPTIONAL)],
+                  70000, max_page_size=96 * 1024)
+    checked, skipped = _run_file(pq, ctx, data)
+    assert checked == 6 and skipped == 0
+
+    s = strings(30000, "ascii")
+    img = _plain_chain(s)
+    defects = {
+        "trailing records": (O.DATA_PAGE, 20000, W.PLAIN, 0, 0, img),
+        "ends early": (O.DATA_PAGE, 30000, W.PLAIN, 0, 0, img[: len(img) * 2 // 3]),
+        "negative length": (O.DATA_PAGE, 30000, W.PLAIN, 0, 0,
+                            _plain_chain(s[:17000]) + b"\x00\x00\x00\x80" + _plain_chain(s[17000:])),
+        "fewer bytes than lengths": (O.DATA_PAGE, 30000, W.PLAIN, 0, 0, img[:100000]),
+        "trailing garbage": (O.DATA_PAGE, 30000, W.PLAIN, 0, 0, img + b"\x07\x00"),
+    }
+    for name, page in defects.items():
+        stats = {}
+        compared, _ = _run_cases(pq, ctx, clean[:3] + [(col, None, page)] + clean[3:], stats)
+        assert compared == len(clean) + 1, name
+        assert stats.get("k_ba_wspec", 0) == 1 and stats.get("k_ba_wcopy", 0) == 1, (name, stats)
+    ctx.close()
 
 
 def _dba_page(strs, total=None, plens=None, slens=None, geom=(128, 4)):
