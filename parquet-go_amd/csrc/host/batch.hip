@@ -289,6 +289,8 @@ struct pqh_batch {
   int32_t ba_fuse_fallbacks = 0;
   uint32_t* d_bafuse = nullptr;
   uint64_t* d_bawords = nullptr;
+  std::vector<int32_t> ba_forder;   // k_ba_chain's dispatch order: fused windows by (window in page, page)
+  int32_t* d_ba_forder = nullptr;
   std::vector<int64_t> chunk_bytes; // host copy after sync
   std::vector<DevNest> nests;       // repeated chunks with nesting outputs
   std::vector<int32_t> chunk_nest;  // chunk -> nests index, -1
@@ -769,6 +771,12 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     }
     b->ba_wlist_nf = int32_t(std::count_if(b->ba_wlist.begin(), b->ba_wlist.end(),
                                            [&](const int2& x) { return x.x < b->ba_wins_nf; }));
+    // k_ba_chain takes every page's window 0 first, then every window 1, ...: a window's
+    // predecessors started a whole round of pages before it, so its look-back rarely waits
+    for (int32_t i = 0; i < int32_t(b->ba_wins.size()) - b->ba_wins_nf; i++) b->ba_forder.push_back(i);
+    std::stable_sort(b->ba_forder.begin(), b->ba_forder.end(), [&](int32_t x, int32_t y) {
+      return b->ba_wins[size_t(b->ba_wins_nf + x)].y < b->ba_wins[size_t(b->ba_wins_nf + y)].y;
+    });
     b->delta_page_mode = b->delta_streams.size() >= kDeltaPageModeMin;
     if (const char* f = getenv("PQH_DELTA_PAGE_MODE"))  // tests: force either path ("0" / "1")
       b->delta_page_mode = f[0] == '1';
@@ -841,6 +849,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums2), sizeof(int64_t) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bafuse), sizeof(uint32_t) * 4)) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bawords), sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_forder), sizeof(int32_t) * b->ba_forder.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
@@ -967,6 +976,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       {b->d_ba_pwin, b->ba_pwin.data(), sizeof(int2) * b->ba_pwin.size()},
       {b->d_ba_wlist, b->ba_wlist.data(), sizeof(int2) * b->ba_wlist.size()},
       {b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size()},
+      {b->d_ba_forder, b->ba_forder.data(), sizeof(int32_t) * b->ba_forder.size()},
       {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
       {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
   };
@@ -1056,12 +1066,32 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     });
   // repeated columns carry long level streams: a workgroup per page splits their notNull count
   const bool wide = std::any_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& c) { return c.max_rep > 0; });
+  if (e == hipSuccess && b->ba_fuse_on) {  // fused chains: tickets, fallback flag (k_scan's too), look-back words
+    e = hipMemsetAsync(b->d_bafuse, 0, sizeof(uint32_t) * 2, s);
+    if (e == hipSuccess)
+      e = hipMemsetAsync(b->d_bawords, 0, sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)), s);
+  }
   if (e == hipSuccess)
     e = timed(0, int32_t(b->pages.size()), s, [&](hipStream_t st) { return launch_prologue(d, wide, st); });
   // (while the fused chains are on, the scratch path covers the lists' non-fused prefixes)
   const bool fuse = b->ba_fuse_on;
   const int32_t nbp = fuse ? b->ba_pages_nf : int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()),
                 nbc = fuse ? b->ba_chunks_nf : int32_t(b->ba_chunks.size());
+  // fused PLAIN chains: need only the prologue's page states; compute bound (chain resolution), so
+  // they run on a stream of their own beside everything after the prologue
+  const int32_t nfw = fuse ? int32_t(b->ba_wins.size()) - b->ba_wins_nf : 0;
+  bool fuse_open = false;
+  if (e == hipSuccess && nfw) {
+    hipStream_t fs = s;
+    hipStream_t side2 = side ? b->ctx->side2 : nullptr;
+    if (side2) {
+      e = dep(s, side2, 4);
+      fs = side2;
+      fuse_open = true;
+    }
+    if (e == hipSuccess)
+      e = timed(29, nfw, fs, [&](hipStream_t st) { return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, b->d_ba_forder, nfw, st); });
+  }
   bool chain_open = false;  // the chain branch has not rejoined the main stream yet
   if (e == hipSuccess && nbp) {
     hipStream_t cs = s;
@@ -1099,25 +1129,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     e = timed(16, ndp - ni, s, [&](hipStream_t st) { return launch_delta_spec(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess && ndp > ni)
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
-  const int32_t nfw = fuse ? int32_t(b->ba_wins.size()) - b->ba_wins_nf : 0;
-  if (e == hipSuccess && nfw) {  // fused chains: tickets, fallback flag, FINAL words
-    e = hipMemsetAsync(b->d_bafuse, 0, sizeof(uint32_t) * 2, s);
-    if (e == hipSuccess) e = hipMemsetAsync(b->d_bawords, 0, sizeof(uint64_t) * size_t(nfw), s);
-  }
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
-  // fused PLAIN chains: need the value and (guessed) byte bases only; latency bound, beside the rest
-  bool fuse_open = false;
-  if (e == hipSuccess && nfw) {
-    hipStream_t fs = s;
-    hipStream_t side2 = side ? b->ctx->side2 : nullptr;
-    if (side2) {
-      e = dep(s, side2, 4);
-      fs = side2;
-      fuse_open = true;
-    }
-    if (e == hipSuccess)
-      e = timed(29, nfw, fs, [&](hipStream_t st) { return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, nfw, st); });
-  }
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });

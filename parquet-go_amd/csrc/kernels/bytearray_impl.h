@@ -48,6 +48,9 @@ struct ChainLds {
   int32_t guess;
   int32_t pad;
   uint64_t wsum[4];
+#ifdef PQH_FUSE_PROF
+  uint64_t prof[4];  // experiments: walk, rounds, marks + scan, records (thread 0's clocks)
+#endif
 };
 
 // Workgroup sum (every thread gets it).
@@ -76,34 +79,48 @@ __device__ __forceinline__ int chain_step(const ChainLds& C, int32_t wb, int32_t
   return PQH_OK;
 }
 
+// chain_step's validity test without its error codes (branch-free: the walks' inner loops):
+// avail >= 4 and 0 <= len <= avail - 4  <=>  avail >= 4 and unsigned(len) <= unsigned(avail - 4).
+__device__ __forceinline__ bool chain_ok(const ChainLds& C, int32_t wb, int32_t e0, int32_t p, int32_t& next,
+                                         int32_t& len) {
+  const int32_t avail = e0 - p;
+  const int32_t o = p - wb;
+  const uint32_t w0 = C.win[o >> 2], w1 = C.win[(o >> 2) + 1];
+  len = int32_t(__builtin_amdgcn_alignbit(w1, w0, uint32_t(o & 3) * 8));
+  next = p + 4 + len;
+  return avail >= 4 && uint32_t(len) <= uint32_t(avail - 4);
+}
+
 __device__ __forceinline__ int32_t seg_end(int j, int32_t wb, int32_t wend) {
   const int32_t s1 = wb + (j + 1) * kChainSeg;
   return s1 < wend ? s1 : wend;
 }
 
-// Walk segment j [s0, s1) from `start` (must lie in the segment): marks + exit.
+// Walk segment j [s0, s1) from `start` (must lie in the segment): marks + exit.  The marks go
+// straight to the segment's LDS words by one fire-and-forget OR per record (the thread's own words);
+// the error code of the record that stops the walk is taken once, after the loop.
 __device__ void chain_walk(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t e0, int32_t start) {
   const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
-  uint64_t m[kChainWords];
+  uint32_t* mw = reinterpret_cast<uint32_t*>(&C.mask[j][0]);
 #pragma unroll
-  for (int k = 0; k < kChainWords; k++) m[k] = 0;
+  for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
   int32_t p = start;
-  uint8_t bad = 0;
+  bool stop = false;
   while (p < s1) {
     int32_t nx, l;
-    const int st = chain_step(C, wb, e0, p, nx, l);
-    if (st) {
-      bad = uint8_t(st);
+    if (!chain_ok(C, wb, e0, p, nx, l)) {
+      stop = true;
       break;
     }
     const int q = p - s0;
-#pragma unroll
-    for (int k = 0; k < kChainWords; k++)
-      if ((q >> 6) == k) m[k] |= 1ull << (q & 63);
+    atomicOr(mw + (q >> 5), 1u << (q & 31));
     p = nx;
   }
-#pragma unroll
-  for (int k = 0; k < kChainWords; k++) C.mask[j][k] = m[k];
+  uint8_t bad = 0;
+  if (stop) {
+    int32_t nx, l;
+    bad = uint8_t(chain_step(C, wb, e0, p, nx, l));
+  }
   C.exitv[j] = p;
   C.exitbad[j] = bad;
 }
@@ -152,8 +169,8 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
                                                int32_t staged_end) {
   auto plausible = [&](int32_t x, int32_t& l) {
     int32_t nx, nx2, l2;
-    if (chain_step(C, wb, e0, x, nx, l) != PQH_OK) return false;
-    return nx + 4 <= staged_end && (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
+    if (!chain_ok(C, wb, e0, x, nx, l)) return false;
+    return nx + 4 <= staged_end && (nx >= e0 || chain_ok(C, wb, e0, nx, nx2, l2));
   };
   // scan 16 positions per step from 5 dwords loaded together (independent LDS reads; the length at
   // each byte offset is a funnel shift of two of them): a mask of the positions whose own record is
@@ -169,11 +186,11 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
     const int32_t lo = s0 > base ? s0 - base : 0, hi = lim - base < 16 ? lim - base : 16;
     uint32_t cand = 0;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int32_t len = int32_t(__builtin_amdgcn_alignbit(w[(i >> 2) + 1], w[i >> 2], uint32_t(i & 3) * 8));
-      const int32_t avail = rel - i;
-      if (i >= lo && i < hi && avail >= 4 && len >= 0 && (len == 0 || avail - 4 >= len)) cand |= 1u << i;
+    for (int i = 0; i < 16; i++) {  // (chain_ok's test; positions with fewer than 4 bytes left fail it)
+      const uint32_t len = __builtin_amdgcn_alignbit(w[(i >> 2) + 1], w[i >> 2], uint32_t(i & 3) * 8);
+      cand |= uint32_t(rel - i >= 4 && len <= uint32_t(rel - i - 4)) << i;
     }
+    cand &= ((1u << hi) - 1) & ~((1u << lo) - 1);  // (0 <= lo < hi <= 16)
     for (; cand; cand &= cand - 1) {
       int32_t l;
       const int32_t p = base + __builtin_ctz(cand);
@@ -205,6 +222,9 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
 // whose walk ended on an invalid record (kBlock if none).
 __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0, int32_t entry) {
   const int j = threadIdx.x;
+#ifdef PQH_FUSE_PROF
+  const uint64_t k0 = wall_clock64();
+#endif
   {
     const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
     int32_t start = -1;
@@ -233,7 +253,17 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
   }
   __syncthreads();
   // the first segment whose walk misses its true entry has an exact predecessor: re-walk it; repeat
+#ifdef PQH_FUSE_PROF
+  const uint64_t k1 = wall_clock64();
+  if (j == 0) {
+    C.pad = 0;
+    C.prof[0] = k1 - k0;
+  }
+#endif
   for (;;) {
+#ifdef PQH_FUSE_PROF
+    if (j == 0) C.pad++;
+#endif
     if (j == 0) C.stop = kBlock;
     __syncthreads();
     if (!chain_good(C, j, wb, wend, entry)) atomicMin(&C.stop, j);
@@ -247,6 +277,9 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
   __syncthreads();
   if (C.exitbad[j]) atomicMin(&C.first_bad, j);  // segments before the chain's end are exact
   __syncthreads();
+#ifdef PQH_FUSE_PROF
+  if (j == 0) C.prof[1] = wall_clock64() - k1;
+#endif
 }
 
 // Segment j's marks on the true chain (starts before its true entry dropped; none past the end).
@@ -331,6 +364,9 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   }
   const int32_t wb = int32_t(ba_wbase(c, w)), wend = int32_t(wend64), entry = int32_t(entry64);
   chain_resolve(C, wb, wend, int32_t(c.e0), entry);
+#ifdef PQH_FUSE_PROF
+  const uint64_t k2 = wall_clock64();
+#endif
   const int fb = C.first_bad;
   uint64_t m[kChainWords];
   const int cnt = chain_marks(C, j, wb, entry, fb, m);
@@ -347,6 +383,10 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   uint64_t tot;
   const uint64_t ex = block_exclusive_scan((uint64_t(uint32_t(cnt)) << 32) | uint32_t(bytes), C.wsum, &tot);
   int32_t li = int32_t(ex >> 32), lb = int32_t(uint32_t(ex));
+#ifdef PQH_FUSE_PROF
+  const uint64_t k3 = wall_clock64();
+  if (j == 0) C.prof[2] = k3 - k2;
+#endif
   int32_t prev = -1;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
@@ -356,6 +396,9 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
       wrec[li++] = uint16_t(lb);
       prev = pos;
     }
+#ifdef PQH_FUSE_PROF
+  if (j == 0) C.prof[3] = wall_clock64() - k3;
+#endif
   if (j == 0) {
     const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
     r.count = nrec;
@@ -382,8 +425,8 @@ __device__ __forceinline__ int32_t ba_guess_entry(const ChainLds& C, int32_t e0,
   for (int32_t x0 = Bw; x0 < Bw + 1024 && x0 < e0; x0 += 64) {
     const int32_t x = x0 + lane;
     int32_t nx, nx2, l = 0, l2;
-    bool ok = x < e0 && chain_step(C, wb, e0, x, nx, l) == PQH_OK && nx + 4 <= staged_end &&
-              (nx >= e0 || chain_step(C, wb, e0, nx, nx2, l2) == PQH_OK);
+    bool ok = x < e0 && chain_ok(C, wb, e0, x, nx, l) && nx + 4 <= staged_end &&
+              (nx >= e0 || chain_ok(C, wb, e0, nx, nx2, l2));
     const uint64_t m = __ballot(ok);
     if (m == 0) continue;
     const int f = __builtin_ctzll(m);
@@ -403,6 +446,10 @@ __device__ __forceinline__ int32_t ba_guess_entry(const ChainLds& C, int32_t e0,
 
 __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, uint16_t* wrec) {
   __shared__ ChainLds C;
+#ifdef PQH_WSPEC_PAD  // experiments: k_ba_chain's LDS footprint
+  __shared__ uint16_t pad[kChainRecs + 8];
+  if (b.num_pages < 0) pad[threadIdx.x] = 0;
+#endif
   const int2 pw = wins[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, pw.x);
   BaWin* r = res + blockIdx.x;
@@ -1325,39 +1372,110 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
 
 // ------------------------------------------------------------------------------------------------
 // Fused PLAIN chains (k_ba_chain): chunks whose data pages are all PLAIN byte arrays and which have
-// no dictionary page (DevChunk.ba_fused) read their page bytes once.  One workgroup per window, in
-// ticket order (a window's predecessor in its page always holds an earlier ticket, so it is resident
-// or done):
+// no dictionary page (DevChunk.ba_fused) read their page bytes once.  One workgroup per window,
+// taken by ticket in the order (window in page, page) -- every page's window 0, then every window
+// 1, ... -- so a window's predecessors in its page hold earlier tickets (resident or done: no
+// deadlock) and started a whole round of pages before it (its look-back rarely waits), with a
+// decoupled look-back over one 64-bit word per window:
 //   * the window is staged and resolved from its guessed entry as in k_ba_wspec, its records into
-//     LDS (no scratch);
-//   * its predecessor's FINAL word (records on the page's chain before this window's end, and the
-//     chain's position there) is read by a relaxed agent-scope spin -- one 64-bit word, so no fence;
-//     a wrong guess re-resolves the window from the true entry (LDS still holds the bytes);
-//   * the window publishes its own FINAL word at once, before its copies, so the page's chain moves
-//     on while it writes its offsets and strings straight from LDS.
-// Output byte bases come from k_scan: a page whose chain is exactly notNull records filling its
-// values section has val_e - val_s - 4 * notNull string bytes.  The window holding record notNull checks that record's end is
-// val_e; a chain that ends early, runs on, fails, or a page that failed earlier sets the batch's
-// fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again with the scratch path
-// (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and limits exactly.
+//     LDS (no scratch), and publishes PARTIAL = (records, guessed entry, exit, invalid record seen);
+//     window 0 of a page knows its entry and publishes FINAL = (records of the page up to its end,
+//     exit) at once;
+//   * wave 0 reads the predecessors' words 64 at a time, newest first (relaxed agent-scope loads:
+//     each word is self-contained, so no fence is needed): the nearest FINAL plus the PARTIALs after
+//     it give this window's base when every PARTIAL's guessed entry is its predecessor's exit (by
+//     induction from the FINAL, each of those windows was resolved from its true entry).  Anything
+//     else (a wrong guess, a chain that ended) waits for the predecessor's own FINAL instead;
+//   * a wrong guess of its own re-resolves the window from the true entry (LDS still holds the
+//     bytes); then it publishes FINAL and writes its offsets and strings straight from LDS.
+// Output bases need only the prologue's page states, so the kernel runs beside everything after
+// the prologue: a page whose chain is exactly notNull records filling its values section has
+// val_e - val_s - 4 * notNull string bytes, and its value / byte bases are the sums over the
+// chunk's pages before it (k_scan writes the same bases into the page states for the host).  The window holding record notNull
+// checks that record's end is val_e; a chain that ends early, runs on, fails, or a page that failed
+// earlier sets the batch's fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again
+// with the scratch path (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and
+// limits exactly.
+// Words: PARTIAL 01 | bad | count:13 | entry - B_w:16 | exit:32;  FINAL 10 | ended | incl:29 | exit:32.
 // ------------------------------------------------------------------------------------------------
-constexpr uint64_t kFinal = 1ull << 63, kEnded = 1ull << 62;
-constexpr int64_t kInclMax = (int64_t(1) << 30) - 1;
+constexpr uint64_t kPartial = 1ull << 62, kFinal = 2ull << 62, kBadBit = 1ull << 61;
+constexpr int64_t kInclMax = (int64_t(1) << 29) - 1;
+constexpr int kFuseSpinCap = 1 << 22;  // (never reached: every window a look-back reads is resident)
 
 __device__ __forceinline__ void fuse_fail(const DevBatch& b) {
   __hip_atomic_store(b.bafuse + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, int32_t nwin) {
+__device__ __forceinline__ uint64_t fuse_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0: window t (page window w >= 1, guessed entry g) -> records before it, the chain's position
+// at its start, whether the chain ended before it.  False: no decisive look-back (the caller waits
+// for window t - 1's FINAL).
+__device__ bool fuse_lookback(const DevBatch& b, int t, int w, int64_t val_s, int64_t* pincl, int64_t* pexit,
+                              bool* pended) {
+  const int lane = threadIdx.x & 63;
+  const int first = t - w;  // the page's window 0 (publishes FINAL only)
+  int hi = t - 1;
+  int64_t acc = 0, need = -1, exit1 = -1;
+  bool ended1 = false;  // window t - 1 ended the chain
+  for (bool round0 = true;; round0 = false) {
+    const int j = hi - lane;
+    const bool in = j >= first;
+    uint64_t v = 0;
+    for (int spin = 0;; spin++) {
+      if (in && v == 0) v = fuse_load(b.bawords + j);
+      if (__ballot(in && v == 0) == 0) break;
+      if (spin > kFuseSpinCap) {
+        if (lane == 0) fuse_fail(b);
+        *pended = true;
+        return true;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const bool fin = in && (v >> 62) == 2;
+    const uint64_t fm = __ballot(fin);
+    const int f = fm ? __builtin_ctzll(fm) : 64;
+    const int64_t ex = int64_t(uint32_t(v));
+    const int64_t ent = val_s + int64_t(w - (t - j)) * kChainStride + int64_t((v >> 32) & 0xffff);
+    const bool bad = (v & kBadBit) != 0;
+    int64_t nxt = __shfl_up(ent, 1, 64);  // the entry window j + 1 guessed
+    if (lane == 0) nxt = need;
+    if (round0) {
+      exit1 = __shfl(ex, 0, 64);
+      ended1 = __shfl(int(bad), 0, 64) != 0;
+    }
+    // lanes up to the FINAL: each exit meets its successor's guess; a chain may end only right
+    // before window t
+    const bool lead = round0 && lane == 0;
+    const bool ok = !in || lane > f || ((nxt < 0 || ex == nxt) && (!bad || lead));
+    if (__ballot(!ok)) return false;
+    int64_t cnt = (in && lane < f) ? int64_t((v >> 48) & 0x1fff) : 0;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (f < 64) {
+      const uint64_t vf = __shfl(v, f, 64);
+      *pincl = int64_t((vf >> 32) & uint64_t(kInclMax)) + acc + cnt;
+      *pexit = exit1;
+      *pended = ended1;
+      return true;
+    }
+    acc += cnt;
+    need = __shfl(ent, 63, 64);
+    hi -= 64;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
   __shared__ ChainLds C;
   __shared__ uint16_t recs[kChainRecs + 8];
   __shared__ BaWin R;
-  __shared__ uint64_t sh[2];
+  __shared__ int64_t sh[6];
   const int tid = threadIdx.x;
   if (tid == 0) sh[0] = atomicAdd(b.bafuse, 1u);
   __syncthreads();
-  const int t = int(sh[0]);
-  if (t >= nwin) return;
+  if (int(sh[0]) >= nwin) return;
+  const int t = order[sh[0]];  // (the window's page-major index: its look-back word)
   const int2 pw = wins[t];
   const int p = pw.x, w = pw.y;
   const PageState S = b.states[p];
@@ -1372,71 +1490,145 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   c.img = b.payload + P.image_off;
   const int64_t Bw = c.entry + int64_t(w) * kChainStride;
   const int64_t wend = Bw + kChainStride;
-  const bool staged = c.ok && Bw < c.e0;
-  int64_t wb = 0, entry = c.entry;
-  if (staged) {
-    wb = ba_wbase(c, w);
-    ba_stage(C, c, wb);
-    __syncthreads();
-    if (w > 0) {
-      if (tid < 64) {
-        const int32_t g = ba_guess_entry(C, int32_t(c.e0), int32_t(wb), int32_t(Bw));
-        if (tid == 0) C.guess = g;
+  // a window starting past the values holds nothing of any chain, and no window of its page that
+  // does looks back at it (their bases come first); failed pages were flagged by k_scan
+  if (!c.ok || Bw >= c.e0) return;
+#ifdef PQH_FUSE_PROF  // experiments: phase clocks of every 997th window
+  const uint64_t q0 = wall_clock64();
+  bool slow = false, again = false;
+#endif
+  const int64_t wb = ba_wbase(c, w);
+  ba_stage(C, c, wb);
+  __syncthreads();
+#ifdef PQH_FUSE_PROF
+  const uint64_t q1 = wall_clock64();
+#endif
+  const DevChunk D = b.chunks[P.chunk];
+  if (tid >= 64 && tid < 128) {
+    // the page's value and byte bases from the prologue's page states (what k_scan computes; the
+    // kernel runs beside it): notNull and string bytes of the chunk's pages before this one
+    int64_t vb = 0, bb = 0;
+    for (int q = D.first_page + (tid - 64); q < p; q += 64) {
+      const int32_t qn = b.states[q].nn;
+      if (qn > 0) {
+        vb += qn;
+        bb += int64_t(b.states[q].val_e) - b.states[q].val_s - 4 * int64_t(qn);
       }
-      __syncthreads();
-      entry = C.guess;
     }
-    ba_window(C, c, w, entry, &R, recs);
+    for (int off = 32; off > 0; off >>= 1) {
+      vb += __shfl_xor(vb, off, 64);
+      bb += __shfl_xor(bb, off, 64);
+    }
+    if (tid == 64) {
+      sh[4] = vb;
+      sh[5] = bb;
+    }
   }
-  // the predecessor's chain position
-  int64_t pincl = 0, pexit = c.entry;
+  int64_t entry = c.entry;
+  if (w > 0) {
+    if (tid < 64) {
+      const int32_t g = ba_guess_entry(C, int32_t(c.e0), int32_t(wb), int32_t(Bw));
+      if (tid == 0) C.guess = g;
+    }
+    __syncthreads();
+    entry = C.guess;
+  }
+#ifdef PQH_FUSE_PROF
+  const uint64_t q1b = wall_clock64();
+#endif
+  ba_window(C, c, w, entry, &R, recs);
+  __syncthreads();
+  const int64_t value_base = sh[4], byte_base = sh[5];
+#ifdef PQH_FUSE_PROF
+  const uint64_t q2 = wall_clock64();
+  const int rounds = C.pad;
+  const uint64_t pw0 = C.prof[0], pw1 = C.prof[1], pw2 = C.prof[2], pw3 = C.prof[3];
+#endif
+  int64_t pincl = 0;
   bool pended = false;
   if (w > 0) {
-    if (tid == 0) {
-      uint64_t v = 0;
-      for (int spin = 0;; spin++) {
-        v = __hip_atomic_load(b.bawords + t - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v & kFinal) break;
-        if (spin > (1 << 22)) {  // (never: the predecessor is resident) -- give up on the fused path
-          fuse_fail(b);
-          v = kFinal | kEnded;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    if (tid == 0) {  // PARTIAL
+      const BaWin r0 = R;
+      __hip_atomic_store(b.bawords + t,
+                         kPartial | (r0.bad ? kBadBit : 0) | (uint64_t(r0.count) << 48) |
+                             (uint64_t(entry - Bw) << 32) | uint64_t(uint32_t(r0.exit)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < 64) {
+      int64_t pi = 0, pe = 0;
+      bool en = false;
+#ifdef PQH_FUSE_NOLOOK  // experiments: no look-back (the guess taken as the entry)
+      pe = entry;
+      if (false) {
+#else
+      if (!fuse_lookback(b, t, w, c.entry, &pi, &pe, &en)) {
+#endif
+#ifdef PQH_FUSE_PROF
+        slow = true;
+#endif
+        // no decisive look-back: the predecessor's FINAL
+        uint64_t v = 0;
+        if (tid == 0)
+          for (int spin = 0;; spin++) {
+            v = fuse_load(b.bawords + t - 1);
+            if ((v >> 62) == 2) break;
+            if (spin > kFuseSpinCap) {
+              fuse_fail(b);
+              v = kFinal | kBadBit;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        v = __shfl(v, 0, 64);
+        pi = int64_t((v >> 32) & uint64_t(kInclMax));
+        pe = int64_t(uint32_t(v));
+        en = (v & kBadBit) != 0;
       }
-      sh[1] = v;
+      if (tid == 0) {
+        sh[1] = pi;
+        sh[2] = pe;
+        sh[3] = en;
+      }
     }
     __syncthreads();
-    const uint64_t v = sh[1];
-    pended = (v & kEnded) != 0;
-    pincl = int64_t((v >> 32) & uint64_t(kInclMax));
-    pexit = int64_t(uint32_t(v));
-  }
-  if (!c.ok || pended || pexit >= c.e0 || pexit >= wend || !staged) {
-    // nothing of the chain starts here (a live chain reaches Bw before window w, so pexit < e0
-    // means Bw < e0: the window is staged)
-    if (tid == 0) {
-      const int bad = (c.ok && !pended && pexit >= c.e0 && pexit < wend) ? PQH_ERR_EOF : 0;
-      R = BaWin{int32_t(pexit), int32_t(pexit), 0, bad, 0, 0, 0, 0};
+#ifdef PQH_FUSE_PROF
+    if (tid == 0) sh[3] |= int64_t(slow) << 1;
+    __syncthreads();
+    slow = (sh[3] >> 1) & 1;
+    if (tid == 0) sh[3] &= 1;
+    __syncthreads();
+#endif
+    pincl = sh[1];
+    const int64_t pexit = sh[2];
+    pended = sh[3] != 0;
+    if (pended || pexit >= c.e0 || pexit >= wend) {
+      // nothing of the chain starts here
+      if (tid == 0) {
+        const int bad = (!pended && pexit >= c.e0 && pexit < wend) ? PQH_ERR_EOF : 0;
+        R = BaWin{int32_t(pexit), int32_t(pexit), 0, bad, 0, 0, 0, 0};
+      }
+      __syncthreads();
+    } else if (pexit != entry) {
+      // a wrong guess: resolve again from the true entry
+      ba_window(C, c, w, pexit, &R, recs);
+      __syncthreads();
+#ifdef PQH_FUSE_PROF
+      again = true;
+#endif
     }
-    __syncthreads();
-  } else if (w > 0 && pexit != entry) {
-    // wrong guess: resolve again from the true entry
-    __syncthreads();
-    ba_window(C, c, w, pexit, &R, recs);
-    __syncthreads();
-  } else {
-    __syncthreads();
   }
+#ifdef PQH_FUSE_PROF
+  const uint64_t q3 = wall_clock64();
+#endif
   const BaWin r = R;
   if (tid == 0) {
     int64_t incl = pincl + r.count;
     if (incl > kInclMax) incl = kInclMax;
-    const bool ended = pended || !c.ok || r.bad != 0;
-    __hip_atomic_store(b.bawords + t, kFinal | (ended ? kEnded : 0) | (uint64_t(incl) << 32) | uint64_t(uint32_t(r.exit)),
+    const bool ended = pended || r.bad != 0;
+    __hip_atomic_store(b.bawords + t, kFinal | (ended ? kBadBit : 0) | (uint64_t(incl) << 32) | uint64_t(uint32_t(r.exit)),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the page's check: record nn ends at val_e, or the chain falls short of nn records
-    if (c.ok && !pended && pincl < nn) {
+    if (!pended && pincl < nn) {
       if (pincl + r.count >= nn) {
         const int64_t k = nn - pincl;  // records of the page up to and including record nn, in this window
         const int64_t end = int64_t(r.entry) + 4 * k + (k < r.count ? int64_t(recs[k]) : r.bytes);
@@ -1446,17 +1638,19 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
       }
     }
   }
-  if (!c.ok || pended || pincl >= nn || r.count == 0) return;
+  if (pended || pincl >= nn || r.count == 0) return;
+#ifdef PQH_FUSE_NOEMIT  // experiments: the resolution alone
+  return;
+#endif
   // emit: the window's records before the page's notNull, at the page's guessed byte base
   const int n = int(nn - pincl < r.count ? nn - pincl : r.count);
-  const DevChunk D = b.chunks[P.chunk];
-  const int64_t obase = S.byte_base + (int64_t(r.entry) - c.entry) - 4 * pincl;
+  const int64_t obase = byte_base + (int64_t(r.entry) - c.entry) - 4 * pincl;
   const int64_t endo = n < r.count ? int64_t(recs[n]) : r.bytes;
-  if (obase < 0 || obase + endo > D.bytes_cap || S.value_base + pincl + n > D.values_cap) {
+  if (obase < 0 || obase + endo > D.bytes_cap || value_base + pincl + n > D.values_cap) {
     if (tid == 0) fuse_fail(b);  // a wrong guess somewhere: never written, the batch goes again
     return;
   }
-  PQH_G int64_t* offs = D.offsets + S.value_base + 1 + pincl;
+  PQH_G int64_t* offs = D.offsets + value_base + 1 + pincl;
   PQH_G uint8_t* dst = D.bytes + obase;
   const int lead = int(r.entry - wb);  // the entry in the stage
   constexpr int kStaged = kChainWin + 64;
@@ -1465,6 +1659,9 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     const int o = recs[i];
     const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
     offs[i] = obase + e;
+#ifdef PQH_FUSE_NOSTR  // experiments: offsets only
+    continue;
+#endif
     const int l = e - o;
     const int sx = lead + 4 * (i + 1) + o;
     if (sx + l + 20 <= kStaged) stage_string_out(C.win, sx, l, dst + o);
@@ -1478,4 +1675,13 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     if (sx + (e - o) + 20 <= kStaged) break;
     if (e - o >= kLong) block_copy(dst + o, (const PQH_G uint8_t*)(c.img + r.entry + 4 * (i + 1) + o), e - o);
   }
+#ifdef PQH_FUSE_PROF
+  __syncthreads();
+  if (tid == 0 && t % 997 == 0)
+    printf("fuse t %d w %d stage %llu guess %llu resolve %llu [walk %llu rounds %llu scan %llu recs %llu] rounds %d look %llu emit %llu slow %d again %d n %d\n", t, w,
+           (unsigned long long)(q1 - q0), (unsigned long long)(q1b - q1), (unsigned long long)(q2 - q1b),
+           (unsigned long long)pw0, (unsigned long long)pw1, (unsigned long long)pw2, (unsigned long long)pw3, rounds,
+           (unsigned long long)(q3 - q2),
+           (unsigned long long)(wall_clock64() - q3), int(slow), int(again), n);
+#endif
 }

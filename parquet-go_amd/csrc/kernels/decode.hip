@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256) void k_scan(DevBatch b) {
     int64_t g = 0;
     if (i < C.num_pages) {
       const PageState s = b.states[p];
-      if (s.err != kNoError || s.nn > (1 << 30) - 1) fail = true;
+      if (s.err != kNoError || s.nn > (1 << 29) - 1) fail = true;
       if (s.nn > 0) g = int64_t(s.val_e) - s.val_s - 4 * int64_t(s.nn);
       if (g < 0) fail = true;
     }
@@ -1395,9 +1395,9 @@ hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const
   return hipGetLastError();
 }
 
-hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, int32_t n, hipStream_t s) {
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, n);
+  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n);
   return hipGetLastError();
 }
 

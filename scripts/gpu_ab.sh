@@ -10,7 +10,7 @@ fi
 for w in ${WORKLOADS:-c4}; do
   for v in ${VARIANTS:-X=1}; do
     log=gpurun_out/ab/bench_${w}_${v//[=,]/_}.log
-    env ${v//,/ } timeout -k 10 300 python -u bench.py --workload $w --steps ${STEPS:-10} --warmup 2 --no-cpu --no-e2e > $log 2>&1
+    env ${v//,/ } timeout -k 10 300 python -u bench.py --workload $w --steps ${STEPS:-10} --warmup 2 --no-cpu --no-e2e ${AB_ARGS} > $log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "bench $w $v rc=$rc"; tail -5 $log; exit $rc; }
     python - "$log" "$w $v" <<'P'
 import json, sys
