@@ -48,9 +48,6 @@ struct ChainLds {
   int32_t guess;
   int32_t pad;
   uint64_t wsum[4];
-#ifdef PQH_FUSE_PROF
-  uint64_t prof[4];  // experiments: walk, rounds, marks + scan, records (thread 0's clocks)
-#endif
 };
 
 // Workgroup sum (every thread gets it).
@@ -222,9 +219,6 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
 // whose walk ended on an invalid record (kBlock if none).
 __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0, int32_t entry) {
   const int j = threadIdx.x;
-#ifdef PQH_FUSE_PROF
-  const uint64_t k0 = wall_clock64();
-#endif
   {
     const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
     int32_t start = -1;
@@ -253,17 +247,7 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
   }
   __syncthreads();
   // the first segment whose walk misses its true entry has an exact predecessor: re-walk it; repeat
-#ifdef PQH_FUSE_PROF
-  const uint64_t k1 = wall_clock64();
-  if (j == 0) {
-    C.pad = 0;
-    C.prof[0] = k1 - k0;
-  }
-#endif
   for (;;) {
-#ifdef PQH_FUSE_PROF
-    if (j == 0) C.pad++;
-#endif
     if (j == 0) C.stop = kBlock;
     __syncthreads();
     if (!chain_good(C, j, wb, wend, entry)) atomicMin(&C.stop, j);
@@ -277,9 +261,6 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
   __syncthreads();
   if (C.exitbad[j]) atomicMin(&C.first_bad, j);  // segments before the chain's end are exact
   __syncthreads();
-#ifdef PQH_FUSE_PROF
-  if (j == 0) C.prof[1] = wall_clock64() - k1;
-#endif
 }
 
 // Segment j's marks on the true chain (starts before its true entry dropped; none past the end).
@@ -364,9 +345,6 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   }
   const int32_t wb = int32_t(ba_wbase(c, w)), wend = int32_t(wend64), entry = int32_t(entry64);
   chain_resolve(C, wb, wend, int32_t(c.e0), entry);
-#ifdef PQH_FUSE_PROF
-  const uint64_t k2 = wall_clock64();
-#endif
   const int fb = C.first_bad;
   uint64_t m[kChainWords];
   const int cnt = chain_marks(C, j, wb, entry, fb, m);
@@ -383,10 +361,6 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   uint64_t tot;
   const uint64_t ex = block_exclusive_scan((uint64_t(uint32_t(cnt)) << 32) | uint32_t(bytes), C.wsum, &tot);
   int32_t li = int32_t(ex >> 32), lb = int32_t(uint32_t(ex));
-#ifdef PQH_FUSE_PROF
-  const uint64_t k3 = wall_clock64();
-  if (j == 0) C.prof[2] = k3 - k2;
-#endif
   int32_t prev = -1;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++)
@@ -396,9 +370,6 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
       wrec[li++] = uint16_t(lb);
       prev = pos;
     }
-#ifdef PQH_FUSE_PROF
-  if (j == 0) C.prof[3] = wall_clock64() - k3;
-#endif
   if (j == 0) {
     const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
     r.count = nrec;
@@ -446,10 +417,6 @@ __device__ __forceinline__ int32_t ba_guess_entry(const ChainLds& C, int32_t e0,
 
 __global__ __launch_bounds__(256) void k_ba_wspec(DevBatch b, const int2* wins, BaWin* res, uint16_t* wrec) {
   __shared__ ChainLds C;
-#ifdef PQH_WSPEC_PAD  // experiments: k_ba_chain's LDS footprint
-  __shared__ uint16_t pad[kChainRecs + 8];
-  if (b.num_pages < 0) pad[threadIdx.x] = 0;
-#endif
   const int2 pw = wins[blockIdx.x];
   const BaPageCtx c = ba_page_ctx(b, pw.x);
   BaWin* r = res + blockIdx.x;
@@ -1495,7 +1462,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   if (!c.ok || Bw >= c.e0) return;
 #ifdef PQH_FUSE_PROF  // experiments: phase clocks of every 997th window
   const uint64_t q0 = wall_clock64();
-  bool slow = false, again = false;
 #endif
   const int64_t wb = ba_wbase(c, w);
   ba_stage(C, c, wb);
@@ -1533,16 +1499,11 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     __syncthreads();
     entry = C.guess;
   }
-#ifdef PQH_FUSE_PROF
-  const uint64_t q1b = wall_clock64();
-#endif
   ba_window(C, c, w, entry, &R, recs);
   __syncthreads();
   const int64_t value_base = sh[4], byte_base = sh[5];
 #ifdef PQH_FUSE_PROF
   const uint64_t q2 = wall_clock64();
-  const int rounds = C.pad;
-  const uint64_t pw0 = C.prof[0], pw1 = C.prof[1], pw2 = C.prof[2], pw3 = C.prof[3];
 #endif
   int64_t pincl = 0;
   bool pended = false;
@@ -1557,15 +1518,7 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     if (tid < 64) {
       int64_t pi = 0, pe = 0;
       bool en = false;
-#ifdef PQH_FUSE_NOLOOK  // experiments: no look-back (the guess taken as the entry)
-      pe = entry;
-      if (false) {
-#else
       if (!fuse_lookback(b, t, w, c.entry, &pi, &pe, &en)) {
-#endif
-#ifdef PQH_FUSE_PROF
-        slow = true;
-#endif
         // no decisive look-back: the predecessor's FINAL
         uint64_t v = 0;
         if (tid == 0)
@@ -1591,13 +1544,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
       }
     }
     __syncthreads();
-#ifdef PQH_FUSE_PROF
-    if (tid == 0) sh[3] |= int64_t(slow) << 1;
-    __syncthreads();
-    slow = (sh[3] >> 1) & 1;
-    if (tid == 0) sh[3] &= 1;
-    __syncthreads();
-#endif
     pincl = sh[1];
     const int64_t pexit = sh[2];
     pended = sh[3] != 0;
@@ -1612,9 +1558,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
       // a wrong guess: resolve again from the true entry
       ba_window(C, c, w, pexit, &R, recs);
       __syncthreads();
-#ifdef PQH_FUSE_PROF
-      again = true;
-#endif
     }
   }
 #ifdef PQH_FUSE_PROF
@@ -1639,9 +1582,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     }
   }
   if (pended || pincl >= nn || r.count == 0) return;
-#ifdef PQH_FUSE_NOEMIT  // experiments: the resolution alone
-  return;
-#endif
   // emit: the window's records before the page's notNull, at the page's guessed byte base
   const int n = int(nn - pincl < r.count ? nn - pincl : r.count);
   const int64_t obase = byte_base + (int64_t(r.entry) - c.entry) - 4 * pincl;
@@ -1659,9 +1599,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     const int o = recs[i];
     const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
     offs[i] = obase + e;
-#ifdef PQH_FUSE_NOSTR  // experiments: offsets only
-    continue;
-#endif
     const int l = e - o;
     const int sx = lead + 4 * (i + 1) + o;
     if (sx + l + 20 <= kStaged) stage_string_out(C.win, sx, l, dst + o);
@@ -1678,10 +1615,8 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
 #ifdef PQH_FUSE_PROF
   __syncthreads();
   if (tid == 0 && t % 997 == 0)
-    printf("fuse t %d w %d stage %llu guess %llu resolve %llu [walk %llu rounds %llu scan %llu recs %llu] rounds %d look %llu emit %llu slow %d again %d n %d\n", t, w,
-           (unsigned long long)(q1 - q0), (unsigned long long)(q1b - q1), (unsigned long long)(q2 - q1b),
-           (unsigned long long)pw0, (unsigned long long)pw1, (unsigned long long)pw2, (unsigned long long)pw3, rounds,
-           (unsigned long long)(q3 - q2),
-           (unsigned long long)(wall_clock64() - q3), int(slow), int(again), n);
+    printf("fuse t %d w %d stage %llu guess+resolve %llu look %llu emit %llu n %d\n", t, w,
+           (unsigned long long)(q1 - q0), (unsigned long long)(q2 - q1), (unsigned long long)(q3 - q2),
+           (unsigned long long)(wall_clock64() - q3), n);
 #endif
 }
