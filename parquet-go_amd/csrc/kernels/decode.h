@@ -230,6 +230,9 @@ struct Tile {
 };
 
 constexpr int kLevelSpan = 4;  // 32768 level slots per tile
-constexpr int kDictSpan = 2;   // 16384 values per tile
+#ifndef PQH_DICT_SPAN
+#define PQH_DICT_SPAN 2
+#endif
+constexpr int kDictSpan = PQH_DICT_SPAN;  // 16384 values per tile
 
 }  // namespace pqhip
