@@ -91,6 +91,9 @@ struct DevChunk {
   int64_t bytes_cap;
   PQH_G int32_t* aux;    // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH / suffix) or dictionary key
   PQH_G int32_t* aux2;   // DELTA_BYTE_ARRAY: per value slot, prefix length
+  PQH_G uint8_t* lev4;   // repeated chunks with max_rep, max_def <= 3: def | rep << 2 per level slot, two
+                         // slots per byte (low nibble first), packed by k_expand's level tiles for the
+                         // nesting passes (0.5 B per slot read instead of 2)
   int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
   int32_t batile_n;
   int32_t ba_fused;      // PLAIN byte-array data pages only: byte bases guessed by k_scan, k_ba_chain

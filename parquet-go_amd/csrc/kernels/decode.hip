@@ -927,6 +927,48 @@ struct KeySink {
 // ------------------------------------------------------------------------------------------------
 // Tile bodies.  Every body reads its page/state/chunk records itself (all depend on t.page only).
 // ------------------------------------------------------------------------------------------------
+// The nesting passes' copy of a tile's levels [a, e) (chunk slots; the workgroup wrote their rep and
+// def bytes just before, so they come from L2): nibble def | rep << 2, slot s in byte s / 2 (low
+// nibble for even s).  Groups of 32 slots aligned in the chunk (the level buffers are 256-byte
+// aligned): two 16-byte loads per stream, one 16-byte store; the slots of a group shared with a
+// neighbouring tile by bit-disjoint atomics on their dwords.
+__device__ __forceinline__ void lev4_set(PQH_G uint8_t* lev4, int64_t s, uint32_t v) {
+  unsigned int* w = reinterpret_cast<unsigned int*>(lev4) + (s >> 3);
+  const uint32_t sh = 4u * uint32_t(s & 7);
+  atomicAnd(w, ~(0xfu << sh));
+  atomicOr(w, (v & 0xfu) << sh);
+}
+
+// 8 level bytes (values <= 3) of each stream -> 8 nibbles (one dword).
+__device__ __forceinline__ uint32_t lev4_pack8(uint32_t d0, uint32_t d1, uint32_t r0, uint32_t r1) {
+  uint64_t c = (uint64_t(d0) | (uint64_t(d1) << 32)) | ((uint64_t(r0) | (uint64_t(r1) << 32)) << 2);
+  c = (c | (c >> 4)) & 0x00ff00ff00ff00ffull;  // byte 2k = slot 2k | slot 2k+1 << 4
+  c = (c | (c >> 8)) & 0x0000ffff0000ffffull;
+  return uint32_t(c | (c >> 16));
+}
+
+__device__ __forceinline__ void pack_levels(const DevChunk& C, int64_t a, int64_t e) {
+  const PQH_G uint8_t* rp = C.rep_levels;
+  const PQH_G uint8_t* dp = C.def_levels;
+  const int64_t g0 = (a + 31) >> 5, g1 = e >> 5;  // whole 32-slot groups inside [a, e)
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
+    const PQH_G uint4* r4 = reinterpret_cast<const PQH_G uint4*>(rp + 32 * g);
+    const PQH_G uint4* d4 = reinterpret_cast<const PQH_G uint4*>(dp + 32 * g);
+    const uint4 ra = r4[0], rb = r4[1], da = d4[0], db = d4[1];
+    uint4 o;
+    o.x = lev4_pack8(da.x, da.y, ra.x, ra.y);
+    o.y = lev4_pack8(da.z, da.w, ra.z, ra.w);
+    o.z = lev4_pack8(db.x, db.y, rb.x, rb.y);
+    o.w = lev4_pack8(db.z, db.w, rb.z, rb.w);
+    *reinterpret_cast<PQH_G uint4*>(C.lev4 + 16 * g) = o;
+  }
+  // the slots outside whole groups (at most 31 at each end, or the whole tile if it is short)
+  const int64_t h0 = g0 < g1 ? 32 * g0 : e;  // [a, h0) and [h1, e)
+  const int64_t h1 = g0 < g1 ? 32 * g1 : e;
+  for (int64_t s = a + threadIdx.x; s < h0; s += kBlock) lev4_set(C.lev4, s, uint32_t(dp[s]) | (uint32_t(rp[s]) << 2));
+  for (int64_t s = h1 + threadIdx.x; s < e; s += kBlock) lev4_set(C.lev4, s, uint32_t(dp[s]) | (uint32_t(rp[s]) << 2));
+}
+
 __device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
@@ -946,6 +988,7 @@ __device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, Ti
     expand_hybrid(img, s == 0 ? S.rep_e : S.def_e, bits_len32(uint32_t(maxl)), c, t0, t1, L, stage, sink);
     __syncthreads();
   }
+  if (C.lev4) pack_levels(C, P.level_base + t0, P.level_base + t1);
 }
 
 template <bool LDS>

@@ -44,10 +44,27 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
   for (int l = 0; l < kMaxNest; l++) V[l] = 0;
   LV = 0;
   if (m <= 0) return;
-  // 32 level bytes of each stream (the level buffers carry 64 bytes of slack past n)
+  // 32 level bytes of each stream (the level buffers carry 64 bytes of slack past n), or their
+  // nibble copy (DevChunk.lev4: 16 bytes, spread back to bytes four slots per dword)
   uint32_t dw[8], rw[8];
-  __builtin_memcpy(dw, C.def_levels + s0, 32);
-  __builtin_memcpy(rw, C.rep_levels + s0, 32);
+  if (C.lev4) {
+    const uint4 q = *reinterpret_cast<const PQH_G uint4*>(C.lev4 + (s0 >> 1));  // (s0 % 32 == 0)
+    const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint32_t t = (xw[k] >> (16 * h)) & 0xffffu;
+        t = (t | (t << 8)) & 0x00ff00ffu;
+        t = (t | (t << 4)) & 0x0f0f0f0fu;
+        dw[2 * k + h] = t & 0x03030303u;
+        rw[2 * k + h] = (t >> 2) & 0x03030303u;
+      }
+    }
+  } else {
+    __builtin_memcpy(dw, C.def_levels + s0, 32);
+    __builtin_memcpy(rw, C.rep_levels + s0, 32);
+  }
   uint32_t hi = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) hi |= dw[k] | rw[k];

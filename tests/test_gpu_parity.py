@@ -584,10 +584,13 @@ def test_nesting_list_map(pq, ctx, v2):
     assert _check_nesting(pq, ctx, fixtures.nested_list_map(n=6000, v2=v2)) == 6
 
 
-@pytest.fixture(params=["one_pass", "three_passes"])
+@pytest.fixture(params=["one_pass", "three_passes", "three_passes_bytes"])
 def nest_passes(request, monkeypatch):
-    """The count / scan / write passes (default) and the one-pass write with look-back bases."""
-    monkeypatch.setenv("PQH_NEST_PASSES", "3" if request.param == "three_passes" else "1")
+    """The count / scan / write passes (default) and the one-pass write with look-back bases, both
+    reading the nibble copy of the levels (DevChunk.lev4) where max_rep, max_def <= 3; and the three
+    passes over the level bytes (PQH_LEV4=0)."""
+    monkeypatch.setenv("PQH_NEST_PASSES", "1" if request.param == "one_pass" else "3")
+    monkeypatch.setenv("PQH_LEV4", "0" if request.param == "three_passes_bytes" else "1")
     return request.param
 
 
