@@ -152,6 +152,8 @@ def pmc_traffic(kernel, workload, rows):
         lines = s.get("bench_lines") or []
         if not lines or lines[0]["config"]["workload"] != workload or lines[0]["config"]["rows_per_gpu"] != rows:
             continue
+        if s.get("variant"):  # an experiment's profile (a non-default switch), not this build's path
+            continue
         k = s["kernels"].get(kernel) or {}
         if k.get("hbm_traffic_bytes_per_launch"):
             return k["hbm_traffic_bytes_per_launch"], f"profiles/{tag}/pmc_summary.json"
