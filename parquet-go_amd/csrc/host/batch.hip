@@ -1091,21 +1091,29 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   const bool fuse = b->ba_fuse_on;
   const int32_t nbp = fuse ? b->ba_pages_nf : int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()),
                 nbc = fuse ? b->ba_chunks_nf : int32_t(b->ba_chunks.size());
-  // fused PLAIN chains: need only the prologue's page states; compute bound (chain resolution), so
-  // they run on a stream of their own beside everything after the prologue
+  // fused PLAIN chains: compute bound (chain resolution), so they run on a stream of their own
+  // beside the rest; launched after k_scan, whose page byte bases they use (PQH_FUSE_AT=prologue:
+  // right after the prologue, summing the bases from the page states themselves)
   const int32_t nfw = fuse ? int32_t(b->ba_wins.size()) - b->ba_wins_nf : 0;
+  const char* fat = getenv("PQH_FUSE_AT");
+  const bool fuse_early = fat && fat[0] == 'p';
   bool fuse_open = false;
-  if (e == hipSuccess && nfw) {
+  auto launch_fused = [&]() -> hipError_t {
+    hipError_t r = hipSuccess;
     hipStream_t fs = s;
     hipStream_t side2 = side ? b->ctx->side2 : nullptr;
     if (side2) {
-      e = dep(s, side2, 4);
+      r = dep(s, side2, 4);
       fs = side2;
       fuse_open = true;
     }
-    if (e == hipSuccess)
-      e = timed(29, nfw, fs, [&](hipStream_t st) { return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, b->d_ba_forder, nfw, st); });
-  }
+    if (r == hipSuccess)
+      r = timed(29, nfw, fs, [&](hipStream_t st) {
+        return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, b->d_ba_forder, nfw, fuse_early, st);
+      });
+    return r;
+  };
+  if (e == hipSuccess && nfw && fuse_early) e = launch_fused();
   bool chain_open = false;  // the chain branch has not rejoined the main stream yet
   if (e == hipSuccess && nbp) {
     hipStream_t cs = s;
@@ -1144,6 +1152,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   if (e == hipSuccess && ndp > ni)
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
+  if (e == hipSuccess && nfw && !fuse_early) e = launch_fused();
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });

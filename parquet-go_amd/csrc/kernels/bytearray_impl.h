@@ -1355,10 +1355,11 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
 //     else (a wrong guess, a chain that ended) waits for the predecessor's own FINAL instead;
 //   * a wrong guess of its own re-resolves the window from the true entry (LDS still holds the
 //     bytes); then it publishes FINAL and writes its offsets and strings straight from LDS.
-// Output bases need only the prologue's page states, so the kernel runs beside everything after
-// the prologue: a page whose chain is exactly notNull records filling its values section has
-// val_e - val_s - 4 * notNull string bytes, and its value / byte bases are the sums over the
-// chunk's pages before it (k_scan writes the same bases into the page states for the host).  The window holding record notNull
+// Output bases: a page whose chain is exactly notNull records filling its values section has
+// val_e - val_s - 4 * notNull string bytes; k_scan sums them into the pages' byte bases (and the
+// value bases), and the kernel is launched after it (own_bases: launched right after the prologue,
+// it sums the chunk's earlier pages itself -- measured 2% slower on C4: a second round of global
+// loads before each window's resolution).  The window holding record notNull
 // checks that record's end is val_e; a chain that ends early, runs on, fails, or a page that failed
 // earlier sets the batch's fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again
 // with the scratch path (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and
@@ -1433,7 +1434,8 @@ __device__ bool fuse_lookback(const DevBatch& b, int t, int w, int64_t val_s, in
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
+__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin,
+                                                   int own_bases) {
   __shared__ ChainLds C;
   __shared__ uint16_t recs[kChainRecs + 8];
   __shared__ BaWin R;
@@ -1470,7 +1472,12 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   const uint64_t q1 = wall_clock64();
 #endif
   const DevChunk D = b.chunks[P.chunk];
-  if (tid >= 64 && tid < 128) {
+  if (!own_bases) {  // k_scan's
+    if (tid == 64) {
+      sh[4] = S.value_base;
+      sh[5] = S.byte_base;
+    }
+  } else if (tid >= 64 && tid < 128) {
     // the page's value and byte bases from the prologue's page states (what k_scan computes; the
     // kernel runs beside it): notNull and string bytes of the chunk's pages before this one
     int64_t vb = 0, bb = 0;

@@ -1438,9 +1438,10 @@ hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const
   return hipGetLastError();
 }
 
-hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s) {
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, bool own_bases,
+                           hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n);
+  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n, int(own_bases));
   return hipGetLastError();
 }
 

@@ -68,7 +68,8 @@ hipError_t launch_gzip(const pqh_codec_page* pages, int32_t n, const uint8_t* sr
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // Fused PLAIN byte-array chains (bytearray_impl.h k_ba_chain): one workgroup per window of wins
 // (page-major), dispatched in `order`.
-hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s);
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, bool own_bases,
+                           hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
