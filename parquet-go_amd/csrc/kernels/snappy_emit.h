@@ -12,7 +12,7 @@ struct __attribute__((aligned(16))) SnEmitLds {
                               // 2^24 - 1: any larger one reaches before the unit) + length << 24
   int32_t l_out[kSnMaxL], l_src[kSnMaxL], l_len[kSnMaxL];  // literals of > 64 unit bytes
   int32_t wred[kSnT / 64];
-  int32_t nlong, bad, ext, cut, tmax, win;
+  int32_t nlong, nmed, bad, ext, cut, tmax, win;
 #ifdef PQH_SNAP_PROF  // timing experiments: clock64() per phase, printed for the first units
   uint64_t prof[12];
 #endif
@@ -402,16 +402,37 @@ __device__ bool sn_unit(SnEmitLds& L, const uint8_t* src, int32_t n, int32_t hl,
       *bad = true;
       return false;
     }
-    {  // short literals: one wave each, a lane per byte (stage bytes, or HBM past the stage)
+    {  // literals of up to kSnShortLit bytes: a thread each, byte by byte; longer ones (up to
+       // kSnLongLit) listed for the waves: a lane per byte, four literals per step (bytes from the
+       // stage, or HBM past it)
+      int32_t* med = reinterpret_cast<int32_t*>(L.ptr);  // (ptr is free until sn_copies)
+      if (tid == 0) L.nmed = 0;
+      __syncthreads();
+      for (int32_t li = tid; li < Lt; li += kSnT) {
+        const int32_t ln = lit_len[li];
+        if (ln == 0) continue;
+        if (ln > kSnShortLit) {
+          med[atomicAdd(&L.nmed, 1)] = li;
+          continue;
+        }
+        const int32_t lo2 = lit_out[li], ls = lit_src[li];
+        for (int32_t x = 0; x < ln; x++) {
+          const int32_t sx = ls + x;
+          L.out[lo2 + x] = sx < stage_hi ? L.in[sx - a0] : src[sx];
+        }
+      }
+      __syncthreads();
+      const int32_t nmed = L.nmed;
       const int lane = tid & 63;
-      for (int32_t e0 = 4 * (tid >> 6); e0 < Lt; e0 += 4 * (kSnT / 64)) {  // four literals per step
+      for (int32_t e0 = 4 * (tid >> 6); e0 < nmed; e0 += 4 * (kSnT / 64)) {  // four literals per step
         int32_t ln[4], lo2[4], ls[4], mx = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          const bool on = e0 + k < Lt;
-          ln[k] = on ? lit_len[e0 + k] : 0;
-          lo2[k] = on ? lit_out[e0 + k] : 0;
-          ls[k] = on ? lit_src[e0 + k] : 0;
+          const bool on = e0 + k < nmed;
+          const int32_t li = on ? med[e0 + k] : 0;
+          ln[k] = on ? lit_len[li] : 0;
+          lo2[k] = on ? lit_out[li] : 0;
+          ls[k] = on ? lit_src[li] : 0;
           mx = ln[k] > mx ? ln[k] : mx;
         }
         for (int32_t x = lane; x < mx; x += 64) {

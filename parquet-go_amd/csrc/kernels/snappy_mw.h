@@ -47,6 +47,7 @@ constexpr int kSnSub = kSnT / kBlock;        // walker segments per spec thread
 constexpr int kSnPer = kSnSpan / kSnT;       // span bytes per thread
 constexpr int kSnMaxC = kSnWin / 2 + 16;     // copies starting in one window (a copy is >= 2 bytes)
 constexpr int kSnLongLit = 1024;             // literals of more unit bytes are copied by the whole workgroup
+constexpr int kSnShortLit = 32;              // literals of at most this many unit bytes: a thread each
 constexpr int kSnMaxL = kSnWin / kSnLongLit + 4;  // (at most this many start in one window)
 constexpr int kSnSpecStage = kSnWin + kSnWarm0 + 64;
 constexpr int kSnSpecRounds = 12;            // a speculative window that needs more rounds (inside a long
