@@ -85,7 +85,7 @@ __device__ __forceinline__ bool chain_ok(const ChainLds& C, int32_t wb, int32_t 
   const uint32_t w0 = C.win[o >> 2], w1 = C.win[(o >> 2) + 1];
   len = int32_t(__builtin_amdgcn_alignbit(w1, w0, uint32_t(o & 3) * 8));
   next = p + 4 + len;
-  return avail >= 4 && uint32_t(len) <= uint32_t(avail - 4);
+  return (avail >= 4) & (uint32_t(len) <= uint32_t(avail - 4));  // (bitwise: no branch)
 }
 
 __device__ __forceinline__ int32_t seg_end(int j, int32_t wb, int32_t wend) {
@@ -183,11 +183,14 @@ __device__ __forceinline__ int32_t chain_guess(const ChainLds& C, int32_t wb, in
     const int32_t lo = s0 > base ? s0 - base : 0, hi = lim - base < 16 ? lim - base : 16;
     uint32_t cand = 0;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {  // (chain_ok's test; positions with fewer than 4 bytes left fail it)
+    for (int i = 0; i < 16; i++) {  // chain_ok's test, one compare per position (a position with
+                                    // fewer than 4 bytes left is masked below)
       const uint32_t len = __builtin_amdgcn_alignbit(w[(i >> 2) + 1], w[i >> 2], uint32_t(i & 3) * 8);
-      cand |= uint32_t(rel - i >= 4 && len <= uint32_t(rel - i - 4)) << i;
+      cand |= uint32_t(len <= uint32_t(rel - i - 4)) << i;
     }
-    cand &= ((1u << hi) - 1) & ~((1u << lo) - 1);  // (0 <= lo < hi <= 16)
+    const int32_t n4 = rel - 3;  // positions i < n4 have 4 bytes or more left
+    const uint32_t m4 = n4 >= 16 ? 0xffffu : (n4 <= 0 ? 0u : (1u << n4) - 1);
+    cand &= m4 & ((1u << hi) - 1) & ~((1u << lo) - 1);  // (0 <= lo < hi <= 16)
     for (; cand; cand &= cand - 1) {
       int32_t l;
       const int32_t p = base + __builtin_ctz(cand);
