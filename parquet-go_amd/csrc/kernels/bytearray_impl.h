@@ -1362,11 +1362,10 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
 // val_e - val_s - 4 * notNull string bytes; k_scan sums them into the pages' byte bases (and the
 // value bases), and the kernel is launched after it (own_bases: launched right after the prologue,
 // it sums the chunk's earlier pages itself -- measured 2% slower on C4: a second round of global
-// loads before each window's resolution).  The window holding record notNull
-// checks that record's end is val_e; a chain that ends early, runs on, fails, or a page that failed
-// earlier sets the batch's fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again
-// with the scratch path (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and
-// limits exactly.
+// loads before each window's resolution).  The window holding record notNull checks that record's
+// end is val_e; a chain that ends early, runs on, fails, or a page that failed earlier sets the
+// batch's fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again with the scratch
+// path (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and limits exactly.
 // Words: PARTIAL 01 | bad | count:13 | entry - B_w:16 | exit:32;  FINAL 10 | ended | incl:29 | exit:32.
 // ------------------------------------------------------------------------------------------------
 constexpr uint64_t kPartial = 1ull << 62, kFinal = 2ull << 62, kBadBit = 1ull << 61;
@@ -1381,7 +1380,7 @@ __device__ __forceinline__ uint64_t fuse_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0: window t (page window w >= 1, guessed entry g) -> records before it, the chain's position
+// Wave 0: window t (page window w >= 1) -> records before it, the chain's position
 // at its start, whether the chain ended before it.  False: no decisive look-back (the caller waits
 // for window t - 1's FINAL).
 __device__ bool fuse_lookback(const DevBatch& b, int t, int w, int64_t val_s, int64_t* pincl, int64_t* pexit,
