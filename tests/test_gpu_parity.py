@@ -708,7 +708,8 @@ def test_plain_chain_layouts(pq, ctx):
     assert compared == len(cases) and errors >= 10
 
 
-def test_fused_plain_chains(pq):
+@pytest.mark.parametrize("fuse_at", ["scan", "prologue"])
+def test_fused_plain_chains(pq, monkeypatch, fuse_at):
     """Chunks of PLAIN byte-array pages only take the fused k_ba_chain (one read of the page bytes,
     byte bases from the page sizes, look-back between windows): the layouts of
     test_plain_chain_layouts, several pages per chunk, in one batch that decodes without the scratch
@@ -718,6 +719,9 @@ def test_fused_plain_chains(pq):
     W = fixtures.W
     rng = np.random.default_rng(47)
     col = (W.BYTE_ARRAY, 0, 0, 0)
+    # launched after k_scan (its byte bases; the default) or right after the prologue, summing the
+    # page bases itself (PQH_FUSE_AT=prologue)
+    monkeypatch.setenv("PQH_FUSE_AT", fuse_at)
     ctx = pq.native.Context(0, profile=True)
 
     def strings(n, kind):
