@@ -80,8 +80,8 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
                               "k_ba_wcopy",   "k_gzip",      "k_snap_spec",  "k_snap_stitch",
-                              "k_snap_emit",  "k_snap_fixup", "k_ba_chain"};
-constexpr int kNumKernels = 30;
+                              "k_snap_emit",  "k_snap_fixup", "k_ba_chain",   "k_flat"};
+constexpr int kNumKernels = 31;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -370,6 +370,13 @@ struct pqh_batch {
   hipGraph_t graph = nullptr;        // unprofiled runs: the captured launch sequence
   hipGraphExec_t gexec = nullptr;
   bool graph_failed = false;
+  bool flat_on = false;   // the last run went through k_flat
+  bool flat_off = false;  // a k_flat speculation failed once: the three kernels from then on
+  int32_t flat_fallbacks = 0;
+  std::vector<int64_t> flat_base;   // k_flat: page value bases if every page is clean (num_values prefixes)
+  std::vector<int32_t> flat_jobs;   // k_flat: pages without a k == 0 tile (checked by a job of their own)
+  int64_t* d_flat_base = nullptr;
+  int32_t* d_flat_jobs = nullptr;
 };
 
 namespace {
@@ -828,6 +835,24 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       if (!fused) b->ba_sum_nf = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
     }
 
+  {  // k_flat's speculation tables (small; built for every batch, used when k_flat is eligible)
+    b->flat_base.assign(size_t(num_pages), 0);
+    std::vector<char> tile0(size_t(num_pages), 0);
+    for (const Tile& t : b->expand_tiles)
+      if (t.k == 0) tile0[size_t(t.page)] = 1;
+    for (int32_t c = 0; c < num_chunks; c++) {
+      const DevChunk& D = b->hchunks[size_t(c)];
+      int64_t acc = 0;
+      for (int32_t i = 0; i < D.num_pages; i++) {
+        const DevPage& P = b->hpages[size_t(D.first_page + i)];
+        b->flat_base[size_t(D.first_page + i)] = acc;
+        if (P.page_type != PQH_DICTIONARY_PAGE) acc += std::max(0, P.num_values);
+      }
+    }
+    for (int32_t p = 0; p < num_pages; p++)
+      if (!tile0[size_t(p)]) b->flat_jobs.push_back(p);
+  }
+
   // ---- device allocations ----
   int rc;
   const size_t ntiles = b->expand_tiles.size() + b->global_tiles.size();
@@ -856,7 +881,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dcum), sizeof(int32_t) * size_t(dcum_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums), sizeof(int64_t) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums2), sizeof(int64_t) * b->ba_tiles.size())) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bafuse), sizeof(uint32_t) * 4)) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bafuse), sizeof(uint32_t) * 8)) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_base), sizeof(int64_t) * size_t(num_pages))) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_jobs), sizeof(int32_t) * b->flat_jobs.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bawords), sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_forder), sizeof(int32_t) * b->ba_forder.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
@@ -993,12 +1020,15 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       {b->d_ba_forder, b->ba_forder.data(), sizeof(int32_t) * b->ba_forder.size()},
       {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
       {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
+      {b->d_flat_base, b->flat_base.data(), sizeof(int64_t) * size_t(num_pages)},
+      {b->d_flat_jobs, b->flat_jobs.data(), sizeof(int32_t) * b->flat_jobs.size()},
   };
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
   for (const Up& u : ups)
     if (e == hipSuccess && u.bytes) e = bounce_h2d(ctx, u.dst, u.src, u.bytes);
   if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
+  if (e == hipSuccess) e = hipMemsetAsync(b->d_bafuse, 0, sizeof(uint32_t) * 8, s);  // ([4]: k_flat's flag)
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   for (hipEvent_t& ev : b->ev_dep)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -1019,6 +1049,28 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
 namespace {
 
 // Enqueue every kernel of one decode of the batch on stream s (timed with HIP events when prof).
+// k_flat (one launch, no workgroup waiting for another; decode.hip): small batches of required
+// flat fixed-width columns whose data pages are dictionary, PLAIN fixed / INT96 or PLAIN boolean.
+// PQH_FLAT=0 disables it; a failed speculation disables it for the batch.
+constexpr size_t kFlatMaxPages = 1024, kFlatMaxTiles = 4096;
+
+bool flat_batch(const pqh_batch* b) {
+  const char* f = getenv("PQH_FLAT");
+  if ((f && f[0] == '0') || b->flat_off || b->codec_n || b->codec_gzip || b->ba_fuse_on) return false;
+  if (!b->delta_pages.empty() || !b->ba_pages.empty() || !b->ba_tiles.empty() || !b->nest_tiles.empty() ||
+      !b->global_tiles.empty())
+    return false;
+  if (b->pages.empty() || b->pages.size() > kFlatMaxPages || b->expand_tiles.size() > kFlatMaxTiles) return false;
+  if (!std::all_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& C) {
+        return C.max_rep == 0 && C.max_def == 0 && C.value_size > 0 && !C.lev4;
+      }))
+    return false;
+  return std::all_of(b->hpages.begin(), b->hpages.end(), [](const DevPage& P) {
+    return P.page_type == PQH_DICTIONARY_PAGE || P.kind == K_DICT || P.kind == K_PLAIN_FIXED ||
+           P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
+  });
+}
+
 hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
@@ -1057,6 +1109,12 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     return r == hipSuccess ? hipStreamWaitEvent(to, b->ev_dep[k], 0) : r;
   };
   const int32_t ndp = int32_t(b->delta_pages.size()), ndt = int32_t(b->delta_tiles.size());
+  b->flat_on = flat_batch(b);
+  if (b->flat_on)
+    return timed(30, int32_t(b->expand_tiles.size()), s, [&](hipStream_t st) {
+      return launch_flat(d, b->d_tiles, int32_t(b->expand_tiles.size()), b->d_flat_jobs, int32_t(b->flat_jobs.size()),
+                         b->d_flat_base, b->d_bafuse + 4, b->expand_lds, st);
+    });
   if (b->codec_n) {  // device codecs: the page images first
     if (snappy_page_mode()) {
       e = timed(22, b->codec_n, s, [&](hipStream_t st) {
@@ -1300,6 +1358,27 @@ int pqh_batch_sync(pqh_batch* b) {
   if (b->codec_n)
     HIP_TRY(ctx, bounce_d2h(ctx, b->codec_status.data(), b->d_codec_status, sizeof(int32_t) * size_t(b->codec_n)));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  // k_flat's speculation failed (a page not clean and simple, a key out of range): decode the batch
+  // again through the three kernels, and keep it there
+  if (b->flat_on) {
+    uint32_t flag = 0;
+    HIP_TRY(ctx, bounce_d2h(ctx, &flag, b->d_bafuse + 4, sizeof(uint32_t)));
+    if (flag) {
+      b->flat_on = false;
+      b->flat_off = true;
+      b->flat_fallbacks++;
+      HIP_TRY(ctx, hipMemsetAsync(b->d_bafuse + 4, 0, sizeof(uint32_t), ctx->stream));
+      if (b->gexec) hipGraphExecDestroy(b->gexec);
+      if (b->graph) hipGraphDestroy(b->graph);
+      b->gexec = nullptr;
+      b->graph = nullptr;
+      b->pending.clear();
+      b->event_next = 0;
+      int rc = pqh_batch_run(b);
+      if (rc != PQH_OK) return rc;
+      return pqh_batch_sync(b);
+    }
+  }
   // The per-page results bound every later copy of the outputs (pqh_batch_chunk_out): refuse
   // results that would reach past the planned output buffers instead of handing them out.
   for (size_t p = 0; p < b->pages.size(); p++) {
@@ -1482,6 +1561,11 @@ int pqh_batch_sync(pqh_batch* b) {
     if (N.lbase == 0) b->k_read[13] += 2.0 * double(N.n);  // (the algorithmic bytes read the levels once)
   }
   b->bytes_written = wr;
+  if (b->flat_on) {  // k_flat moved k_expand's bytes
+    b->k_read[30] += b->k_read[2];
+    b->k_written[30] += b->k_written[2];
+    b->k_read[2] = b->k_written[2] = 0;
+  }
   for (int k = 0; k < kNumKernels; k++) {
     b->stats[size_t(k)].bytes_read = b->k_read[size_t(k)];
     b->stats[size_t(k)].bytes_written = b->k_written[size_t(k)];

@@ -110,6 +110,8 @@ struct WalkOut {
 // Every wave of the page's workgroup walks the same headers (wave-uniform, L2-hot after the first);
 // the value counting inside bit-packed runs is split over the nwv waves (wave wv takes every nwv-th
 // 64-lane slice) and count is this wave's share; wave 0 alone writes the checkpoints.
+// kCount = false compiles the counting out (match must be -1): k_flat's walks, which count nothing.
+template <bool kCount = true>
 __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, int64_t e, int w, int64_t N, int phase, Ckpt* ck,
                                int match, int lane, int wv = 0, int nwv = 1) {
   WalkOut o{kNoError, 0, N};
@@ -186,7 +188,7 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
         next_ck++;
       }
     }
-    if (match >= 0) {
+    if (kCount && match >= 0) {
       const int64_t lim = (valid_end < N ? valid_end : N) - produced;
       if (!bp) {
         if (lane == 0 && wv == 0 && data == match) cnt_lane += lim;
@@ -278,13 +280,11 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
 // its four waves run the same (wave-uniform) framing and run walks and split the notNull count
 // over bit-packed definition levels.
 // ------------------------------------------------------------------------------------------------
-template <int kNwv>
-__global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
-  __shared__ int64_t s_nn[4];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6) % kNwv);
-  const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * (4 / kNwv) + int(threadIdx.x >> 6) / kNwv);
-  if (p >= b.num_pages) return;
+// kLevels = false (k_flat): the page's column has no level streams (a page that has one gets
+// PQH_ERR_INTERNAL, which k_flat's check turns into a decode by the three kernels).
+template <int kNwv, bool kLevels = true>
+__device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int lane, int wv, int64_t* s_nn,
+                                                   bool store = true) {
   const DevPage P = b.pages[p];
   const DevChunk C = b.chunks[P.chunk];
   const uint8_t* img = b.payload + P.image_off;
@@ -390,8 +390,11 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
     S.val_s = int32_t(hs);
     S.val_e = int32_t(he);
     // --- readValues(numValues) ---
+    if constexpr (!kLevels) {
+      if (rw > 0 || dw > 0) err = err_key(0, 0, PQH_ERR_INTERNAL);
+    }
     if (err == kNoError && n > 0) {
-      if (rw > 0) {  // decodePackedArray(rDecoder, n)
+      if (kLevels && rw > 0) {  // decodePackedArray(rDecoder, n)
         if (rep_s < 0) {
           err = err_key(1, 0, PQH_ERR_READER_NOT_INITIALIZED);
         } else {
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
         }
       }
       int64_t nn = n;
-      if (err == kNoError && dw > 0) {  // decodePackedArray(dDecoder, n) + notNull
+      if (kLevels && err == kNoError && dw > 0) {  // decodePackedArray(dDecoder, n) + notNull
         if (def_s < 0) {
           err = err_key(2, 0, PQH_ERR_READER_NOT_INITIALIZED);
         } else {
@@ -422,7 +425,8 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
           switch (P.kind) {
             case K_DICT:
             case K_RLE_BOOL: {
-              WalkOut r = walk_hybrid(img, hs, he, S.width, nn, 3, P.ck_val >= 0 ? b.ckpts + P.ck_val : nullptr, -1, lane, wv, kNwv);
+              WalkOut r = walk_hybrid<kLevels>(img, hs, he, S.width, nn, 3, P.ck_val >= 0 ? b.ckpts + P.ck_val : nullptr, -1,
+                                               lane, wv, kNwv);
               err = r.err;
               limit = r.fail_index;
               break;
@@ -472,7 +476,18 @@ __global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
     }
   }
   S.err = err;
-  if (lane == 0 && wv == 0) b.states[p] = S;
+  if (store && lane == 0 && wv == 0) b.states[p] = S;
+  return S;
+}
+
+template <int kNwv>
+__global__ __launch_bounds__(256) void k_prologue(DevBatch b) {
+  __shared__ int64_t s_nn[4];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6) % kNwv);
+  const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * (4 / kNwv) + int(threadIdx.x >> 6) / kNwv);
+  if (p >= b.num_pages) return;
+  prologue_page<kNwv>(b, p, lane, wv, s_nn);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -969,9 +984,17 @@ __device__ __forceinline__ void pack_levels(const DevChunk& C, int64_t a, int64_
   for (int64_t s = h1 + threadIdx.x; s < e; s += kBlock) lev4_set(C.lev4, s, uint32_t(dp[s]) | (uint32_t(rp[s]) << 2));
 }
 
-__device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
+// The tile bodies take the page's state (and checkpoints) from their caller: k_expand reads them
+// after k_prologue / k_scan, k_flat from the words its prologue jobs published.
+// Ckpt loader for a page's stream table at entry i.
+struct CkptPlain {
+  const Ckpt* ck;
+  __device__ __forceinline__ Ckpt operator()(int32_t i) const { return ck[i]; }
+};
+
+template <class CkLoad>
+__device__ __forceinline__ void tile_levels_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
+                                              const CkLoad& ckl, TileLds& L, uint32_t* stage) {
   if (page_failed_before_values(S)) return;
   const DevChunk C = b.chunks[P.chunk];
   const uint8_t* img = b.payload + P.image_off;
@@ -984,12 +1007,23 @@ __device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, Ti
     const int maxl = s == 0 ? C.max_rep : C.max_def;
     if (maxl <= 0) continue;
     LevelSink sink{(s == 0 ? C.rep_levels : C.def_levels) + P.level_base};
-    const Ckpt c = b.ckpts[(s == 0 ? P.ck_rep : P.ck_def) + t.k];
+    const Ckpt c = ckl((s == 0 ? P.ck_rep : P.ck_def) + t.k);
     expand_hybrid(img, s == 0 ? S.rep_e : S.def_e, bits_len32(uint32_t(maxl)), c, t0, t1, L, stage, sink);
     __syncthreads();
   }
   if (C.lev4) pack_levels(C, P.level_base + t0, P.level_base + t1);
 }
+
+__device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  tile_levels_s(b, t, P, S, CkptPlain{b.ckpts}, L, stage);
+}
+
+template <class CkLoad>
+__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
+                                            uint32_t K, const uint8_t* dict, const CkLoad& ckl, TileLds& L,
+                                            uint32_t* stage, uint32_t* bad_flag = nullptr);
 
 template <bool LDS>
 __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage,
@@ -1001,7 +1035,6 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
   int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
   if (t1 > S.val_limit) t1 = S.val_limit;
   if (t0 >= t1) return;
-  const DevChunk C = b.chunks[P.chunk];
   const int vs = P.value_size;
   uint32_t K = 0;
   const uint8_t* dict = nullptr;
@@ -1026,10 +1059,27 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
     // no barrier here: expand_hybrid passes one (run list or the unpack's first stage) before any
     // value is gathered
   }
+  tile_dict_s(b, t, P, S, K, dict, CkptPlain{b.ckpts}, L, stage);
+}
+
+// The gather itself: dictionary `dict` (LDS or global) of K entries.
+// bad_flag (k_flat): a key out of range sets it (the batch is decoded again by the three kernels)
+// instead of lowering the page's error key.
+template <class CkLoad>
+__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
+                                            uint32_t K, const uint8_t* dict, const CkLoad& ckl, TileLds& L,
+                                            uint32_t* stage, uint32_t* bad_flag) {
+  if (page_failed_before_values(S)) return;
+  const int64_t t0 = int64_t(t.k) * kHybridTile;
+  int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
+  if (t1 > S.val_limit) t1 = S.val_limit;
+  if (t0 >= t1) return;
+  const DevChunk C = b.chunks[P.chunk];
+  const int vs = P.value_size;
   const uint8_t* img = b.payload + P.image_off;
   int64_t first_bad = INT64_MAX;
   uint8_t* out = C.values + S.value_base * vs;
-  const Ckpt c = b.ckpts[P.ck_val + t.k];
+  const Ckpt c = ckl(P.ck_val + t.k);
   if (vs == 0) {
     KeySink sink{C.aux + S.value_base, K, &first_bad};
     expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
@@ -1043,13 +1093,15 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
     DictSink<0> sink{dict, out, K, vs, &first_bad};
     expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
   }
-  if (first_bad != INT64_MAX)
-    atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, PQH_ERR_DICT_INDEX));
+  if (first_bad != INT64_MAX) {
+    if (bad_flag) __hip_atomic_store(bad_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else atomicMin(&b.states[t.page].err, (unsigned long long)err_key(3, first_bad, PQH_ERR_DICT_INDEX));
+  }
 }
 
-__device__ __forceinline__ void tile_rle_bool(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
+template <class CkLoad>
+__device__ __forceinline__ void tile_rle_bool_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
+                                                const CkLoad& ckl, TileLds& L, uint32_t* stage) {
   if (page_failed_before_values(S)) return;
   const int64_t t0 = int64_t(t.k) * kHybridTile;
   int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
@@ -1057,14 +1109,18 @@ __device__ __forceinline__ void tile_rle_bool(const DevBatch& b, const Tile& t, 
   if (t0 >= t1) return;
   const DevChunk C = b.chunks[P.chunk];
   BoolSink sink{C.values + S.value_base};
-  expand_hybrid(b.payload + P.image_off, S.val_e, 1, b.ckpts[P.ck_val + t.k], t0, t1, L, stage, sink);
+  expand_hybrid(b.payload + P.image_off, S.val_e, 1, ckl(P.ck_val + t.k), t0, t1, L, stage, sink);
+}
+
+__device__ __forceinline__ void tile_rle_bool(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  tile_rle_bool_s(b, t, P, S, CkptPlain{b.ckpts}, L, stage);
 }
 
 // PLAIN fixed-width values (int32/int64/float/double/INT96/FLBA): little-endian copy of
 // notNull * size bytes (type_int32.go:21-31 ...), 16-byte vector loads and stores, 4 in flight.
-__device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
+__device__ __forceinline__ void tile_copy_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S) {
   if (page_failed_before_values(S)) return;
   const int64_t total = int64_t(S.val_limit) * P.value_size;
   const int64_t c0 = int64_t(t.k) * kCopyTileBytes;
@@ -1111,9 +1167,8 @@ __device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
 // booleanPlainDecoder (type_boolean.go:43-69): LSB-first bits -> 0/1 bytes.
 __device__ __forceinline__ uint32_t nibble_bytes(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
 
-__device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t) {
-  const DevPage P = b.pages[t.page];
-  const PageState S = b.states[t.page];
+__device__ __forceinline__ void tile_bool_plain_s(const DevBatch& b, const Tile& t, const DevPage& P,
+                                                  const PageState& S) {
   if (page_failed_before_values(S)) return;
   const int64_t lim = S.val_limit;
   const DevChunk C = b.chunks[P.chunk];
@@ -1137,6 +1192,18 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
       for (int64_t j = 0; v0 + j < lim; j++) dst[j] = (in[j >> 3] >> (j & 7)) & 1;
     }
   }
+}
+
+__device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  tile_copy_s(b, t, P, S);
+}
+
+__device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t) {
+  const DevPage P = b.pages[t.page];
+  const PageState S = b.states[t.page];
+  tile_bool_plain_s(b, t, P, S);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1173,6 +1240,161 @@ __global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* til
   __shared__ TileLds L;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   tile_dict<false>(b, tiles[blockIdx.x], L, reinterpret_cast<uint32_t*>(lds), nullptr);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_flat: a small batch of required flat fixed-width columns (dictionary, PLAIN fixed / INT96,
+// PLAIN booleans) in ONE launch, with no workgroup waiting for another.  Every tile assumes its page
+// is clean and simple -- the header the planner saw, the notNull count = num_values, a dictionary
+// stream that is one bit-packed run over all its values, enough bytes, no earlier page failing --
+// and decodes from that speculative state (flat_spec: k_prologue's result for such a page, read
+// from the page's first bytes) and the host's page value bases (prefix sums of num_values, k_scan's
+// result for such a chunk).  The tile at k == 0 of each page (and one job per page without tiles:
+// dictionary pages, empty pages) then runs k_prologue's body on the page, stores the state, and
+// checks it against the speculation.  Any difference -- or a dictionary key out of range -- sets
+// `flag`: pqh_batch_sync decodes the batch again through k_prologue / k_scan / k_expand (which give
+// the reference's errors and limits) and keeps the batch off k_flat from then on.
+// ------------------------------------------------------------------------------------------------
+// k_prologue's state for a clean, simple page (false: the page is not one; nothing is assumed).
+__device__ __forceinline__ bool flat_spec(const DevBatch& b, const DevPage& P, int64_t value_base, PageState& S,
+                                          Ckpt& ck) {
+  S.err = kNoError;
+  S.nn = 0;
+  S.width = 0;
+  S.ba_summed = 0;
+  S.rep_s = S.rep_e = S.def_s = S.def_e = -1;
+  S.dict_n = 0;
+  S.value_base = value_base;
+  S.byte_base = 0;
+  ck = Ckpt{0, 0x7fffffff, 0, 0};
+  if (P.host_err != kNoError) return false;
+  const int64_t L = P.image_len, n = P.num_values;
+  if (P.page_type == PQH_DICTIONARY_PAGE) {  // dictPageReader: num_values PLAIN entries
+    if (P.value_size <= 0 || int64_t(P.value_size) * n > L) return false;
+    S.rep_s = S.rep_e = S.def_s = S.def_e = -1;
+    S.dict_n = int32_t(n);
+    S.val_s = S.val_e = 0;
+    S.val_limit = 0;
+    return true;
+  }
+  const int64_t vs = P.page_type == PQH_DATA_PAGE ? 0 : int64_t(P.rep_len) + P.def_len;  // (no level streams)
+  S.val_s = int32_t(vs);
+  S.val_e = int32_t(L);
+  S.val_limit = 0;
+  if (P.kind == K_DICT) {
+    if (vs >= L) return false;
+    const uint8_t* img = b.payload + P.image_off;
+    const uint64_t q0 = ld64_masked(img + vs, img + L);  // the width and up to 5 header bytes
+    const int w = int(q0 & 0xff);
+    if (w > 32) return false;
+    S.width = int16_t(w);
+    S.val_s = int32_t(vs + 1);
+    if (n <= 0) return true;
+    S.nn = int32_t(n);
+    S.val_limit = int32_t(n);
+    if (w == 0) return true;  // no reads: ck = {0, 2^31-1, 0, 0}, as walk_hybrid's
+    // the first run header (at most 5 bytes for a count < 2^31), then one bit-packed run over all n
+    uint64_t h = 0;
+    int len = 0;
+    for (int k = 0; k < 5; k++) {
+      const uint32_t c = uint32_t(q0 >> (8 * (k + 1))) & 0xff;
+      h |= uint64_t(c & 0x7f) << (7 * k);
+      if (c < 0x80) {
+        len = k + 1;
+        break;
+      }
+    }
+    if (len == 0 || vs + 1 + len > L || h > 0x7fffffffull || !(h & 1)) return false;
+    const int64_t groups = int64_t(h >> 1), data = vs + 1 + len;
+    if (groups * 8 < n) return false;
+    const int64_t gf = (L - data + w - 1) / w;  // groups readable before EOF
+    if (data >= L || gf < (n + 7) / 8) return false;
+    const int64_t next = data + groups * w, cnt = groups * 8;
+    ck = Ckpt{0, int32_t(cnt < 0x7fffffff ? cnt : 0x7fffffff), int32_t(data),
+              int32_t(next < 0x7fffffff ? next : 0x7fffffff) | int32_t(0x80000000u)};
+    return true;
+  }
+  if (n <= 0) return P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
+  const int64_t avail = L - vs;
+  if (P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96) {
+    if (P.value_size <= 0 || avail / P.value_size < n) return false;
+  } else if (P.kind == K_PLAIN_BOOL) {
+    if (avail * 8 < n) return false;
+  } else {
+    return false;
+  }
+  S.nn = int32_t(n);
+  S.val_limit = int32_t(n);
+  return true;
+}
+
+struct CkptConst {
+  Ckpt c;
+  __device__ __forceinline__ Ckpt operator()(int32_t) const { return c; }
+};
+
+// One wave: k_prologue's body on page p, its state stored with the page's value base, and the
+// speculation checked (flag on any difference).
+__device__ __forceinline__ void flat_check(const DevBatch& b, int32_t p, const int64_t* spec_base, uint32_t* flag) {
+  const int lane = threadIdx.x & 63;
+  const DevPage P = b.pages[p];
+  const int64_t vb = spec_base[p];
+  PageState spec;
+  Ckpt ck;
+  const bool ok = flat_spec(b, P, vb, spec, ck);
+  PageState S = prologue_page<1, false>(b, p, lane, 0, nullptr, false);
+  S.value_base = vb;
+  if (lane == 0) {
+    b.states[p] = S;
+    const bool same = ok && S.err == spec.err && S.nn == spec.nn && S.width == spec.width && S.rep_s == spec.rep_s &&
+                      S.rep_e == spec.rep_e && S.def_s == spec.def_s && S.def_e == spec.def_e &&
+                      S.val_s == spec.val_s && S.val_e == spec.val_e && S.val_limit == spec.val_limit &&
+                      S.dict_n == spec.dict_n;
+    if (!same) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// blocks [0, ntiles): k_expand's tiles; [ntiles, ntiles + njobs): the pages without tiles
+__global__ __launch_bounds__(256) void k_flat(DevBatch b, const Tile* tiles, int32_t ntiles, const int32_t* jobs,
+                                              const int64_t* spec_base, uint32_t* flag) {
+  __shared__ TileLds L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // as k_expand
+  uint32_t* stage = reinterpret_cast<uint32_t*>(lds);
+  uint8_t* dict_lds = lds + kStageBytes + 16;
+  if (int32_t(blockIdx.x) >= ntiles) {
+    if (threadIdx.x < 64) flat_check(b, jobs[blockIdx.x - ntiles], spec_base, flag);
+    return;
+  }
+  const Tile t = tiles[blockIdx.x];
+  const DevPage P = b.pages[t.page];
+  uint32_t K = 0;  // the dictionary as its header declares it
+  if (t.kind == TK_DICT && P.dict_page >= 0) {
+    const DevPage D = b.pages[P.dict_page];
+    const int64_t bytes = int64_t(D.num_values) * P.value_size;
+    if (D.host_err == kNoError && bytes <= int64_t(D.image_len)) {
+      K = uint32_t(D.num_values);
+      const uint8_t* dict = b.payload + D.image_off;
+      const int64_t words = (bytes + 3) >> 2;
+      for (int64_t i = threadIdx.x; i < words; i += kBlock) {
+        uint32_t x = 0;
+        const int64_t o = i * 4;
+        if (o + 4 <= bytes) __builtin_memcpy(&x, dict + o, 4);
+        else for (int k = 0; o + k < bytes; k++) x |= uint32_t(dict[o + k]) << (8 * k);
+        reinterpret_cast<uint32_t*>(dict_lds)[i] = x;
+      }
+    }
+  }
+  PageState S;
+  Ckpt ck;
+  if (flat_spec(b, P, spec_base[t.page], S, ck)) {  // (otherwise flat_check flags the page)
+    switch (t.kind) {
+      case TK_COPY: tile_copy_s(b, t, P, S); break;
+      case TK_BOOL: tile_bool_plain_s(b, t, P, S); break;
+      case TK_DICT: tile_dict_s(b, t, P, S, K, dict_lds, CkptConst{ck}, L, stage, flag); break;
+      default: break;
+    }
+  }
+  if (t.k == 0 && threadIdx.x < 64) flat_check(b, t.page, spec_base, flag);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1248,6 +1470,14 @@ hipError_t launch_scan(const DevBatch& b, hipStream_t s) {
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_expand, dim3(n), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_flat(const DevBatch& b, const Tile* tiles, int32_t ntiles, const int32_t* jobs, int32_t njobs,
+                       const int64_t* spec_base, uint32_t* flag, size_t lds_bytes, hipStream_t s) {
+  if (ntiles + njobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_flat, dim3(ntiles + njobs), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles, ntiles,
+                     jobs, spec_base, flag);
   return hipGetLastError();
 }
 

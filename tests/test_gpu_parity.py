@@ -164,8 +164,11 @@ def _mutate(rng, img):
 
 
 def _fuzz(pq, ctx, data, seed, per_page=3):
+    return _run_cases(pq, ctx, _fuzz_cases(pq, data, seed, per_page))
+
+
+def _fuzz_cases(pq, data, seed, per_page=3):
     rng = np.random.default_rng(seed)
-    N = pq.native
     cases = []
     for (path, pt, tl, md, mr), dict_img, dpages in _page_sets(pq, data):
         col = (pt, tl, md, mr)
@@ -176,13 +179,14 @@ def _fuzz(pq, ctx, data, seed, per_page=3):
                 if ptype == O.DATA_PAGE_V2 and rl + dl > len(img2):
                     continue  # the host walker rejects such headers before the device sees them
                 cases.append((col, dict_img, (ptype, nv, enc, dl, rl, img2)))
-    return _run_cases(pq, ctx, cases)
+    return cases
 
 
-def _run_cases(pq, ctx, cases, stats=None):
+def _run_cases(pq, ctx, cases, stats=None, runs=1):
     """Decode `cases` = [(column, dictionary (num_values, encoding, image) or None, data page)] in ONE
     batch (every case its own chunk) and compare each against the oracle's decode_page.  stats: a
-    dict that gets the batch's kernel launch counts by name (profiled contexts)."""
+    dict that gets the batch's kernel launch counts by name (profiled contexts).  runs: decodes of
+    the batch before its one sync (each must leave the batch's device counters as it found them)."""
     N = pq.native
     # every case is its own chunk (dictionary page first when present)
     blobs, chunks, pages = [], [], []
@@ -210,7 +214,8 @@ def _run_cases(pq, ctx, cases, stats=None):
         ctx.h2d(d, arr.ctypes.data, len(arr))
         ctx.sync()
         b = N.Batch.from_tables(ctx, chunks, pages, d, off)
-        b.run()
+        for _ in range(runs):
+            b.run()
         b.sync()
         compared = errors = 0
         for i, (col, dict_img, (ptype, nv, enc, dl, rl, img)) in enumerate(cases):
@@ -259,6 +264,72 @@ def test_fuzz_pyarrow_pages(pq, ctx, seed):
 def test_fuzz_nested_pages(pq, ctx):
     compared, errors = _fuzz(pq, ctx, fixtures.nested_list_map(n=1500), 6)
     assert compared > 5
+
+
+def _required_flat(n, v2, seed=21):
+    """Required flat fixed-width columns of every kind k_flat takes (dictionary, PLAIN, INT96, FLBA,
+    PLAIN booleans), reference-writer pages."""
+    W = fixtures.W
+    rng = np.random.default_rng(seed)
+    cols = [("i32_dict", W.Column(W.INT32, rng.integers(-2**31, 2**31 - 1, 4096).astype(np.int32)[rng.integers(0, 4096, n)]), W.REQUIRED),
+            ("i64", W.Column(W.INT64, rng.integers(-2**62, 2**62, n), use_dict=False), W.REQUIRED),
+            ("f32_dict", W.Column(W.FLOAT, rng.standard_normal(7).astype(np.float32)[rng.integers(0, 7, n)]), W.REQUIRED),
+            ("bool", W.Column(W.BOOLEAN, (rng.random(n) < 0.5).astype(np.uint8)), W.REQUIRED),
+            ("flba", W.Column(W.FIXED_LEN_BYTE_ARRAY, rng.integers(0, 256, (n, 16), dtype=np.uint8), type_length=16,
+                              use_dict=False), W.REQUIRED),
+            ("i96_dict", W.Column(W.INT96, rng.integers(0, 256, (40, 12), dtype=np.uint8)[rng.integers(0, 40, n)]),
+             W.REQUIRED),
+            ("d_const", W.Column(W.DOUBLE, np.full(n, 2.5)), W.REQUIRED)]  # one-entry dictionary: width 0
+    return W.flat(cols, n // 2, v2=v2, max_page_size=48 * 1024)
+
+
+@pytest.mark.parametrize("flat", ["one_launch", "three_kernels"])
+def test_flat_one_launch(pq, monkeypatch, flat):
+    """Small batches of required flat fixed-width columns decode in ONE launch, k_flat: every tile
+    decodes from its page's speculative state (clean page, one bit-packed run, enough bytes) and the
+    host's value bases, and the page checks (k_prologue's body) compare; with PQH_FLAT=0 through
+    k_prologue / k_scan / k_expand.  Clean pages stay on k_flat; the mutation fuzzer's pages (errors,
+    limits, failed dictionaries, keys out of range) and pyarrow-style streams (many runs) fail the
+    speculation, and the batch is decoded again by the three kernels: the reference's results
+    either way.  Each batch is run three times before its sync."""
+    W = fixtures.W
+    monkeypatch.setenv("PQH_FLAT", "1" if flat == "one_launch" else "0")
+    ctx = pq.native.Context(0, profile=True)
+    for v2 in (False, True):
+        data = _required_flat(60000, v2)
+        checked, _ = _run_file(pq, ctx, data)
+        assert checked == 2 * 7
+        # the same pages as explicit cases (each its own chunk): clean, then with mutants among them
+        clean = _page_sets_cases(pq, data)
+        stats = {}
+        compared, errors = _run_cases(pq, ctx, clean, stats, runs=3)
+        assert compared == len(clean) and errors == 0
+        want = {"k_flat": 3, "k_expand": 0} if flat == "one_launch" else {"k_flat": 0, "k_expand": 3}
+        assert {k: stats.get(k, 0) for k in want} == want, stats
+        mutants = _fuzz_cases(pq, data, 13 + v2, per_page=2)
+        stats = {}
+        compared, errors = _run_cases(pq, ctx, clean[:20] + mutants[:200] + clean[20:], stats, runs=3)
+        assert compared == len(clean) + min(len(mutants), 200) and errors > 10, (compared, errors)
+        # (k_flat's runs are dropped with its speculation; the rerun is the three kernels')
+        assert stats.get("k_expand", 0) == (1 if flat == "one_launch" else 3), stats
+    # the fixture's required fixed-width pages (V1 / V2), mutated
+    for seed, v2 in ((11, False), (12, True)):
+        data = fixtures.flat_all_types(n=3000, v2=v2, page=8 * 1024, rows_per_group=3000)
+        skip = (W.DELTA_BINARY_PACKED, W.DELTA_LENGTH_BYTE_ARRAY, W.DELTA_BYTE_ARRAY)
+        cases = [c for c in _fuzz_cases(pq, data, seed, per_page=6)
+                 if c[0][0] != W.BYTE_ARRAY and c[0][2] == 0 and c[2][2] not in skip]
+        compared, errors = _run_cases(pq, ctx, cases[:300], runs=3)
+        assert compared == min(len(cases), 300) and compared > 100 and errors > 20, (compared, errors)
+    ctx.close()
+
+
+def _page_sets_cases(pq, data):
+    """Every data page of `data` as an unmutated case."""
+    out = []
+    for (path, pt, tl, md, mr), dict_img, dpages in _page_sets(pq, data):
+        for pg in dpages:
+            out.append(((pt, tl, md, mr), dict_img, pg))
+    return out
 
 
 # ---------------------------------------------------------------------------------------------
