@@ -374,9 +374,9 @@ struct pqh_batch {
   bool flat_off = false;  // a k_flat speculation failed once: the three kernels from then on
   int32_t flat_fallbacks = 0;
   std::vector<int64_t> flat_base;   // k_flat: page value bases if every page is clean (num_values prefixes)
-  std::vector<int32_t> flat_jobs;   // k_flat: pages without a k == 0 tile (checked by a job of their own)
+  std::vector<FlatTile> flat_tiles; // k_flat: expand_tiles with their pages' fields
   int64_t* d_flat_base = nullptr;
-  int32_t* d_flat_jobs = nullptr;
+  FlatTile* d_flat_tiles = nullptr;
 };
 
 namespace {
@@ -835,11 +835,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       if (!fused) b->ba_sum_nf = int32_t(b->ba_xlist.size()) - b->ba_sum_off;
     }
 
-  {  // k_flat's speculation tables (small; built for every batch, used when k_flat is eligible)
+  {  // k_flat's speculative value bases (built for every batch, used when k_flat is eligible)
     b->flat_base.assign(size_t(num_pages), 0);
-    std::vector<char> tile0(size_t(num_pages), 0);
-    for (const Tile& t : b->expand_tiles)
-      if (t.k == 0) tile0[size_t(t.page)] = 1;
     for (int32_t c = 0; c < num_chunks; c++) {
       const DevChunk& D = b->hchunks[size_t(c)];
       int64_t acc = 0;
@@ -849,8 +846,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
         if (P.page_type != PQH_DICTIONARY_PAGE) acc += std::max(0, P.num_values);
       }
     }
-    for (int32_t p = 0; p < num_pages; p++)
-      if (!tile0[size_t(p)]) b->flat_jobs.push_back(p);
   }
 
   // ---- device allocations ----
@@ -883,7 +878,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_basums2), sizeof(int64_t) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bafuse), sizeof(uint32_t) * 8)) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_base), sizeof(int64_t) * size_t(num_pages))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_jobs), sizeof(int32_t) * b->flat_jobs.size())) ||
+      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_tiles), sizeof(FlatTile) * b->expand_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bawords), sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_forder), sizeof(int32_t) * b->ba_forder.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
@@ -997,6 +992,33 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   }
   std::vector<Tile> all(b->expand_tiles);
   all.insert(all.end(), b->global_tiles.begin(), b->global_tiles.end());
+  for (const Tile& t : b->expand_tiles) {  // k_flat's records (the chunks' value buffers are known now)
+    const DevPage& P = b->hpages[size_t(t.page)];
+    FlatTile f;
+    memset(&f, 0, sizeof(f));
+    f.image_off = P.image_off;
+    f.dict_off = -1;
+    if (P.dict_page >= 0) {
+      const DevPage& D = b->hpages[size_t(P.dict_page)];
+      if (D.host_err == kNoError) f.dict_off = D.image_off;
+      f.dict_n = D.num_values;
+      f.dict_len = D.image_len;
+    }
+    f.value_base = b->flat_base[size_t(t.page)];
+    f.values = b->hchunks[size_t(P.chunk)].values;
+    f.image_len = P.image_len;
+    f.num_values = P.num_values;
+    f.page_type = P.page_type;
+    f.kind = P.kind;
+    f.value_size = P.value_size;
+    f.rep_len = P.rep_len;
+    f.def_len = P.def_len;
+    f.k = t.k;
+    f.span = t.span;
+    f.tkind = t.kind;
+    f.host_err = P.host_err;
+    b->flat_tiles.push_back(f);
+  }
   // page mode: the (shorter) stream list takes the delta tile list's place
   const std::vector<Tile>& dl = b->delta_page_mode ? b->delta_streams : b->delta_tiles;
   struct Up {
@@ -1021,7 +1043,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
       {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
       {b->d_flat_base, b->flat_base.data(), sizeof(int64_t) * size_t(num_pages)},
-      {b->d_flat_jobs, b->flat_jobs.data(), sizeof(int32_t) * b->flat_jobs.size()},
+      {b->d_flat_tiles, b->flat_tiles.data(), sizeof(FlatTile) * b->flat_tiles.size()},
   };
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
@@ -1112,8 +1134,8 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   b->flat_on = flat_batch(b);
   if (b->flat_on)
     return timed(30, int32_t(b->expand_tiles.size()), s, [&](hipStream_t st) {
-      return launch_flat(d, b->d_tiles, int32_t(b->expand_tiles.size()), b->d_flat_jobs, int32_t(b->flat_jobs.size()),
-                         b->d_flat_base, b->d_bafuse + 4, b->expand_lds, st);
+      return launch_flat(d, b->d_flat_tiles, int32_t(b->flat_tiles.size()), b->d_flat_base, b->d_bafuse + 4,
+                         b->expand_lds, st);
     });
   if (b->codec_n) {  // device codecs: the page images first
     if (snappy_page_mode()) {

@@ -232,6 +232,19 @@ struct Tile {
   int32_t span;
 };
 
+// k_flat's tile: the tile and its page's fields, so that loading it is the tile's last dependent
+// load before the page bytes.
+struct FlatTile {
+  int64_t image_off;       // the page image in the payload
+  int64_t dict_off;        // its dictionary page's image, -1 if none (or the header failed)
+  int64_t value_base;      // speculative: num_values of the chunk's earlier data pages
+  PQH_G uint8_t* values;   // the chunk's values
+  int32_t image_len, num_values, page_type, kind;
+  int32_t value_size, rep_len, def_len, dict_n;  // dict_n: the dictionary page's num_values
+  int32_t dict_len, k, span, tkind;
+  uint64_t host_err;
+};
+
 constexpr int kLevelSpan = 4;  // 32768 level slots per tile
 #ifndef PQH_DICT_SPAN
 #define PQH_DICT_SPAN 2

@@ -1021,9 +1021,37 @@ __device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, Ti
 }
 
 template <class CkLoad>
-__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
-                                            uint32_t K, const uint8_t* dict, const CkLoad& ckl, TileLds& L,
-                                            uint32_t* stage, uint32_t* bad_flag = nullptr);
+__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const DevChunk& C,
+                                            const PageState& S, uint32_t K, const uint8_t* dict, const CkLoad& ckl,
+                                            TileLds& L, uint32_t* stage, uint32_t* bad_flag = nullptr);
+
+// A dictionary page's `bytes` value bytes (any alignment) into LDS (16-aligned): 16-byte loads, four
+// per thread in flight, the tail by dwords.  No barrier: the unpack passes one before any gather.
+__device__ __forceinline__ void stage_dict(uint8_t* lds_dst, const uint8_t* src_, int64_t bytes) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  const PQH_G uint8_t* src = (const PQH_G uint8_t*)(src_);
+  const int64_t nv = bytes >> 4;
+  for (int64_t base = 0; base < nv; base += 4 * kBlock) {
+    u32x4 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int64_t k = base + threadIdx.x + j * kBlock;
+      x[j] = *reinterpret_cast<const PQH_G u32x4_u*>(src + 16 * (k < nv ? k : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int64_t k = base + threadIdx.x + j * kBlock;
+      if (k < nv) *reinterpret_cast<u32x4*>(lds_dst + 16 * k) = x[j];
+    }
+  }
+  for (int64_t o = 16 * nv + 4 * int64_t(threadIdx.x); o < bytes; o += 4 * kBlock) {
+    uint32_t x = 0;
+    if (o + 4 <= bytes) __builtin_memcpy(&x, src_ + o, 4);
+    else for (int k = 0; o + k < bytes; k++) x |= uint32_t(src_[o + k]) << (8 * k);
+    *reinterpret_cast<uint32_t*>(lds_dst + o) = x;
+  }
+}
 
 template <bool LDS>
 __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage,
@@ -1046,35 +1074,27 @@ __device__ __forceinline__ void tile_dict(const DevBatch& b, const Tile& t, Tile
     }
   }
   if constexpr (LDS) {  // stage the dictionary page's values in LDS (kDictLdsMax bytes at most)
-    const int64_t bytes = int64_t(K) * vs;
-    const int64_t words = (bytes + 3) >> 2;
-    for (int64_t i = threadIdx.x; i < words; i += kBlock) {
-      uint32_t x = 0;
-      const int64_t o = i * 4;
-      if (o + 4 <= bytes) __builtin_memcpy(&x, dict + o, 4);
-      else for (int k = 0; o + k < bytes; k++) x |= uint32_t(dict[o + k]) << (8 * k);
-      reinterpret_cast<uint32_t*>(dict_lds)[i] = x;
-    }
+    stage_dict(dict_lds, dict, int64_t(K) * vs);
     dict = dict_lds;
     // no barrier here: expand_hybrid passes one (run list or the unpack's first stage) before any
     // value is gathered
   }
-  tile_dict_s(b, t, P, S, K, dict, CkptPlain{b.ckpts}, L, stage);
+  const DevChunk C = b.chunks[P.chunk];
+  tile_dict_s(b, t, P, C, S, K, dict, CkptPlain{b.ckpts}, L, stage);
 }
 
 // The gather itself: dictionary `dict` (LDS or global) of K entries.
 // bad_flag (k_flat): a key out of range sets it (the batch is decoded again by the three kernels)
 // instead of lowering the page's error key.
 template <class CkLoad>
-__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S,
-                                            uint32_t K, const uint8_t* dict, const CkLoad& ckl, TileLds& L,
-                                            uint32_t* stage, uint32_t* bad_flag) {
+__device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, const DevPage& P, const DevChunk& C,
+                                            const PageState& S, uint32_t K, const uint8_t* dict, const CkLoad& ckl,
+                                            TileLds& L, uint32_t* stage, uint32_t* bad_flag) {
   if (page_failed_before_values(S)) return;
   const int64_t t0 = int64_t(t.k) * kHybridTile;
   int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
   if (t1 > S.val_limit) t1 = S.val_limit;
   if (t0 >= t1) return;
-  const DevChunk C = b.chunks[P.chunk];
   const int vs = P.value_size;
   const uint8_t* img = b.payload + P.image_off;
   int64_t first_bad = INT64_MAX;
@@ -1120,14 +1140,14 @@ __device__ __forceinline__ void tile_rle_bool(const DevBatch& b, const Tile& t, 
 
 // PLAIN fixed-width values (int32/int64/float/double/INT96/FLBA): little-endian copy of
 // notNull * size bytes (type_int32.go:21-31 ...), 16-byte vector loads and stores, 4 in flight.
-__device__ __forceinline__ void tile_copy_s(const DevBatch& b, const Tile& t, const DevPage& P, const PageState& S) {
+__device__ __forceinline__ void tile_copy_s(const DevBatch& b, const Tile& t, const DevPage& P, const DevChunk& C,
+                                            const PageState& S) {
   if (page_failed_before_values(S)) return;
   const int64_t total = int64_t(S.val_limit) * P.value_size;
   const int64_t c0 = int64_t(t.k) * kCopyTileBytes;
   int64_t c1 = c0 + kCopyTileBytes;
   if (c1 > total) c1 = total;
   if (c0 >= c1) return;
-  const DevChunk C = b.chunks[P.chunk];
   const PQH_G uint8_t* src = b.payload + P.image_off + S.val_s;
   PQH_G uint8_t* dst = C.values + S.value_base * P.value_size;
   int64_t o = c0 + 16 * int64_t(threadIdx.x);
@@ -1168,10 +1188,9 @@ __device__ __forceinline__ void tile_copy_s(const DevBatch& b, const Tile& t, co
 __device__ __forceinline__ uint32_t nibble_bytes(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
 
 __device__ __forceinline__ void tile_bool_plain_s(const DevBatch& b, const Tile& t, const DevPage& P,
-                                                  const PageState& S) {
+                                                  const DevChunk& C, const PageState& S) {
   if (page_failed_before_values(S)) return;
   const int64_t lim = S.val_limit;
-  const DevChunk C = b.chunks[P.chunk];
   for (int q = 0; q < 2; q++) {
     const int64_t v0 = int64_t(t.k) * kBoolTile + int64_t(q) * (kBoolTile / 2) + int64_t(threadIdx.x) * 64;
     if (v0 >= lim) return;
@@ -1197,13 +1216,17 @@ __device__ __forceinline__ void tile_bool_plain_s(const DevBatch& b, const Tile&
 __device__ __forceinline__ void tile_copy(const DevBatch& b, const Tile& t) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
-  tile_copy_s(b, t, P, S);
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  tile_copy_s(b, t, P, C, S);
 }
 
 __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t) {
   const DevPage P = b.pages[t.page];
   const PageState S = b.states[t.page];
-  tile_bool_plain_s(b, t, P, S);
+  if (page_failed_before_values(S)) return;
+  const DevChunk C = b.chunks[P.chunk];
+  tile_bool_plain_s(b, t, P, C, S);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1249,9 +1272,9 @@ __global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* til
 // stream that is one bit-packed run over all its values, enough bytes, no earlier page failing --
 // and decodes from that speculative state (flat_spec: k_prologue's result for such a page, read
 // from the page's first bytes) and the host's page value bases (prefix sums of num_values, k_scan's
-// result for such a chunk).  The tile at k == 0 of each page (and one job per page without tiles:
-// dictionary pages, empty pages) then runs k_prologue's body on the page, stores the state, and
-// checks it against the speculation.  Any difference -- or a dictionary key out of range -- sets
+// result for such a chunk), all carried by its FlatTile record.  Beside the tiles, one wave per page
+// (the launch's first workgroups) runs k_prologue's body on the page, stores the state, and checks
+// it against the speculation.  Any difference -- or a dictionary key out of range -- sets
 // `flag`: pqh_batch_sync decodes the batch again through k_prologue / k_scan / k_expand (which give
 // the reference's errors and limits) and keeps the batch off k_flat from then on.
 // ------------------------------------------------------------------------------------------------
@@ -1354,47 +1377,72 @@ __device__ __forceinline__ void flat_check(const DevBatch& b, int32_t p, const i
   }
 }
 
-// blocks [0, ntiles): k_expand's tiles; [ntiles, ntiles + njobs): the pages without tiles
-__global__ __launch_bounds__(256) void k_flat(DevBatch b, const Tile* tiles, int32_t ntiles, const int32_t* jobs,
+// blocks [0, njob): the page checks, four pages each (one wave per page); [njob, njob + ntiles):
+// k_expand's tiles, from their FlatTile records
+__global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles, int32_t ntiles, int32_t njob,
                                               const int64_t* spec_base, uint32_t* flag) {
   __shared__ TileLds L;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // as k_expand
   uint32_t* stage = reinterpret_cast<uint32_t*>(lds);
   uint8_t* dict_lds = lds + kStageBytes + 16;
-  if (int32_t(blockIdx.x) >= ntiles) {
-    if (threadIdx.x < 64) flat_check(b, jobs[blockIdx.x - ntiles], spec_base, flag);
+#ifdef PQH_FLAT_PROF  // experiments: clocks of the jobs and every 31st tile
+  const uint64_t q0 = wall_clock64();
+#endif
+  if (int32_t(blockIdx.x) < njob) {
+    const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
+    if (p < b.num_pages) flat_check(b, p, spec_base, flag);
+#ifdef PQH_FLAT_PROF
+    if (threadIdx.x == 0)
+      printf("flatj %d t0 %llu end %llu\n", int(blockIdx.x), (unsigned long long)q0, (unsigned long long)(wall_clock64() - q0));
+#endif
     return;
   }
-  const Tile t = tiles[blockIdx.x];
-  const DevPage P = b.pages[t.page];
+  const FlatTile f = tiles[blockIdx.x - njob];
+  DevPage P;  // the fields the tile bodies and flat_spec read
+  __builtin_memset(&P, 0, sizeof(P));
+  P.image_off = f.image_off;
+  P.image_len = f.image_len;
+  P.page_type = f.page_type;
+  P.num_values = f.num_values;
+  P.kind = f.kind;
+  P.value_size = f.value_size;
+  P.rep_len = f.rep_len;
+  P.def_len = f.def_len;
+  P.host_err = f.host_err;
+  DevChunk C;
+  __builtin_memset(&C, 0, sizeof(C));
+  C.values = f.values;
+  const Tile t{0, f.k, f.tkind, f.span};
   uint32_t K = 0;  // the dictionary as its header declares it
-  if (t.kind == TK_DICT && P.dict_page >= 0) {
-    const DevPage D = b.pages[P.dict_page];
-    const int64_t bytes = int64_t(D.num_values) * P.value_size;
-    if (D.host_err == kNoError && bytes <= int64_t(D.image_len)) {
-      K = uint32_t(D.num_values);
-      const uint8_t* dict = b.payload + D.image_off;
-      const int64_t words = (bytes + 3) >> 2;
-      for (int64_t i = threadIdx.x; i < words; i += kBlock) {
-        uint32_t x = 0;
-        const int64_t o = i * 4;
-        if (o + 4 <= bytes) __builtin_memcpy(&x, dict + o, 4);
-        else for (int k = 0; o + k < bytes; k++) x |= uint32_t(dict[o + k]) << (8 * k);
-        reinterpret_cast<uint32_t*>(dict_lds)[i] = x;
-      }
+  if (f.tkind == TK_DICT && f.dict_off >= 0) {
+    const int64_t bytes = int64_t(f.dict_n) * f.value_size;
+    if (bytes <= int64_t(f.dict_len)) {
+      K = uint32_t(f.dict_n);
+      const uint8_t* dict = b.payload + f.dict_off;
+      stage_dict(dict_lds, dict, bytes);
     }
   }
   PageState S;
   Ckpt ck;
-  if (flat_spec(b, P, spec_base[t.page], S, ck)) {  // (otherwise flat_check flags the page)
-    switch (t.kind) {
-      case TK_COPY: tile_copy_s(b, t, P, S); break;
-      case TK_BOOL: tile_bool_plain_s(b, t, P, S); break;
-      case TK_DICT: tile_dict_s(b, t, P, S, K, dict_lds, CkptConst{ck}, L, stage, flag); break;
+  const bool spec_ok = flat_spec(b, P, f.value_base, S, ck);
+#ifdef PQH_FLAT_PROF
+  __syncthreads();
+  const uint64_t q1 = wall_clock64();
+#endif
+  if (spec_ok) {  // (otherwise the page's check flags it)
+    switch (f.tkind) {
+      case TK_COPY: tile_copy_s(b, t, P, C, S); break;
+      case TK_BOOL: tile_bool_plain_s(b, t, P, C, S); break;
+      case TK_DICT: tile_dict_s(b, t, P, C, S, K, dict_lds, CkptConst{ck}, L, stage, flag); break;
       default: break;
     }
   }
-  if (t.k == 0 && threadIdx.x < 64) flat_check(b, t.page, spec_base, flag);
+#ifdef PQH_FLAT_PROF
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x % 31 == 0)
+    printf("flatt %d k %d t0 %llu spec %llu work %llu end %llu\n", int(blockIdx.x), t.k, (unsigned long long)q0,
+           (unsigned long long)(q1 - q0), (unsigned long long)(wall_clock64() - q0), (unsigned long long)(wall_clock64() - q0));
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1473,11 +1521,12 @@ hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t
   return hipGetLastError();
 }
 
-hipError_t launch_flat(const DevBatch& b, const Tile* tiles, int32_t ntiles, const int32_t* jobs, int32_t njobs,
-                       const int64_t* spec_base, uint32_t* flag, size_t lds_bytes, hipStream_t s) {
-  if (ntiles + njobs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_flat, dim3(ntiles + njobs), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles, ntiles,
-                     jobs, spec_base, flag);
+hipError_t launch_flat(const DevBatch& b, const FlatTile* tiles, int32_t ntiles, const int64_t* spec_base,
+                       uint32_t* flag, size_t lds_bytes, hipStream_t s) {
+  const int32_t njob = (b.num_pages + 3) / 4;
+  if (ntiles + njob <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_flat, dim3(njob + ntiles), dim3(256), size_t(kStageBytes + 16) + lds_bytes, s, b, tiles, ntiles,
+                     njob, spec_base, flag);
   return hipGetLastError();
 }
 

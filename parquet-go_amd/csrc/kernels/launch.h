@@ -32,11 +32,10 @@ struct DevBatch {
 };
 
 hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s);
-// A small batch of required flat fixed-width columns in one launch (k_flat: speculative tiles, the
-// page checks at their k == 0 tiles and `jobs`, the pages without tiles); flag set = decode again
-// through the three kernels.
-hipError_t launch_flat(const DevBatch& b, const Tile* tiles, int32_t ntiles, const int32_t* jobs, int32_t njobs,
-                       const int64_t* spec_base, uint32_t* flag, size_t lds_bytes, hipStream_t s);
+// A small batch of required flat fixed-width columns in one launch (k_flat: a check per page,
+// speculative tiles from their FlatTile records); flag set = decode again through the three kernels.
+hipError_t launch_flat(const DevBatch& b, const FlatTile* tiles, int32_t ntiles, const int64_t* spec_base,
+                       uint32_t* flag, size_t lds_bytes, hipStream_t s);
 // pqh_hybrid_decode: walk (res[0] = first error key, res[1] = values before it) + unpack (G = group)
 hipError_t launch_hybrid_raw(const uint8_t* stream, int64_t len, int32_t width, int64_t n, int group, Ckpt* ck,
                              uint64_t* res, uint32_t* out, hipStream_t s);
