@@ -321,6 +321,15 @@ def test_flat_one_launch(pq, monkeypatch, flat):
         compared, errors = _run_cases(pq, ctx, cases[:300], runs=3)
         assert compared == min(len(cases), 300) and compared > 100 and errors > 20, (compared, errors)
     ctx.close()
+    # unprofiled: the runs replay a captured graph, which the fallback drops and captures again
+    ctx = pq.native.Context(0)
+    data = _required_flat(20000, True, seed=5)
+    clean = _page_sets_cases(pq, data)
+    compared, errors = _run_cases(pq, ctx, clean, runs=3)
+    assert compared == len(clean) and errors == 0
+    compared, errors = _run_cases(pq, ctx, clean + _fuzz_cases(pq, data, 17, per_page=2)[:100], runs=3)
+    assert compared > len(clean) and errors > 5, (compared, errors)
+    ctx.close()
 
 
 def _page_sets_cases(pq, data):
