@@ -769,7 +769,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
-            "launch": "hipGraph replay per step (profiled direct launches: %.4f ms/step)" % prof_ms,
+            "launch": ("direct launch of the one kernel (k_flat) per step" if "k_flat" in kernels else
+                       "hipGraph replay per step") + " (profiled direct launches: %.4f ms/step)" % prof_ms,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
