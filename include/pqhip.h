@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 6
+#define PQH_ABI_VERSION 7
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -103,7 +103,7 @@ typedef enum pqh_status {
   PQH_ERR_NEGATIVE_DLBA_LENGTH = 17,  /* negative DELTA_LENGTH length: a runtime panic in the reference */
   PQH_ERR_DBA_PREFIX = 18,            /* "invalid prefix len in the stream" (type_bytearray.go:223-226) */
   PQH_ERR_DBA_COUNT = 19,             /* "different number of suffixes and prefixes" (type_bytearray.go:206-208) */
-  PQH_ERR_INT96_SHORT = 20,           /* "not enough byte to read Int96" (type_int96.go:34-36) */
+  PQH_ERR_INT96_SHORT = 20,           /* (unused since ABI 7: a short last INT96 value is a nil slot) */
   PQH_ERR_UNSUPPORTED = 21,           /* getValuesDecoder: unsupported (type, encoding) (chunk_reader.go:106-159) */
   PQH_ERR_PAGE_HEADER = 22,           /* negative NumValues / sizes, missing sub-header (page_v1.go:88-94 ...) */
   PQH_ERR_DECOMPRESS = 23,            /* decompression failed or size mismatch (compress.go:131-152) */
@@ -206,6 +206,13 @@ typedef struct pqh_chunk_out {
   int64_t num_bytes;     /* BYTE_ARRAY data size */
   uint8_t* def_levels;   /* one byte per level slot, NULL when max_def == 0 (device) */
   uint8_t* rep_levels;   /* one byte per level slot, NULL when max_rep == 0 (device) */
+  /* The reference's nil values (INT96 only, type_int96.go:21-42): a PLAIN page whose last value is
+   * short returns success with that slot never assigned, and a dictionary page whose last entry is
+   * short hands that nil entry to every value that indexes it (type_dict.go:57).  Such values are
+   * 12 zero bytes in `values`; value_nil (device, num_non_null bytes) marks them with 1.  NULL for
+   * every chunk that cannot hold one (num_nil is then 0). */
+  uint8_t* value_nil;
+  int64_t num_nil;
 } pqh_chunk_out;
 
 /* Nesting of a repeated column, the columnar form of the reference's record
@@ -237,7 +244,7 @@ typedef struct pqh_page_result {
   int32_t phase;        /* enum pqh_phase of that error */
   int64_t index;        /* index at which it happened (level slot, value, or load sub-step) */
   int32_t num_non_null; /* notNull of the page */
-  int32_t reserved;
+  int32_t num_nil;      /* of those values, the reference's nil ones (pqh_chunk_out.value_nil) */
   int64_t value_offset; /* first value of this page in pqh_chunk_out.values */
   int64_t level_offset; /* first level slot of this page in pqh_chunk_out.{def,rep}_levels */
 } pqh_page_result;
@@ -252,7 +259,7 @@ typedef struct pqh_page_values {
   int64_t values_read;  /* values decodeValues produced (< num_non_null on a value error) */
   int64_t num_bytes;    /* BYTE_ARRAY: bytes of the returned values */
   int32_t value_size;   /* bytes per fixed-width value, 0 for BYTE_ARRAY */
-  int32_t reserved;
+  int32_t num_nil;      /* returned values that are the reference's nil (INT96; marked in value_nil) */
 } pqh_page_values;
 
 typedef struct pqh_kernel_stat {
@@ -303,10 +310,29 @@ int pqh_sync(pqh_ctx* ctx);
 int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks,
                      const pqh_page* pages, int32_t num_pages, const void* d_payload,
                      int64_t payload_bytes, pqh_batch** out);
-/* Enqueue the whole decode on the context stream (asynchronous; may be re-run). */
+/* Enqueue the whole decode on the context stream (asynchronous; may be re-run).  Small flat batches
+ * (one k_flat launch) and chunks of PLAIN byte-array pages (k_ba_chain) decode speculatively: a
+ * speculation that fails is only seen by pqh_batch_sync, so several runs before one sync all replay
+ * the speculative path, and their outputs are not the reference's until that sync has re-decoded
+ * the batch. */
 int pqh_batch_run(pqh_batch* batch);
-/* Wait for the last run and copy back per-page results. */
+/* Wait for the last run and copy back per-page results.  When the last run's speculation failed
+ * (see pqh_batch_run) or a byte-array output came out short, this re-decodes the batch before
+ * returning -- on the three-kernel / scratch path, which the batch then keeps for every later run
+ * (pqh_batch_paths counts these fallbacks). */
 int pqh_batch_sync(pqh_batch* batch);
+/* Which decode paths the batch takes now, and how often pqh_batch_sync fell back (for benchmarks
+ * that must report whether a timed run used a fallback path). */
+typedef struct pqh_batch_paths {
+  int32_t flat_active;       /* runs launch the one k_flat kernel */
+  int32_t flat_fallbacks;    /* k_flat speculations that failed (then the three kernels) */
+  int32_t ba_fuse_active;    /* runs launch k_ba_chain for PLAIN byte-array chunks */
+  int32_t ba_fuse_fallbacks; /* k_ba_chain verifications that failed (then the scratch path) */
+  int32_t regrows;           /* re-decodes after growing short byte-array outputs */
+  int32_t graph_replay;      /* unprofiled runs replay a captured hipGraph */
+  int32_t reserved[2];
+} pqh_batch_paths;
+int pqh_batch_path_info(const pqh_batch* batch, pqh_batch_paths* out);
 int pqh_batch_chunk_out(const pqh_batch* batch, int32_t chunk, pqh_chunk_out* out);
 /* Nesting outputs of one chunk (after pqh_batch_sync).  Chunks with max_rep > PQH_MAX_NEST return
  * PQH_ERR_NOT_IMPLEMENTED. */
@@ -318,14 +344,16 @@ int pqh_batch_page_results(const pqh_batch* batch, pqh_page_result* out, int32_t
  * Level slots [first, first + count) of the page (count clipped to the page, as readValues clips
  * size); def_levels / rep_levels receive num_slots bytes each (NULL = skip); fixed-width values
  * go to `values` (num_non_null * value_size bytes), byte arrays to offsets (num_non_null + 1,
- * relative to the first returned value) + data (num_bytes).  With NULL value buffers only the
- * sizes are filled in.  On a readValues error (out->status != PQH_OK) nothing is copied, as the
+ * relative to the first returned value) + data (num_bytes); value_nil (NULL = skip) receives
+ * num_non_null bytes, 1 where the value is the reference's nil (INT96, see pqh_chunk_out), which
+ * the shim boxes as a nil interface{}.  With NULL value buffers only the sizes are filled in.  On a readValues error (out->status != PQH_OK) nothing is copied, as the
  * reference returns nil slices.  Errors are those of the whole-page call the reference makes
  * (ColumnStore.readNextPage, data_store.go:236-260); a ranged call reports a level error once its
  * range reaches the failing slot and a value error once its values reach the failing value. */
 int pqh_batch_page_read(const pqh_batch* batch, int32_t page, int64_t first, int64_t count, void* values,
                         int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data,
-                        int64_t data_cap, uint8_t* def_levels, uint8_t* rep_levels, pqh_page_values* out);
+                        int64_t data_cap, uint8_t* def_levels, uint8_t* rep_levels, uint8_t* value_nil,
+                        pqh_page_values* out);
 /* Kernel timing accumulated since the last reset (requires PQH_CTX_PROFILE). */
 int pqh_batch_kernel_stats(const pqh_batch* batch, pqh_kernel_stat* out, int32_t max_stats,
                            int32_t* num_stats);

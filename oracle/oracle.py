@@ -69,7 +69,7 @@ class OrcPage(ctypes.Structure):
 class OrcDict(ctypes.Structure):
     _fields_ = [("num_values", ctypes.c_int32), ("value_size", ctypes.c_int32),
                 ("values", ctypes.POINTER(ctypes.c_uint8)), ("offsets", ctypes.POINTER(ctypes.c_int64)),
-                ("num_bytes", ctypes.c_int64)]
+                ("num_bytes", ctypes.c_int64), ("nil_last", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class OrcOut(ctypes.Structure):
@@ -78,7 +78,8 @@ class OrcOut(ctypes.Structure):
                 ("def_", ctypes.POINTER(ctypes.c_uint8)), ("rep", ctypes.POINTER(ctypes.c_uint8)),
                 ("value_size", ctypes.c_int32), ("values", ctypes.POINTER(ctypes.c_uint8)),
                 ("values_bytes", ctypes.c_int64), ("offsets", ctypes.POINTER(ctypes.c_int64)),
-                ("num_offsets", ctypes.c_int64)]
+                ("num_offsets", ctypes.c_int64), ("nil", ctypes.POINTER(ctypes.c_uint8)),
+                ("num_nil", ctypes.c_int64)]
 
 
 _lib = None
@@ -165,13 +166,16 @@ def delta_decode(data, n, bits=64):
 
 
 class Dictionary:
-    def __init__(self, status, num_values=0, value_size=0, values=b"", offsets=None, index=0):
+    def __init__(self, status, num_values=0, value_size=0, values=b"", offsets=None, index=0, nil_last=False):
         self.status = status
         self.index = index  # the values read before the failing one
         self.num_values = num_values
         self.value_size = value_size
         self.values = values
         self.offsets = offsets
+        # the last entry is the reference's nil (INT96 dictionary page whose last value is short,
+        # type_int96.go:21-42); its bytes in `values` are zeros
+        self.nil_last = nil_last
 
 
 def decode_dict_page(col, num_values, encoding, image):
@@ -187,7 +191,7 @@ def decode_dict_page(col, num_values, encoding, image):
     offs = None
     if d.value_size == 0:
         offs = np.ctypeslib.as_array(d.offsets, shape=(d.num_values + 1,)).copy()
-    res = Dictionary(OK, d.num_values, d.value_size, vals, offs)
+    res = Dictionary(OK, d.num_values, d.value_size, vals, offs, nil_last=bool(d.nil_last))
     lib().orc_dict_free(ctypes.byref(d))
     return res
 
@@ -206,6 +210,9 @@ class PageResult:
         self.value_size = 0
         self.values = b""
         self.offsets = None
+        # None, or a uint8 array of nn: 1 = the value slot is the reference's nil (an INT96 value
+        # left unassigned by a short read, type_int96.go:21-42); its bytes in `values` are zeros
+        self.nil = None
 
 
 def _to_cdict(d):
@@ -219,6 +226,7 @@ def _to_cdict(d):
     keep.append(va)
     cd.values = va.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
     cd.num_bytes = len(d.values)
+    cd.nil_last = int(getattr(d, "nil_last", False))
     if d.offsets is not None:
         oa = np.ascontiguousarray(d.offsets, dtype=np.int64)
         keep.append(oa)
@@ -251,6 +259,8 @@ def decode_page(col, page_type, num_values, encoding, def_len, rep_len, image, d
         r.values = ctypes.string_at(o.values, o.values_bytes)
     if o.offsets and o.num_offsets:
         r.offsets = np.ctypeslib.as_array(o.offsets, shape=(o.num_offsets,)).copy()
+    if o.nil:
+        r.nil = np.ctypeslib.as_array(o.nil, shape=(o.nn,)).copy()
     lib().orc_out_free(ctypes.byref(o))
     return r
 

@@ -12,7 +12,7 @@
 
 #include "../include/pqhip.h"
 
-#define ORC_ABI 1
+#define ORC_ABI 2
 
 int orc_abi_version(void) { return ORC_ABI; }
 
@@ -697,9 +697,25 @@ static int dlba_next(vdec_t *v, buf_t *vals, int64_t *len_out) {
 
 static int off_push(buf_t *offs, int64_t v) { return buf_append(offs, (const uint8_t *)&v, 8); }
 
-/* decodeValues(dst[:nn]) */
+/* Slot i of dst[:nn] stays the reference's nil (an interface{} never assigned): nil->p becomes an
+ * nn-byte mask on the first one. */
+static int nil_mark(buf_t *nil, int32_t nn, int32_t i) {
+  if (!nil) return PQH_OK;
+  if (!nil->p) {
+    int st = buf_reserve(nil, nn);
+    if (st) return st;
+    memset(nil->p, 0, (size_t)nn);
+    nil->len = nn;
+  }
+  nil->p[i] = 1;
+  return PQH_OK;
+}
+
+static const uint8_t kZero12[12] = {0};
+
+/* decodeValues(dst[:nn]); nil (may be NULL) receives the mask of the slots left nil */
 static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals, buf_t *offs,
-                       int64_t *err_index) {
+                       int64_t *err_index, buf_t *nil) {
   int st = PQH_OK;
   int32_t i;
   int is_ba = (v->size == 0) || v->kind == VD_DBA || v->kind == VD_DLBA;
@@ -714,7 +730,7 @@ static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals,
         vals->len += v->size;
       }
       break;
-    case VD_PLAIN_INT96: /* type_int96.go:21-39 */
+    case VD_PLAIN_INT96: /* int96PlainDecoder.decodeValues (type_int96.go:21-42) */
       for (i = 0; i < nn; i++) {
         uint8_t d[12];
         int64_t got;
@@ -723,13 +739,17 @@ static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals,
           if ((st = buf_append(vals, d, 12))) return st;
           continue;
         }
-        if (st) break; /* n == 0: EOF */
-        /* short read: the value is dropped and the reader is at its end, so the NEXT iteration's
-         * Read returns io.EOF.  On the last value the reference returns success with a nil slot;
-         * the oracle (and the product) report that case as PQH_ERR_INT96_SHORT: a nil slot has no
-         * columnar form (documented divergence). */
+        if (st) break; /* n == 0: io.EOF, returned with the values read so far */
+        /* a short read (0 < n < 12, err == nil: bytes.Reader hands out what is left) drops the
+         * value and leaves the reader at its end.  Before the last slot, the NEXT iteration's Read
+         * returns (0, io.EOF).  On the last slot the loop simply ends: decodeValues returns
+         * (len(dst), nil) with dst[nn-1] never assigned -- the reference's nil value.  Its 12
+         * output bytes are zeros and the nil mask marks it. */
         if (i == nn - 1) {
-          st = PQH_ERR_INT96_SHORT;
+          if ((st = buf_append(vals, kZero12, 12))) return st;
+          if ((st = nil_mark(nil, nn, i))) return st;
+          st = PQH_OK;
+          i++;
         } else {
           st = PQH_ERR_EOF;
           i++;
@@ -773,6 +793,8 @@ static int vdec_decode(vdec_t *v, const orc_dict *dict, int32_t nn, buf_t *vals,
         }
         if (dict->value_size > 0) {
           if ((st = buf_append(vals, dict->values + (int64_t)key * dict->value_size, dict->value_size))) return st;
+          /* dst[i] = uniqueValues[key]: the nil entry of a short INT96 dictionary page stays nil */
+          if (dict->nil_last && key == size - 1 && (st = nil_mark(nil, nn, i))) return st;
         } else {
           int64_t a = dict->offsets[key], b = dict->offsets[key + 1];
           if ((st = buf_append(vals, dict->values + a, b - a))) return st;
@@ -875,11 +897,14 @@ int orc_decode_dict_page_ex(const orc_column *col, int32_t num_values, int32_t e
   int st = vdec_select(col, PQH_ENC_PLAIN, &v);
   if (st) return st;
   vdec_init(&v, img, img_len);
-  buf_t vals = {0, 0, 0}, offs = {0, 0, 0};
+  buf_t vals = {0, 0, 0}, offs = {0, 0, 0}, nil = {0, 0, 0};
   int64_t ei;
-  st = vdec_decode(&v, NULL, num_values, &vals, &offs, &ei);
+  st = vdec_decode(&v, NULL, num_values, &vals, &offs, &ei, &nil);
   vdec_free(&v);
   *err_index = st ? ei : 0;
+  /* (only an INT96 dictionary's last entry can be nil: a short read of it, type_int96.go:21-42) */
+  out->nil_last = nil.p != NULL;
+  free(nil.p);
   int is_ba = col->physical_type == PQH_BYTE_ARRAY ||
               (col->physical_type == PQH_FIXED_LEN_BYTE_ARRAY && col->type_length == 0);
   if (st) {
@@ -1018,11 +1043,17 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
     if (x == col->max_def) nn++;
   }
   out->nn = nn;
-  buf_t vals = {0, 0, 0}, offs = {0, 0, 0};
+  buf_t vals = {0, 0, 0}, offs = {0, 0, 0}, nil = {0, 0, 0};
   int64_t ei = 0;
-  if (nn != 0) st = vdec_decode(&v, dict, nn, &vals, &offs, &ei);
+  if (nn != 0) st = vdec_decode(&v, dict, nn, &vals, &offs, &ei, &nil);
   else st = PQH_OK;
   vdec_free(&v);
+  if (!st && nil.p) {
+    out->nil = nil.p;
+    for (int32_t k = 0; k < nn; k++) out->num_nil += nil.p[k];
+  } else {
+    free(nil.p);
+  }
   out->values = vals.p;
   out->values_bytes = vals.len;
   out->offsets = (int64_t *)offs.p;
@@ -1045,6 +1076,7 @@ int orc_decode_page(const orc_column *col, const orc_page *pg, const uint8_t *im
 }
 
 void orc_out_free(orc_out *o) {
+  free(o->nil);
   free(o->def);
   free(o->rep);
   free(o->values);

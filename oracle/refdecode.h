@@ -45,6 +45,9 @@ typedef struct orc_dict {
   uint8_t *values;      /* fixed: num_values * value_size bytes; byte arrays: data */
   int64_t *offsets;     /* byte arrays: num_values + 1 */
   int64_t num_bytes;
+  int32_t nil_last;     /* the last entry is the reference's nil: an INT96 dictionary page whose
+                           last value is short (type_int96.go:21-42); its 12 bytes are zeros */
+  int32_t reserved;
 } orc_dict;
 
 typedef struct orc_out {
@@ -60,6 +63,9 @@ typedef struct orc_out {
   int64_t values_bytes;
   int64_t *offsets;     /* byte arrays: num_offsets (nn + 1, fewer when the values fail) */
   int64_t num_offsets;
+  uint8_t *nil;         /* NULL, or nn bytes: 1 = the value slot is the reference's nil (INT96: a short
+                           last PLAIN value, or the nil entry of a short dictionary), zeros in values */
+  int64_t num_nil;
 } orc_out;
 
 int orc_abi_version(void);

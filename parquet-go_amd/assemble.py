@@ -231,10 +231,10 @@ class ColumnarAssembler:
         self.fail = {}
         for c in self._order:
             lf = self.leaves[c]
-            for first, status, phase, index in lf.pages:
-                if status:
+            for page, (first, status, phase, index) in enumerate(lf.pages):
+                if status:  # (page = the data page's position in the chunk, as records.LeafStore counts)
                     row = int(np.count_nonzero(lf.r[:first] == 0)) if lf.max_r else first
-                    self.fail[c] = (row, status, phase, index, lf.path)
+                    self.fail[c] = (row, status, phase, index, lf.path, page)
                     break
         self.ok_rows = min([f[0] for f in self.fail.values()] + [self.num_rows])
 

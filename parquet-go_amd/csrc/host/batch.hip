@@ -103,15 +103,6 @@ bool snappy_page_mode() {
   return f && f[0] == '1';
 }
 
-// PQH_LEV4=1: k_expand's level tiles also pack a nibble copy of the levels of chunks with max_rep,
-// max_def <= 3, which the nesting passes read instead of the level bytes (0.5 B per slot instead
-// of 2 in each pass).  Opt-in: on C4 it removes 0.6 GB of the nesting passes' reads but the packing
-// costs k_expand more time than the count pass saves (step 1.32 vs 1.29 ms, same box).
-bool lev4_enabled() {
-  const char* f = getenv("PQH_LEV4");
-  return f && f[0] == '1';
-}
-
 // PQH_BA_FUSE=0 (A/B experiments, tests): PLAIN-only byte-array chunks take the scratch path
 // (k_ba_wspec / wstitch / wcopy) instead of the fused k_ba_chain.
 bool fuse_enabled() {
@@ -373,6 +364,9 @@ struct pqh_batch {
   bool flat_on = false;   // the last run went through k_flat
   bool flat_off = false;  // a k_flat speculation failed once: the three kernels from then on
   int32_t flat_fallbacks = 0;
+  int32_t regrows = 0;
+  std::vector<int32_t> page_nil;   // (after sync) nil INT96 values per page / chunk (value_nil marks)
+  std::vector<int64_t> chunk_nil;
   std::vector<int64_t> flat_base;   // k_flat: page value bases if every page is clean (num_values prefixes)
   std::vector<FlatTile> flat_tiles; // k_flat: expand_tiles with their pages' fields
   int64_t* d_flat_base = nullptr;
@@ -897,6 +891,25 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
                                                                 ? std::max(D.type_length, 0) : 0);
     if ((rc = dalloc(b, &p, vsz == 0 && ba_chunk ? 64 : size_t(n) * size_t(std::max(vsz, 1)) + 64))) break;
     D.values = static_cast<uint8_t*>(p);
+    if (D.physical_type == PQH_INT96) {
+      // the reference's nil values (type_int96.go:21-42): a PLAIN page may end with a short value
+      // (known only once notNull is), a dictionary page's last entry may be short (known now)
+      bool plain = false, dnil = false;
+      for (int32_t i = 0; i < D.num_pages; i++) {
+        const DevPage& Q = b->hpages[size_t(D.first_page + i)];
+        plain = plain || (Q.page_type != PQH_DICTIONARY_PAGE && Q.kind == K_PLAIN_INT96);
+      }
+      if (D.dict_page >= 0) {
+        const DevPage& Q = b->hpages[size_t(D.dict_page)];
+        dnil = Q.host_err == kNoError && Q.kind == K_PLAIN_INT96 && Q.num_values > 0 &&
+               int64_t(Q.image_len) / 12 == int64_t(Q.num_values) - 1 && Q.image_len % 12 != 0;
+      }
+      if (plain || dnil) {
+        if ((rc = dalloc(b, &p, size_t(n) + 64))) break;
+        D.value_nil = static_cast<uint8_t*>(p);
+        D.dict_nil = dnil ? 1 : 0;
+      }
+    }
     if (ba_chunk) {
       if ((rc = dalloc(b, &p, size_t(n + 1) * sizeof(int64_t)))) break;
       D.offsets = static_cast<int64_t*>(p);
@@ -933,11 +946,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     if (!ok) continue;
     // windows of kMaxNest levels: one DevNest each (the chunk's are consecutive in b->nests)
     b->chunk_nest[size_t(c)] = int32_t(b->nests.size());
-    if (col.max_rep <= 3 && col.max_def <= 3 && lev4_enabled()) {  // the nesting passes' nibble levels
-      void* q = nullptr;
-      if ((rc = dalloc(b, &q, size_t(n / 2) + 64))) break;
-      b->hchunks[size_t(c)].lev4 = static_cast<uint8_t*>(q);
-    }
     void* leaf = nullptr;
     if ((rc = dalloc(b, &leaf, size_t(n) + 64))) break;
     for (int32_t l0 = 0; l0 < col.max_rep && !rc; l0 += kMaxNest) {
@@ -982,7 +990,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   }
   if (!rc && !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nests), sizeof(DevNest) * b->nests.size())) &&
       !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nest_tiles), sizeof(Tile) * b->nest_tiles.size())) &&
-      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nsums), sizeof(int64_t) * kNestFlags * (b->nest_tiles.size() + 1))))
+      !(rc = dalloc(b, reinterpret_cast<void**>(&b->d_nsums), sizeof(int64_t) * kNestFlags * b->nest_tiles.size())))
     rc = dalloc(b, reinterpret_cast<void**>(&b->d_ntotals), sizeof(int64_t) * kNestFlags * b->nests.size());
   for (size_t i = 0; i < b->nests.size(); i++) b->nests[i].totals = b->d_ntotals + i * kNestFlags;
   if (rc || (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunks), sizeof(DevChunk) * size_t(std::max(num_chunks, 1))))) {
@@ -1084,7 +1092,7 @@ bool flat_batch(const pqh_batch* b) {
     return false;
   if (b->pages.empty() || b->pages.size() > kFlatMaxPages || b->expand_tiles.size() > kFlatMaxTiles) return false;
   if (!std::all_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& C) {
-        return C.max_rep == 0 && C.max_def == 0 && C.value_size > 0 && !C.lev4;
+        return C.max_rep == 0 && C.max_def == 0 && C.value_size > 0 && !C.value_nil;
       }))
     return false;
   return std::all_of(b->hpages.begin(), b->hpages.end(), [](const DevPage& P) {
@@ -1172,11 +1180,8 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   const int32_t nbp = fuse ? b->ba_pages_nf : int32_t(b->ba_pages.size()), nbt = int32_t(b->ba_tiles.size()),
                 nbc = fuse ? b->ba_chunks_nf : int32_t(b->ba_chunks.size());
   // fused PLAIN chains: compute bound (chain resolution), so they run on a stream of their own
-  // beside the rest; launched after k_scan, whose page byte bases they use (PQH_FUSE_AT=prologue:
-  // right after the prologue, summing the bases from the page states themselves)
+  // beside the rest; launched after k_scan, whose page byte bases they use
   const int32_t nfw = fuse ? int32_t(b->ba_wins.size()) - b->ba_wins_nf : 0;
-  const char* fat = getenv("PQH_FUSE_AT");
-  const bool fuse_early = fat && fat[0] == 'p';
   bool fuse_open = false;
   auto launch_fused = [&]() -> hipError_t {
     hipError_t r = hipSuccess;
@@ -1189,11 +1194,10 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     }
     if (r == hipSuccess)
       r = timed(29, nfw, fs, [&](hipStream_t st) {
-        return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, b->d_ba_forder, nfw, fuse_early, st);
+        return launch_ba_chain(d, b->d_ba_wins + b->ba_wins_nf, b->d_ba_forder, nfw, st);
       });
     return r;
   };
-  if (e == hipSuccess && nfw && fuse_early) e = launch_fused();
   bool chain_open = false;  // the chain branch has not rejoined the main stream yet
   if (e == hipSuccess && nbp) {
     hipStream_t cs = s;
@@ -1232,7 +1236,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   if (e == hipSuccess && ndp > ni)
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
-  if (e == hipSuccess && nfw && !fuse_early) e = launch_fused();
+  if (e == hipSuccess && nfw) e = launch_fused();
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
@@ -1266,18 +1270,12 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       ns = side;
       nest_open = true;
     }
-    // count / scan / write passes; PQH_NEST_PASSES=1 reads the levels once (look-back bases in
-    // k_nest_write) when every chunk has a tile.  Measured on C4 (same box): one pass moves 0.39 GB
-    // less but its write takes 0.36 ms against 0.27 ms for the three kernels, and the graph step
-    // 1.60 ms against 1.35 ms (look-back waits hold workgroup slots the byte-array copies need)
-    const char* np = getenv("PQH_NEST_PASSES");
-    const bool one_pass = np && np[0] == '1' &&
-                          std::all_of(b->nests.begin(), b->nests.end(), [](const DevNest& N) { return N.tile_n > 0; });
-    if (e == hipSuccess && !one_pass)
-      e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
-    if (e == hipSuccess && !one_pass) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    // count / scan / write passes (a one-pass write with look-back bases measured slower: DESIGN §5)
     if (e == hipSuccess)
-      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, one_pass, st); });
+      e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
+    if (e == hipSuccess) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    if (e == hipSuccess)
+      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
   }
   if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
   if (e == hipSuccess && nbt) {
@@ -1469,10 +1467,31 @@ int pqh_batch_sync(pqh_batch* b) {
     regrow = true;
   }
   if (regrow) {
+    b->regrows++;
     HIP_TRY(ctx, bounce_h2d(ctx, b->d_chunks, b->hchunks.data(), sizeof(DevChunk) * b->hchunks.size()));
     int rc = pqh_batch_run(b);
     if (rc != PQH_OK) return rc;
     return pqh_batch_sync(b);
+  }
+  // the reference's nil INT96 values: per page and chunk counts of the value_nil marks
+  b->page_nil.assign(b->pages.size(), 0);
+  b->chunk_nil.assign(b->chunks.size(), 0);
+  for (size_t c = 0; c < b->hchunks.size(); c++) {
+    const DevChunk& D = b->hchunks[c];
+    if (!D.value_nil || D.values_cap <= 0) continue;
+    std::vector<uint8_t> m(static_cast<size_t>(D.values_cap));
+    HIP_TRY(ctx, bounce_d2h(ctx, m.data(), D.value_nil, m.size()));
+    for (int32_t i = 0; i < D.num_pages; i++) {
+      const int32_t p = D.first_page + i;
+      const PageState& S = b->states[size_t(p)];
+      if (b->hpages[size_t(p)].page_type == PQH_DICTIONARY_PAGE || S.nn <= 0 || S.value_base < 0 ||
+          S.value_base + S.nn > D.values_cap)
+        continue;
+      int32_t k = 0;
+      for (int64_t v = S.value_base; v < S.value_base + S.nn; v++) k += m[size_t(v)] != 0;
+      b->page_nil[size_t(p)] = k;
+      b->chunk_nil[c] += k;
+    }
   }
   for (auto& r : b->pending) {
     float ms = 0;
@@ -1614,6 +1633,7 @@ int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num
       r.index = int64_t((S.err >> 8) & 0xffffffffffffull);
     }
     r.num_non_null = S.nn;
+    r.num_nil = size_t(p) < b->page_nil.size() ? b->page_nil[size_t(p)] : 0;
     r.value_offset = S.value_base;
     r.level_offset = b->hpages[size_t(p)].level_base;
   }
@@ -1626,7 +1646,7 @@ int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num
 // the non-null ones.  Sizes only when the buffers are NULL.
 int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t count, void* values,
                         int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data, int64_t data_cap,
-                        uint8_t* def_levels, uint8_t* rep_levels, pqh_page_values* out) {
+                        uint8_t* def_levels, uint8_t* rep_levels, uint8_t* value_nil, pqh_page_values* out) {
   if (!b || !out || page < 0 || size_t(page) >= b->pages.size() || first < 0 || count < 0)
     return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad page read arguments");
   if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
@@ -1694,6 +1714,14 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   out->num_non_null = nn1;
   out->values_read = nn1;
   const int64_t v0 = S.value_base + nn0;
+  if (C.value_nil && nn1 > 0) {  // the reference's nil INT96 values among the returned ones
+    std::vector<uint8_t> m(static_cast<size_t>(nn1));
+    HIP_TRY(ctx, bounce_d2h(ctx, m.data(), C.value_nil + v0, size_t(nn1)));
+    for (uint8_t x : m) out->num_nil += x != 0;
+    if (value_nil) memcpy(value_nil, m.data(), size_t(nn1));
+  } else if (value_nil && nn1 > 0) {
+    memset(value_nil, 0, size_t(nn1));
+  }
   if (C.value_size > 0) {
     const int64_t bytes = nn1 * C.value_size;
     if (values) {
@@ -1781,6 +1809,8 @@ int pqh_batch_chunk_out(const pqh_batch* b, int32_t chunk, pqh_chunk_out* out) {
   out->num_bytes = D.offsets ? std::max<int64_t>(0, std::min(b->chunk_bytes[size_t(chunk)], D.bytes_cap)) : 0;
   out->def_levels = D.def_levels;
   out->rep_levels = D.rep_levels;
+  out->value_nil = D.value_nil;
+  out->num_nil = size_t(chunk) < b->chunk_nil.size() ? b->chunk_nil[size_t(chunk)] : 0;
   const ChunkErr e = chunk_error(b, chunk);
   out->status = e.status;
   out->error_page = e.page;
@@ -1841,6 +1871,18 @@ int pqh_batch_kernel_stats(const pqh_batch* b, pqh_kernel_stat* out, int32_t max
   int32_t n = 0;
   for (int k = 0; k < kNumKernels && n < max_stats; k++) out[n++] = b->stats[size_t(k)];
   *num_stats = n;
+  return PQH_OK;
+}
+
+int pqh_batch_path_info(const pqh_batch* b, pqh_batch_paths* out) {
+  if (!b || !out) return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "null batch or output");
+  memset(out, 0, sizeof(*out));
+  out->flat_active = flat_batch(b) ? 1 : 0;
+  out->flat_fallbacks = b->flat_fallbacks;
+  out->ba_fuse_active = b->ba_fuse_on ? 1 : 0;
+  out->ba_fuse_fallbacks = b->ba_fuse_fallbacks;
+  out->regrows = b->regrows;
+  out->graph_replay = (graphs_enabled() && !b->graph_failed && !flat_batch(b)) ? 1 : 0;
   return PQH_OK;
 }
 

@@ -1360,9 +1360,8 @@ __global__ __launch_bounds__(256) void k_ba_wcopy(DevBatch b, const WGeo* geo, i
 //     bytes); then it publishes FINAL and writes its offsets and strings straight from LDS.
 // Output bases: a page whose chain is exactly notNull records filling its values section has
 // val_e - val_s - 4 * notNull string bytes; k_scan sums them into the pages' byte bases (and the
-// value bases), and the kernel is launched after it (own_bases: launched right after the prologue,
-// it sums the chunk's earlier pages itself -- measured 2% slower on C4: a second round of global
-// loads before each window's resolution).  The window holding record notNull checks that record's
+// value bases), and the kernel is launched after it (summing the chunk's earlier pages itself, right
+// after the prologue, measured 2% slower on C4: a second round of global loads per window).  The window holding record notNull checks that record's
 // end is val_e; a chain that ends early, runs on, fails, or a page that failed earlier sets the
 // batch's fallback flag (bafuse[1]), and pqh_batch_sync decodes the batch again with the scratch
 // path (k_ba_wspec / wstitch / wcopy), which produces the reference's errors and limits exactly.
@@ -1436,8 +1435,7 @@ __device__ bool fuse_lookback(const DevBatch& b, int t, int w, int64_t val_s, in
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin,
-                                                   int own_bases) {
+__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
   __shared__ ChainLds C;
   __shared__ uint16_t recs[kChainRecs + 8];
   __shared__ BaWin R;
@@ -1464,40 +1462,13 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   // a window starting past the values holds nothing of any chain, and no window of its page that
   // does looks back at it (their bases come first); failed pages were flagged by k_scan
   if (!c.ok || Bw >= c.e0) return;
-#ifdef PQH_FUSE_PROF  // experiments: phase clocks of every 997th window
-  const uint64_t q0 = wall_clock64();
-#endif
   const int64_t wb = ba_wbase(c, w);
   ba_stage(C, c, wb);
   __syncthreads();
-#ifdef PQH_FUSE_PROF
-  const uint64_t q1 = wall_clock64();
-#endif
   const DevChunk D = b.chunks[P.chunk];
-  if (!own_bases) {  // k_scan's
-    if (tid == 64) {
-      sh[4] = S.value_base;
-      sh[5] = S.byte_base;
-    }
-  } else if (tid >= 64 && tid < 128) {
-    // the page's value and byte bases from the prologue's page states (what k_scan computes; the
-    // kernel runs beside it): notNull and string bytes of the chunk's pages before this one
-    int64_t vb = 0, bb = 0;
-    for (int q = D.first_page + (tid - 64); q < p; q += 64) {
-      const int32_t qn = b.states[q].nn;
-      if (qn > 0) {
-        vb += qn;
-        bb += int64_t(b.states[q].val_e) - b.states[q].val_s - 4 * int64_t(qn);
-      }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      vb += __shfl_xor(vb, off, 64);
-      bb += __shfl_xor(bb, off, 64);
-    }
-    if (tid == 64) {
-      sh[4] = vb;
-      sh[5] = bb;
-    }
+  if (tid == 64) {  // k_scan's bases
+    sh[4] = S.value_base;
+    sh[5] = S.byte_base;
   }
   int64_t entry = c.entry;
   if (w > 0) {
@@ -1511,9 +1482,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   ba_window(C, c, w, entry, &R, recs);
   __syncthreads();
   const int64_t value_base = sh[4], byte_base = sh[5];
-#ifdef PQH_FUSE_PROF
-  const uint64_t q2 = wall_clock64();
-#endif
   int64_t pincl = 0;
   bool pended = false;
   if (w > 0) {
@@ -1569,9 +1537,6 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
       __syncthreads();
     }
   }
-#ifdef PQH_FUSE_PROF
-  const uint64_t q3 = wall_clock64();
-#endif
   const BaWin r = R;
   if (tid == 0) {
     int64_t incl = pincl + r.count;
@@ -1621,11 +1586,4 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     if (sx + (e - o) + 20 <= kStaged) break;
     if (e - o >= kLong) block_copy(dst + o, (const PQH_G uint8_t*)(c.img + r.entry + 4 * (i + 1) + o), e - o);
   }
-#ifdef PQH_FUSE_PROF
-  __syncthreads();
-  if (tid == 0 && t % 997 == 0)
-    printf("fuse t %d w %d stage %llu guess+resolve %llu look %llu emit %llu n %d\n", t, w,
-           (unsigned long long)(q1 - q0), (unsigned long long)(q2 - q1), (unsigned long long)(q3 - q2),
-           (unsigned long long)(wall_clock64() - q3), n);
-#endif
 }

@@ -91,13 +91,13 @@ struct DevChunk {
   int64_t bytes_cap;
   PQH_G int32_t* aux;    // byte arrays: per value slot, length (PLAIN / DELTA_LENGTH / suffix) or dictionary key
   PQH_G int32_t* aux2;   // DELTA_BYTE_ARRAY: per value slot, prefix length
-  PQH_G uint8_t* lev4;   // repeated chunks with max_rep, max_def <= 3: def | rep << 2 per level slot, two
-                         // slots per byte (low nibble first), packed by k_expand's level tiles for the
-                         // nesting passes (0.5 B per slot read instead of 2)
+  PQH_G uint8_t* value_nil;  // INT96 chunks that can hold the reference's nil values (a PLAIN page, or a
+                             // dictionary whose last entry is short): 1 per nil dense value, else NULL;
+                             // zeroed at plan time, only nil slots are ever written (type_int96.go:21-42)
   int32_t batile_base;   // the chunk's byte-array tiles [batile_base, batile_base + batile_n)
   int32_t batile_n;
   int32_t ba_fused;      // PLAIN byte-array data pages only: byte bases guessed by k_scan, k_ba_chain
-  int32_t pad2;
+  int32_t dict_nil;      // the INT96 dictionary's last entry is nil (its page's last value is short)
 };
 
 // Written by the prologue (one wave per page) and the scan kernel.  64 bytes.
@@ -246,9 +246,6 @@ struct FlatTile {
 };
 
 constexpr int kLevelSpan = 4;  // 32768 level slots per tile
-#ifndef PQH_DICT_SPAN
-#define PQH_DICT_SPAN 2
-#endif
-constexpr int kDictSpan = PQH_DICT_SPAN;  // 16384 values per tile
+constexpr int kDictSpan = 2;  // 16384 values per tile (8192 / 32768 / 65536 measured slower on C1)
 
 }  // namespace pqhip

@@ -310,8 +310,10 @@ __device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int
     if (vs > 0) {
       const int64_t cap = L / vs, rem = L - cap * vs;
       if (cap < n) {
-        if (P.kind == K_PLAIN_INT96 && rem != 0)
-          err = cap == n - 1 ? err_key(0, cap, PQH_ERR_INT96_SHORT) : err_key(0, cap + 1, PQH_ERR_EOF);
+        if (P.kind == K_PLAIN_INT96 && rem != 0 && cap == n - 1)
+          S.dict_n = int32_t(n);  // the short last entry stays nil: no error (type_int96.go:21-42)
+        else if (P.kind == K_PLAIN_INT96 && rem != 0)
+          err = err_key(0, cap + 1, PQH_ERR_EOF);
         else
           err = err_key(0, cap, rem == 0 ? PQH_ERR_EOF : PQH_ERR_UNEXPECTED_EOF);
       } else {
@@ -439,12 +441,13 @@ __device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int
               }
               break;
             }
-            case K_PLAIN_INT96: {  // type_int96.go:21-39
+            case K_PLAIN_INT96: {  // int96PlainDecoder.decodeValues (type_int96.go:21-42)
               const int64_t cap = avail / 12, rem = avail - cap * 12;
               if (cap < nn) {
+                // a short LAST value ends the loop with dst[nn-1] never assigned: success, a nil slot
+                // (zeros; k_scan marks it in value_nil); a short value before it: io.EOF next read
                 if (rem == 0) err = err_key(3, cap, PQH_ERR_EOF);
-                else if (cap == nn - 1) err = err_key(3, cap, PQH_ERR_INT96_SHORT);
-                else err = err_key(3, cap + 1, PQH_ERR_EOF);
+                else if (cap != nn - 1) err = err_key(3, cap + 1, PQH_ERR_EOF);
                 limit = cap;
               }
               break;
@@ -522,6 +525,13 @@ __global__ __launch_bounds__(256) void k_scan(DevBatch b) {
     int64_t before = carry;
     for (int k = 0; k < wv; k++) before += wsum[k];
     if (i < C.num_pages) b.states[p].value_base = before + x - nn;
+    // a PLAIN INT96 page whose short last value is the reference's nil (prologue: no error, limit =
+    // notNull - 1): mark that dense slot (its 12 bytes stay the zeros of the plan-time fill)
+    if (C.value_nil && i < C.num_pages && nn > 0 && b.pages[p].kind == K_PLAIN_INT96 &&
+        b.pages[p].page_type != PQH_DICTIONARY_PAGE) {
+      const PageState s = b.states[p];
+      if (s.err == kNoError && s.val_limit == s.nn - 1) C.value_nil[before + x - 1] = 1;
+    }
     __syncthreads();
     if (t == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
@@ -838,14 +848,19 @@ struct DictSink {
   uint32_t K;
   int vs;               // runtime size when VS == 0
   int64_t* first_bad;   // per-thread min failing index
+  uint8_t* nil = nullptr;  // VS == 0 (INT96): value_nil + value_base when the dictionary's last entry
+                           // (key K - 1) is the reference's nil: such values are zeros, marked 1
   __device__ __forceinline__ void operator()(int64_t i0, const uint32_t* v, int cnt) const {
     if constexpr (VS == 4) {  // full group of in-range keys: one 16-byte store
       if (cnt == 4 && v[0] < K && v[1] < K && v[2] < K && v[3] < K) {
         const uint32_t* d = reinterpret_cast<const uint32_t*>(dict);
         if constexpr (NT) {
+          // out + i0 * 4 is only 4-byte aligned in general (value bases are sums of page value
+          // counts), so the vector type says so
           typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
           const u32x4 a = {d[v[0]], d[v[1]], d[v[2]], d[v[3]]};
-          __builtin_nontemporal_store(a, reinterpret_cast<PQH_G u32x4*>((PQH_G uint8_t*)(out) + i0 * 4));
+          __builtin_nontemporal_store(a, reinterpret_cast<PQH_G u32x4_a4*>((PQH_G uint8_t*)(out) + i0 * 4));
         } else {
           const uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
           __builtin_memcpy(out + i0 * 4, &a, 16);
@@ -898,6 +913,11 @@ struct DictSink {
         if (v[j] >= K) continue;
         const uint8_t* src = dict + int64_t(v[j]) * vs;
         uint8_t* dst = out + (i0 + j) * vs;
+        if (nil && v[j] == K - 1) {  // dst[i] = uniqueValues[K-1] = nil (type_dict.go:57)
+          for (int k = 0; k < vs; k++) dst[k] = 0;
+          nil[i0 + j] = 1;
+          continue;
+        }
         int k = 0;
         for (; k + 4 <= vs; k += 4) {
           uint32_t x;
@@ -950,48 +970,6 @@ struct KeySink {
 // ------------------------------------------------------------------------------------------------
 // Tile bodies.  Every body reads its page/state/chunk records itself (all depend on t.page only).
 // ------------------------------------------------------------------------------------------------
-// The nesting passes' copy of a tile's levels [a, e) (chunk slots; the workgroup wrote their rep and
-// def bytes just before, so they come from L2): nibble def | rep << 2, slot s in byte s / 2 (low
-// nibble for even s).  Groups of 32 slots aligned in the chunk (the level buffers are 256-byte
-// aligned): two 16-byte loads per stream, one 16-byte store; the slots of a group shared with a
-// neighbouring tile by bit-disjoint atomics on their dwords.
-__device__ __forceinline__ void lev4_set(PQH_G uint8_t* lev4, int64_t s, uint32_t v) {
-  unsigned int* w = reinterpret_cast<unsigned int*>(lev4) + (s >> 3);
-  const uint32_t sh = 4u * uint32_t(s & 7);
-  atomicAnd(w, ~(0xfu << sh));
-  atomicOr(w, (v & 0xfu) << sh);
-}
-
-// 8 level bytes (values <= 3) of each stream -> 8 nibbles (one dword).
-__device__ __forceinline__ uint32_t lev4_pack8(uint32_t d0, uint32_t d1, uint32_t r0, uint32_t r1) {
-  uint64_t c = (uint64_t(d0) | (uint64_t(d1) << 32)) | ((uint64_t(r0) | (uint64_t(r1) << 32)) << 2);
-  c = (c | (c >> 4)) & 0x00ff00ff00ff00ffull;  // byte 2k = slot 2k | slot 2k+1 << 4
-  c = (c | (c >> 8)) & 0x0000ffff0000ffffull;
-  return uint32_t(c | (c >> 16));
-}
-
-__device__ __forceinline__ void pack_levels(const DevChunk& C, int64_t a, int64_t e) {
-  const PQH_G uint8_t* rp = C.rep_levels;
-  const PQH_G uint8_t* dp = C.def_levels;
-  const int64_t g0 = (a + 31) >> 5, g1 = e >> 5;  // whole 32-slot groups inside [a, e)
-  for (int64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
-    const PQH_G uint4* r4 = reinterpret_cast<const PQH_G uint4*>(rp + 32 * g);
-    const PQH_G uint4* d4 = reinterpret_cast<const PQH_G uint4*>(dp + 32 * g);
-    const uint4 ra = r4[0], rb = r4[1], da = d4[0], db = d4[1];
-    uint4 o;
-    o.x = lev4_pack8(da.x, da.y, ra.x, ra.y);
-    o.y = lev4_pack8(da.z, da.w, ra.z, ra.w);
-    o.z = lev4_pack8(db.x, db.y, rb.x, rb.y);
-    o.w = lev4_pack8(db.z, db.w, rb.z, rb.w);
-    *reinterpret_cast<PQH_G uint4*>(C.lev4 + 16 * g) = o;
-  }
-  // the slots outside whole groups (at most 31 at each end, or the whole tile if it is short)
-  const int64_t h0 = g0 < g1 ? 32 * g0 : e;  // [a, h0) and [h1, e)
-  const int64_t h1 = g0 < g1 ? 32 * g1 : e;
-  for (int64_t s = a + threadIdx.x; s < h0; s += kBlock) lev4_set(C.lev4, s, uint32_t(dp[s]) | (uint32_t(rp[s]) << 2));
-  for (int64_t s = h1 + threadIdx.x; s < e; s += kBlock) lev4_set(C.lev4, s, uint32_t(dp[s]) | (uint32_t(rp[s]) << 2));
-}
-
 // The tile bodies take the page's state (and checkpoints) from their caller: k_expand reads them
 // after k_prologue / k_scan, k_flat from the words its prologue jobs published.
 // Ckpt loader for a page's stream table at entry i.
@@ -1019,7 +997,6 @@ __device__ __forceinline__ void tile_levels_s(const DevBatch& b, const Tile& t, 
     expand_hybrid(img, s == 0 ? S.rep_e : S.def_e, bits_len32(uint32_t(maxl)), c, t0, t1, L, stage, sink);
     __syncthreads();
   }
-  if (C.lev4) pack_levels(C, P.level_base + t0, P.level_base + t1);
 }
 
 __device__ __forceinline__ void tile_levels(const DevBatch& b, const Tile& t, TileLds& L, uint32_t* stage) {
@@ -1118,7 +1095,7 @@ __device__ __forceinline__ void tile_dict_s(const DevBatch& b, const Tile& t, co
     DictSink<8> sink{dict, out, K, vs, &first_bad};
     expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
   } else {
-    DictSink<0> sink{dict, out, K, vs, &first_bad};
+    DictSink<0> sink{dict, out, K, vs, &first_bad, C.dict_nil && C.value_nil ? C.value_nil + S.value_base : nullptr};
     expand_hybrid(img, S.val_e, S.width, c, t0, t1, L, stage, sink);
   }
   if (first_bad != INT64_MAX) {
@@ -1393,16 +1370,9 @@ __global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles,
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // as k_expand
   uint32_t* stage = reinterpret_cast<uint32_t*>(lds);
   uint8_t* dict_lds = lds + kStageBytes + 16;
-#ifdef PQH_FLAT_PROF  // experiments: clocks of the jobs and every 31st tile
-  const uint64_t q0 = wall_clock64();
-#endif
   if (int32_t(blockIdx.x) < njob) {
     const int p = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
     if (p < b.num_pages) flat_check(b, p, spec_base, flag);
-#ifdef PQH_FLAT_PROF
-    if (threadIdx.x == 0)
-      printf("flatj %d t0 %llu end %llu\n", int(blockIdx.x), (unsigned long long)q0, (unsigned long long)(wall_clock64() - q0));
-#endif
     return;
   }
   const FlatTile f = tiles[blockIdx.x - njob];
@@ -1433,10 +1403,6 @@ __global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles,
   PageState S;
   Ckpt ck;
   const bool spec_ok = flat_spec(b, P, f.value_base, S, ck);
-#ifdef PQH_FLAT_PROF
-  __syncthreads();
-  const uint64_t q1 = wall_clock64();
-#endif
   if (spec_ok) {  // (otherwise the page's check flags it)
     switch (f.tkind) {
       case TK_COPY: tile_copy_s(b, t, P, C, S); break;
@@ -1445,12 +1411,6 @@ __global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles,
       default: break;
     }
   }
-#ifdef PQH_FLAT_PROF
-  __syncthreads();
-  if (threadIdx.x == 0 && blockIdx.x % 31 == 0)
-    printf("flatt %d k %d t0 %llu spec %llu work %llu end %llu\n", int(blockIdx.x), t.k, (unsigned long long)q0,
-           (unsigned long long)(q1 - q0), (unsigned long long)(wall_clock64() - q0), (unsigned long long)(wall_clock64() - q0));
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1725,10 +1685,9 @@ hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const
   return hipGetLastError();
 }
 
-hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, bool own_bases,
-                           hipStream_t s) {
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n, int(own_bases));
+  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n);
   return hipGetLastError();
 }
 
@@ -1764,15 +1723,9 @@ hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s)
   return hipGetLastError();
 }
 
-hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, bool one_pass, hipStream_t s) {
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (one_pass) {  // the look-back words and the ticket start at zero
-    const hipError_t e = hipMemsetAsync(b.nsums, 0, sizeof(int64_t) * kNestFlags * (size_t(n) + 1), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_nest_write<true>, dim3(n), dim3(256), 0, s, b, tiles, n);
-  } else {
-    hipLaunchKernelGGL(k_nest_write<false>, dim3(n), dim3(256), 0, s, b, tiles, n);
-  }
+  hipLaunchKernelGGL(k_nest_write, dim3(n), dim3(256), 0, s, b, tiles);
   return hipGetLastError();
 }
 

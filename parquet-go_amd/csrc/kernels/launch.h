@@ -72,8 +72,7 @@ hipError_t launch_gzip(const pqh_codec_page* pages, int32_t n, const uint8_t* sr
 hipError_t launch_scan(const DevBatch& b, hipStream_t s);
 // Fused PLAIN byte-array chains (bytearray_impl.h k_ba_chain): one workgroup per window of wins
 // (page-major), dispatched in `order`.
-hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, bool own_bases,
-                           hipStream_t s);
+hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s);
 // One launch for every data-parallel tile (levels, PLAIN copies, booleans, dictionaries staged in
 // LDS, RLE booleans); lds_bytes = the largest LDS-staged dictionary of the batch.
 hipError_t launch_expand(const DevBatch& b, const Tile* tiles, int32_t n, size_t lds_bytes, hipStream_t s);
@@ -115,8 +114,7 @@ hipError_t launch_dba_prefix(const DevBatch& b, const Tile* tiles, int32_t n, hi
 // Nesting (levels -> list offsets / presence / leaf validity): counts, per-chunk scan, write.
 hipError_t launch_nest_count(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 hipError_t launch_nest_scan(const DevBatch& b, int32_t num_nests, hipStream_t s);
-// one_pass: flag bases by decoupled look-back (no k_nest_count / k_nest_scan before it)
-hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, bool one_pass, hipStream_t s);
+hipError_t launch_nest_write(const DevBatch& b, const Tile* tiles, int32_t n, hipStream_t s);
 // Delta pages outside the fast-path geometry (exact sequential decode, one wave per delta page).
 hipError_t launch_delta_serial(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 // Dictionaries too large for LDS.

@@ -44,27 +44,10 @@ __device__ __forceinline__ void nest_masks(const DevNest& N, const DevChunk& C, 
   for (int l = 0; l < kMaxNest; l++) V[l] = 0;
   LV = 0;
   if (m <= 0) return;
-  // 32 level bytes of each stream (the level buffers carry 64 bytes of slack past n), or their
-  // nibble copy (DevChunk.lev4: 16 bytes, spread back to bytes four slots per dword)
+  // 32 level bytes of each stream (the level buffers carry 64 bytes of slack past n)
   uint32_t dw[8], rw[8];
-  if (C.lev4) {
-    const uint4 q = *reinterpret_cast<const PQH_G uint4*>(C.lev4 + (s0 >> 1));  // (s0 % 32 == 0)
-    const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        uint32_t t = (xw[k] >> (16 * h)) & 0xffffu;
-        t = (t | (t << 8)) & 0x00ff00ffu;
-        t = (t | (t << 4)) & 0x0f0f0f0fu;
-        dw[2 * k + h] = t & 0x03030303u;
-        rw[2 * k + h] = (t >> 2) & 0x03030303u;
-      }
-    }
-  } else {
-    __builtin_memcpy(dw, C.def_levels + s0, 32);
-    __builtin_memcpy(rw, C.rep_levels + s0, 32);
-  }
+  __builtin_memcpy(dw, C.def_levels + s0, 32);
+  __builtin_memcpy(rw, C.rep_levels + s0, 32);
   uint32_t hi = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) hi |= dw[k] | rw[k];
@@ -203,82 +186,18 @@ __device__ __forceinline__ void nest_flush(PQH_G T* dst, const T* lds, int lead,
   }
 }
 
-// Single pass (kOnePass): each tile's flag bases come from a decoupled look-back over the tiles
-// before it in its chunk instead of k_nest_count + k_nest_scan, so the level bytes are read once.
-// Per tile and flag one 64-bit word of b.nsums (zeroed before the launch) carries the state in its
-// top two bits (kNestAgg: the tile's own count; kNestIncl: count incl. every tile before it in the
-// chunk) and the value below.  Workgroups take tiles in list order from a ticket (b.nsums after the
-// words): a tile waits only on tiles with smaller tickets of its chunk, which are running or done and
-// publish their own counts without waiting, so every wave reaches its exit.  State and value share
-// one word, so relaxed agent-scope atomics suffice (they go to the coherence point across XCDs); a
-// release / acquire pair would write back / invalidate the XCD's whole L2 per tile (measured: the
-// write pass 5 ms instead of 0.2).
-constexpr uint64_t kNestAgg = 1ull << 62, kNestIncl = 2ull << 62, kNestVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ void nest_publish(int64_t* w, uint64_t v) {
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One wave: the exclusive base of flag f for tile k of the chunk whose words start at `words`
-// (count = the tile's own count); the tile's inclusive value is published on the way.  The wave
-// reads 64 predecessors at once (lane i: tile k-1-i): the nearest inclusive word ends the walk,
-// otherwise the 64 counts are added and the window moves back; a window with an unpublished word
-// before the nearest inclusive one is read again.
-__device__ __forceinline__ int64_t nest_lookback(int64_t* words, int k, int f, int64_t count, bool* stuck) {
-  const int lane = threadIdx.x & 63;
-  uint64_t* mine = reinterpret_cast<uint64_t*>(words + int64_t(k) * kNestFlags + f);
-  if (k == 0) {
-    if (lane == 0) nest_publish(reinterpret_cast<int64_t*>(mine), kNestIncl | uint64_t(count));
-    return 0;
-  }
-  if (lane == 0) nest_publish(reinterpret_cast<int64_t*>(mine), kNestAgg | uint64_t(count));
-  int64_t excl = 0;
-  int spins = 0;
-  for (int j0 = k - 1;;) {
-    const int j = j0 - lane;
-    const uint64_t w = j >= 0 ? __hip_atomic_load(reinterpret_cast<uint64_t*>(words + int64_t(j) * kNestFlags + f),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : kNestIncl;  // before the chunk's first tile: inclusive 0
-    const uint64_t notready = __ballot((w >> 62) == 0), incl = __ballot((w & kNestIncl) != 0);
-    const uint64_t need = incl ? (incl & (0 - incl)) * 2 - 1 : ~0ull;  // lanes up to the nearest inclusive
-    if (notready & need) {  // bounded: those workgroups are running (never expected to run out)
-      if (++spins > (1 << 20)) {  // the base would be partial: the caller fails the chunk (INTERNAL)
-        *stuck = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    excl += wave_sum((need >> lane) & 1 ? int64_t(w & kNestVal) : 0);
-    if (incl) break;
-    j0 -= 64;
-  }
-  if (lane == 0) nest_publish(reinterpret_cast<int64_t*>(mine), kNestIncl | uint64_t(excl + count));
-  return excl;
-}
-
 // Write pass: the tile's list offsets / presence per level and its leaf validity are staged in LDS
 // (each output range of a tile is contiguous) and flushed with coalesced 16-byte stores.  Per thread
 // the 32 slots' flags are bit masks (bit j = slot j): E_f (element / list starts), V_l (list of
 // level l present), LV (leaf non-null), so counts are popcounts and positions prefix popcounts.
-template <bool kOnePass>
-__global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tiles, int32_t ntiles) {
+__global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tiles) {
   __shared__ uint64_t wsum[4];
-  __shared__ int32_t ticket;
-  __shared__ int64_t sflag[2][kNestFlags];
   // list offsets are staged kListPart at a time (a tile rarely starts more lists than that), which
   // halves the LDS of a workgroup (occupancy)
   constexpr int kListPart = kNestTile / 2;
   __shared__ __attribute__((aligned(16))) int32_t st32[kListPart + 4];
   __shared__ __attribute__((aligned(16))) uint8_t st8[kNestTile + 16];
-  int tix = blockIdx.x;
-  if (kOnePass) {
-    if (threadIdx.x == 0)
-      ticket = atomicAdd(reinterpret_cast<int32_t*>(b.nsums + int64_t(ntiles) * kNestFlags), 1);
-    __syncthreads();
-    tix = ticket;
-  }
-  const Tile t = tiles[tix];
+  const Tile t = tiles[blockIdx.x];
   const DevNest N = b.nests[t.page];
   const DevChunk C = b.chunks[N.chunk];
   const int64_t s0 = int64_t(t.k) * kNestTile + int64_t(threadIdx.x) * kNestPer;
@@ -293,7 +212,7 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
   for (int f = 0; f < kNestFlags; f++) {
     lpos[f] = 0;
     tot[f] = 0;
-    gbase[f] = !kOnePass && f <= L ? base[f] : 0;
+    gbase[f] = f <= L ? base[f] : 0;
   }
 #pragma unroll
   for (int f = 0; f < kNestFlags; f += 2) {
@@ -311,38 +230,9 @@ __global__ __launch_bounds__(256) void k_nest_write(DevBatch b, const Tile* tile
     __syncthreads();
     lpos[f] = int32_t(ex & 0xffffu);
     tot[f] = int32_t(tt & 0xffffu);
-    if (kOnePass && threadIdx.x == 0) {  // the tile's counts for the look-back threads
-      sflag[1][f] = int32_t(tt & 0xffffu);
-      if (f + 1 < kNestFlags) sflag[1][f + 1] = int32_t(tt >> 16);
-    }
     if (f + 1 < kNestFlags) {
       lpos[f + 1] = int32_t(ex >> 16);
       tot[f + 1] = int32_t(tt >> 16);
-    }
-  }
-  if (kOnePass) {
-    const int f = int(threadIdx.x);
-    __syncthreads();
-    // wave v looks back for flags v, v + 4, ... (the counts were staged before the scans' barrier)
-    for (int g = int(threadIdx.x >> 6); g <= L; g += kBlock / 64) {
-      const int64_t cnt = sflag[1][g];
-      bool stuck = false;
-      const int64_t excl = nest_lookback(b.nsums + int64_t(N.tile_base) * kNestFlags, t.k, g, cnt, &stuck);
-      if (stuck && (threadIdx.x & 63) == 0)  // never a property of the input: PQH_ERR_INTERNAL
-        atomicMin(&b.states[b.chunks[N.chunk].first_page].err,
-                  (unsigned long long)err_key(PQH_PHASE_LOAD, 0, PQH_ERR_INTERNAL));
-      if ((threadIdx.x & 63) == 0) {
-        sflag[0][g] = excl;
-        sflag[1][g] = excl + cnt;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < kNestFlags; g++) gbase[g] = g <= L ? sflag[0][g] : 0;
-    if (t.k == N.tile_n - 1 && f <= L) {  // the chunk's last tile: totals and closing offsets
-      const DevNest& G = b.nests[t.page];  // by reference: offsets[] indexed at run time
-      N.totals[f] = sflag[1][f];
-      if (f >= 1) G.offsets[f - 1][sflag[1][f - 1]] = int32_t(sflag[1][f]);
     }
   }
 #pragma unroll

@@ -52,7 +52,8 @@ class Chunk(ctypes.Structure):
 class ChunkOut(ctypes.Structure):
     _fields_ = [("num_values", i64), ("num_non_null", i64), ("value_size", i32), ("status", i32),
                 ("error_page", i32), ("error_phase", i32), ("error_index", i64), ("values", vp),
-                ("offsets", vp), ("bytes", vp), ("num_bytes", i64), ("def_levels", vp), ("rep_levels", vp)]
+                ("offsets", vp), ("bytes", vp), ("num_bytes", i64), ("def_levels", vp), ("rep_levels", vp),
+                ("value_nil", vp), ("num_nil", i64)]
 
 
 class NestLevel(ctypes.Structure):
@@ -65,7 +66,7 @@ class NestOut(ctypes.Structure):
 
 
 class PageResult(ctypes.Structure):
-    _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_non_null", i32), ("reserved", i32),
+    _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_non_null", i32), ("num_nil", i32),
                 ("value_offset", i64), ("level_offset", i64)]
 
 
@@ -85,7 +86,7 @@ class SchemaElement(ctypes.Structure):
 
 class PageValues(ctypes.Structure):
     _fields_ = [("status", i32), ("phase", i32), ("index", i64), ("num_slots", i64), ("num_non_null", i64),
-                ("values_read", i64), ("num_bytes", i64), ("value_size", i32), ("reserved", i32)]
+                ("values_read", i64), ("num_bytes", i64), ("value_size", i32), ("num_nil", i32)]
 
 
 class KernelStat(ctypes.Structure):
@@ -93,8 +94,13 @@ class KernelStat(ctypes.Structure):
                 ("bytes_read", f64), ("bytes_written", f64)]
 
 
+class BatchPaths(ctypes.Structure):
+    _fields_ = [("flat_active", i32), ("flat_fallbacks", i32), ("ba_fuse_active", i32), ("ba_fuse_fallbacks", i32),
+                ("regrows", i32), ("graph_replay", i32), ("reserved", i32 * 2)]
+
+
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 6  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 7  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -119,9 +125,10 @@ PROTOTYPES = [
     ("pqh_batch_chunk_out", ctypes.c_int, [vp, i32, ctypes.POINTER(ChunkOut)]),
     ("pqh_batch_nesting", ctypes.c_int, [vp, i32, ctypes.POINTER(NestOut)]),
     ("pqh_batch_page_results", ctypes.c_int, [vp, ctypes.POINTER(PageResult), i32]),
-    ("pqh_batch_page_read", ctypes.c_int, [vp, i32, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp,
+    ("pqh_batch_page_read", ctypes.c_int, [vp, i32, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp,
                                            ctypes.POINTER(PageValues)]),
     ("pqh_batch_kernel_stats", ctypes.c_int, [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]),
+    ("pqh_batch_path_info", ctypes.c_int, [vp, ctypes.POINTER(BatchPaths)]),
     ("pqh_batch_reset_stats", ctypes.c_int, [vp]),
     ("pqh_batch_traffic", ctypes.c_int, [vp, ctypes.POINTER(f64), ctypes.POINTER(f64)]),
     ("pqh_batch_destroy", None, [vp]),
@@ -489,15 +496,16 @@ class Batch:
         self.ctx.check(self.L.pqh_batch_page_results(self.h, arr, n))
         return [arr[i] for i in range(n)]
 
-    def page_read(self, page, first=0, count=None):
+    def page_read(self, page, first=0, count=None, nil=None):
         """readValues(count) of one page from level slot `first` (the compat path of the cgo shim):
         (PageValues, values or (offsets, data), def levels or None, rep levels or None) as host
-        numpy arrays; values are None when the call fails."""
+        numpy arrays; values are None when the call fails.  nil: a list that receives the returned
+        values' nil mask (uint8 per value, 1 = the reference's nil INT96 value) when pv.num_nil."""
         if count is None:
             count = 1 << 62
         pv = PageValues()
         self.ctx.check(self.L.pqh_batch_page_read(self.h, page, first, count, None, 0, None, 0, None, 0, None, None,
-                                                  ctypes.byref(pv)))
+                                                  None, ctypes.byref(pv)))
         ns = pv.num_slots
         d = np.empty(ns, np.uint8)
         r = np.empty(ns, np.uint8)
@@ -508,12 +516,16 @@ class Batch:
             else:
                 offs = np.empty(pv.num_non_null + 1, np.int64)
                 data = np.empty(max(pv.num_bytes, 1), np.uint8)
+        m = np.zeros(max(pv.num_non_null, 1), np.uint8) if pv.status == OK else None
         p = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
         self.ctx.check(self.L.pqh_batch_page_read(
             self.h, page, first, count, p(vals), 0 if vals is None else vals.nbytes, p(offs),
-            0 if offs is None else len(offs), p(data), 0 if data is None else data.nbytes, p(d), p(r), ctypes.byref(pv)))
+            0 if offs is None else len(offs), p(data), 0 if data is None else data.nbytes, p(d), p(r), p(m),
+            ctypes.byref(pv)))
         if data is not None:
             data = data[:pv.num_bytes]
+        if nil is not None and m is not None:
+            nil.append(m[:pv.num_non_null])
         return pv, (vals if pv.value_size > 0 else (offs, data)), d, r
 
     def kernel_stats(self):
@@ -521,6 +533,13 @@ class Batch:
         n = i32()
         self.ctx.check(self.L.pqh_batch_kernel_stats(self.h, arr, 32, ctypes.byref(n)))
         return [arr[i] for i in range(n.value)]
+
+    def paths(self):
+        """{flat_active, flat_fallbacks, ba_fuse_active, ba_fuse_fallbacks, regrows, graph_replay}:
+        the decode paths the batch takes now and the fallbacks pqh_batch_sync made."""
+        p = BatchPaths()
+        self.ctx.check(self.L.pqh_batch_path_info(self.h, ctypes.byref(p)))
+        return {k: getattr(p, k) for k, _ in BatchPaths._fields_ if k != "reserved"}
 
     def reset_stats(self):
         self.L.pqh_batch_reset_stats(self.h)

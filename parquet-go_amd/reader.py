@@ -50,6 +50,8 @@ class ColumnData:
         self.offsets = None
         self.data = None
         self.nesting = None
+        # the reference's nil INT96 values (pqh_chunk_out.value_nil): None, or uint8 per value
+        self.value_nil = None
         # readChunk errors (host walker, codecs, page load / decoder init: phase 0) fail the whole row
         # group (chunk_reader.go:394-400); otherwise the outputs of the pages before the first failing
         # one stay readable, as the reference decodes page by page (data_store.go:236-260)
@@ -65,6 +67,8 @@ class ColumnData:
         elif out.offsets:
             self.offsets = ctx.d2h_array(out.offsets, out.num_non_null + 1, np.int64)
             self.data = ctx.d2h_array(out.bytes, out.num_bytes)
+        if out.value_nil and out.num_nil:
+            self.value_nil = ctx.d2h_array(out.value_nil, out.num_non_null)
         if out.def_levels:
             self.def_levels = ctx.d2h_array(out.def_levels, out.num_values)
         if out.rep_levels:
@@ -214,6 +218,7 @@ class FileReader:
         rg = self.row_group_position - 1
         self._loaded = None
         self._rows = None
+        self._pending = None  # a NextBatch error belongs to the row group it came from
         loaded = decode_chunks(self.ctx, self.file, rg, rg + 1, self.selected, self.validate_crc)
         # readRowGroupData (chunk_reader.go:375-404): column by column in schema order, the column
         # checks (skipChunk for the unselected ones), then readChunk; the first failure fails the group
@@ -245,10 +250,12 @@ class FileReader:
             raise IndexError(f"index out of range [{position - 1}]")
         self.row_group_position = position - 1
         self.current_record = 0
+        self._pending = None
         self._read_row_group()
 
     def SkipRowGroup(self):
         self.skip_row_group = True
+        self._pending = None
 
     def PreLoad(self):
         self._advance_if_needed()
@@ -279,8 +286,8 @@ class FileReader:
                 pages = [(res.level_offset, res.status, res.phase, res.index)
                          for pt, n, res in c.page_info if pt != 2]
                 levels, leaf = c.nesting if c.nesting is not None else (None, None)
-                if c.max_rep and c.nesting is None:
-                    break
+                if (c.max_rep and c.nesting is None) or c.value_nil is not None:
+                    break  # (Go nil values, type_int96.go:21-42: the value-by-value assembly)
                 leaves[ci] = assemble.Leaf(c.path, c.max_def, c.max_rep, self.file.rep_def(ci), c.def_levels,
                                            c.rep_levels, levels, leaf,
                                            lambda c=c: assemble.dense_values(c, c.physical_type), pages, c.num_values)
@@ -318,8 +325,9 @@ class FileReader:
         if k < len(rows):
             return rows[k]
         e = errs[k - len(rows)]
-        raise records.RecordError(f"{e[4]}: page failed to decode (status {e[1]}, phase {e[2]}, index {e[3]})",
-                                  e[1], e[2], e[3])
+        # the same message and attributes as the value-by-value path (records.LeafStore._read_next_page)
+        raise records.RecordError(f"{e[4]}: page {e[5]} failed to decode (status {e[1]}, phase {e[2]}, index {e[3]})",
+                                  e[1], e[2], e[3], e[5])
 
     def NextBatch(self, n):
         """Up to n records of the current row group (the next one when it is exhausted), stopping
@@ -329,6 +337,8 @@ class FileReader:
             e, self._pending = self._pending, None
             raise e
         out = []
+        if n <= 0:
+            return out
         try:
             out.append(self.NextRow())
         except EOFError:

@@ -33,9 +33,15 @@ class RecordError(RuntimeError):
         self.status, self.phase, self.index, self.page = status, phase, index, page
 
 
+class ReferencePanic(RecordError):
+    """Where the reference's record assembly panics with a runtime.Error, which FileReader.recover
+    re-panics (file_reader.go:177-184): the process would crash; here the call raises this."""
+
+
 def page_values(ptype, col, v0, nn):
     """Dense values [v0, v0 + nn) of a decoded chunk as the reference's Go values (int32/int64 ->
-    int, float32/float64 -> float, bool, []byte / [12]byte -> bytes)."""
+    int, float32/float64 -> float, bool, []byte / [12]byte -> bytes; the nil interface{} of a short
+    INT96 value, col.value_nil, -> None)."""
     if nn == 0:
         return []
     if col.values is not None:
@@ -43,6 +49,9 @@ def page_values(ptype, col, v0, nn):
         if ptype == BOOLEAN:
             return [bool(x) for x in v]
         if v.ndim == 2:
+            nil = getattr(col, "value_nil", None)
+            if nil is not None:
+                return [None if nil[v0 + i] else bytes(r) for i, r in enumerate(v)]
             return [bytes(r) for r in v]
         return v.tolist()
     d = col.data.tobytes()
@@ -121,13 +130,21 @@ class LeafStore:
         if self.rep_typ != REPEATED:
             self.read_pos += 1
             return v, max_d
-        ret = [v]
+        ret = [self._append(v)]
         while True:
             self.read_pos += 1
             rl, _, last = self.rd_level_at(self.read_pos)
             if last or rl < max_r:
                 return ret, max_d
-            ret.append(self._next())
+            ret.append(self._append(self._next()))
+
+    def _append(self, v):
+        """typedColumnStore.append: a nil value of a repeated leaf (a short INT96 value,
+        type_int96.go:21-42) fails int96Store.append's type assertion value.([12]byte)
+        (type_int96.go:113-118) -- a runtime panic the reference re-panics."""
+        if v is None:
+            raise ReferencePanic(f"{self.path}: panic: interface conversion: interface {{}} is nil, not [12]uint8")
+        return v
 
 
 class Node:

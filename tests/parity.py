@@ -20,6 +20,7 @@ class Expected:
         self.rep_levels = None
         self.nn = 0
         self.n = 0
+        self.nil = None  # uint8 per value: the reference's nil INT96 values, None when there are none
 
 
 def oracle_chunk(fr, rg, ci):
@@ -31,7 +32,7 @@ def oracle_chunk(fr, rg, ci):
         return e
     col = ch.column
     res = O.decode_chunk(ch)
-    vals, defs, reps, offs, data = [], [], [], [], []
+    vals, defs, reps, offs, data, nils = [], [], [], [], [], []
     base = 0
     # FIXED_LEN_BYTE_ARRAY pages with DELTA_BYTE_ARRAY yield variable-length []byte
     # (type_bytearray.go:189-240): the product lays such a chunk out as offsets + bytes throughout
@@ -57,7 +58,10 @@ def oracle_chunk(fr, rg, ci):
             data.append(r.values)
         else:
             vals.append(r.values)
+        nils.append(r.nil if r.nil is not None else np.zeros(r.nn if not r.status else 0, np.uint8))
     e.values = b"".join(vals)
+    if any(r.nil is not None for r in res):
+        e.nil = np.concatenate(nils)
     e.data = b"".join(data)
     if offs:
         e.offsets = np.concatenate([np.zeros(1, np.int64)] + offs)
@@ -84,6 +88,10 @@ def assert_chunk(gpu, exp, where=""):
         exp_offsets = exp.offsets if exp.offsets is not None else np.zeros(1, np.int64)
         assert np.array_equal(gpu.offsets, exp_offsets), f"{where}: offsets differ"
         assert gpu.data.tobytes() == exp.data, f"{where}: byte data differs"
+    got_nil = getattr(gpu, "value_nil", None)
+    assert (got_nil is None) == (exp.nil is None), f"{where}: nil values {got_nil is not None} vs {exp.nil is not None}"
+    if exp.nil is not None:
+        assert np.array_equal(got_nil, exp.nil), f"{where}: nil value marks differ"
     if exp.def_levels is not None:
         assert np.array_equal(gpu.def_levels, exp.def_levels), f"{where}: def levels differ"
     if exp.rep_levels is not None:

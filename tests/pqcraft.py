@@ -77,3 +77,66 @@ def file_with_blocks(chunks, codec):
     meta = struct_([(1, I32, 1), (2, LIST, (STRUCT, schema)), (3, I64, nrows), (4, LIST, (STRUCT, rgs))])
     out += meta + struct.pack("<I", len(meta)) + b"PAR1"
     return bytes(out)
+
+
+INT96 = 3
+REQUIRED, OPTIONAL, REPEATED = 0, 1, 2
+
+
+def _hybrid_levels(levels, width):
+    """V1 level stream: u32 length + one bit-packed run (the reference writer's layout)."""
+    from parquet_go_amd import writer as W  # (tests put the package on the path as parquet_go_amd)
+
+    enc = W.hybrid_encode(width, levels)
+    return struct.pack("<I", len(enc)) + enc
+
+
+def int96_file(row_groups, repetition=REQUIRED):
+    """One INT96 column "t" (REQUIRED, OPTIONAL or REPEATED directly under the root), V1 pages,
+    UNCOMPRESSED.  row_groups: [(dictionary or None, [page, ...])] with dictionary = (values block,
+    num_values) and page = (values block, num_values, encoding, def levels or None, rep levels or
+    None); the level streams are prepended to the page block as the reference writer lays them out.
+    Page blocks are taken verbatim, so a block may end inside a value (the short INT96 reads of
+    type_int96.go:21-42)."""
+    out = bytearray(b"PAR1")
+    rgs, nrows_total = [], 0
+    for dictionary, pages in row_groups:
+        start = len(out)
+        dict_off = None
+        tot = nv_total = 0
+        if dictionary is not None:
+            blk, n = dictionary
+            h = struct_([(1, I32, 2), (2, I32, len(blk)), (3, I32, len(blk)),
+                         (7, STRUCT, [(1, I32, n), (2, I32, 0)])])
+            dict_off = len(out)
+            out += h + blk
+            tot += len(h) + len(blk)
+        data_off = len(out)
+        rows = 0
+        for blk, n, enc, d, r in pages:
+            lv = b""
+            if r is not None:
+                lv += _hybrid_levels(r, 1)
+                rows += sum(1 for x in r if x == 0)
+            else:
+                rows += n
+            if d is not None:
+                lv += _hybrid_levels(d, 1)
+            body = lv + blk
+            dph = [(1, I32, n), (2, I32, enc), (3, I32, 3), (4, I32, 3)]
+            h = struct_([(1, I32, 0), (2, I32, len(body)), (3, I32, len(body)), (5, STRUCT, dph)])
+            out += h + body
+            tot += len(h) + len(body)
+            nv_total += n
+        encs = [3, 0] + ([8] if dictionary is not None else [])
+        md = [(1, I32, INT96), (2, LIST, (I32, encs)), (3, LIST, (BINARY, [b"t"])), (4, I32, 0), (5, I64, nv_total),
+              (6, I64, tot), (7, I64, tot), (9, I64, data_off)]
+        if dict_off is not None:
+            md.append((11, I64, dict_off))
+        cc = [(2, I64, start), (3, STRUCT, md)]
+        rgs.append([(1, LIST, (STRUCT, [cc])), (2, I64, tot), (3, I64, rows)])
+        nrows_total += rows
+    schema = [[(4, BINARY, b"schema"), (5, I32, 1)], [(1, I32, INT96), (3, I32, repetition), (4, BINARY, b"t")]]
+    meta = struct_([(1, I32, 1), (2, LIST, (STRUCT, schema)), (3, I64, nrows_total), (4, LIST, (STRUCT, rgs))])
+    out += meta + struct.pack("<I", len(meta)) + b"PAR1"
+    return bytes(out)

@@ -119,6 +119,12 @@ class OraclePage:
         return slice_result(self.res, self.pos, size, self)
 
 
+def boxed_with_nil(raw, size, mask):
+    """Fixed-width values as the list boxValues builds when some are the reference's nil (a short
+    INT96 value, type_int96.go:21-42): bytes per value, None for a nil one."""
+    return [None if mask[i] else bytes(raw[i * size:(i + 1) * size]) for i in range(len(mask))]
+
+
 def slice_result(res, first, size, reader):
     """readValues(size) from a whole-page oracle result: (status, phase, index, values, def, rep).
     Mirrors pqh_batch_page_read's contract (include/pqhip.h): a level error fails every call of the
@@ -140,6 +146,8 @@ def slice_result(res, first, size, reader):
     else:
         vs = res.value_size
         vals = res.values[nn0 * vs:(nn0 + nn1) * vs]
+        if res.nil is not None and res.nil[nn0:nn0 + nn1].any():
+            vals = boxed_with_nil(vals, vs, res.nil[nn0:nn0 + nn1])
     return O.OK, 0, vals, d, rl
 
 
@@ -215,11 +223,14 @@ class Shim:
 
     def read_values(self, page, size):
         if self.backend == "device":
-            pv, vals, d, rl = self.batch.page_read(page.index, page.pos, size)
+            nil = []
+            pv, vals, d, rl = self.batch.page_read(page.index, page.pos, size, nil=nil)
             page.pos += pv.num_slots
             if pv.status:
                 return pv.status, pv.phase, None, None, None
             c = self.desc
+            if pv.num_nil:  # boxValues with its nil slots (INTEGRATION.md readValues): one entry per value
+                vals = boxed_with_nil(vals.tobytes(), pv.value_size, nil[0])
             return O.OK, 0, (vals if pv.value_size > 0 else (vals[0], vals[1].tobytes())), \
                 (d if c[2] > 0 else None), (rl if c[3] > 0 else None)
         return slice_result(self._page_result(page.index), page.pos, size, page)

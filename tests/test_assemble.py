@@ -12,7 +12,7 @@ import pytest
 import fixtures
 from oracle import oracle as O
 from test_records import ERROR_CASES, KATS, _corrupt, _error_file, _go_values, _norm, _oracle_schema, _pkg, \
-    kat_file, oracle_next_rows
+    error_outcome, kat_file, oracle_next_rows
 
 
 def columnar_next_rows(data, columns=None, stats=None):
@@ -26,7 +26,7 @@ def columnar_next_rows(data, columns=None, stats=None):
     leaf_el = [e for _, e in schema if e.num_children == 0]
     out = []
     for rg in range(len(fr.row_groups)):
-        leaves, stores, rg_err = {}, {}, None
+        leaves, stores, rg_err, nil_values = {}, {}, None, False
         for ci in sel:
             col = fr.columns[ci]
             ch = fr.read_chunk(rg, ci)
@@ -38,6 +38,7 @@ def columnar_next_rows(data, columns=None, stats=None):
             if load:
                 rg_err = load[0].status
                 break
+            nil_values = nil_values or any(r.nil is not None for r in res)
             n = sum(r.num_values for r in res)
             cat = lambda a: np.concatenate([np.asarray(getattr(r, a) if getattr(r, a) is not None else  # noqa: E731
                                                        np.zeros(r.num_values, np.uint8), np.uint8)[:r.num_values]
@@ -72,6 +73,8 @@ def columnar_next_rows(data, columns=None, stats=None):
             continue
         nrows = fr.row_group_num_rows(rg)
         try:
+            if nil_values:  # reader.FileReader assembles these value by value (Go nil values)
+                raise A.NotColumnar("nil INT96 values")
             asm = A.ColumnarAssembler(schema, leaves, nrows)
             rows = asm.rows()
         except A.NotColumnar:
@@ -85,12 +88,13 @@ def columnar_next_rows(data, columns=None, stats=None):
                 try:
                     out.append(ra.next_row())
                 except R.RecordError as e:
-                    out.append(("error", e.status))
+                    out.append(error_outcome(e))
             continue
         if stats is not None:
             stats["columnar"] = stats.get("columnar", 0) + 1
         out.extend(rows)
-        out.extend(("error", e[1]) for e in asm.errors())
+        # (status, phase, index, page) as records.RecordError carries them: reader.NextRow raises these
+        out.extend(("error", e[1], e[2], e[3], e[5]) for e in asm.errors())
     return out
 
 

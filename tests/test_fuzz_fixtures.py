@@ -104,7 +104,7 @@ def test_fixture_next_row(pq, ctx, m):
     """GPU: reading every row as readAllData does (NextRow until the file's row count or an error)
     never crashes, and every NextRow call returns the row or error status the oracle-driven
     assembly returns (test_records.oracle_next_rows)."""
-    from test_records import _norm, oracle_next_rows
+    from test_records import _norm, error_outcome, oracle_next_rows
 
     data = _data(m)
     fr, f = _open_both(pq, data)
@@ -120,6 +120,6 @@ def test_fixture_next_row(pq, ctx, m):
         except EOFError:
             break
         except (pq.reader.DecodeError, pq.records.RecordError) as e:
-            got.append(("error", e.status))
+            got.append(error_outcome(e))
     r.close()
     assert [_norm(g) for g in got] == [_norm(w) for w in want]

@@ -299,6 +299,12 @@ def test_flat_one_launch(pq, monkeypatch, flat):
         data = _required_flat(60000, v2)
         checked, _ = _run_file(pq, ctx, data)
         assert checked == 2 * 7
+        # dictionary pages of the file start at value bases that are not multiples of 4 (k_flat's
+        # 16-byte streaming stores of gathered INT32 values are then only 4-byte aligned)
+        fr = O.FileReader(data)
+        bases = [int(b) for ci in range(len(fr.columns)) if fr.columns[ci].physical_type == W.INT32
+                 for b in np.cumsum([r.num_values for r in O.decode_chunk(fr.read_chunk(0, ci))])[:-1]]
+        assert any(b % 4 for b in bases), bases
         # the same pages as explicit cases (each its own chunk): clean, then with mutants among them
         clean = _page_sets_cases(pq, data)
         stats = {}
@@ -664,23 +670,13 @@ def test_nesting_list_map(pq, ctx, v2):
     assert _check_nesting(pq, ctx, fixtures.nested_list_map(n=6000, v2=v2)) == 6
 
 
-@pytest.fixture(params=["one_pass", "three_passes", "three_passes_bytes"])
-def nest_passes(request, monkeypatch):
-    """The count / scan / write passes (default) and the one-pass write with look-back bases, both
-    reading the nibble copy of the levels (DevChunk.lev4) where max_rep, max_def <= 3; and the three
-    passes over the level bytes (PQH_LEV4=0)."""
-    monkeypatch.setenv("PQH_NEST_PASSES", "1" if request.param == "one_pass" else "3")
-    monkeypatch.setenv("PQH_LEV4", "0" if request.param == "three_passes_bytes" else "1")
-    return request.param
-
-
-def test_nesting_c4_multi_tile(pq, ctx, nest_passes):
+def test_nesting_c4_multi_tile(pq, ctx):
     from parquet_go_amd import datasets
 
     assert _check_nesting(pq, ctx, datasets.c4(rows=150_000, row_groups=2)) == 6
 
 
-def test_nesting_sparse_lists(pq, ctx, nest_passes):
+def test_nesting_sparse_lists(pq, ctx):
     """Mostly null / empty lists: nest tiles starting more than half a tile of lists (the list
     offsets are staged in parts), for one and two repetition levels."""
     import io
@@ -707,7 +703,7 @@ def test_nesting_sparse_lists(pq, ctx, nest_passes):
     assert _check_nesting(pq, ctx, buf.getvalue()) == 2
 
 
-def test_nesting_deep_lists(pq, ctx, nest_passes):
+def test_nesting_deep_lists(pq, ctx):
     """list<list<int32>> and list<struct<list<string>>> from pyarrow (max_rep 2)."""
     import io
 
@@ -733,7 +729,7 @@ def test_nesting_deep_lists(pq, ctx, nest_passes):
 
 
 @pytest.mark.parametrize("depth,rows", [(9, 3000), (10, 3000), (17, 600), (32, 40)])
-def test_nesting_deeper_than_a_window(pq, ctx, nest_passes, depth, rows):
+def test_nesting_deeper_than_a_window(pq, ctx, depth, rows):
     """Chains of up to 32 repeated groups (schema.go:893-990 takes any depth): the nesting outputs
     come in windows of 8 levels (one count / scan / write set per window, DevNest.lbase), every
     level's offsets and presence and the leaf validity equal oracle.nest_levels."""
@@ -788,8 +784,7 @@ def test_plain_chain_layouts(pq, ctx):
     assert compared == len(cases) and errors >= 10
 
 
-@pytest.mark.parametrize("fuse_at", ["scan", "prologue"])
-def test_fused_plain_chains(pq, monkeypatch, fuse_at):
+def test_fused_plain_chains(pq):
     """Chunks of PLAIN byte-array pages only take the fused k_ba_chain (one read of the page bytes,
     byte bases from the page sizes, look-back between windows): the layouts of
     test_plain_chain_layouts, several pages per chunk, in one batch that decodes without the scratch
@@ -799,9 +794,6 @@ def test_fused_plain_chains(pq, monkeypatch, fuse_at):
     W = fixtures.W
     rng = np.random.default_rng(47)
     col = (W.BYTE_ARRAY, 0, 0, 0)
-    # launched after k_scan (its byte bases; the default) or right after the prologue, summing the
-    # page bases itself (PQH_FUSE_AT=prologue)
-    monkeypatch.setenv("PQH_FUSE_AT", fuse_at)
     ctx = pq.native.Context(0, profile=True)
 
     def strings(n, kind):

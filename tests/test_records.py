@@ -110,7 +110,10 @@ def _go_values(r, col):
     if np_t is not None:
         return np.frombuffer(r.values, np_t).tolist()
     size = r.value_size
-    return [r.values[i:i + size] for i in range(0, len(r.values), size)]
+    vals = [r.values[i:i + size] for i in range(0, len(r.values), size)]
+    if r.nil is not None:  # the reference's nil INT96 values (type_int96.go:21-42)
+        vals = [None if r.nil[i] else v for i, v in enumerate(vals)]
+    return vals
 
 
 O_BOOLEAN, O_INT32, O_INT64, O_INT96, O_FLOAT, O_DOUBLE = range(6)
@@ -197,15 +200,27 @@ def _read_all(pq, ctx, data, *columns, columnar=True, stats=None):
     return rows
 
 
+def error_outcome(e):
+    """A failing NextRow call as recorded by the tests: ("error", status) when a row group fails to
+    load (reader.DecodeError; the oracle side records its status), ("error", status, phase, index,
+    page) when the assembly reaches a page that failed to decode (records.RecordError: the same
+    attributes from the columnar and the value-by-value assembly)."""
+    if isinstance(e, _pkg().records.ReferencePanic):  # (the reference would crash here)
+        return ("panic",)
+    if isinstance(e, _pkg().records.RecordError):
+        return ("error", e.status, e.phase, e.index, e.page)
+    return ("error", e.status)
+
+
 def _read_batches(pq, ctx, data, n):
-    """NextBatch(n) until the end, errors recorded as NextRow's are (("error", status))."""
+    """NextBatch(n) until the end, errors recorded as NextRow's are (error_outcome)."""
     fr = pq.reader.FileReader(data, ctx=ctx)
     out = []
     while True:
         try:
             b = fr.NextBatch(n)
         except (pq.reader.DecodeError, pq.records.RecordError) as e:
-            out.append(("error", e.status))
+            out.append(error_outcome(e))
             continue
         if not b:
             break
@@ -330,7 +345,7 @@ def oracle_next_rows(data):
             try:
                 out.append(asm.next_row())
             except R.RecordError as e:
-                out.append(("error", e.status))
+                out.append(error_outcome(e))
     return out
 
 
@@ -429,10 +444,40 @@ def test_next_row_error_timing(pq, ctx, case):
         except EOFError:
             break
         except (pq.reader.DecodeError, pq.records.RecordError) as e:
-            got.append(("error", e.status))
+            got.append(error_outcome(e))
         assert len(got) <= len(want) + 1
     fr.close()
     assert fr.assembled["columnar"] >= 1
     assert len(got) == len(want)
     for i, (g, w) in enumerate(zip(got, want)):
         assert _norm(g) == _norm(w), f"call {i}: {g} vs {w}"
+
+
+@pytest.mark.gpu
+def test_next_batch_pending_error_cleared_by_seek(pq, ctx):
+    """NextBatch stops before a failing row and keeps its error for the next call; moving the cursor
+    (SeekToRowGroup / SkipRowGroup) leaves that row group, so its error is dropped with it -- the
+    reference keeps no such state.  NextBatch(n <= 0) returns no rows and consumes none."""
+    data = _corrupt(_error_file(), ERROR_CASES["dict_index_page2"])
+    want = oracle_next_rows(data)
+    first_err = next(i for i, w in enumerate(want) if isinstance(w, tuple))
+    nrg0 = O.FileReader(data).row_group_num_rows(0)
+    assert 0 < first_err < nrg0
+    for move in ("seek", "skip"):
+        fr = pq.reader.FileReader(data, ctx=ctx)
+        assert fr.NextBatch(0) == [] and fr.NextBatch(-3) == []
+        got = fr.NextBatch(nrg0)
+        assert [_norm(g) for g in got] == [_norm(w) for w in want[:first_err]]
+        if move == "seek":
+            fr.SeekToRowGroup(2)
+        else:
+            fr.SkipRowGroup()
+        assert _norm(fr.NextRow()) == _norm(want[nrg0])
+        fr.close()
+    # without a move the kept error is raised by the next call, as NextRow would have raised it
+    fr = pq.reader.FileReader(data, ctx=ctx)
+    fr.NextBatch(nrg0)
+    with pytest.raises(pq.records.RecordError) as ei:
+        fr.NextBatch(10)
+    assert error_outcome(ei.value) == want[first_err]
+    fr.close()
