@@ -192,12 +192,14 @@ def check_statuses(batch, num_chunks, native, where):
                                f"page {o.error_page} phase {o.error_phase}")
 
 
-def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync):
+def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync, pinned=True):
     """Load row groups [rg0, rg1) of f into one HBM-resident batch and time `steps` decode runs
     (graph replays) between barriers; statuses checked before and after the timed runs.
-    Returns (seconds, decoded bytes per run, algorithmic bytes read per run, pages)."""
+    pinned: the walk writes the page images into the context's pinned pool (False: pageable host
+    memory, for blocks of tens of GB).  Returns (seconds, decoded bytes per run, algorithmic bytes
+    read per run, pages)."""
     ncols = len(f.columns())
-    hb = f.load(rg0, rg1, list(range(ncols)), ctx=ctx)
+    hb = f.load(rg0, rg1, list(range(ncols)), ctx=ctx if pinned else None)
     b = native.Batch.from_host(ctx, hb)
     try:
         b.run()
@@ -218,6 +220,130 @@ def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync):
     finally:
         b.close()
         hb.close()
+
+
+def kernel_table(stats, workload, rows):
+    """Per-kernel averages of profiled runs (HIP events on the decode stream) and the roofline of the
+    dominant kernel = the longest one that moves algorithmic bytes (walks that only read headers
+    carry none).  Returns (kernels, roofline, kernel ms of one profiled step)."""
+    kernels = {}
+    dom = None
+    nsteps = 0
+    for s in stats:
+        if s.launches == 0:
+            continue
+        avg_ms = s.total_ms / s.launches
+        algo = s.bytes_read + s.bytes_written
+        kernels[s.name.decode()] = {"avg_ms": round(avg_ms, 4), "launches": s.launches, "work_items": s.work_items,
+                                    "algo_bytes": algo,
+                                    "gbps": round(algo / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
+        if algo > 0 and (dom is None or s.total_ms > dom.total_ms):
+            dom = s
+        nsteps = max(nsteps, s.launches)
+    roof = None
+    if dom is not None:
+        avg_ms = dom.total_ms / dom.launches
+        ach = (dom.bytes_read + dom.bytes_written) / (avg_ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic(dom.name.decode(), workload, rows)
+        roof = {"bound": "hbm", "kernel": dom.name.decode(), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_source": src,
+                "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
+                "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
+    all_ms = sum(s.total_ms for s in stats) / max(1, nsteps)
+    return kernels, roof, all_ms
+
+
+def mixed_record(args, ctx, native, pkg, datasets, barrier_sync):
+    """north_star's headline workload: ONE 1B-row mixed-encoding file (C2's six columns -- int32 and
+    float dictionaries, int64 / double / FLBA(16) / boolean PLAIN, an optional column -- plus C3's
+    DELTA_BINARY_PACKED timestamps; V2 pages, 128 row groups; datasets.mixed) decoded HBM-resident
+    on this GPU: step time, decoded GB/s, the whole step against the HBM roofline (algorithmic bytes
+    read + written / step time / 8 TB/s) and the dominant kernel's.  Row groups 0 and 127 (every
+    chunk) are checked against the oracle outside the timed region.  Then rank 0's block of
+    shard.row_group_block(128, N, 0) for N = 2, 4, 8 timed alone: the 1->8 proxy on this file."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    rows = args.mixed_rows or datasets.MIXED_ROWS
+    desc = datasets.WORKLOADS["mixed"][0]
+    steps = max(3, min(args.steps, 10))
+    warm = max(1, min(args.warmup, 2))
+    t0 = time.perf_counter()
+    data = datasets.mixed(rows=rows)
+    gen_s = time.perf_counter() - t0
+    log(f"mixed: generated {rows} rows ({len(data) / 1e9:.2f} GB file) in {gen_s:.1f}s")
+    f = native.File(data)
+    try:
+        nrg, ncols = f.num_row_groups, len(f.columns())
+        t0 = time.perf_counter()
+        hb = f.load(0, nrg, list(range(ncols)))
+        walk_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        b = native.Batch.from_host(ctx, hb)
+        h2d_s = time.perf_counter() - t0
+        payload, pages, nch = hb.payload_bytes, hb.num_pages, hb.num_chunks
+        hb.close()
+        try:
+            b.run()
+            b.sync()
+            check_statuses(b, nch, native, "mixed: first run")
+            rd, wr = b.traffic()
+            for _ in range(warm):
+                b.run()
+            barrier_sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                b.run()
+            barrier_sync()
+            el = time.perf_counter() - t0
+            b.sync()
+            check_statuses(b, nch, native, "mixed: after the timed steps")
+            paths = b.paths()
+            ctx.set_profile(True)
+            b.reset_stats()
+            for _ in range(3):
+                b.run()
+            b.sync()
+            check_statuses(b, nch, native, "mixed: after the profiled steps")
+            kernels, roof, all_ms = kernel_table(b.kernel_stats(), desc, rows)
+            ctx.set_profile(False)
+            # bit-exact sample vs the oracle (outside every timed region)
+            fr = O.FileReader(data)
+            sample = sorted({0, nrg - 1})
+            for rg in sample:
+                for ci in range(ncols):
+                    check_chunk(ctx, b, rg * ncols + ci, O.decode_chunk(fr.read_chunk(rg, ci)), np)
+            del fr
+        finally:
+            b.close()
+        t1 = el / steps
+        rec = {"workload": desc, "rows_total": f.num_rows, "row_groups": nrg, "pages": pages,
+               "file_bytes": len(data), "payload_bytes": payload, "steps": steps, "ms_per_step": round(t1 * 1e3, 4),
+               "value": round(wr / t1 / 1e9, 2), "unit": "GB/s (decoded output)",
+               "algo_read_bytes_per_step": rd, "decoded_bytes_per_step": wr,
+               "step_roofline": {"bound": "hbm", "achieved": round((rd + wr) / t1 / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": round((rd + wr) / t1 / 1e9 / HBM_PEAK_GBS, 4),
+                                 "note": "algorithmic bytes of the whole step (page bytes read once + decoded "
+                                         "bytes written) / graph-replay step time"},
+               "roofline": roof, "kernels": kernels,
+               "profiled_kernel_ms_per_step": round(all_ms, 4), "paths": paths,
+               "verified": f"row groups {sample}: {len(sample) * ncols} chunks bit-exact vs the oracle",
+               "host": {"generate_s": round(gen_s, 2), "walk_s": round(walk_s, 2), "h2d_s": round(h2d_s, 2)},
+               "proxy": []}
+        for n in (2, 4, 8):
+            a, bb = pkg.shard.row_group_block(nrg, n, 0)
+            eln, wrn, _, _ = timed_block(ctx, native, f, a, bb, steps, warm, barrier_sync, pinned=False)
+            tn = eln / steps
+            rec["proxy"].append({"n_gpus": n, "rank0_row_groups": [a, bb], "rank0_ms_per_step": round(tn * 1e3, 4),
+                                 "predicted_whole_node_gbps": round(wr / tn / 1e9, 2),
+                                 "predicted_efficiency": round(t1 / (n * tn), 4)})
+        rec["proxy_method"] = ("rank 0's block of shard.row_group_block(128, N, 0) decoded alone on this one GPU: "
+                               "predicted whole-node GB/s = the file's decoded bytes / that time")
+        return rec
+    finally:
+        f.close()
 
 
 def c3_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync, log):
@@ -462,8 +588,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5z"],
-                    help="default: c2 (weak scaling: a C2 file per GPU) at every N; c3 = strong scaling")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5z", "mixed"],
+                    help="default: c2 (weak scaling: a C2 file per GPU) at every N; c3 / mixed = strong scaling "
+                         "of one file")
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (default: the config's)")
     ap.add_argument("--codec", default=None, choices=["snappy", "gzip"],
                     help="c5 / c5z: the page codec (default SNAPPY, as configs[4] names)")
@@ -471,6 +598,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
     ap.add_argument("--no-c3", action="store_true", help="skip the c3_strong sub-record")
+    ap.add_argument("--no-mixed", action="store_true", help="skip the mixed_1b sub-record (N=1)")
+    ap.add_argument("--mixed-rows", type=int, default=0, help=argparse.SUPPRESS)  # tests: a smaller mixed file
     ap.add_argument("--e2e-dev-ranges", type=int, default=4,
                     help="end-to-end with device codecs: staged batches (H2D of one overlaps the codec of the last)")
     ap.add_argument("--no-next-row", action="store_true", help="skip the NextRow records/s sub-record")
@@ -512,8 +641,11 @@ def main():
     # C3 (BASELINE configs[2]: 128 row groups of ONE file sharded across 1/2/4/8 GPUs) is strong
     # scaling: every rank opens the same file and decodes its contiguous block of row groups
     # (shard.row_group_block).  The other workloads give every rank its own file (weak scaling).
-    strong = args.workload == "c3"
-    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40, "c5z": 41}[args.workload] + (0 if strong else 1000 * rank)
+    strong = args.workload in ("c3", "mixed")
+    seed_kw = {"c1": 1, "c2": 10, "c3": 20, "c4": 30, "c5": 40, "c5z": 41, "mixed": 50}[args.workload] + \
+        (0 if strong else 1000 * rank)
+    if args.workload == "mixed" and args.mixed_rows:
+        kw["rows"] = args.mixed_rows
     if args.dry_run:
         return dry_run(args, world, rank, dist, pkg, datasets, builder, kw, seed_kw, strong, desc)
     t0 = time.perf_counter()
@@ -595,31 +727,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_written * args.steps / elapsed / 1e9
 
-    kernels = {}
-    dom = None
-    for s in stats:
-        if s.launches == 0:
-            continue
-        avg_ms = s.total_ms / s.launches
-        algo = s.bytes_read + s.bytes_written
-        kernels[s.name.decode()] = {"avg_ms": round(avg_ms, 4), "launches": s.launches, "work_items": s.work_items,
-                                    "algo_bytes": algo,
-                                    "gbps": round(algo / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None}
-        # the dominant kernel = the longest one that moves algorithmic bytes (walks that only read
-        # headers carry none)
-        if algo > 0 and (dom is None or s.total_ms > dom.total_ms):
-            dom = s
-    roof = None
-    if dom is not None:
-        avg_ms = dom.total_ms / dom.launches
-        ach = (dom.bytes_read + dom.bytes_written) / (avg_ms * 1e-3) / 1e9
-        traffic, src = pmc_traffic(dom.name.decode(), desc, my_rows)
-        roof = {"bound": "hbm", "kernel": dom.name.decode(), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": round(traffic) if traffic else None, "traffic_source": src,
-                "algo_bytes_per_launch": dom.bytes_read + dom.bytes_written,
-                "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
-    all_ms = sum(s.total_ms for s in stats) / max(1, args.steps)  # kernel time of one profiled step
+    kernels, roof, all_ms = kernel_table(stats, desc, my_rows)
     cpu = cpu_mt = cpu_pa = None
     verified = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -755,11 +863,17 @@ def main():
     next_row = None
     if rank == 0 and world == 1 and not args.no_next_row:
         next_row = next_row_record(ctx, pkg, rows=args.next_row_rows)
-    c3 = None
-    if not args.no_c3 and args.workload != "c3":
+    c3 = mixed = None
+    if not args.no_c3 and args.workload not in ("c3", "mixed"):
         hb.close()
         hb = None
         c3 = c3_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync, log)
+    if world == 1 and not args.no_mixed and args.workload != "mixed":
+        if hb is not None:
+            hb.close()
+            hb = None
+        data = None  # (the main file: its memory back before the 1B-row file is built)
+        mixed = mixed_record(args, ctx, native, pkg, datasets, barrier_sync)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -799,6 +913,7 @@ def main():
             "e2e": e2e,
             ("e2e_device_gzip" if args.codec == "gzip" else "e2e_device_snappy"): e2e_dev,
             "c3_strong": c3,
+            "mixed_1b": mixed,
             "next_row": next_row,
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,

@@ -44,6 +44,16 @@ def gen():
         L.pqg_delta_encode32.restype = i64
         L.pqg_delta_encode64.argtypes = [vp, i64, vp, i64]
         L.pqg_delta_encode64.restype = i64
+        L.pqg_stream_open.argtypes = [vp, i32, vp, ctypes.c_char_p, i32]
+        L.pqg_stream_open.restype = vp
+        L.pqg_stream_write.argtypes = [vp, vp, i32, vp, i32, vp, i64, vp, ctypes.c_char_p, i32]
+        L.pqg_stream_write.restype = ctypes.c_int
+        L.pqg_stream_finish.argtypes = [vp, vp, i64, vp, ctypes.c_char_p, i32]
+        L.pqg_stream_finish.restype = ctypes.c_int
+        L.pqg_stream_close.argtypes = [vp]
+        L.pqg_mixed_dicts.argtypes = [ctypes.c_uint64, vp, vp]
+        L.pqg_mixed_row_group.argtypes = [ctypes.c_uint64, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, i32]
+        L.pqg_mixed_row_group.restype = i64
         _gen = L
     return _gen
 

@@ -50,6 +50,7 @@ typedef struct pqg_options {
   int64_t max_page_size;    /* 0 => 1 MiB */
   int32_t enable_crc;
   int32_t num_threads;      /* 0 => hardware concurrency */
+  int32_t no_fast_paths;    /* 1: every chunk through the general page-cut loop (tests: same bytes) */
 } pqg_options;
 
 /* Write a whole file to memory.  rg_rows[i] = records in row group i. */
@@ -57,6 +58,28 @@ int pqg_write(const pqg_schema_element* schema, int32_t num_schema, const pqg_co
               int32_t num_columns, const int64_t* rg_rows, int32_t num_row_groups,
               const pqg_options* opt, uint8_t** out, int64_t* out_len, char* err, int32_t err_cap);
 void pqg_free(uint8_t* p);
+
+/* Streaming writer for files too large to build in one call (the 1B-row bench file): row groups are
+ * encoded batch by batch (each call's columns hold exactly its rows) and appended to a caller's
+ * buffer at *pos ("PAR1" first); finish appends the footer, its length and "PAR1".  The file is
+ * byte-identical to pqg_write of the same rows. */
+typedef struct pqg_stream pqg_stream;
+pqg_stream* pqg_stream_open(const pqg_schema_element* schema, int32_t num_schema, const pqg_options* opt, char* err,
+                            int32_t err_cap);
+int pqg_stream_write(pqg_stream* s, const pqg_column_data* columns, int32_t num_columns, const int64_t* rg_rows,
+                     int32_t num_row_groups, uint8_t* dst, int64_t cap, int64_t* pos, char* err, int32_t err_cap);
+int pqg_stream_finish(pqg_stream* s, uint8_t* dst, int64_t cap, int64_t* pos, char* err, int32_t err_cap);
+void pqg_stream_close(pqg_stream* s);
+
+/* The mixed-encoding bench workload (north_star's 1B-row file: BASELINE configs[1]'s six columns plus
+ * configs[2]'s DELTA timestamps), generated per row group from a counter-based hash so any row group
+ * is regenerated exactly: int32 from a 1000-entry dictionary, int64 uniform, float from a 256-entry
+ * dictionary, double (1% null: f64_def per row, f64 the non-null values compacted), boolean,
+ * 16-byte uuid, int64 timestamps rising by 1e6 + U[0, 4096) from a per-row-group base.  Returns the
+ * non-null double count.  threads <= 0: hardware concurrency (at most 16). */
+void pqg_mixed_dicts(uint64_t seed, int32_t* d_i32, float* d_f32);
+int64_t pqg_mixed_row_group(uint64_t seed, int32_t g, int64_t rows, int32_t* i32, int64_t* i64, float* f32,
+                            double* f64, uint8_t* f64_def, uint8_t* b, uint8_t* uuid, int64_t* ts, int32_t threads);
 
 /* Encoders exposed for unit tests: the reference writer's stream formats. */
 int64_t pqg_hybrid_encode(int32_t width, const int32_t* values, int64_t n, uint8_t* out, int64_t cap);

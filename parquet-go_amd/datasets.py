@@ -181,6 +181,73 @@ def c5z(rows=10_000_000, row_groups=8, seed=41, codec=W.SNAPPY):
     return W.flat([("url", col, W.REQUIRED)], per, v2=False, codec=codec, as_array=True)
 
 
+MIXED_ROWS, MIXED_ROW_GROUPS = 1_000_000_000, 128
+
+
+def _mixed_arrays(rows):
+    return {"i32": np.empty(rows, np.int32), "i64": np.empty(rows, np.int64), "f32": np.empty(rows, np.float32),
+            "f64": np.empty(rows, np.float64), "d64": np.empty(rows, np.uint8), "b": np.empty(rows, np.uint8),
+            "uuid": np.empty((rows, 16), np.uint8), "ts": np.empty(rows, np.int64)}
+
+
+def _mixed_fill(A, r0, f0, g, rows, seed, threads):
+    """Row group g into the arrays A at row r0 (compacted doubles at f0); returns its non-null
+    double count."""
+    L = W._lib.gen()
+    at = lambda a, o: a.ctypes.data + o * a.strides[0]  # noqa: E731
+    return L.pqg_mixed_row_group(seed, g, rows, at(A["i32"], r0), at(A["i64"], r0), at(A["f32"], r0),
+                                 at(A["f64"], f0), at(A["d64"], r0), at(A["b"], r0), at(A["uuid"], r0),
+                                 at(A["ts"], r0), threads)
+
+
+def _mixed_columns(A, rows, nn):
+    return [
+        ("c_int32", W.Column(W.INT32, A["i32"][:rows]), W.REQUIRED),
+        ("c_int64", W.Column(W.INT64, A["i64"][:rows], use_dict=False), W.REQUIRED),
+        ("c_float", W.Column(W.FLOAT, A["f32"][:rows]), W.REQUIRED),
+        ("c_double", W.Column(W.DOUBLE, A["f64"][:nn], def_levels=A["d64"][:rows], use_dict=False), W.OPTIONAL),
+        ("c_bool", W.Column(W.BOOLEAN, A["b"][:rows]), W.REQUIRED),
+        ("c_uuid", W.Column(W.FIXED_LEN_BYTE_ARRAY, A["uuid"][:rows], type_length=16, use_dict=False), W.REQUIRED),
+        ("ts", W.Column(W.INT64, A["ts"][:rows], encoding=W.DELTA_BINARY_PACKED, use_dict=False), W.REQUIRED),
+    ]
+
+
+def mixed_row_group(g, rows, seed=50, threads=0):
+    """Row group g of the mixed workload (north_star's target file): the columns as
+    [(name, Column, repetition)] -- C2's six (int32 dictionary K=1000, int64 PLAIN, float
+    dictionary K=256, optional double PLAIN 1% null, boolean PLAIN, FLBA(16) PLAIN) and C3's
+    timestamps (INT64 DELTA_BINARY_PACKED 128/4), generated by libpqgen from a counter-based hash
+    (pqg_mixed_row_group), so any row group is regenerated exactly for checking."""
+    A = _mixed_arrays(rows)
+    nn = _mixed_fill(A, 0, 0, g, rows, seed, threads)
+    return _mixed_columns(A, rows, nn)
+
+
+def mixed_sizes(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS):
+    per = -(-rows // row_groups)
+    return [min(per, rows - g * per) for g in range(row_groups) if rows - g * per > 0]
+
+
+def mixed(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS, seed=50, batch=4, threads=0):
+    """The mixed-encoding workload file (BASELINE north_star: "a 1B-row mixed-encoding Parquet
+    file"): `row_groups` row groups of ceil(rows / row_groups) records, V2 pages, UNCOMPRESSED, in
+    the reference writer's layout, streamed `batch` row groups at a time into one buffer (the
+    columns of all 1B rows never exist at once).  Returns the file as a uint8 array."""
+    sizes = mixed_sizes(rows, row_groups)
+    schema = W.flat_schema(mixed_row_group(0, 0, seed))
+    # upper bound: 57 bytes per row of values + levels + page / chunk overheads
+    sw = W.StreamWriter(schema, 57 * rows + (64 << 20), v2=True, threads=threads)
+    A = _mixed_arrays(sum(sizes[:batch]))
+    for g0 in range(0, len(sizes), batch):
+        part = sizes[g0:g0 + batch]
+        r0 = nn = 0
+        for k, n in enumerate(part):  # the batch's row groups generated in place, one after another
+            nn += _mixed_fill(A, r0, nn, g0 + k, n, seed, threads)
+            r0 += n
+        sw.write([c for _, c, _ in _mixed_columns(A, r0, nn)], part)
+    return sw.finish()
+
+
 WORKLOADS = {
     "c1": ("C1: 10M rows, required INT32 dictionary K=4096 (width 13), UNCOMPRESSED, data page V1", c1),
     "c2": ("C2: 100M rows x 6 columns (int32 dict / int64 PLAIN / float dict / optional double PLAIN "
@@ -192,4 +259,7 @@ WORKLOADS = {
            "then DELTA_LENGTH_BYTE_ARRAY fallback, SNAPPY, 8 row groups", c5),
     "c5z": ("C5z (supplementary, not a BASELINE config): 10M URL-like strings, DELTA_LENGTH_BYTE_ARRAY, "
             "SNAPPY-compressible, 8 row groups", c5z),
+    "mixed": ("mixed (north_star's target file): 1B rows x 7 columns -- C2's six (int32 dict / int64 PLAIN / "
+              "float dict / optional double PLAIN 1% null / boolean PLAIN / FLBA(16) PLAIN) + C3's INT64 "
+              "timestamps DELTA_BINARY_PACKED -- data page V2, 128 row groups", mixed),
 }

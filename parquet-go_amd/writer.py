@@ -32,7 +32,7 @@ class ColumnData(ctypes.Structure):
 
 class Options(ctypes.Structure):
     _fields_ = [("data_page_v2", ctypes.c_int32), ("codec", ctypes.c_int32), ("max_page_size", ctypes.c_int64),
-                ("enable_crc", ctypes.c_int32), ("num_threads", ctypes.c_int32)]
+                ("enable_crc", ctypes.c_int32), ("num_threads", ctypes.c_int32), ("no_fast_paths", ctypes.c_int32)]
 
 
 def element(name, ptype=-1, repetition=REQUIRED, num_children=0, type_length=0, converted_type=-1):
@@ -92,7 +92,7 @@ class Column:
 
 
 def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0,
-          as_array=False):
+          as_array=False, fast_paths=True):
     """Write a file to bytes (or a uint8 numpy array with as_array=True, for multi-GB files).
     schema: list of element(...) tuples, root first, DFS order."""
     L = _lib.gen()
@@ -104,7 +104,7 @@ def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=
     for i, c in enumerate(columns):
         cols[i] = c.cstruct()
     rows = np.ascontiguousarray(rg_rows, dtype=np.int64)
-    opt = Options(int(v2), codec, max_page_size, int(crc), threads)
+    opt = Options(int(v2), codec, max_page_size, int(crc), threads, int(not fast_paths))
     out = ctypes.POINTER(ctypes.c_uint8)()
     out_len = ctypes.c_int64()
     err = ctypes.create_string_buffer(512)
@@ -120,11 +120,62 @@ def write(schema, columns, rg_rows, v2=False, codec=UNCOMPRESSED, max_page_size=
         L.pqg_free(out)
 
 
-def flat(columns, rows_per_group, **kw):
-    """Flat schema helper.  columns: list of (name, Column, repetition)."""
+class StreamWriter:
+    """A file written row-group batch by row-group batch into one preallocated buffer (pqg_stream_*):
+    for files larger than the columns of all their rows should be in memory at once.  `capacity`
+    is an upper bound of the file size (the buffer is np.empty: pages never written are never
+    touched).  The result equals write() of the same rows, byte for byte."""
+
+    def __init__(self, schema, capacity, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0):
+        L = _lib.gen()
+        self.L = L
+        self._names = [x[0].encode() for x in schema]
+        self._els = (SchemaElement * len(schema))()
+        for i, x in enumerate(schema):
+            self._els[i] = SchemaElement(self._names[i], x[1], x[2], x[3], x[4], x[5])
+        self._opt = Options(int(v2), codec, max_page_size, int(crc), threads, 0)
+        err = ctypes.create_string_buffer(512)
+        self.h = L.pqg_stream_open(self._els, len(schema), ctypes.byref(self._opt), err, 512)
+        if not self.h:
+            raise ValueError("pqg_stream_open: " + err.value.decode())
+        self.buf = np.empty(int(capacity), dtype=np.uint8)
+        self.pos = ctypes.c_int64(0)
+
+    def write(self, columns, rg_rows):
+        """Append row groups rg_rows (records each) whose data `columns` (Column list, schema leaf
+        order) hold exactly."""
+        cols = (ColumnData * len(columns))()
+        for i, c in enumerate(columns):
+            cols[i] = c.cstruct()
+        rows = np.ascontiguousarray(rg_rows, dtype=np.int64)
+        err = ctypes.create_string_buffer(512)
+        rc = self.L.pqg_stream_write(self.h, cols, len(columns), rows.ctypes.data, len(rows), self.buf.ctypes.data,
+                                     len(self.buf), ctypes.byref(self.pos), err, 512)
+        if rc != 0:
+            raise ValueError("pqg_stream_write: " + err.value.decode())
+
+    def finish(self):
+        """The file: a view of the buffer's first bytes."""
+        err = ctypes.create_string_buffer(512)
+        rc = self.L.pqg_stream_finish(self.h, self.buf.ctypes.data, len(self.buf), ctypes.byref(self.pos), err, 512)
+        self.L.pqg_stream_close(self.h)
+        self.h = None
+        if rc != 0:
+            raise ValueError("pqg_stream_finish: " + err.value.decode())
+        return self.buf[:self.pos.value]
+
+
+def flat_schema(columns):
+    """The schema list of a flat file.  columns: list of (name, Column, repetition)."""
     schema = [element("schema", num_children=len(columns), repetition=-1)]
     for name, col, rep in columns:
         schema.append(element(name, col.ptype, rep, type_length=col.type_length))
+    return schema
+
+
+def flat(columns, rows_per_group, **kw):
+    """Flat schema helper.  columns: list of (name, Column, repetition)."""
+    schema = flat_schema(columns)
     n = columns[0][1].num_slots
     rg = []
     left = n

@@ -209,3 +209,44 @@ def test_c4_full(pq, ctx):
             vstart += nn
     b.close()
     hb.close()
+
+
+def test_mixed_1b_full(pq, ctx):
+    """north_star's target file: ONE 1,000,000,000-row mixed-encoding file -- C2's six columns
+    (int32 / float dictionaries, int64 / double / FLBA(16) / boolean PLAIN, the double optional) plus
+    C3's DELTA_BINARY_PACKED timestamps, V2 pages, 128 row groups (datasets.mixed, the reference
+    writer's layout) -- decoded in ONE HBM-resident batch.  Every chunk equals the seeded input it
+    was written from (values, definition levels), and row groups 0, 64 and 127 equal the oracle's
+    decode bit for bit."""
+    from oracle import oracle as O
+    from parity import assert_chunk, oracle_chunk
+    from parquet_go_amd import datasets
+
+    data = datasets.mixed()
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    assert f.num_row_groups == 128 and f.num_rows == 1_000_000_000 and ncols == 7
+    hb = f.load(0, f.num_row_groups, list(range(ncols)))
+    b = pq.native.Batch.from_host(ctx, hb)
+    hb.close()
+    b.run()
+    b.sync()
+    for rg, n in enumerate(datasets.mixed_sizes()):
+        for ci, (name, col, _) in enumerate(datasets.mixed_row_group(rg, n)):
+            o = b.chunk_out(rg * ncols + ci)
+            assert o.status == pq.native.OK, (rg, name, o.status)
+            nn = n
+            if col.def_levels is not None:
+                assert np.array_equal(ctx.d2h_array(o.def_levels, n), col.def_levels), (rg, name, "def levels")
+                nn = int(np.count_nonzero(col.def_levels))
+            assert o.num_non_null == nn, (rg, name)
+            got = ctx.d2h_array(o.values, nn * o.value_size)
+            assert np.array_equal(got, col.data[:nn * o.value_size]), (rg, name, "values")
+    fr = O.FileReader(data)
+    cols = f.columns()
+    for rg in (0, 64, 127):
+        for ci in range(ncols):
+            cd = pq.reader.ColumnData(cols[ci][0], cols[ci][1:], b.chunk_out(rg * ncols + ci), [], ctx)
+            assert_chunk(cd, oracle_chunk(fr, rg, ci), where=f"mixed rg{rg} c{ci}")
+    b.close()
+    f.close()

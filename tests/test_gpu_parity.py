@@ -234,6 +234,7 @@ def _run_cases(pq, ctx, cases, stats=None, runs=1):
             e = Expected()
             e.status, e.phase, e.index = r.status, r.phase, r.index
             e.nn, e.values, e.def_levels, e.rep_levels = r.nn, r.values, r.def_levels, r.rep_levels
+            e.nil = r.nil
             if r.offsets is not None:
                 e.offsets, e.data = r.offsets, r.values
             assert_chunk(cd, e, where=f"case {i} col {col} enc {enc} type {ptype}")

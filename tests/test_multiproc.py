@@ -162,3 +162,15 @@ def test_bench_strong_main_line():
     d = _bench_dry(2, "--workload", "c3", "--rows", str(rows))
     assert d["scaling"] == "strong" and d["config"]["rows_total"] == rows and d["c3_strong"] is None
     assert [s["row_groups"] for s in d["shards"]] == [[0, 64], [64, 128]]
+
+
+def test_bench_mixed_strong_main_line():
+    """--workload mixed: north_star's target file (C2's six columns + C3's DELTA timestamps, 128 row
+    groups) as the strong-scaling main line: the blocks of one file tile it across the ranks."""
+    rows = 256_000
+    d = _bench_dry(2, "--workload", "mixed", "--mixed-rows", str(rows))
+    assert d["scaling"] == "strong" and d["config"]["rows_total"] == rows and d["config"]["workload"].startswith("mixed")
+    assert [s["row_groups"] for s in d["shards"]] == [[0, 64], [64, 128]]
+    assert sum(s["rows"] for s in d["shards"]) == rows
+    # every row decodes 4 + 8 + 4 + 1 (def level) + 1 + 16 + 8 bytes, plus 8 per non-null double
+    assert d["decoded_bytes_total"] > 42 * rows
