@@ -137,10 +137,16 @@ def cpu_comparator_pyarrow(data, rgs, bytes_per_row, threads):
 def pmc_traffic(kernel, workload, rows):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the same
     workload (profiles/*/pmc_summary.json, written by scripts/pmc_summary.py from FETCH_SIZE x2 +
-    WRITE_SIZE passes of this bench).  bench.py cannot collect PMC counters itself."""
+    WRITE_SIZE passes of this bench) that was measured on THIS build: its stamped source hash must
+    equal the loaded library's (pqh_build_id).  Returns (bytes or None, source or the reason there
+    is none).  bench.py cannot collect PMC counters itself."""
+    from parquet_go_amd import native
+
+    mine = native.build_info()["source_hash"]
     prof = os.path.join(ROOT, "profiles")
     if not os.path.isdir(prof):
-        return None, None
+        return None, "no profiles/ directory"
+    stale = []
     for tag in sorted(os.listdir(prof), reverse=True):
         p = os.path.join(prof, tag, "pmc_summary.json")
         if not os.path.exists(p):
@@ -155,9 +161,15 @@ def pmc_traffic(kernel, workload, rows):
         if s.get("variant"):  # an experiment's profile (a non-default switch), not this build's path
             continue
         k = s["kernels"].get(kernel) or {}
-        if k.get("hbm_traffic_bytes_per_launch"):
-            return k["hbm_traffic_bytes_per_launch"], f"profiles/{tag}/pmc_summary.json"
-    return None, None
+        if not k.get("hbm_traffic_bytes_per_launch"):
+            continue
+        theirs = (s.get("build") or {}).get("source_hash")
+        if theirs != mine:
+            stale.append(f"profiles/{tag} ({theirs or 'unstamped'})")
+            continue
+        return k["hbm_traffic_bytes_per_launch"], f"profiles/{tag}/pmc_summary.json (build {mine})"
+    return None, (f"no PMC summary of this build ({mine}) for this workload"
+                  + (f"; refused, measured on other builds: {', '.join(stale[:3])}" if stale else ""))
 
 
 def check_chunk(ctx, batch, chunk, res, np):
@@ -892,6 +904,7 @@ def main():
             else "int32" if args.workload == "c1" else "bytes (int64 offsets + string bytes)" if args.workload in ("c5", "c5z")
             else "int64/int32/bytes + u8 levels + int32 list offsets" if args.workload == "c4" else "int64",
             "data": "synthetic, seeded, written in the reference writer's layout (libpqgen)",
+            "build": native.build_info(),
             "config": {"workload": desc, "rows_total": f.num_rows if strong else f.num_rows * world,
                        "rows_per_gpu": my_rows, "row_groups_per_gpu": rg1 - rg0,
                        "pages_per_gpu": pages_per_gpu,

@@ -277,6 +277,9 @@ typedef struct pqh_batch pqh_batch;
 #define PQH_CTX_PROFILE 1u /* time every kernel launch with HIP events */
 
 int pqh_abi_version(void);
+/* The build's source hash (sha256 prefix of every source compiled into the library): profiles are
+ * stamped with it, so measurements are tied to the code they measured. */
+const char* pqh_build_id(void);
 int pqh_device_count(int32_t* count);
 int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out);
 /* Replace the context's flags (e.g. turn PQH_CTX_PROFILE on for a few runs).  Unprofiled batch runs

@@ -70,6 +70,30 @@ def build_gen(force=False):
     return out
 
 
+def source_hash():
+    """sha256 (16 hex digits) of every source compiled into libpqhip.so: the build id that PMC summaries
+    (profiles/*/pmc_summary.json) are stamped with, so bench.py only quotes counters of this build."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(set(HOST_SRCS + HIP_SRCS + HEADERS))
+    for rel in files:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(CSRC, rel), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(INCLUDE, "pqhip.h"), "rb") as fh:
+        h.update(b"include/pqhip.h\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def _git_head():
+    try:
+        return subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], text=True,
+                                       stderr=subprocess.DEVNULL).strip()
+    except Exception:
+        return None
+
+
 def build_hip(force=False):
     # PQH_HIP_LIB names an experiment variant (built with its own PQH_HIPFLAGS, loaded with the same
     # variable set); the product is libpqhip.so
@@ -79,11 +103,12 @@ def build_hip(force=False):
         objs = []
         bdir = os.path.join(PKG, "build", ("san-" if SANITIZE else "") + os.path.basename(out))
         os.makedirs(bdir, exist_ok=True)
+        sh = source_hash()
         for s in HIP_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                  "-munsafe-fp-atomics", "-I", INCLUDE] + os.environ.get("PQH_HIPFLAGS", "").split()
-                 + ["-c", os.path.join(CSRC, s), "-o", o])
+                  "-munsafe-fp-atomics", "-I", INCLUDE, f'-DPQH_SOURCE_HASH="{sh}"']
+                 + os.environ.get("PQH_HIPFLAGS", "").split() + ["-c", os.path.join(CSRC, s), "-o", o])
             objs.append(o)
         for s in HOST_SRCS:
             o = os.path.join(bdir, os.path.basename(s) + ".o")
@@ -93,6 +118,12 @@ def build_hip(force=False):
             objs.append(o)
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lz", "-lpthread"]
              + _san_link())
+        import json
+
+        # (travels with the tree to the GPU box, which has no .git: the commit the sources were built at)
+        with open(out + ".buildinfo.json", "w") as fh:
+            json.dump({"source_hash": sh, "git_head": _git_head(),
+                       "hipflags": os.environ.get("PQH_HIPFLAGS", "")}, fh)
     return out
 
 

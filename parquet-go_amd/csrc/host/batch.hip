@@ -424,6 +424,11 @@ extern "C" {
 
 int pqh_abi_version(void) { return PQH_ABI_VERSION; }
 
+#ifndef PQH_SOURCE_HASH
+#define PQH_SOURCE_HASH "unknown"
+#endif
+const char* pqh_build_id(void) { return PQH_SOURCE_HASH; }
+
 int pqh_device_count(int32_t* count) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);

@@ -104,6 +104,7 @@ ABI_VERSION = 7  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
+    ("pqh_build_id", cp, []),
     ("pqh_device_count", ctypes.c_int, [ctypes.POINTER(i32)]),
     ("pqh_ctx_create", ctypes.c_int, [i32, u32, ctypes.POINTER(vp)]),
     ("pqh_ctx_destroy", None, [vp]),
@@ -189,6 +190,26 @@ class PqhError(RuntimeError):
 def _check(rc, msg=""):
     if rc != OK:
         raise PqhError(rc, msg)
+
+
+def build_info():
+    """{"source_hash", "git_head"} of the loaded libpqhip: the hash compiled into it (pqh_build_id)
+    and the commit build.py recorded beside it (lib/*.buildinfo.json; None when it does not match)."""
+    import json
+    import os
+
+    h = (_lib.hip().pqh_build_id() or b"").decode()
+    info = {"source_hash": h, "git_head": None}
+    try:
+        with open(_lib.hip_path() + ".buildinfo.json") as fh:
+            bi = json.load(fh)
+        if bi.get("source_hash") == h:
+            info["git_head"] = bi.get("git_head")
+            if bi.get("hipflags"):
+                info["hipflags"] = bi["hipflags"]
+    except (OSError, ValueError):
+        pass
+    return info
 
 
 def device_count():

@@ -65,6 +65,15 @@ def main():
             for line in open(p):
                 if line.startswith("{"):
                     summary.setdefault("bench_lines", []).append(json.loads(line))
+    # the build the counters measured: the bench line's (pqh_build_id of the library that ran), else
+    # the build record beside the in-tree library.  bench.py quotes a summary only for this build.
+    builds = [ln.get("build") for ln in summary.get("bench_lines", []) if ln.get("build")]
+    if builds:
+        summary["build"] = builds[0]
+    else:
+        bi = os.path.join(root, "parquet-go_amd", "lib", "libpqhip.so.buildinfo.json")
+        if os.path.exists(bi):
+            summary["build"] = json.load(open(bi))
     json.dump(summary, open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
     print(json.dumps({k: v["hbm_traffic_bytes_per_launch"] for k, v in kernels.items()}, indent=1))
 
