@@ -1615,8 +1615,8 @@ hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int3
 // streams [0, n - n_lens): DELTA_BINARY_PACKED / DELTA_BYTE_ARRAY prefixes; [n - n_lens, n):
 // DELTA_LENGTH_BYTE_ARRAY lengths (with their tile byte sums)
 hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, int32_t n_lens, hipStream_t s) {
-  if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_fused<false>, dim3(n - n_lens), dim3(256), 0, s, b, streams);
-  if (n_lens > 0) hipLaunchKernelGGL(k_delta_fused<true>, dim3(n_lens), dim3(256), 0, s, b, streams + (n - n_lens));
+  if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_fused, dim3(n - n_lens), dim3(256), 0, s, b, streams);
+  if (n_lens > 0) hipLaunchKernelGGL(k_delta_fused_lens, dim3(n_lens), dim3(256), 0, s, b, streams + (n - n_lens));
   return hipGetLastError();
 }
 

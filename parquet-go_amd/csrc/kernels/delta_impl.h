@@ -1361,8 +1361,10 @@ __global__ __launch_bounds__(256) void k_delta_expand(DevBatch b, const Tile* ti
 // by bytes: as many blocks (<= 64) as fit a 16 KiB stage, so that several workgroups share a CU.
 constexpr int kPageStage = 16384 + 64;  // >= one block of 2048 64-bit deltas + alignment lead
 
-struct PageTileLds {
-  uint32_t data[kPageStage / 4 + 4];
+template <int kStage>
+struct PageTileLdsT {
+  static constexpr int kStageBytes = kStage;
+  uint32_t data[kStage / 4 + 4];
   int32_t mbbit[kTileBlocks][8];  // first bit of each miniblock's data in `data`
   uint8_t mbw[kTileBlocks][8];
   uint64_t md[kTileBlocks];
@@ -1375,6 +1377,15 @@ struct PageTileLds {
   int32_t narrow;
   int32_t pad;
 };
+using PageTileLds = PageTileLdsT<kPageStage>;
+
+// k_delta_fused's stage: 14.5 KiB, so that its LDS (20448 B) and registers (64 VGPRs, 8 waves per
+// SIMD) let 8 workgroups share a CU (2048 streams in flight instead of 1536: C3 32 row groups
+// k_delta_fused 0.504 -> 0.461 ms, 128 row groups 1.649 -> 1.605 ms, same box,
+// profiles/r05_exp/c3_probe_*.log).  A block whose bytes do not fit the stage (2048 values wider than
+// ~57 bits) ends the fused head; k_delta_walk / k_delta_page (16 KiB stage) take the rest.
+constexpr int kFusedStage = 14848;
+#define PQH_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 
 __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* streams) {
   __shared__ PageTileLds T;
@@ -1643,8 +1654,8 @@ __device__ __forceinline__ bool lds_block(const uint32_t* data, int32_t loc, int
 
 __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int32_t est, int nmax, bool is64, int mbc,
                           int gbytes, int16_t (*lst)[64], int32_t* blkbit, uint64_t* blkw, uint64_t* mdt, int lane,
-                          int& n_out, int32_t& next_out, bool& stop_out) {
-  const int32_t plim = kPageStage - 32, dlim = kPageStage - 16;
+                          int& n_out, int32_t& next_out, bool& stop_out, int32_t stage = kPageStage) {
+  const int32_t plim = stage - 32, dlim = stage - 16;
   const uint64_t lim = is64 ? 64 : 32;
   if (est <= 0) {  // first tile: the span of block 0
     int32_t d0 = -1;
@@ -1829,8 +1840,8 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
 // kLens: the DELTA_LENGTH streams' launch (tile byte sums in the row loop); the other streams run
 // the instantiation without them, which keeps its register budget (occupancy) unchanged.
 template <bool kLens>
-__global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* streams) {
-  __shared__ PageTileLds T;
+__device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams) {
+  __shared__ PageTileLdsT<kLens ? kPageStage : kFusedStage> T;
   __shared__ int32_t s_blkbit[kTileBlocks];
   __shared__ uint64_t s_blkw[kTileBlocks];
   __shared__ int64_t s_h;
@@ -1899,7 +1910,7 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
     for (;;) {
       __syncthreads();  // the previous tile's readers of T are done
       const int64_t a0 = h - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(h)) & 15);
-      stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, kPageStage / 16, img_len - a0);
+      stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, T.kStageBytes / 16, img_len - a0);
       __syncthreads();
       if (tid < 64) {
         int n;
@@ -1907,7 +1918,7 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
         bool stop;
         const int nmax = kmax - r < kTileBlocks ? kmax - r : kTileBlocks;
         lds_chase(T.data, int32_t(h - a0), int32_t(e - a0), est, nmax, is64, mbc,
-                  gbytes, s_lst, s_blkbit, s_blkw, T.md, lane, n, nxt, stop);
+                  gbytes, s_lst, s_blkbit, s_blkw, T.md, lane, n, nxt, stop, T.kStageBytes);
         if (tid == 0) {
           s_n = n;
           s_stop = stop;
@@ -1952,6 +1963,13 @@ __global__ __launch_bounds__(256) void k_delta_fused(DevBatch b, const Tile* str
     b.dstates[p].head_carry = carry;
     b.dstates[p].head_neg = int64_t(s_neg);  // counts only if k_delta_walk accepts the head
   }
+}
+
+__global__ __launch_bounds__(256) PQH_FUSED_ATTR void k_delta_fused(DevBatch b, const Tile* streams) {
+  delta_fused_body<false>(b, streams);
+}
+__global__ __launch_bounds__(256) void k_delta_fused_lens(DevBatch b, const Tile* streams) {
+  delta_fused_body<true>(b, streams);
 }
 
 // k_delta_init (page mode, before k_scan): deltaBitPackDecoder.init of every DELTA_BINARY_PACKED
