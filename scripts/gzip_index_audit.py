@@ -99,6 +99,10 @@ class Page:
         self.dst = bytearray(total)
         self.reads = {"dst": [0, 0, None, None], "src": [0, 0, None, None]}  # count, oob, min, max
         self.oob = []
+        # the write side: batches (gz_batch: [d, d + T)) and bulk stored copies ([d, d + left)), the
+        # highest byte each writes, and how many would end past the page (what the pre-177f91c kernel,
+        # without gz_batch's d + T > total guard, would have stored out of bounds)
+        self.writes = {"batches": 0, "bulk": 0, "bytes": 0, "max_end": 0, "past_page": 0}
 
     # ---- the stage: bytes [a0, a0 + STAGE + 96) of src, past the input end read as 0
     def stage(self, a0):
@@ -152,7 +156,15 @@ class Page:
         return (pos if f < 0 else f), pos, o, k, 0
 
     # ---- one batch of T bytes (tokens 1..nE-1) at page offset d: gz_batch's reads, checked
+    def write(self, d, n, kind):
+        w = self.writes
+        w[kind] += 1
+        w["bytes"] += n
+        w["max_end"] = max(w["max_end"], d + n)
+        w["past_page"] += d + n > self.total
+
     def batch(self, T, tokens, litb, d):
+        self.write(d, T, "batches")
         if T < 0 or T > OUT or not (1 <= len(tokens) + 1 <= MAXE) or d + T > self.total:
             raise Corrupt("internal: batch geometry")  # gz_batch's first guard
         emap = [0] * T
@@ -419,6 +431,7 @@ class Page:
                     if T == 0 and not tokens and left >= OUT:  # bulk copy
                         if q + left > self.n or d + left > self.total:
                             raise Corrupt("stored past")
+                        self.write(d, left, "bulk")
                         self.dst[d:d + left] = self.src[q:q + left]
                         d += left
                         self.stored_left = 0
@@ -483,6 +496,15 @@ def audit(name, stream, size, stats):
         r[0] += a[0]
         r[1] += a[1]
     stats["oob"] += pg.oob[:5]
+    w = stats["writes"]
+    for k in ("batches", "bulk", "bytes", "past_page"):
+        w[k] += pg.writes[k]
+    if pg.writes["past_page"]:
+        stats["oob"].append(("write past the page", name, pg.writes["max_end"], total))
+    if pg.writes["max_end"] > total:
+        w["pages_past"] += 1
+    if st == "ok":
+        w["ok_pages_ending_at_size"] += pg.writes["max_end"] == total or total == 0
 
 
 def main():
@@ -498,7 +520,9 @@ def main():
     from parquet_go_amd import datasets
     from parquet_go_amd import writer as W
 
-    stats = {"pages": 0, "match": 0, "mismatch": [], "internal": [], "oob": [], "dst": [0, 0], "src": [0, 0]}
+    stats = {"pages": 0, "match": 0, "mismatch": [], "internal": [], "oob": [], "dst": [0, 0], "src": [0, 0],
+             "writes": {"batches": 0, "bulk": 0, "bytes": 0, "past_page": 0, "pages_past": 0,
+                        "ok_pages_ending_at_size": 0}}
     # 1. the C5z --codec gzip pages (the workload of the r03 fault): the walker's compressed blocks
     data = datasets.c5z(rows=400_000, row_groups=1, codec=W.GZIP)
     fr = O.FileReader(data)
@@ -513,9 +537,12 @@ def main():
         pos += ph[3]
         k += 1
     n_c5z = stats["pages"]
-    # 2. every crafted valid stream and error class of the device-codec tests, plus seeded mutants
+    # 2. every crafted valid stream and error class of the device-codec tests (valid_cases includes the
+    # stored-block streams whose stored bytes lie past the 8 KiB stage: gz_batch's `src` read-backs),
+    # plus seeded mutants of the valid ones and of the stored-block streams
     valid = [(n, s, len(O.gzip_decode(s))) for n, s, _ in G.valid_cases()]
-    for name, s, size in valid + G.error_cases() + G.mutants(valid[::2], per=args.mutants):
+    stored = [(n, s, len(O.gzip_decode(s))) for n, s, _ in G.stored_mix_cases()]
+    for name, s, size in valid + G.error_cases() + G.mutants(valid[::2] + stored, per=args.mutants):
         audit(name, s, size, stats)
     print(f"pages emulated: {stats['pages']} ({n_c5z} C5z gzip pages of 1 MiB, {stats['pages'] - n_c5z} crafted "
           f"streams and mutants)")
@@ -523,6 +550,10 @@ def main():
     print(f"HBM read-backs: dst (back-references before the batch) {stats['dst'][0]}, out of [0, d): "
           f"{stats['dst'][1]}; src (stored bytes outside the stage) {stats['src'][0]}, out of [0, n): "
           f"{stats['src'][1]}")
+    w = stats["writes"]
+    print(f"writes: {w['batches']} batches + {w['bulk']} bulk stored copies, {w['bytes']} bytes; ending past the "
+          f"page's size: {w['past_page']} (pages: {w['pages_past']}); decoded pages whose last write ends exactly "
+          f"at their size: {w['ok_pages_ending_at_size']}")
     print(f"internal inconsistencies (stale tokens, token outside its batch, two cuts): {len(stats['internal'])}")
     for x in stats["mismatch"][:10] + stats["internal"][:10] + stats["oob"][:10]:
         print("  ", x)

@@ -179,6 +179,42 @@ def valid_cases(seed=5):
     stored = b2.bytes() + big
     tail = fixed_block([(258, 32768), (3, 32768), 256]).bytes()
     out.append(("max-distance", member(stored + tail, big + big[:258] + big[258:261]), None))
+    return out + stored_mix_cases()
+
+
+def stored_block(data, final=False):
+    """A byte-aligned stored block (BFINAL, BTYPE 00, LEN, NLEN, bytes)."""
+    return bytes([1 if final else 0]) + struct.pack("<HH", len(data), ~len(data) & 0xFFFF) + data
+
+
+def stored_mix_cases(seed=8):
+    """Streams whose stored bytes lie outside k_gzip's 8 KiB stage within one serial batch (the
+    HBM `src` read-back path of gz_batch): runs of empty stored blocks that carry the input ahead
+    without output, then stored data starting near the stage's end; many tiny stored blocks (the
+    1024-token batch spans more input than the stage); Huffman segments (full flushes) between
+    them.  (name, stream, None)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for empties, ln in ((1400, 8000), (1500, 8191), (1510, 5000), (1000, 8192), (1509, 1), (700, 20000)):
+        data = rng.bytes(ln)
+        raw_ = stored_block(b"") * empties + stored_block(data) + stored_block(b"", final=True)
+        out.append((f"stored-after-{empties}-empty-{ln}", member(raw_, data), None))
+    for sizes in ((1, 16), (4, 9), (0, 3)):
+        chunks = [rng.bytes(int(rng.integers(sizes[0], sizes[1] + 1))) for _ in range(3000)]
+        data = b"".join(chunks)
+        raw_ = b"".join(stored_block(c) for c in chunks) + stored_block(b"", final=True)
+        out.append((f"stored-tiny-{sizes[0]}-{sizes[1]}", member(raw_, data), None))
+    # Huffman segments (each its own compressor, ended by a full flush: byte aligned, no reference
+    # into earlier segments), empty stored blocks and stored data, interleaved
+    parts, data = [], b""
+    for k in range(12):
+        t = _text(rng, int(rng.integers(100, 30000)))
+        c = zlib.compressobj(int(rng.integers(1, 10)), zlib.DEFLATED, -15)
+        parts.append(c.compress(t) + c.flush(zlib.Z_FULL_FLUSH))
+        d2 = rng.bytes(int(rng.integers(1, 12000)))
+        parts.append(stored_block(b"") * int(rng.integers(0, 1600)) + stored_block(d2))
+        data += t + d2
+    out.append(("stored-huffman-mix", member(b"".join(parts) + stored_block(b"", final=True), data), None))
     return out
 
 
