@@ -163,7 +163,9 @@ typedef struct pqh_page {
   int32_t def_levels_byte_length; /* DataPageHeaderV2 only (else 0) */
   int32_t rep_levels_byte_length; /* DataPageHeaderV2 only (else 0) */
   int32_t chunk;                  /* index of the owning pqh_chunk */
-  int32_t reserved;
+  int32_t num_nulls;              /* DataPageHeaderV2.num_nulls (else 0): a hint only -- the decode counts
+                                     the definition levels as the reference does (k_flat speculates
+                                     notNull = num_values - num_nulls and checks it) */
 } pqh_page;
 
 /* Device-side decompression: where one page's source bytes lie and how its image

@@ -596,6 +596,7 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       P.encoding = Q.encoding;
       P.def_len = Q.def_levels_byte_length;
       P.rep_len = Q.rep_levels_byte_length;
+      P.num_nulls = Q.page_type == PQH_DATA_PAGE_V2 ? Q.num_nulls : 0;
       P.chunk = c;
       P.dict_page = -1;
       P.ck_rep = P.ck_def = P.ck_val = -1;
@@ -842,7 +843,9 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       for (int32_t i = 0; i < D.num_pages; i++) {
         const DevPage& P = b->hpages[size_t(D.first_page + i)];
         b->flat_base[size_t(D.first_page + i)] = acc;
-        if (P.page_type != PQH_DICTIONARY_PAGE) acc += std::max(0, P.num_values);
+        // (nullable chunks: V2 pages' notNull = num_values - num_nulls, checked by k_flat's page checks)
+        if (P.page_type != PQH_DICTIONARY_PAGE)
+          acc += std::max(0, P.num_values - (D.max_def > 0 ? std::max(0, P.num_nulls) : 0));
       }
     }
   }
@@ -1030,6 +1033,10 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     f.span = t.span;
     f.tkind = t.kind;
     f.host_err = P.host_err;
+    const DevChunk& C = b->hchunks[size_t(P.chunk)];
+    f.max_def = C.max_def;
+    f.num_nulls = P.num_nulls;
+    f.def_out = C.def_levels ? C.def_levels + P.level_base : nullptr;
     b->flat_tiles.push_back(f);
   }
   // page mode: the (shorter) stream list takes the delta tile list's place
@@ -1096,13 +1103,16 @@ bool flat_batch(const pqh_batch* b) {
       !b->global_tiles.empty())
     return false;
   if (b->pages.empty() || b->pages.size() > kFlatMaxPages || b->expand_tiles.size() > kFlatMaxTiles) return false;
+  // flat columns, required or nullable (max_def 1: only with V2 pages, whose headers give the
+  // speculative notNull and whose levels sit raw at the image's start)
   if (!std::all_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& C) {
-        return C.max_rep == 0 && C.max_def == 0 && C.value_size > 0 && !C.value_nil;
+        return C.max_rep == 0 && C.max_def <= 1 && C.value_size > 0 && !C.value_nil;
       }))
     return false;
-  return std::all_of(b->hpages.begin(), b->hpages.end(), [](const DevPage& P) {
-    return P.page_type == PQH_DICTIONARY_PAGE || P.kind == K_DICT || P.kind == K_PLAIN_FIXED ||
-           P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
+  return std::all_of(b->hpages.begin(), b->hpages.end(), [&](const DevPage& P) {
+    if (P.page_type == PQH_DICTIONARY_PAGE) return true;
+    if (b->hchunks[size_t(P.chunk)].max_def > 0 && P.page_type != PQH_DATA_PAGE_V2) return false;
+    return P.kind == K_DICT || P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
   });
 }
 

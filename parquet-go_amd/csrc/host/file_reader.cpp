@@ -245,6 +245,7 @@ struct PageHdr {
   int32_t num_values = 0, encoding = 0;
   int32_t def_enc = 0, rep_enc = 0;  // DataPageHeader level encodings
   int32_t def_len = 0, rep_len = 0;
+  int32_t num_nulls = 0;             // DataPageHeaderV2 (a hint for k_flat's speculation)
 };
 
 bool parse_page_header(TReader& r, PageHdr& h) {
@@ -274,6 +275,7 @@ bool parse_page_header(TReader& r, PageHdr& h) {
     h.has_v2 = true;
     if (h.type == PQH_DATA_PAGE_V2) {
       h.num_values = int32_t(d->get_i(1));
+      h.num_nulls = int32_t(d->get_i(2));
       h.encoding = int32_t(d->get_i(4));
       h.def_len = int32_t(d->get_i(5));
       h.rep_len = int32_t(d->get_i(6));
@@ -446,6 +448,7 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if ((rc = block_reader(levels))) return fail(rc);
       op.pg.def_levels_byte_length = h.def_len;
       op.pg.rep_levels_byte_length = h.rep_len;
+      op.pg.num_nulls = h.num_nulls;
     } else {
       return fail(PQH_ERR_PAGE_HEADER);  // "DATA_PAGE or DATA_PAGE_V2 type supported"
     }

@@ -74,7 +74,7 @@ struct DevPage {
   int32_t aux_base;      // byte-array dictionary page: first entry of its dcum table
   int32_t batile_base;   // byte-array data page: first kBaTile tile sum (chunk-contiguous)
   int32_t batile_n;
-  int32_t pad;
+  int32_t num_nulls;     // DataPageHeaderV2.num_nulls: k_flat's speculative notNull (checked), else 0
 };
 
 struct DevChunk {
@@ -243,6 +243,8 @@ struct FlatTile {
   int32_t value_size, rep_len, def_len, dict_n;  // dict_n: the dictionary page's num_values
   int32_t dict_len, k, span, tkind;
   uint64_t host_err;
+  PQH_G uint8_t* def_out;  // nullable flat chunks (max_def 1, V2 pages): the page's definition levels
+  int32_t num_nulls, max_def;
 };
 
 constexpr int kLevelSpan = 4;  // 32768 level slots per tile

@@ -280,8 +280,38 @@ __device__ __forceinline__ WalkOut walk_hybrid(const uint8_t* img, int64_t s, in
 // its four waves run the same (wave-uniform) framing and run walks and split the notNull count
 // over bit-packed definition levels.
 // ------------------------------------------------------------------------------------------------
-// kLevels = false (k_flat): the page's column has no level streams (a page that has one gets
-// PQH_ERR_INTERNAL, which k_flat's check turns into a decode by the three kernels).
+// k_flat's nullable flat pages (max_def 1, V2): the definition levels [s, e) as ONE bit-packed run of
+// width 1 covering the n slots (the reference writer's layout, hybrid_encoder.go:55-70) -> notNull =
+// the popcount of its first n bits; -1 for any other stream (the page check then fails and the three
+// kernels decode the batch, walking the levels exactly).  Wave-uniform.
+__device__ __forceinline__ int64_t flat_def_count(const uint8_t* img, int64_t s, int64_t e, int64_t n, int lane) {
+  if (n <= 0) return 0;
+  uint64_t h = 0;
+  int len = 0;
+  for (int k = 0; k < 5 && s + k < e; k++) {
+    const uint32_t c = img[s + k];
+    h |= uint64_t(c & 0x7f) << (7 * k);
+    if (c < 0x80) {
+      len = k + 1;
+      break;
+    }
+  }
+  if (len == 0 || h > 0x7fffffffull || !(h & 1) || int64_t(h >> 1) * 8 < n) return -1;
+  const int64_t data = s + len, nbytes = (n + 7) >> 3;
+  if (data + nbytes > e) return -1;
+  int64_t cnt = 0;
+  for (int64_t i = lane; i < nbytes; i += 64) {
+    uint32_t x = img[data + i];
+    if (i == nbytes - 1 && (n & 7)) x &= (1u << (n & 7)) - 1;
+    cnt += __popc(x);
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  return cnt;
+}
+
+// kLevels = false (k_flat): the page's column has no level streams, or (nullable flat, V2) one
+// single-run definition stream counted by flat_def_count; any other page gets PQH_ERR_INTERNAL,
+// which k_flat's check turns into a decode by the three kernels.
 template <int kNwv, bool kLevels = true>
 __device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int lane, int wv, int64_t* s_nn,
                                                    bool store = true) {
@@ -392,8 +422,11 @@ __device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int
     S.val_s = int32_t(hs);
     S.val_e = int32_t(he);
     // --- readValues(numValues) ---
+    int64_t flat_nn = -1;  // k_flat: the notNull of a nullable flat page's single-run definition levels
     if constexpr (!kLevels) {
-      if (rw > 0 || dw > 0) err = err_key(0, 0, PQH_ERR_INTERNAL);
+      if (rw > 0 || dw > 1 || (dw == 1 && (P.page_type != PQH_DATA_PAGE_V2 || def_s < 0 ||
+                                           (flat_nn = flat_def_count(img, def_s, def_e, n, lane)) < 0)))
+        err = err_key(0, 0, PQH_ERR_INTERNAL);
     }
     if (err == kNoError && n > 0) {
       if (kLevels && rw > 0) {  // decodePackedArray(rDecoder, n)
@@ -404,7 +437,7 @@ __device__ __forceinline__ PageState prologue_page(const DevBatch& b, int p, int
           err = r.err;
         }
       }
-      int64_t nn = n;
+      int64_t nn = !kLevels && dw == 1 ? flat_nn : n;
       if (kLevels && err == kNoError && dw > 0) {  // decodePackedArray(dDecoder, n) + notNull
         if (def_s < 0) {
           err = err_key(2, 0, PQH_ERR_READER_NOT_INITIALIZED);
@@ -1270,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_dict_global(DevBatch b, const Tile* til
 // ------------------------------------------------------------------------------------------------
 // k_prologue's state for a clean, simple page (false: the page is not one; nothing is assumed).
 __device__ __forceinline__ bool flat_spec(const DevBatch& b, const DevPage& P, int64_t value_base, PageState& S,
-                                          Ckpt& ck) {
+                                          Ckpt& ck, int max_def = 0, Ckpt* ckd = nullptr) {
   S.err = kNoError;
   S.nn = 0;
   S.width = 0;
@@ -1294,6 +1327,38 @@ __device__ __forceinline__ bool flat_spec(const DevBatch& b, const DevPage& P, i
   S.val_s = int32_t(vs);
   S.val_e = int32_t(L);
   S.val_limit = 0;
+  int64_t nn = n;  // notNull
+  if (max_def > 0) {
+    // nullable flat (V2): the definition levels raw at [rep_len, rep_len + def_len), ONE bit-packed
+    // run of width 1 over the n slots; notNull = num_values - num_nulls from the header (the page
+    // check counts the levels)
+    if (P.page_type != PQH_DATA_PAGE_V2 || max_def != 1 || P.def_len <= 0 || P.num_nulls < 0 || P.num_nulls > n)
+      return false;
+    S.def_s = P.rep_len;
+    S.def_e = P.rep_len + P.def_len;
+    nn = n - P.num_nulls;
+    if (n > 0) {
+      const uint8_t* img = b.payload + P.image_off;
+      const uint64_t q = ld64_masked(img + S.def_s, img + S.def_e);
+      uint64_t h = 0;
+      int len = 0;
+      for (int k = 0; k < 5; k++) {
+        const uint32_t c = uint32_t(q >> (8 * k)) & 0xff;
+        h |= uint64_t(c & 0x7f) << (7 * k);
+        if (c < 0x80) {
+          len = k + 1;
+          break;
+        }
+      }
+      if (len == 0 || S.def_s + len > S.def_e || h > 0x7fffffffull || !(h & 1)) return false;
+      const int64_t groups = int64_t(h >> 1), data = S.def_s + len;
+      if (groups * 8 < n || data + (n + 7) / 8 > S.def_e) return false;
+      const int64_t next = data + groups, cnt = groups * 8;
+      if (ckd)
+        *ckd = Ckpt{0, int32_t(cnt < 0x7fffffff ? cnt : 0x7fffffff), int32_t(data),
+                    int32_t(next < 0x7fffffff ? next : 0x7fffffff) | int32_t(0x80000000u)};
+    }
+  }
   if (P.kind == K_DICT) {
     if (vs >= L) return false;
     const uint8_t* img = b.payload + P.image_off;
@@ -1302,9 +1367,9 @@ __device__ __forceinline__ bool flat_spec(const DevBatch& b, const DevPage& P, i
     if (w > 32) return false;
     S.width = int16_t(w);
     S.val_s = int32_t(vs + 1);
-    if (n <= 0) return true;
-    S.nn = int32_t(n);
-    S.val_limit = int32_t(n);
+    if (nn <= 0) return true;
+    S.nn = int32_t(nn);
+    S.val_limit = int32_t(nn);
     if (w == 0) return true;  // no reads: ck = {0, 2^31-1, 0, 0}, as walk_hybrid's
     // the first run header (at most 5 bytes for a count < 2^31), then one bit-packed run over all n
     uint64_t h = 0;
@@ -1319,25 +1384,25 @@ __device__ __forceinline__ bool flat_spec(const DevBatch& b, const DevPage& P, i
     }
     if (len == 0 || vs + 1 + len > L || h > 0x7fffffffull || !(h & 1)) return false;
     const int64_t groups = int64_t(h >> 1), data = vs + 1 + len;
-    if (groups * 8 < n) return false;
+    if (groups * 8 < nn) return false;
     const int64_t gf = (L - data + w - 1) / w;  // groups readable before EOF
-    if (data >= L || gf < (n + 7) / 8) return false;
+    if (data >= L || gf < (nn + 7) / 8) return false;
     const int64_t next = data + groups * w, cnt = groups * 8;
     ck = Ckpt{0, int32_t(cnt < 0x7fffffff ? cnt : 0x7fffffff), int32_t(data),
               int32_t(next < 0x7fffffff ? next : 0x7fffffff) | int32_t(0x80000000u)};
     return true;
   }
-  if (n <= 0) return P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
+  if (nn <= 0) return P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96 || P.kind == K_PLAIN_BOOL;
   const int64_t avail = L - vs;
   if (P.kind == K_PLAIN_FIXED || P.kind == K_PLAIN_INT96) {
-    if (P.value_size <= 0 || avail / P.value_size < n) return false;
+    if (P.value_size <= 0 || avail / P.value_size < nn) return false;
   } else if (P.kind == K_PLAIN_BOOL) {
-    if (avail * 8 < n) return false;
+    if (avail * 8 < nn) return false;
   } else {
     return false;
   }
-  S.nn = int32_t(n);
-  S.val_limit = int32_t(n);
+  S.nn = int32_t(nn);
+  S.val_limit = int32_t(nn);
   return true;
 }
 
@@ -1354,7 +1419,7 @@ __device__ __forceinline__ void flat_check(const DevBatch& b, int32_t p, const i
   const int64_t vb = spec_base[p];
   PageState spec;
   Ckpt ck;
-  const bool ok = flat_spec(b, P, vb, spec, ck);
+  const bool ok = flat_spec(b, P, vb, spec, ck, b.chunks[P.chunk].max_def);
   PageState S = prologue_page<1, false>(b, p, lane, 0, nullptr, false);
   S.value_base = vb;
   if (lane == 0) {
@@ -1392,6 +1457,7 @@ __global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles,
   P.rep_len = f.rep_len;
   P.def_len = f.def_len;
   P.host_err = f.host_err;
+  P.num_nulls = f.num_nulls;
   DevChunk C;
   __builtin_memset(&C, 0, sizeof(C));
   C.values = f.values;
@@ -1406,10 +1472,18 @@ __global__ __launch_bounds__(256) void k_flat(DevBatch b, const FlatTile* tiles,
     }
   }
   PageState S;
-  Ckpt ck;
-  const bool spec_ok = flat_spec(b, P, f.value_base, S, ck);
+  Ckpt ck, ckd;
+  const bool spec_ok = flat_spec(b, P, f.value_base, S, ck, f.max_def, &ckd);
   if (spec_ok) {  // (otherwise the page's check flags it)
     switch (f.tkind) {
+      case TK_LEVELS: {  // nullable flat: the definition levels (one bit-packed run of width 1)
+        const int64_t t0 = int64_t(t.k) * kHybridTile;
+        int64_t t1 = t0 + int64_t(t.span) * kHybridTile;
+        if (t1 > P.num_values) t1 = P.num_values;
+        LevelSink sink{f.def_out};
+        if (f.def_out && t0 < t1) expand_hybrid(b.payload + P.image_off, S.def_e, 1, ckd, t0, t1, L, stage, sink);
+        break;
+      }
       case TK_COPY: tile_copy_s(b, t, P, C, S); break;
       case TK_BOOL: tile_bool_plain_s(b, t, P, C, S); break;
       case TK_DICT: tile_dict_s<CkptConst, true>(b, t, P, C, S, K, dict_lds, CkptConst{ck}, L, stage, flag); break;

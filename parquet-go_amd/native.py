@@ -41,7 +41,7 @@ class Column(ctypes.Structure):
 class Page(ctypes.Structure):
     _fields_ = [("image_offset", i64), ("image_len", i32), ("page_type", i32), ("num_values", i32),
                 ("encoding", i32), ("def_levels_byte_length", i32), ("rep_levels_byte_length", i32),
-                ("chunk", i32), ("reserved", i32)]
+                ("chunk", i32), ("num_nulls", i32)]
 
 
 class Chunk(ctypes.Structure):

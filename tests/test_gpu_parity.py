@@ -339,6 +339,61 @@ def test_flat_one_launch(pq, monkeypatch, flat):
     ctx.close()
 
 
+def _nullable_flat(n, seed=23, null_frac=0.01):
+    """Nullable (max_def 1) flat fixed-width columns, V2 pages (reference-writer levels: one
+    bit-packed run of width 1), plus a required column: the mixed workload's shape."""
+    W = fixtures.W
+    rng = np.random.default_rng(seed)
+
+    def defs():
+        return (rng.random(n) >= null_frac).astype(np.uint8)
+
+    d0, d1, d2 = defs(), defs(), defs()
+    cols = [("f64", W.Column(W.DOUBLE, rng.standard_normal(int(d0.sum())), def_levels=d0, use_dict=False), W.OPTIONAL),
+            ("i32_dict", W.Column(W.INT32, rng.integers(0, 900, int(d1.sum())).astype(np.int32), def_levels=d1),
+             W.OPTIONAL),
+            ("flba", W.Column(W.FIXED_LEN_BYTE_ARRAY, rng.integers(0, 256, (int(d2.sum()), 16), dtype=np.uint8),
+                              def_levels=d2, type_length=16, use_dict=False), W.OPTIONAL),
+            ("i64", W.Column(W.INT64, rng.integers(-2**62, 2**62, n), use_dict=False), W.REQUIRED)]
+    return W.flat(cols, n // 2, v2=True, max_page_size=48 * 1024)
+
+
+@pytest.mark.parametrize("flat", ["one_launch", "three_kernels"])
+def test_flat_nullable_v2(pq, monkeypatch, flat):
+    """Nullable flat columns with V2 pages decode in k_flat's one launch too: the speculative
+    notNull is the header's num_values - num_nulls, the definition levels (one bit-packed run) are
+    expanded by level tiles of the same launch, and the page checks count the levels.  A page whose
+    num_nulls hint is wrong (the explicit cases below carry 0) fails the speculation and the batch is
+    decoded again by the three kernels: the reference's results either way."""
+    monkeypatch.setenv("PQH_FLAT", "1" if flat == "one_launch" else "0")
+    ctx = pq.native.Context(0, profile=True)
+    for null_frac in (0.01, 0.5, 0.0, 1.0):
+        data = _nullable_flat(30000, null_frac=null_frac)
+        f = pq.native.File(data)
+        res, b, hb = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(4)), return_batch=True)
+        paths = b.paths()
+        stats = {s.name.decode(): s.launches for s in b.kernel_stats() if s.launches}
+        assert paths["flat_fallbacks"] == 0, (null_frac, paths)
+        want = {"k_flat": 1, "k_expand": 0} if flat == "one_launch" else {"k_flat": 0, "k_expand": 1}
+        assert {k: stats.get(k, 0) for k in want} == want, (null_frac, stats)
+        fr = O.FileReader(data)
+        for k, col in enumerate(res):
+            rg, ci = divmod(k, 4)
+            assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"nulls {null_frac} rg{rg} {col.path}")
+        assert sum(1 for c in res if c.def_levels is not None and (c.def_levels == 0).any()) == \
+            (0 if null_frac == 0.0 else 6)
+        b.close()
+        hb.close()
+    # the same pages as explicit cases: num_nulls hint 0 on pages that hold nulls
+    data = _nullable_flat(20000)
+    clean = _page_sets_cases(pq, data)
+    stats = {}
+    compared, errors = _run_cases(pq, ctx, clean, stats, runs=3)
+    assert compared == len(clean) and errors == 0
+    assert stats.get("k_expand", 0) == (1 if flat == "one_launch" else 3), stats
+    ctx.close()
+
+
 def _page_sets_cases(pq, data):
     """Every data page of `data` as an unmutated case."""
     out = []
