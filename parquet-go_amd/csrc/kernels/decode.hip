@@ -1260,12 +1260,7 @@ __device__ __forceinline__ void tile_bool_plain(const DevBatch& b, const Tile& t
 #include "snappy_emit.h"
 #include "gzip_impl.h"
 
-#ifdef PQH_EXPAND_OCC  // experiments: waves per SIMD the register allocation must allow
-#define PQH_EXPAND_ATTR __attribute__((amdgpu_waves_per_eu(PQH_EXPAND_OCC)))
-#else
-#define PQH_EXPAND_ATTR
-#endif
-__global__ __launch_bounds__(256) PQH_EXPAND_ATTR void k_expand(DevBatch b, const Tile* tiles) {
+__global__ __launch_bounds__(256) void k_expand(DevBatch b, const Tile* tiles) {
   __shared__ TileLds L;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // [stage kStageBytes+16][dictionary]
   uint32_t* stage = reinterpret_cast<uint32_t*>(lds);
