@@ -330,27 +330,33 @@ __device__ __forceinline__ void ba_stage(ChainLds& C, const BaPageCtx& c, int64_
   }
 }
 
-// Resolve and summarise one window (whole workgroup; C.win staged from ba_wbase(c, w)).  Its records
-// go to the window's scratch in order as the bytes of the records before each one within the window
-// (16 bits: a record starts inside the window, so fewer than kChainWin bytes precede it); the window's
-// total is res->bytes: record i's length is wrec[i + 1] - wrec[i], the last one's bytes - wrec[count - 1].
-__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res, uint16_t* wrec) {
+// Segment j's records on the true chain after a window's resolution (per thread, in registers):
+// their start marks, their count, the index of the first one in the window, and the bytes of the
+// window's records before it.
+struct SegRecs {
+  uint64_t m[kChainWords];
+  int32_t cnt, li, lb;
+};
+
+// Resolve and summarise one window (whole workgroup; C.win staged from ba_wbase(c, w)): *res (thread
+// 0) and every segment's records (sr).
+__device__ void ba_window_segs(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res,
+                               SegRecs& sr) {
   const int j = threadIdx.x;
   const int64_t wend64 = c.entry + (w + 1) * kChainStride;
   BaWin r{int32_t(entry64), int32_t(entry64), 0, 0, 0, -1, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++) sr.m[k] = 0;
+  sr.cnt = sr.li = sr.lb = 0;
   if (entry64 >= c.e0 || entry64 >= wend64) {  // no record starts in the window (or no bytes left)
     if (entry64 >= c.e0 && entry64 < wend64) r.bad = PQH_ERR_EOF;
-    if (j == 0) {
-      *res = r;
-      wrec[0] = 0;
-    }
+    if (j == 0) *res = r;
     return;
   }
   const int32_t wb = int32_t(ba_wbase(c, w)), wend = int32_t(wend64), entry = int32_t(entry64);
   chain_resolve(C, wb, wend, int32_t(c.e0), entry);
   const int fb = C.first_bad;
-  uint64_t m[kChainWords];
-  const int cnt = chain_marks(C, j, wb, entry, fb, m);
+  const int cnt = chain_marks(C, j, wb, entry, fb, sr.m);
   // The segment's records are consecutive on the chain, so their lengths need no LDS reads: record
   // r's length is the next record's start - r's start - 4, and the last one ends at the segment's
   // exit (the start of the next record, or of the invalid record that ended the chain).
@@ -358,21 +364,14 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
   int32_t first = -1;
 #pragma unroll
   for (int k = kChainWords - 1; k >= 0; k--)
-    if (m[k]) first = 64 * k + __builtin_ctzll(m[k]);
+    if (sr.m[k]) first = 64 * k + __builtin_ctzll(sr.m[k]);
   const int32_t bytes = cnt > 0 ? exj - (s0 + first) - 4 * cnt : 0;
   // records and bytes of the window both fit 32 bits: one scan of the pair
   uint64_t tot;
   const uint64_t ex = block_exclusive_scan((uint64_t(uint32_t(cnt)) << 32) | uint32_t(bytes), C.wsum, &tot);
-  int32_t li = int32_t(ex >> 32), lb = int32_t(uint32_t(ex));
-  int32_t prev = -1;
-#pragma unroll
-  for (int k = 0; k < kChainWords; k++)
-    for (uint64_t x = m[k]; x; x &= x - 1) {
-      const int32_t pos = 64 * k + __builtin_ctzll(x);
-      if (prev >= 0) lb += pos - prev - 4;
-      wrec[li++] = uint16_t(lb);
-      prev = pos;
-    }
+  sr.cnt = cnt;
+  sr.li = int32_t(ex >> 32);
+  sr.lb = int32_t(uint32_t(ex));
   if (j == 0) {
     const int32_t nrec = int32_t(tot >> 32), btot = int32_t(uint32_t(tot));
     r.count = nrec;
@@ -386,6 +385,38 @@ __device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t en
     }
     *res = r;
   }
+}
+
+// The segment's records with window indices in [lo, hi) as their exclusive byte offsets within the
+// window: list[i - lo] for record i.
+template <class T>
+__device__ __forceinline__ void seg_list(const SegRecs& sr, int32_t lo, int32_t hi, T* list) {
+  if (sr.li >= hi || sr.li + sr.cnt <= lo) return;
+  int32_t li = sr.li, lb = sr.lb, prev = -1;
+#pragma unroll
+  for (int k = 0; k < kChainWords; k++)
+    for (uint64_t x = sr.m[k]; x; x &= x - 1) {
+      const int32_t pos = 64 * k + __builtin_ctzll(x);
+      if (prev >= 0) lb += pos - prev - 4;
+      if (li >= hi) return;
+      if (li >= lo) list[li - lo] = uint16_t(lb);
+      li++;
+      prev = pos;
+    }
+}
+
+// Resolve and summarise one window into the scratch: the records go to wrec in order as the bytes
+// of the records before each one within the window (16 bits: a record starts inside the window, so
+// fewer than kChainWin bytes precede it); the window's total is res->bytes: record i's length is
+// wrec[i + 1] - wrec[i], the last one's bytes - wrec[count - 1].
+__device__ void ba_window(ChainLds& C, const BaPageCtx& c, int64_t w, int64_t entry64, BaWin* res, uint16_t* wrec) {
+  SegRecs sr;
+  ba_window_segs(C, c, w, entry64, res, sr);
+  if (sr.cnt == 0 && threadIdx.x == 0) {
+    const int64_t wend64 = c.entry + (w + 1) * kChainStride;
+    if (entry64 >= c.e0 || entry64 >= wend64) wrec[0] = 0;
+  }
+  seg_list(sr, 0, 0x7fffffff, wrec);
 }
 
 // Window w > 0 guesses its entry (the first record start >= B_w) from the staged window itself:
@@ -1435,13 +1466,38 @@ __device__ bool fuse_lookback(const DevBatch& b, int t, int w, int64_t val_s, in
   }
 }
 
+// A wave-uniform value / pointer in scalar registers (the compiler cannot see that a value read from
+// LDS is uniform).
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int32_t(uint64_t(v) >> 32)))) << 32) |
+                 uint32_t(__builtin_amdgcn_readfirstlane(int32_t(v))));
+}
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+  return reinterpret_cast<T*>(uni64(int64_t(reinterpret_cast<uintptr_t>(p))));
+}
+
+// The dword at byte q of a staged dword array (any alignment).
+__device__ __forceinline__ uint32_t stage_dw(const uint32_t* stage, int q) {
+  return __builtin_amdgcn_alignbit(stage[(q >> 2) + 1], stage[q >> 2], uint32_t(q) * 8);  // (shift mod 32)
+}
+
+// Records listed per emission pass of k_ba_chain (the window's records are listed and copied in
+// passes of this many, so that the list's LDS stays small: 4 workgroups per CU).
+constexpr int kChainList = 1024;
+constexpr int kChainLongs = 8;  // records past the stage of kLong bytes or more (at most ~2 per window)
+
 __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
   __shared__ ChainLds C;
-  __shared__ uint16_t recs[kChainRecs + 8];
+  __shared__ uint16_t list[kChainList + 2];
   __shared__ BaWin R;
-  __shared__ int64_t sh[6];
+  __shared__ int64_t sh[7];
+  __shared__ int32_t longs[3 * kChainLongs + 1];  // {index, start, end} of long records past the stage; count
   const int tid = threadIdx.x;
-  if (tid == 0) sh[0] = atomicAdd(b.bafuse, 1u);
+  if (tid == 0) {
+    sh[0] = atomicAdd(b.bafuse, 1u);
+    longs[3 * kChainLongs] = 0;
+  }
   __syncthreads();
   if (int(sh[0]) >= nwin) return;
   const int t = order[sh[0]];  // (the window's page-major index: its look-back word)
@@ -1479,7 +1535,8 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     __syncthreads();
     entry = C.guess;
   }
-  ba_window(C, c, w, entry, &R, recs);
+  SegRecs sr;
+  ba_window_segs(C, c, w, entry, &R, sr);
   __syncthreads();
   const int64_t value_base = sh[4], byte_base = sh[5];
   int64_t pincl = 0;
@@ -1533,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
       __syncthreads();
     } else if (pexit != entry) {
       // a wrong guess: resolve again from the true entry
-      ba_window(C, c, w, pexit, &R, recs);
+      ba_window_segs(C, c, w, pexit, &R, sr);
       __syncthreads();
     }
   }
@@ -1544,46 +1601,77 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
     const bool ended = pended || r.bad != 0;
     __hip_atomic_store(b.bawords + t, kFinal | (ended ? kBadBit : 0) | (uint64_t(incl) << 32) | uint64_t(uint32_t(r.exit)),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (pended || pincl >= nn) return;
+  // the window's records before the page's notNull: n of them, their bytes end at endo (the offset
+  // of record n, or the window's byte total)
+  const int n = int(nn - pincl < r.count ? nn - pincl : r.count);
+  if (n < r.count) seg_list(sr, n, n + 1, reinterpret_cast<int64_t*>(sh) + 6);  // (uint16 offset, widened)
+  __syncthreads();
+  const int64_t endo = n < r.count ? int64_t(uint16_t(sh[6])) : r.bytes;
+  if (tid == 0) {
     // the page's check: record nn ends at val_e, or the chain falls short of nn records
-    if (!pended && pincl < nn) {
-      if (pincl + r.count >= nn) {
-        const int64_t k = nn - pincl;  // records of the page up to and including record nn, in this window
-        const int64_t end = int64_t(r.entry) + 4 * k + (k < r.count ? int64_t(recs[k]) : r.bytes);
-        if (end != c.e0) fuse_fail(b);
-      } else if (r.bad || r.exit >= c.e0) {
-        fuse_fail(b);
-      }
+    if (pincl + r.count >= nn) {
+      if (int64_t(r.entry) + 4 * int64_t(n) + endo != c.e0) fuse_fail(b);
+    } else if (r.bad || r.exit >= c.e0) {
+      fuse_fail(b);
     }
   }
-  if (pended || pincl >= nn || r.count == 0) return;
-  // emit: the window's records before the page's notNull, at the page's guessed byte base
-  const int n = int(nn - pincl < r.count ? nn - pincl : r.count);
+  if (n == 0) return;
+  // emit at the page's guessed byte base
   const int64_t obase = byte_base + (int64_t(r.entry) - c.entry) - 4 * pincl;
-  const int64_t endo = n < r.count ? int64_t(recs[n]) : r.bytes;
   if (obase < 0 || obase + endo > D.bytes_cap || value_base + pincl + n > D.values_cap) {
     if (tid == 0) fuse_fail(b);  // a wrong guess somewhere: never written, the batch goes again
     return;
   }
-  PQH_G int64_t* offs = D.offsets + value_base + 1 + pincl;
-  PQH_G uint8_t* dst = D.bytes + obase;
+  // (wave-uniform bases in scalar registers: the stores below address them by 32-bit offsets)
+  PQH_G int64_t* offs = uni_ptr(D.offsets + value_base + 1 + pincl);
+  PQH_G uint8_t* dst = uni_ptr(D.bytes + obase);
+  const int64_t obase_u = uni64(obase);
   const int lead = int(r.entry - wb);  // the entry in the stage
   constexpr int kStaged = kChainWin + 64;
   constexpr int kLong = 512;
-  for (int i = tid; i < n; i += kBlock) {
-    const int o = recs[i];
-    const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
-    offs[i] = obase + e;
-    const int l = e - o;
-    const int sx = lead + 4 * (i + 1) + o;
-    if (sx + l + 20 <= kStaged) stage_string_out(C.win, sx, l, dst + o);
-    else if (l > 0 && l < kLong) copy_bytes(dst + o, c.img + r.entry + 4 * (i + 1) + o, l);
+  typedef uint32_t u32u __attribute__((aligned(1)));
+  for (int base = 0; base < n; base += kChainList) {
+    const int hi = n - base < kChainList ? n : base + kChainList;
+    seg_list(sr, base, hi < n ? hi + 1 : hi, list);  // records base .. hi (record n's offset is endo)
+    __syncthreads();
+    for (int i = tid; i < hi - base; i += kBlock) {
+      const int gi = base + i;
+      const int o = list[i], e = gi + 1 < n ? int(list[i + 1]) : int(endo);  // (endo may pass 2^16)
+      offs[uint32_t(gi)] = obase_u + e;
+      const int l = e - o;
+      const int sx = lead + 4 * (gi + 1) + o;
+      if (l >= 4 && l <= 16 && sx + l + 20 <= kStaged) {
+        // 4..16 bytes: four dword stores that overlap inside the string (no branch on the length)
+        const int h = l >= 8 ? 4 : 0, t = l >= 8 ? l - 8 : l - 4;
+        const uint32_t x0 = stage_dw(C.win, sx), x1 = stage_dw(C.win, sx + h), x2 = stage_dw(C.win, sx + t),
+                       x3 = stage_dw(C.win, sx + l - 4);
+        *reinterpret_cast<PQH_G u32u*>(dst + uint32_t(o)) = x0;
+        *reinterpret_cast<PQH_G u32u*>(dst + uint32_t(o + h)) = x1;
+        *reinterpret_cast<PQH_G u32u*>(dst + uint32_t(o + t)) = x2;
+        *reinterpret_cast<PQH_G u32u*>(dst + uint32_t(o + l - 4)) = x3;
+      } else if (sx + l + 20 <= kStaged) {
+        stage_string_out(C.win, sx, l, dst + o);
+      } else if (l > 0 && l < kLong) {
+        copy_bytes(dst + o, c.img + r.entry + 4 * (gi + 1) + o, l);
+      } else if (l >= kLong) {  // by the whole workgroup, below
+        const int k = atomicAdd(&longs[3 * kChainLongs], 1);
+        if (k < kChainLongs) {
+          longs[3 * k] = gi;
+          longs[3 * k + 1] = o;
+          longs[3 * k + 2] = e;
+        } else {
+          fuse_fail(b);
+        }
+      }
+    }
+    __syncthreads();  // the list is read before the next pass writes it
   }
-  // the strings past the stage (at most the last few of the window) by the whole workgroup
-  for (int i = n - 1; i >= 0; i--) {
-    const int o = recs[i];
-    const int e = i + 1 < n ? int(recs[i + 1]) : int(endo);
-    const int sx = lead + 4 * (i + 1) + o;
-    if (sx + (e - o) + 20 <= kStaged) break;
-    if (e - o >= kLong) block_copy(dst + o, (const PQH_G uint8_t*)(c.img + r.entry + 4 * (i + 1) + o), e - o);
+  // the long strings past the stage (at most the last few of the window) by the whole workgroup
+  const int nl = longs[3 * kChainLongs] < kChainLongs ? longs[3 * kChainLongs] : kChainLongs;
+  for (int k = 0; k < nl; k++) {
+    const int gi = longs[3 * k], o = longs[3 * k + 1], e = longs[3 * k + 2];
+    block_copy(dst + o, (const PQH_G uint8_t*)(c.img + r.entry + 4 * (gi + 1) + o), e - o);
   }
 }

@@ -660,11 +660,7 @@ __device__ void gz_serial(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, i
   flags |= kGzMemberEnd;
 }
 
-__device__ __forceinline__ int64_t uni64(int64_t x) {
-  return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(uint64_t(x) >> 32)))) << 32) |
-                 uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(x))));
-}
-
+// (uni64: bytearray_impl.h)
 // Wave 0: the non-Huffman states of one batch (lane 0's transitions, broadcast), until the stream
 // reaches Huffman-coded data (gz_huff_stage's), the batch ends, or the member / stream ends.
 __device__ void gz_parse(GzLds& E, const uint8_t* src, int32_t n, int32_t a0, int32_t d, int32_t total) {
