@@ -41,6 +41,7 @@ struct pqh_ctx {
   hipStream_t copy_stream = nullptr;  // staged (end-to-end) runs: pinned -> HBM copies
   hipStream_t side = nullptr;         // unprofiled runs: branches beside the main launch sequence
   hipStream_t side2 = nullptr;        //   (the fused PLAIN chains, beside both)
+  hipStream_t side3 = nullptr;        //   (the DELTA pages after the value scan, beside k_expand)
   std::string err;
   // Pinned bounce buffer for every copy between HBM and pageable host memory (two halves, so the
   // host-side memcpy of one overlaps the DMA of the other).  Pageable copies never reach the HIP
@@ -315,7 +316,7 @@ struct pqh_batch {
   size_t staged_bytes = 0;
   hipEvent_t ev_copied = nullptr, ev_done = nullptr;
   bool done_recorded = false;
-  hipEvent_t ev_dep[6] = {};       // fork / join points of the side branches
+  hipEvent_t ev_dep[8] = {};       // fork / join points of the side branches
   DevPage* d_pages = nullptr;
   DevChunk* d_chunks = nullptr;
   PageState* d_states = nullptr;
@@ -446,9 +447,11 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
   c->flags = flags;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side3, hipStreamNonBlocking) != hipSuccess) {
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->side) hipStreamDestroy(c->side);
+    if (c->side2) hipStreamDestroy(c->side2);
     delete c;
     return set_err(nullptr, PQH_ERR_HIP, "stream creation failed");
   }
@@ -461,7 +464,7 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipStreamDestroy(ctx->stream);
-  for (hipStream_t st : {ctx->side, ctx->side2})
+  for (hipStream_t st : {ctx->side, ctx->side2, ctx->side3})
     if (st) {
       hipStreamSynchronize(st);
       hipStreamDestroy(st);
@@ -1252,23 +1255,38 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     e = timed(4, ndp - ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages + ni, ndp - ni, st); });
   if (e == hipSuccess) e = timed(1, int32_t(b->chunks.size()), s, [&](hipStream_t st) { return launch_scan(d, st); });
   if (e == hipSuccess && nfw) e = launch_fused();
+  // the DELTA pages' decode (latency / ALU bound) runs beside k_expand's fixed-width and level tiles
+  // (bandwidth bound) on a stream of its own when the batch has both; it rejoins before the
+  // byte-array kernels, which read DELTA_LENGTH lengths, and at the end
+  hipStream_t ds = s;
+  bool delta_open = false;
+  if (e == hipSuccess && side && ndp && !b->expand_tiles.empty()) {
+    e = dep(s, b->ctx->side3, 6);
+    ds = b->ctx->side3;
+    delta_open = true;
+  }
   if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
-    e = timed(19, nis, s, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
+    e = timed(19, nis, ds, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
     if (e == hipSuccess)
-      e = timed(4, ni, s, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
+      e = timed(4, ni, ds, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
   }
   if (e == hipSuccess && ndt && b->delta_page_mode) {
     const int32_t nds = int32_t(b->delta_streams.size());
-    e = timed(17, nds, s, [&](hipStream_t st) { return launch_delta_page(d, b->d_dtiles, nds, st); });
+    e = timed(17, nds, ds, [&](hipStream_t st) { return launch_delta_page(d, b->d_dtiles, nds, st); });
   } else if (e == hipSuccess && ndt) {
-    e = timed(6, ndt, s, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
+    e = timed(6, ndt, ds, [&](hipStream_t st) { return launch_delta_sum(d, b->d_dtiles, ndt, st); });
     if (e == hipSuccess)
-      e = timed(6, ndp, s, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
-    if (e == hipSuccess) e = timed(5, ndt, s, [&](hipStream_t st) { return launch_delta_expand(d, b->d_dtiles, ndt, st); });
+      e = timed(6, ndp, ds, [&](hipStream_t st) { return launch_delta_scan(d, b->d_delta_pages, ndp, st); });
+    if (e == hipSuccess) e = timed(5, ndt, ds, [&](hipStream_t st) { return launch_delta_expand(d, b->d_dtiles, ndt, st); });
   }
   if (e == hipSuccess && ndp)  // pages outside the fast-path geometry (most launches exit at once)
-    e = timed(14, ndp, s, [&](hipStream_t st) { return launch_delta_serial(d, b->d_delta_pages, ndp, st); });
+    e = timed(14, ndp, ds, [&](hipStream_t st) { return launch_delta_serial(d, b->d_delta_pages, ndp, st); });
+  auto join_delta = [&]() -> hipError_t {
+    if (!delta_open) return hipSuccess;
+    delta_open = false;
+    return dep(b->ctx->side3, s, 7);
+  };
   // byte-array dictionary keys are checked against the dictionary sizes the chain branch found
   if (e == hipSuccess && b->ba_wdict) e = join_chain();
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
@@ -1293,6 +1311,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
       e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
   }
   if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
+  if (e == hipSuccess) e = join_delta();  // DELTA_LENGTH lengths
   if (e == hipSuccess && nbt) {
     const int32_t nsum = fuse ? b->ba_sum_nf : int32_t(b->ba_xlist.size()) - b->ba_sum_off;
     e = timed(8, nsum, s, [&](hipStream_t st) {
@@ -1323,6 +1342,10 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   }
   if (fuse_open) {
     const hipError_t r = dep(b->ctx->side2, s, 5);
+    if (e == hipSuccess) e = r;
+  }
+  if (delta_open) {
+    const hipError_t r = join_delta();
     if (e == hipSuccess) e = r;
   }
   return e;
