@@ -522,12 +522,48 @@ def next_row_record(ctx, pkg, rows=100_000):
     f.close()
     if not (got_c == got_v == ref):
         raise RuntimeError("NextRow records differ between the assembly paths")
-    out.update({"rows": len(ref), "verified": "identical records from the three paths",
+
+    def arrow_read(blob):
+        """The whole file through ReadRowGroupArrow: (tables, seconds, export seconds)."""
+        t0 = time.perf_counter()
+        fr = reader.FileReader(blob, ctx=ctx)
+        tables, ex = [], 0.0
+        while True:
+            if fr.row_group_position < fr.RowGroupCount():
+                fr.PreLoad()  # (walk + decode of the next row group, outside the export's time)
+            e0 = time.perf_counter()
+            t = fr.ReadRowGroupArrow()
+            if t is None:
+                break
+            ex += time.perf_counter() - e0
+            tables.append(t)
+        el = time.perf_counter() - t0
+        fr.close()
+        return tables, el, ex
+
+    tabs, el_a, ex_a = arrow_read(data)
+    from parquet_go_amd import assemble
+    if [assemble.drop_absent(r) for t in tabs for r in t.to_pylist()] != ref:
+        raise RuntimeError("the Arrow export differs from NextRow's records")
+    big_rows = 20_000_000
+    big = datasets.c4(rows=big_rows, row_groups=4)
+    tabs_b, el_b, ex_b = arrow_read(big)
+    nb = sum(t.num_rows for t in tabs_b)
+    del big, tabs_b
+    out.update({"rows": len(ref), "verified": "identical records from the three paths and the Arrow export",
                 "gpu_columnar_rows_per_s": round(len(ref) / el_c), "gpu_columnar_s": round(el_c, 3),
                 "assembly_paths": paths,
                 "gpu_value_by_value_rows_per_s": round(len(ref) / el_v), "gpu_value_by_value_s": round(el_v, 3),
                 "oracle_value_by_value_rows_per_s": round(len(ref) / el_o), "oracle_value_by_value_s": round(el_o, 3),
-                "note": "each time covers the whole read: host page walk, decode, assembly into Python dicts"})
+                "gpu_arrow_rows_per_s": round(len(ref) / el_a), "gpu_arrow_s": round(el_a, 3),
+                "arrow_c4_full": {"rows": nb, "rows_per_s": round(nb / el_b), "s": round(el_b, 3),
+                                  "export_rows_per_s": round(nb / ex_b), "export_s": round(ex_b, 3),
+                                  "note": "C4 at BASELINE size (20M rows, 4 row groups): host walk + GPU decode + "
+                                          "the Arrow export (ReadRowGroupArrow); export = the Arrow build alone"},
+                "note": "each time covers the whole read: host page walk, decode, assembly into Python dicts "
+                        "(NextRow paths) or into pyarrow Tables from the device's columnar outputs (arrow: "
+                        "ListArray / StructArray over list offsets, presence and leaf validity, no per-row "
+                        "Python objects)"})
     return out
 
 

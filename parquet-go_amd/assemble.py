@@ -45,8 +45,9 @@ class Leaf:
     values(): the dense values as Go-like Python values; pages: [(first slot, status, phase, index)] of
     the chunk's data pages."""
 
-    def __init__(self, path, max_d, max_r, rep_def, d, r, levels, leaf_valid, values, pages, n):
+    def __init__(self, path, max_d, max_r, rep_def, d, r, levels, leaf_valid, values, pages, n, arrow=None):
         self.path, self.max_d, self.max_r, self.rep_def = path, max_d, max_r, tuple(rep_def)
+        self._arrow = arrow  # () -> the dense values as a pyarrow Array (ColumnarAssembler.arrow)
         self.n = n
         self.d = d if d is not None else np.zeros(n, np.uint8)
         self.r = r if r is not None else np.zeros(n, np.uint8)
@@ -60,6 +61,36 @@ class Leaf:
         if self._vals is None:
             self._vals = self._values()
         return self._vals
+
+
+def arrow_type(ptype, type_length):
+    """The Arrow type of a leaf's values (the Go values' types: []byte for byte arrays, FLBA and the
+    12-byte INT96)."""
+    import pyarrow as pa
+
+    return {BOOLEAN: pa.bool_(), INT32: pa.int32(), INT64: pa.int64(), FLOAT: pa.float32(), DOUBLE: pa.float64(),
+            BYTE_ARRAY: pa.large_binary(), INT96: pa.binary(12)}.get(ptype) or pa.binary(int(type_length))
+
+
+def arrow_dense(col, ptype):
+    """The dense values of a decoded chunk (reader.ColumnData) as a pyarrow Array, zero-copy over the
+    host copies of the device outputs where Arrow's layout allows (fixed width, offsets + bytes)."""
+    import pyarrow as pa
+
+    t = arrow_type(ptype, col.type_length)
+    if col.values is not None:
+        v = col.values
+        if ptype == BOOLEAN:
+            return pa.array(v.astype(bool), type=t)
+        if v.ndim == 2:
+            return pa.Array.from_buffers(t, len(v), [None, pa.py_buffer(np.ascontiguousarray(v))])
+        return pa.array(v, type=t)
+    if col.offsets is None:
+        return pa.array([], type=t)
+    # (int64 offsets + bytes: large_binary as is; a FIXED_LEN_BYTE_ARRAY chunk of DELTA_BYTE_ARRAY
+    # pages comes out this way too)
+    n = len(col.offsets) - 1
+    return pa.Array.from_buffers(pa.large_binary(), n, [None, pa.py_buffer(col.offsets), pa.py_buffer(col.data)])
 
 
 def dense_values(col, ptype):
@@ -328,15 +359,20 @@ class ColumnarAssembler:
                 if len(v[0]) != n:
                     raise NotColumnar(f"{c.name}: {len(v[0])} instances under {x.name}, expected {n}")
                 kids.append((c.name, v[0], v[1]))
+        return _dicts(kids, n), ~self._presence(x, lf, k, rows, n)
+
+    def _presence(self, x, lf, k, rows, n):
+        """Group x's presence per level-k instance (d at its first slot >= x's max_d); every selected
+        leaf below x must agree."""
         starts = self._starts(lf, k, rows)[:n]
         present = lf.d[starts] >= x.max_d
-        for c in self._columns(x):  # every selected leaf below x agrees on x's presence
+        for c in self._columns(x):
             o = self.leaves.get(c)
             if o is not None and o is not lf and x.max_d > 0:
                 s2 = self._starts(o, k, rows)[:n]
                 if len(s2) != n or not np.array_equal(o.d[s2] >= x.max_d, present):
                     raise NotColumnar(f"{x.name}: leaves disagree on its instances")
-        return _dicts(kids, n), ~present
+        return present
 
     def rows(self):
         """Every row this row group returns before its first error (cached).  The cyclic garbage
@@ -354,6 +390,75 @@ class ColumnarAssembler:
                     gc.enable()
         return self._rows
 
+    # ------------------------------------------------------------------ Arrow export
+    def arrow(self):
+        """The rows() records as a pyarrow Table, built column by column from the same columnar
+        description without any per-row Python object: a repeated node is a ListArray over its
+        level offsets (an empty list is null: the reference's nil), a group a StructArray whose
+        validity is its presence, a leaf the dense values taken through its leaf validity (nulls at
+        the null slots).  Table.to_pylist() equals rows() once absent fields (None in a struct) are
+        dropped, as the reference's records omit them.  A native consumer of the device's columnar
+        outputs: no value passes through the interpreter."""
+        import pyarrow as pa
+
+        n = self.ok_rows
+        arrays, names = [], []
+        for c in self.root.children:
+            v = self._arrow_values(c, 0, n)
+            if v is not None:
+                if len(v[0]) != n:
+                    raise NotColumnar(f"{c.name}: {len(v[0])} rows, expected {n}")
+                arrays.append(v[0])
+                names.append(c.name)
+        return pa.Table.from_arrays(arrays, names=names)
+
+    def _arrow_values(self, x, k, rows):
+        import pyarrow as pa
+
+        lf = self._rep_leaf(x)
+        if lf is None:
+            return None
+        if x.rep == REPEATED:
+            n_inst = self._count(lf, k, rows)
+            kk = k + 1
+            off = np.ascontiguousarray(lf.levels[kk - 1][0][:n_inst + 1], np.int32)
+            elems, emask = self._arrow_element(x, kk, rows)
+            if x.children is None and emask.any():
+                raise NotColumnar(f"{x.name}: a repeated leaf slot without a value inside a list")
+            empty = np.diff(off) == 0
+            arr = pa.ListArray.from_arrays(pa.array(off), elems, mask=pa.array(empty))
+            return arr, empty
+        return self._arrow_element(x, k, rows)
+
+    def _arrow_element(self, x, k, rows):
+        import pyarrow as pa
+
+        if x.children is None:
+            lf = self.leaves[x.column]
+            if lf._arrow is None:
+                raise NotColumnar(f"{x.name}: no Arrow values")
+            n = self._count(lf, k, rows)
+            valid = lf.leaf_valid[:n].astype(bool)
+            dense = lf._arrow()
+            if valid.all():
+                return dense.slice(0, n), ~valid
+            if not valid.any():
+                return pa.nulls(n, type=dense.type), ~valid
+            idx = np.maximum(np.cumsum(valid, dtype=np.int64) - 1, 0)
+            return dense.take(pa.array(idx, mask=~valid)), ~valid
+        lf = self._rep_leaf(x)
+        n = self._count(lf, k, rows)
+        arrays, names = [], []
+        for c in x.children:
+            v = self._arrow_values(c, k, rows)
+            if v is not None:
+                if len(v[0]) != n:
+                    raise NotColumnar(f"{c.name}: {len(v[0])} instances under {x.name}, expected {n}")
+                arrays.append(v[0])
+                names.append(c.name)
+        present = self._presence(x, lf, k, rows, n)
+        return pa.StructArray.from_arrays(arrays, names=names, mask=pa.array(~present)), ~present
+
     def _build(self):
         n = self.ok_rows
         kids = []
@@ -364,6 +469,16 @@ class ColumnarAssembler:
                     raise NotColumnar(f"{c.name}: {len(v[0])} rows, expected {n}")
                 kids.append((c.name, v[0], v[1]))
         return _dicts(kids, n)
+
+
+def drop_absent(x):
+    """A record of Table.to_pylist() in the reference's form: struct fields that are None (absent)
+    dropped, at every depth (list elements keep their None: a nil element)."""
+    if isinstance(x, dict):
+        return {k: drop_absent(v) for k, v in x.items() if v is not None}
+    if isinstance(x, list):
+        return [drop_absent(v) for v in x]
+    return x
 
 
 def _dicts(kids, n):

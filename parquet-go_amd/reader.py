@@ -270,7 +270,7 @@ class FileReader:
         self.PreLoad()
         return {c.path: c.raise_for_status() for c in self._loaded}
 
-    def _assembler(self):
+    def _assembler(self, arrow=False):
         """The current row group's record assembly: columnar over the device's nesting outputs
         (assemble.ColumnarAssembler), else value by value (records.RowAssembler) when the row group
         breaks one of its preconditions (the reference's page-local cursors / getFirstRDLevel
@@ -290,10 +290,13 @@ class FileReader:
                     break  # (Go nil values, type_int96.go:21-42: the value-by-value assembly)
                 leaves[ci] = assemble.Leaf(c.path, c.max_def, c.max_rep, self.file.rep_def(ci), c.def_levels,
                                            c.rep_levels, levels, leaf,
-                                           lambda c=c: assemble.dense_values(c, c.physical_type), pages, c.num_values)
+                                           lambda c=c: assemble.dense_values(c, c.physical_type), pages, c.num_values,
+                                           arrow=lambda c=c: assemble.arrow_dense(c, c.physical_type))
             else:
                 try:
                     a = assemble.ColumnarAssembler(self._schema, leaves, nrows)
+                    if arrow:
+                        return ("arrow", a)
                     rows, errs = a.rows(), a.errors()
                     self.assembled["columnar"] += 1
                     return ("columnar", rows, errs)
@@ -358,6 +361,43 @@ class FileReader:
                 self._pending = e
                 break
         return out
+
+    def ReadRowGroupArrow(self):
+        """The records of the current row group from the cursor on (the next row group when it is
+        exhausted; None at the end of the file) as a pyarrow Table, built from the device's columnar
+        outputs (assemble.ColumnarAssembler.arrow: list offsets, presence, leaf validity and the dense
+        values, with no per-row Python object); assemble.drop_absent(row) of its to_pylist() rows
+        equals what NextRow returns.  Rows stop before a row whose page fails to decode; that row's
+        error is raised by the next NextRow / NextBatch / ReadRowGroupArrow call, as with NextBatch.
+        Row groups the columnar assembly cannot describe (records.py's corner cases, nil INT96
+        values) go through NextBatch's records into the table."""
+        import pyarrow as pa
+
+        from . import assemble
+
+        if self._pending is not None:
+            e, self._pending = self._pending, None
+            raise e
+        try:
+            self._advance_if_needed()
+        except EOFError:
+            return None
+        nrows = self.file.row_group_num_rows(self.row_group_position - 1)
+        k = self.current_record
+        if self._rows is None and k == 0:
+            a = self._assembler(arrow=True)
+            if a[0] == "arrow":
+                asm = a[1]
+                self.assembled["arrow"] = self.assembled.get("arrow", 0) + 1
+                t = asm.arrow()
+                # the cursor after the table's rows: a failing row's error comes from the next call
+                # (NextRow's columnar path raises errs[k - ok_rows] there)
+                self._rows = ("columnar", [None] * asm.ok_rows, asm.errors())
+                self.current_record = asm.ok_rows
+                return t
+            self._rows = a
+        rows = self.NextBatch(nrows - k)
+        return pa.Table.from_pylist(rows) if rows else pa.table({})
 
     def close(self):
         self.file.close()

@@ -15,6 +15,12 @@ from test_records import ERROR_CASES, KATS, _corrupt, _error_file, _go_values, _
     error_outcome, kat_file, oracle_next_rows
 
 
+def _pa():
+    import pyarrow
+
+    return pyarrow
+
+
 def columnar_next_rows(data, columns=None, stats=None):
     """oracle_next_rows' outcomes through assemble.ColumnarAssembler (records.RowAssembler where a
     row group breaks a precondition; counted in stats)."""
@@ -58,7 +64,9 @@ def columnar_next_rows(data, columns=None, stats=None):
                         break
                     vals += _go_values(r, col)
             leaves[ci] = A.Leaf(col.path, col.max_def, col.max_rep, col.rep_def, d, rr, levels, leaf,
-                                lambda vals=vals: vals, pages, n)
+                                lambda vals=vals: vals, pages, n,
+                                arrow=lambda vals=vals, col=col: _pa().array(
+                                    vals, type=A.arrow_type(col.physical_type, col.type_length or 0)))
             el = leaf_el[ci]
             spages = []
             for r in res:
@@ -92,6 +100,10 @@ def columnar_next_rows(data, columns=None, stats=None):
             continue
         if stats is not None:
             stats["columnar"] = stats.get("columnar", 0) + 1
+        # the same records through the Arrow export (no per-row objects until to_pylist)
+        t = asm.arrow()
+        arows = [A.drop_absent(r) for r in t.to_pylist()] if t.num_columns else [{}] * len(rows)
+        assert len(arows) == len(rows) and all(_norm(a) == _norm(b) for a, b in zip(arows, rows)), "arrow export"
         out.extend(rows)
         # (status, phase, index, page) as records.RecordError carries them: reader.NextRow raises these
         out.extend(("error", e[1], e[2], e[3], e[5]) for e in asm.errors())

@@ -481,3 +481,49 @@ def test_next_batch_pending_error_cleared_by_seek(pq, ctx):
         fr.NextBatch(10)
     assert error_outcome(ei.value) == want[first_err]
     fr.close()
+
+
+def _read_arrow(pq, data):
+    """Every outcome of ReadRowGroupArrow until the end: rows (drop_absent of the tables' to_pylist)
+    and errors (error_outcome), in order, plus the assembly paths used."""
+    A = pq.assemble
+    fr = pq.reader.FileReader(data, ctx=pq.native.Context(0))
+    out = []
+    while True:
+        try:
+            t = fr.ReadRowGroupArrow()
+        except (pq.reader.DecodeError, pq.records.RecordError) as e:
+            out.append(error_outcome(e))
+            continue
+        if t is None:
+            break
+        out.extend(A.drop_absent(r) for r in t.to_pylist())
+    paths = dict(fr.assembled)
+    fr.close()
+    return out, paths
+
+
+@pytest.mark.gpu
+def test_read_row_group_arrow(pq, ctx):
+    """The Arrow export of the columnar assembly (assemble.ColumnarAssembler.arrow: ListArray /
+    StructArray over the device's list offsets, presence and leaf validity, the dense values taken
+    through the leaf validity) gives NextRow's records: the Dremel KATs, nested LIST / MAP files over
+    many pages, the flat all-types file, a C4-shaped file, and the corrupted files of the
+    error-timing tests (rows before a failing row, then its error, then the next row group)."""
+    for kat in KATS:
+        got, paths = _read_arrow(pq, kat_file(kat))
+        assert [_norm(g) for g in got] == [_norm(r) for r in kat["rows"]], kat["name"]
+    files = [fixtures.nested_list_map(n=3000, v2=True), fixtures.flat_all_types(n=4000, v2=False),
+             pq.datasets.c4(rows=30_000, row_groups=2)]
+    for data in files:
+        want = oracle_rows(data)
+        got, paths = _read_arrow(pq, data)
+        assert paths.get("arrow", 0) == len(O.FileReader(data).row_groups), paths
+        assert len(got) == len(want) and all(_norm(g) == _norm(w) for g, w in zip(got, want))
+    for case in sorted(ERROR_CASES):
+        data = _corrupt(_error_file(), ERROR_CASES[case])
+        want = oracle_next_rows(data)
+        got, _ = _read_arrow(pq, data)
+        # (a row group's rows before its failing row come as one table, then one error per call for
+        # each row left, as NextRow raises them; then the next row group)
+        assert [_norm(g) for g in got] == [_norm(w) for w in want], case
