@@ -59,12 +59,16 @@ def main():
                       "hbm_traffic_bytes_per_launch": traffic}
     summary = {"source": "rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE (separate passes)",
                "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md §HBM)", "kernels": kernels}
-    for name in ("bench.log", pre + "_trace.log"):
+    # the bench line of the profiled run itself (its workload keys the summary); a plain bench.log
+    # only when the trace pass left none
+    for name in (pre + "_trace.log", "bench.log"):
         p = os.path.join(src, name)
         if os.path.exists(p):
             for line in open(p):
                 if line.startswith("{"):
                     summary.setdefault("bench_lines", []).append(json.loads(line))
+        if summary.get("bench_lines"):
+            break
     # the build the counters measured: the bench line's (pqh_build_id of the library that ran), else
     # the build record beside the in-tree library.  bench.py quotes a summary only for this build.
     builds = [ln.get("build") for ln in summary.get("bench_lines", []) if ln.get("build")]
