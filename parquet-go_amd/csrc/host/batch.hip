@@ -1244,9 +1244,7 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   };
   // page mode: every delta page gets its init errors now and is chased, decoded and walked after
   // the value scan; tile mode: speculative walk + exact walk now, tiles after the scan
-  int32_t ni = b->delta_page_mode ? b->delta_fused_pages : 0;
-  if (const char* f = getenv("PQH_DELTA_FUSED"))  // experiments: "0" = speculative walk + k_delta_page
-    if (f[0] == '0') ni = 0;
+  const int32_t ni = b->delta_page_mode ? b->delta_fused_pages : 0;
   if (e == hipSuccess && ni)
     e = timed(18, ni, s, [&](hipStream_t st) { return launch_delta_init(d, b->d_delta_pages, ni, st); });
   if (e == hipSuccess && ndp > ni)

@@ -130,6 +130,29 @@ def test_snappy_mutation_fuzz(pq, ctx):
     assert bad > 20
 
 
+def test_snappy_page_mode_everywhere(pq, monkeypatch):
+    """PQH_SNAPPY_PAGE=1 sends every SNAPPY page to k_snappy's one-workgroup-per-page decoder (the
+    path barely compressible pages take anyway): the edge blocks, pyarrow blocks and a mutated subset
+    give the oracle's status and bytes there too."""
+    monkeypatch.setenv("PQH_SNAPPY_PAGE", "1")
+    ctx = pq.native.Context(0)
+    cases = edge_blocks()
+    assert _check(pq, ctx, [c[0] for c in cases], [len(c[1]) for c in cases]) == 0
+    raws = sample_blocks()
+    assert _check(pq, ctx, [pa.compress(r, codec="snappy", asbytes=True) for r in raws], [len(r) for r in raws]) == 0
+    rng = np.random.default_rng(5)
+    blocks, sizes = [], []
+    for r in raws[:6]:
+        comp = bytearray(pa.compress(r, codec="snappy", asbytes=True))
+        for _ in range(6):
+            b = bytearray(comp)
+            b[int(rng.integers(1, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            blocks.append(bytes(b))
+            sizes.append(len(r))
+    _check(pq, ctx, blocks, sizes)
+    ctx.close()
+
+
 def _files():
     yield "writer-v1", fixtures.flat_all_types(n=8000, v2=False, codec=O.SNAPPY, page=16 * 1024, rows_per_group=4000)
     yield "writer-v2", fixtures.flat_all_types(n=8000, v2=True, codec=O.SNAPPY, page=16 * 1024, rows_per_group=4000)
