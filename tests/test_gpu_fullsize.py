@@ -173,15 +173,17 @@ def test_c5_full(pq, ctx):
     hb.close()
 
 
-def test_c4_full(pq, ctx):
-    """C4: 20M rows of LIST<optional int64> + MAP<string, optional int32>, 4 row groups: levels,
-    values and key strings of every chunk equal the written columns."""
+@pytest.mark.parametrize("v2", [False, True])
+def test_c4_full(pq, ctx, v2):
+    """C4: 20M rows of LIST<optional int64> + MAP<string, optional int32>, 4 row groups, data pages
+    V1 and V2: levels, values and key strings of every chunk equal the written
+    columns."""
     from parquet_go_amd import datasets, writer as W
 
     rows, rgs = 20_000_000, 4
     schema, cols = datasets.c4_columns(rows, 30)
     per = -(-rows // rgs)
-    data = W.write(schema, cols, [min(per, rows - i * per) for i in range(rgs)], as_array=True)
+    data = W.write(schema, cols, [min(per, rows - i * per) for i in range(rgs)], v2=v2, as_array=True)
     f, hb, b, ncols, rg_rows = _decode(pq, ctx, data)
     max_def = [3, 2, 3]
     for ci, col in enumerate(cols):
