@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build experiment variants of libpqhip (lib/<name>.so, loaded with PQH_HIP_LIB=<name>.so):
-#   bash scripts/build_variants.sh "copy128:-DPQH_COPY_TILE=131072" "big:-DPQH_COPY_TILE=131072 -DPQH_DICT_SPAN_X=4"
+#   bash scripts/build_variants.sh "seg96:-DPQH_CHAIN_SEG=96" "snapprof:-DPQH_SNAP_PROF"
 cd "$(dirname "$0")/.."
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
