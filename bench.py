@@ -523,6 +523,8 @@ def next_row_record(ctx, pkg, rows=100_000):
     if not (got_c == got_v == ref):
         raise RuntimeError("NextRow records differ between the assembly paths")
 
+    import pyarrow  # noqa: F401  (imported before the clock: the first import takes ~1 s)
+
     def arrow_read(blob):
         """The whole file through ReadRowGroupArrow: (tables, seconds, export seconds)."""
         t0 = time.perf_counter()
