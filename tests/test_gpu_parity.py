@@ -182,7 +182,7 @@ def _fuzz_cases(pq, data, seed, per_page=3):
     return cases
 
 
-def _run_cases(pq, ctx, cases, stats=None, runs=1):
+def _run_cases(pq, ctx, cases, stats=None, runs=1, hints=None):
     """Decode `cases` = [(column, dictionary (num_values, encoding, image) or None, data page)] in ONE
     batch (every case its own chunk) and compare each against the oracle's decode_page.  stats: a
     dict that gets the batch's kernel launch counts by name (profiled contexts).  runs: decodes of
@@ -199,13 +199,14 @@ def _run_cases(pq, ctx, cases, stats=None, runs=1):
         off = base + len(img)
         return base
 
-    for col, dict_img, (ptype, nv, enc, dl, rl, img) in cases:
+    for ci, (col, dict_img, (ptype, nv, enc, dl, rl, img)) in enumerate(cases):
         first = len(pages)
         if dict_img is not None:
             o = add(dict_img[2])
             pages.append(N.Page(o, len(dict_img[2]), O.DICTIONARY_PAGE, dict_img[0], dict_img[1], 0, 0, len(chunks), 0))
         o = add(img)
-        pages.append(N.Page(o, len(img), ptype, nv, enc, dl, rl, len(chunks), 0))
+        # (hints: the V2 header's num_nulls per case -- k_flat's speculative notNull; 0 otherwise)
+        pages.append(N.Page(o, len(img), ptype, nv, enc, dl, rl, len(chunks), hints[ci] if hints else 0))
         chunks.append(N.Chunk(N.Column(*col), first, len(pages) - first, 0, 0))
     payload = b"".join(blobs) + b"\0" * N.PAYLOAD_PAD
     arr = np.frombuffer(payload, dtype=np.uint8).copy()
@@ -391,7 +392,42 @@ def test_flat_nullable_v2(pq, monkeypatch, flat):
     compared, errors = _run_cases(pq, ctx, clean, stats, runs=3)
     assert compared == len(clean) and errors == 0
     assert stats.get("k_expand", 0) == (1 if flat == "one_launch" else 3), stats
+    # with their true hints they stay in one launch; mutants (levels, values, truncation) with the
+    # unmutated page's hint: those whose speculation still holds decode in k_flat, the others fall
+    # back -- the oracle's results and first errors either way
+    hints = _v2_null_hints(pq, data)
+    stats = {}
+    compared, errors = _run_cases(pq, ctx, clean, stats, runs=3, hints=hints)
+    assert compared == len(clean) and errors == 0
+    assert stats.get("k_expand", 0) == (0 if flat == "one_launch" else 3), stats
+    rng = np.random.default_rng(29)
+    mut, mh = [], []
+    for (col, dimg, pg), h in zip(clean, hints):
+        for _ in range(6):
+            img2 = _mutate(rng, pg[5])
+            if pg[3] + pg[4] > len(img2):
+                continue  # (the host walker rejects such headers before the device sees them)
+            mut.append((col, dimg, pg[:5] + (img2,)))
+            mh.append(h)
+    compared, errors = _run_cases(pq, ctx, clean[:10] + mut, runs=3, hints=hints[:10] + mh)
+    assert compared == 10 + len(mut) and errors >= 5, (compared, errors)  # (each case vs the oracle)
     ctx.close()
+
+
+def _v2_null_hints(pq, data):
+    """num_nulls of every data page of `data`, in _page_sets_cases order (the host walker's V2
+    header field)."""
+    f = pq.native.File(data)
+    hb = f.load(0, f.num_row_groups, list(range(len(f.columns()))))
+    pages = hb.pages()
+    out = []
+    for ch in hb.chunks():
+        for p in range(ch.first_page, ch.first_page + ch.num_pages):
+            if pages[p].page_type != O.DICTIONARY_PAGE:
+                out.append(pages[p].num_nulls)
+    hb.close()
+    f.close()
+    return out
 
 
 def _page_sets_cases(pq, data):
