@@ -1134,3 +1134,35 @@ def test_launch_modes(pq, mode, monkeypatch):
             checked, skipped = _run_file(pq, c, data)
             assert checked > 0 and skipped == 0
     c.close()
+
+
+def test_float_bit_patterns(pq, ctx):
+    """NaN payloads (quiet, signalling, negative), +-0, +-inf and subnormals keep their bits through
+    PLAIN and dictionary pages, V1 and V2, required and optional columns (the reference's NaN
+    round trip, readwrite_test.go:1354-1432): the decoded bytes equal the written bit patterns and the
+    oracle's."""
+    W = fixtures.W
+    rng = np.random.default_rng(3)
+    f32_bits = np.array([0x7fc00000, 0x7fc00001, 0xffc00000, 0x7f800001, 0xff800001, 0x7fbfffff, 0x00000000,
+                         0x80000000, 0x7f800000, 0xff800000, 0x00000001, 0x807fffff, 0x3f800000], np.uint32)
+    f64_bits = np.array([0x7ff8000000000000, 0x7ff8000000000001, 0xfff8000000000000, 0x7ff0000000000001,
+                         0xfff0000000000001, 0x7ff7ffffffffffff, 0, 0x8000000000000000, 0x7ff0000000000000,
+                         0xfff0000000000000, 1, 0x800fffffffffffff, 0x3ff0000000000000], np.uint64)
+    n = 6000
+    a = f32_bits[rng.integers(0, len(f32_bits), n)]
+    b = f64_bits[rng.integers(0, len(f64_bits), n)]
+    d = (rng.random(n) < 0.9).astype(np.uint8)
+    for v2 in (False, True):
+        for use_dict in (False, True):
+            cols = [("f", W.Column(W.FLOAT, a.view(np.float32), use_dict=use_dict), W.REQUIRED),
+                    ("d", W.Column(W.DOUBLE, b.view(np.float64), use_dict=use_dict), W.REQUIRED),
+                    ("od", W.Column(W.DOUBLE, b[d.astype(bool)].view(np.float64), def_levels=d, use_dict=use_dict),
+                     W.OPTIONAL)]
+            data = W.flat(cols, n // 2, v2=v2)
+            checked, _ = _run_file(pq, ctx, data)
+            assert checked == 2 * 3
+            f = pq.native.File(data)
+            res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, [0, 1, 2])
+            for ci, want in ((0, a), (1, b), (2, b[d.astype(bool)])):
+                got = np.concatenate([res[k].values.view(want.dtype) for k in range(ci, len(res), 3)])
+                assert np.array_equal(got, want), (v2, use_dict, ci)
