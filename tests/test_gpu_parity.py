@@ -1166,3 +1166,22 @@ def test_float_bit_patterns(pq, ctx):
             for ci, want in ((0, a), (1, b), (2, b[d.astype(bool)])):
                 got = np.concatenate([res[k].values.view(want.dtype) for k in range(ci, len(res), 3)])
                 assert np.array_equal(got, want), (v2, use_dict, ci)
+
+
+@pytest.mark.parametrize("v2", [False, True])
+def test_tiny_snappy_pages(pq, ctx, v2):
+    """1 KiB SNAPPY pages of every type and encoding (the reference's multi-page snappy round trip,
+    readwrite_test.go:1291-1352): hundreds of pages per chunk through the host codec and through the
+    device codecs, every chunk equal to the oracle's."""
+    data = fixtures.flat_all_types(n=6000, v2=v2, codec=O.SNAPPY, page=1024, rows_per_group=3000)
+    fr = O.FileReader(data)
+    f = pq.native.File(data)
+    ncols = len(f.columns())
+    for dev in (False, True):
+        res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(ncols)), device_snappy=dev)
+        for k, col in enumerate(res):
+            rg, ci = divmod(k, ncols)
+            assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"device={dev} rg{rg} {col.path}")
+    hb = f.load(0, f.num_row_groups, list(range(ncols)))
+    assert hb.num_pages > 20 * ncols  # (many pages per chunk)
+    hb.close()
