@@ -88,8 +88,9 @@ def flat_c2_like(n=40000, v2=True, seed=11):
     return W.flat(cols, 10000, v2=v2, max_page_size=32 * 1024)
 
 
-def nested_list_map(n=5000, v2=False, seed=30, codec=0):
-    """optional LIST<optional int64> + optional MAP<string, optional int32> (C4 shape)."""
+def nested_list_map(n=5000, v2=False, seed=30, codec=0, rows_per_group=None):
+    """optional LIST<optional int64> + optional MAP<string, optional int32> (C4 shape); two row groups,
+    or row groups of rows_per_group rows."""
     rng = np.random.default_rng(seed)
     # LIST: levels for path l.list.element: maxD 3, maxR 1
     ld, lr, lv = [], [], []
@@ -139,7 +140,8 @@ def nested_list_map(n=5000, v2=False, seed=30, codec=0):
         W.Column(W.BYTE_ARRAY, mk, def_levels=md_k, rep_levels=mr_k, use_dict=False),
         W.Column(W.INT32, np.array(mv, dtype=np.int32), def_levels=md_v, rep_levels=mr_k, use_dict=False),
     ]
-    rg = [n // 2, n - n // 2]
+    rg = [n // 2, n - n // 2] if rows_per_group is None else \
+        [min(rows_per_group, n - i) for i in range(0, n, rows_per_group)]
     return W.write(schema, cols, rg, v2=v2, codec=codec, max_page_size=16 * 1024)
 
 
