@@ -533,9 +533,11 @@ def test_read_row_group_arrow(pq, ctx):
 def test_next_row_many_small_row_groups(pq, ctx):
     """A row group every 100 rows (the reference's column-selection file, filereader_test.go:13-247):
     100 row groups of the all-types file and of a nested LIST / MAP file, NextRow with every column and
-    with a selection, equal call by call to the assembly over the oracle's pages (the all-types file's
-    FLBA DELTA_BYTE_ARRAY column fails to load in 4 of its tiny row groups, as the oracle's reader
-    says: those row groups fail whole); ReadRowGroupArrow the same."""
+    with a selection, equal call by call to the assembly over the oracle's pages; ReadRowGroupArrow the
+    same.  In 4 of the all-types file's row groups the FLBA column's DELTA_BYTE_ARRAY fallback page
+    holds ONE value, so its length streams hit the reference's DELTA read-ahead failure ((n - 1) % 128
+    == 0, deltabp_decoder.go) when the decoder initialises: those row groups fail
+    whole, on the GPU as in the reference (pyarrow, without that quirk, reads them)."""
     def next_rows(data, *cols):
         fr = pq.reader.FileReader(data, *cols, ctx=ctx)
         out = []
