@@ -364,6 +364,8 @@ def c1_x10_record(args, ctx, native, datasets, barrier_sync):
     (560 MB of page images + output), one batch.  The C1 line itself fits the 256 MiB MALL, so its
     roofline fraction is not HBM evidence; this one is.  (Past k_flat's batch limits, so the three
     kernels run.)"""
+    import numpy as np
+
     W = datasets.W
     rng = np.random.default_rng(1)
     dictionary = rng.integers(-2**31, 2**31 - 1, 4096).astype(np.int32)
