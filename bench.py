@@ -545,6 +545,7 @@ def next_row_record(ctx, pkg, rows=100_000):
         fr.close()
         return tables, el, ex
 
+    arrow_read(data)  # (warm: pyarrow's compute kernels initialise on their first call)
     tabs, el_a, ex_a = arrow_read(data)
     from parquet_go_amd import assemble
     if [assemble.drop_absent(r) for t in tabs for r in t.to_pylist()] != ref:
