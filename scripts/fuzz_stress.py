@@ -19,7 +19,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=40)
+    ap.add_argument("--codecs", type=int, default=0, help="seeds of the SNAPPY / GZIP mutation fuzz instead")
     args = ap.parse_args()
+    if args.codecs:
+        return codecs(args.codecs)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -44,6 +47,50 @@ def main():
             total += compared
             print(f"{name} seed {seed}: {compared} cases, {errors} errors, {time.perf_counter() - t0:.2f}s", flush=True)
     print(f"ok: {total} mutated pages equal to the oracle", flush=True)
+
+
+def codecs(nseeds):
+    """The device codecs' mutation fuzz (tests/test_gpu_codec.py) over many seeds: SNAPPY blocks
+    (pyarrow-compressed samples and edge blocks, byte flips / truncations / size changes) and GZIP
+    streams (gzip_blocks.mutants), each page's status and bytes vs the oracle's codecs."""
+    import numpy as np
+    import pyarrow as pa
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import gzip_blocks as G
+    import test_gpu_codec as TC
+    from oracle import oracle as O
+    from snappy_blocks import edge_blocks, sample_blocks
+
+    ctx = pq.native.Context(0)
+    raws = sample_blocks(seed=9) + [c[1] for c in edge_blocks()]
+    comps = [pa.compress(r, codec="snappy", asbytes=True) if len(r) else b"\0" for r in raws]
+    valid = [(n, s, len(O.gzip_decode(s))) for n, s, _ in G.valid_cases()]
+    total = 0
+    for seed in range(2000, 2000 + nseeds):
+        rng = np.random.default_rng(seed)
+        blocks, sizes = [], []
+        for r, comp in zip(raws, comps):
+            for k in range(6):
+                b = bytearray(comp)
+                mode = k % 4
+                if mode == 0 and len(b) > 1:
+                    for _ in range(int(rng.integers(1, 4))):
+                        b[int(rng.integers(1, len(b)))] = int(rng.integers(0, 256))
+                elif mode == 1:
+                    b = b[:int(rng.integers(0, len(b) + 1))]
+                elif mode == 2 and len(b) > 1:
+                    b[int(rng.integers(1, len(b)))] ^= 1 << int(rng.integers(0, 8))
+                blocks.append(bytes(b))
+                sizes.append(max(0, len(r) + (int(rng.integers(-2, 3)) if mode == 3 else 0)))
+        bad = TC._check(pq, ctx, blocks, sizes)
+        ok, gbad = TC._gzip_check(pq, ctx, G.mutants(valid, seed=seed, per=3))
+        total += len(blocks) + ok + gbad
+        print(f"seed {seed}: snappy {len(blocks)} blocks ({bad} corrupt), gzip {ok + gbad} streams ({gbad} corrupt)",
+              flush=True)
+    print(f"ok: {total} mutated codec pages equal to the oracle", flush=True)
 
 
 if __name__ == "__main__":
