@@ -20,9 +20,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=40)
     ap.add_argument("--codecs", type=int, default=0, help="seeds of the SNAPPY / GZIP mutation fuzz instead")
+    ap.add_argument("--chains", type=int, default=0, help="seeds of random PLAIN byte-array chains instead")
     args = ap.parse_args()
     if args.codecs:
         return codecs(args.codecs)
+    if args.chains:
+        return chains(args.chains)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -91,6 +94,76 @@ def codecs(nseeds):
         print(f"seed {seed}: snappy {len(blocks)} blocks ({bad} corrupt), gzip {ok + gbad} streams ({gbad} corrupt)",
               flush=True)
     print(f"ok: {total} mutated codec pages equal to the oracle", flush=True)
+
+
+def chains(nseeds):
+    """PLAIN byte-array pages of random string-length mixes (empty runs, 4-12 byte keys, long
+    strings, records that look like length fields, strings of 60-140 KiB) through the fused chain
+    (k_ba_chain: every chunk one PLAIN page, no dictionary), clean and with a truncated / trailing /
+    corrupted page among them (the batch falls back to the scratch path): every case vs the oracle."""
+    import numpy as np
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import fixtures
+    import test_gpu_parity as T
+    from oracle import oracle as O
+
+    W = fixtures.W
+    col = (W.BYTE_ARRAY, 0, 0, 0)
+    ctx = pq.native.Context(0, profile=True)
+
+    def strings(rng, n):
+        kind = int(rng.integers(0, 6))
+        out = []
+        for _ in range(n):
+            u = rng.random()
+            if kind == 0:
+                out.append(b"" if u < 0.6 else bytes(int(rng.integers(0, 4))))
+            elif kind == 1:
+                out.append(bytes(rng.integers(97, 123, int(rng.integers(4, 13))).astype(np.uint8)))
+            elif kind == 2:
+                out.append(rng.bytes(int(rng.integers(100, 4000))) if u < 0.7 else b"")
+            elif kind == 3:
+                out.append(b"".join(int(rng.integers(0, 40)).to_bytes(4, "little") for _ in range(int(rng.integers(0, 5)))))
+            elif kind == 4:
+                out.append(rng.bytes(int(rng.integers(60000, 140000))) if u < 0.05 else rng.bytes(int(rng.integers(0, 9))))
+            else:
+                out.append(rng.bytes(int(rng.integers(0, 64))))
+        return out
+
+    total = fused = 0
+    for seed in range(3000, 3000 + nseeds):
+        rng = np.random.default_rng(seed)
+        cases = []
+        for _ in range(int(rng.integers(4, 10))):
+            n = int(rng.integers(0, 30000))
+            cases.append((col, None, (O.DATA_PAGE, n, W.PLAIN, 0, 0, T._plain_chain(strings(rng, n)))))
+        stats = {}
+        compared, errors = T._run_cases(pq, ctx, cases, stats)
+        fused += stats.get("k_ba_chain", 0) > 0
+        # one defect among the clean pages: trailing bytes, a short chain, a cut, a flipped byte
+        k = int(rng.integers(0, len(cases)))
+        c, d, (pt, n, enc, dl, rl, img) = cases[k]
+        defect = int(rng.integers(0, 4))
+        if defect == 0:
+            img = img + rng.bytes(int(rng.integers(1, 9)))
+        elif defect == 1:
+            n = n + int(rng.integers(1, 5))
+        elif defect == 2 and img:
+            img = img[:int(rng.integers(0, len(img)))]
+        elif img:
+            b = bytearray(img)
+            b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            img = bytes(b)
+        bad = cases[:k] + [(c, d, (pt, n, enc, dl, rl, img))] + cases[k + 1:]
+        compared2, errors2 = T._run_cases(pq, ctx, bad, {})
+        total += compared + compared2
+        print(f"seed {seed}: {len(cases)} pages clean ({errors} errors, fused {stats.get('k_ba_chain', 0)}), "
+              f"defect {defect} ({errors2} errors)", flush=True)
+    print(f"ok: {total} byte-array pages equal to the oracle; {fused} of {nseeds} clean batches on the fused chain",
+          flush=True)
 
 
 if __name__ == "__main__":
