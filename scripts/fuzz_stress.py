@@ -21,11 +21,14 @@ def main():
     ap.add_argument("--seeds", type=int, default=40)
     ap.add_argument("--codecs", type=int, default=0, help="seeds of the SNAPPY / GZIP mutation fuzz instead")
     ap.add_argument("--chains", type=int, default=0, help="seeds of random PLAIN byte-array chains instead")
+    ap.add_argument("--delta", type=int, default=0, help="seeds of the DELTA_BINARY_PACKED geometry fuzz instead")
     args = ap.parse_args()
     if args.codecs:
         return codecs(args.codecs)
     if args.chains:
         return chains(args.chains)
+    if args.delta:
+        return delta(args.delta)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -164,6 +167,31 @@ def chains(nseeds):
               f"defect {defect} ({errors2} errors)", flush=True)
     print(f"ok: {total} byte-array pages equal to the oracle; {fused} of {nseeds} clean batches on the fused chain",
           flush=True)
+
+
+def delta(nseeds):
+    """DELTA_BINARY_PACKED streams of every block geometry the reference accepts (14 geometries,
+    int32 / int64, random sizes and value regimes, with the test suite's mutations: counts above /
+    below the stream's, truncations, flipped bytes) over many seeds, alternately in page mode and
+    tile mode: every case vs the oracle."""
+    import numpy as np
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import test_gpu_parity as T
+
+    ctx = pq.native.Context(0)
+    total = 0
+    for seed in range(4000, 4000 + nseeds):
+        rng = np.random.default_rng(seed)
+        os.environ["PQH_DELTA_PAGE_MODE"] = "1" if seed % 2 else "0"
+        sizes = sorted({int(x) for x in rng.integers(1, 5000, 4)} | {int(rng.integers(1, 130))})
+        cases = T._delta_cases(rng, sizes, ["const", "mono", "small", "full", "mixed"], mutate=True)
+        compared, errors = T._run_cases(pq, ctx, cases)
+        total += compared
+        print(f"seed {seed} ({'page' if seed % 2 else 'tile'} mode): {compared} streams, {errors} errors", flush=True)
+    print(f"ok: {total} DELTA streams equal to the oracle", flush=True)
 
 
 if __name__ == "__main__":
