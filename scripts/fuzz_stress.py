@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--codecs", type=int, default=0, help="seeds of the SNAPPY / GZIP mutation fuzz instead")
     ap.add_argument("--chains", type=int, default=0, help="seeds of random PLAIN byte-array chains instead")
     ap.add_argument("--delta", type=int, default=0, help="seeds of the DELTA_BINARY_PACKED geometry fuzz instead")
+    ap.add_argument("--nest", type=int, default=0, help="seeds of random nested files (nesting outputs) instead")
     args = ap.parse_args()
     if args.codecs:
         return codecs(args.codecs)
@@ -29,6 +30,8 @@ def main():
         return chains(args.chains)
     if args.delta:
         return delta(args.delta)
+    if args.nest:
+        return nest(args.nest)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -192,6 +195,65 @@ def delta(nseeds):
         total += compared
         print(f"seed {seed} ({'page' if seed % 2 else 'tile'} mode): {compared} streams, {errors} errors", flush=True)
     print(f"ok: {total} DELTA streams equal to the oracle", flush=True)
+
+
+def nest(nseeds):
+    """Random nested files written by pyarrow (lists of lists, lists of structs of lists, maps;
+    random null / empty / length mixes, V1 / V2 pages, small pages) and the writer's deep repeated
+    chains (depth 1-20): every chunk's list offsets, presence per level and leaf validity vs
+    oracle.nest_levels (the Dremel-KAT-pinned restatement)."""
+    import io
+
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pqa
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import fixtures
+    import test_gpu_parity as T
+
+    ctx = pq.native.Context(0)
+    total = 0
+    for seed in range(5000, 5000 + nseeds):
+        rng = np.random.default_rng(seed)
+        p_null, p_empty, mean = float(rng.uniform(0, 0.5)), float(rng.uniform(0, 0.5)), float(rng.uniform(0.3, 5))
+
+        def lst(f):
+            u = rng.random()
+            if u < p_null:
+                return None
+            if u < p_null + p_empty:
+                return []
+            return [f() for _ in range(rng.poisson(mean))]
+
+        n = int(rng.integers(500, 8000))
+        leaf = lambda: None if rng.random() < p_null else int(rng.integers(-1000, 1000))  # noqa: E731
+        a = [lst(leaf) for _ in range(n)]
+        b = [lst(lambda: lst(leaf)) for _ in range(n)]
+        c = [lst(lambda: {"s": lst(lambda: None if rng.random() < p_null else str(rng.integers(0, 99)))})
+             for _ in range(n)]
+        m = [None if rng.random() < p_null else [(str(rng.integers(0, 50)), leaf()) for _ in range(rng.poisson(mean))]
+             for _ in range(n)]
+        t = pa.table({"a": pa.array(a, pa.list_(pa.int64())), "b": pa.array(b, pa.list_(pa.list_(pa.int32()))),
+                      "c": pa.array(c, pa.list_(pa.struct([("s", pa.list_(pa.string()))]))),
+                      "m": pa.array(m, pa.map_(pa.string(), pa.int64()))})
+        buf = io.BytesIO()
+        pqa.write_table(t, buf, row_group_size=int(rng.integers(200, n + 1)),
+                        data_page_size=int(rng.choice([1024, 8192, 1 << 20])), use_dictionary=bool(seed % 3 == 0),
+                        data_page_version="2.0" if seed % 2 else "1.0",
+                        # (pyarrow marks V2 pages with few values uncompressed; the reference decompresses
+                        # every V2 page regardless -- SURVEY.md A.5 -- so SNAPPY V2 files fail there)
+                        compression="NONE" if seed % 2 else "SNAPPY")
+        checked = T._check_nesting(pq, ctx, buf.getvalue())
+        depth = int(rng.integers(1, 21))
+        deep, _ = fixtures.deep_repeated(n=int(rng.integers(20, 800)), depth=depth, seed=seed)
+        checked += T._check_nesting(pq, ctx, deep)
+        total += checked
+        print(f"seed {seed}: {n} rows, nulls {p_null:.2f} empty {p_empty:.2f} mean {mean:.1f}; depth {depth}: "
+              f"{checked} nested chunks", flush=True)
+    print(f"ok: {total} nested chunks equal to oracle.nest_levels", flush=True)
 
 
 if __name__ == "__main__":
