@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--chains", type=int, default=0, help="seeds of random PLAIN byte-array chains instead")
     ap.add_argument("--delta", type=int, default=0, help="seeds of the DELTA_BINARY_PACKED geometry fuzz instead")
     ap.add_argument("--nest", type=int, default=0, help="seeds of random nested files (nesting outputs) instead")
+    ap.add_argument("--flat", type=int, default=0, help="seeds of random nullable / required k_flat batches instead")
     args = ap.parse_args()
     if args.codecs:
         return codecs(args.codecs)
@@ -32,6 +33,8 @@ def main():
         return delta(args.delta)
     if args.nest:
         return nest(args.nest)
+    if args.flat:
+        return flat(args.flat)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -254,6 +257,68 @@ def nest(nseeds):
         print(f"seed {seed}: {n} rows, nulls {p_null:.2f} empty {p_empty:.2f} mean {mean:.1f}; depth {depth}: "
               f"{checked} nested chunks", flush=True)
     print(f"ok: {total} nested chunks equal to oracle.nest_levels", flush=True)
+
+
+
+
+def flat(nseeds):
+    """k_flat's one-launch path (PQH_FLAT=1) on random small batches: nullable V2 columns (random
+    null fractions, including none and all) must decode in the one launch with no fallback, required
+    V1 / V2 columns beside them; then the same pages as explicit cases with their true num_nulls
+    hints, with wrong hints (the speculation fails, the batch falls back), and mutated: every chunk
+    and case vs the oracle."""
+    import numpy as np
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import test_gpu_parity as T
+    from parity import assert_chunk, oracle_chunk
+    from oracle import oracle as O
+
+    os.environ["PQH_FLAT"] = "1"
+    ctx = pq.native.Context(0, profile=True)
+    total = one_launch = 0
+    for seed in range(6000, 6000 + nseeds):
+        rng = np.random.default_rng(seed)
+        nf = [0.0, 1e-3, float(rng.uniform(0, 1)), 1.0][seed % 4]
+        n = int(rng.integers(2000, 40000))
+        for data in (T._nullable_flat(n, seed=seed, null_frac=nf), T._required_flat(n, bool(seed % 2), seed=seed)):
+            f = pq.native.File(data)
+            nc = len(f.columns())
+            res, b, hb = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, list(range(nc)), return_batch=True)
+            paths = b.paths()
+            stats = {s.name.decode(): s.launches for s in b.kernel_stats() if s.launches}
+            assert paths["flat_fallbacks"] == 0 and stats.get("k_flat", 0) == 1 and "k_expand" not in stats, \
+                (seed, paths, stats)
+            one_launch += 1
+            fr = O.FileReader(data)
+            for k, col in enumerate(res):
+                rg, ci = divmod(k, nc)
+                assert_chunk(col, oracle_chunk(fr, rg, ci), where=f"seed {seed} rg{rg} {col.path}")
+            total += len(res)
+            b.close()
+            hb.close()
+            f.close()
+        data = T._nullable_flat(n, seed=seed, null_frac=nf)
+        clean = T._page_sets_cases(pq, data)
+        hints = T._v2_null_hints(pq, data)
+        wrong = [h + int(rng.integers(1, 4)) if rng.random() < 0.3 else h for h in hints]
+        mut, mh = [], []
+        for (col, dimg, pg), h in zip(clean, hints):
+            for _ in range(3):
+                img2 = T._mutate(rng, pg[5])
+                if pg[3] + pg[4] <= len(img2):
+                    mut.append((col, dimg, pg[:5] + (img2,)))
+                    mh.append(h)
+        c1, e1 = T._run_cases(pq, ctx, clean, runs=2, hints=hints)
+        c2, e2 = T._run_cases(pq, ctx, clean, runs=1, hints=wrong)
+        c3, e3 = T._run_cases(pq, ctx, mut, runs=1 + seed % 2, hints=mh)
+        assert e1 == e2 == 0, (seed, e1, e2)
+        total += c1 + c2 + c3
+        print(f"seed {seed}: n {n} nulls {nf:.3f}: 2 files in one launch; {c1} + {c2} hinted / wrong-hint "
+              f"pages, {c3} mutants ({e3} errors)", flush=True)
+    print(f"ok: {one_launch} batches in k_flat's one launch, {total} chunks and cases equal to the oracle", flush=True)
 
 
 if __name__ == "__main__":
