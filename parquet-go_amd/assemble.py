@@ -502,3 +502,17 @@ def _dicts(kids, n):
     for i in np.flatnonzero(any_absent).tolist():
         out[i] = {nm: c[i] for nm, c, m in kids if not m[i]}
     return out
+
+
+def records_table(rows):
+    """Records (NextBatch's dicts) as a Table, for ReadRowGroupArrow's non-columnar row groups: a
+    column per top-level field any row holds, its type inferred over all rows (pyarrow unions the
+    keys of nested dicts; a field a record omits is null), so drop_absent of to_pylist() gives the
+    records back.  Rows that hold no field at all keep their count (a zero-field struct batch), which
+    Table.from_pylist -- names from the first row only -- loses."""
+    import pyarrow as pa
+
+    names = list(dict.fromkeys(k for r in rows for k in r))
+    if not names:
+        return pa.Table.from_batches([pa.RecordBatch.from_struct_array(pa.array([{}] * len(rows), pa.struct([])))])
+    return pa.table({k: pa.array([r.get(k) for r in rows]) for k in names})

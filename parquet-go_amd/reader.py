@@ -397,7 +397,7 @@ class FileReader:
                 return t
             self._rows = a
         rows = self.NextBatch(nrows - k)
-        return pa.Table.from_pylist(rows) if rows else pa.table({})
+        return assemble.records_table(rows) if rows else pa.table({})
 
     def close(self):
         self.file.close()

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--chains", type=int, default=0, help="seeds of random PLAIN byte-array chains instead")
     ap.add_argument("--delta", type=int, default=0, help="seeds of the DELTA_BINARY_PACKED geometry fuzz instead")
     ap.add_argument("--nest", type=int, default=0, help="seeds of random nested files (nesting outputs) instead")
+    ap.add_argument("--records", type=int, default=0, help="seeds of random nested files read by NextRow / Arrow")
     ap.add_argument("--flat", type=int, default=0, help="seeds of random nullable / required k_flat batches instead")
     args = ap.parse_args()
     if args.codecs:
@@ -35,6 +36,8 @@ def main():
         return nest(args.nest)
     if args.flat:
         return flat(args.flat)
+    if args.records:
+        return records(args.records)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -200,17 +203,53 @@ def delta(nseeds):
     print(f"ok: {total} DELTA streams equal to the oracle", flush=True)
 
 
-def nest(nseeds):
-    """Random nested files written by pyarrow (lists of lists, lists of structs of lists, maps;
-    random null / empty / length mixes, V1 / V2 pages, small pages) and the writer's deep repeated
-    chains (depth 1-20): every chunk's list offsets, presence per level and leaf validity vs
-    oracle.nest_levels (the Dremel-KAT-pinned restatement)."""
+def _nested_file(seed, n_lo=500, n_hi=8000):
+    """A random nested file written by pyarrow (seeded): list<int64>, list<list<int32>>,
+    list<struct<list<string>>>, map<string, int64>; random null / empty / length mixes, row group and
+    page sizes, V1 / V2 pages.  Returns (bytes, rows, p_null, p_empty, mean, the generator)."""
     import io
 
     import numpy as np
     import pyarrow as pa
     import pyarrow.parquet as pqa
 
+    rng = np.random.default_rng(seed)
+    p_null, p_empty, mean = float(rng.uniform(0, 0.5)), float(rng.uniform(0, 0.5)), float(rng.uniform(0.3, 5))
+
+    def lst(f):
+        u = rng.random()
+        if u < p_null:
+            return None
+        if u < p_null + p_empty:
+            return []
+        return [f() for _ in range(rng.poisson(mean))]
+
+    n = int(rng.integers(n_lo, n_hi))
+    leaf = lambda: None if rng.random() < p_null else int(rng.integers(-1000, 1000))  # noqa: E731
+    a = [lst(leaf) for _ in range(n)]
+    b = [lst(lambda: lst(leaf)) for _ in range(n)]
+    c = [lst(lambda: {"s": lst(lambda: None if rng.random() < p_null else str(rng.integers(0, 99)))})
+         for _ in range(n)]
+    m = [None if rng.random() < p_null else [(str(rng.integers(0, 50)), leaf()) for _ in range(rng.poisson(mean))]
+         for _ in range(n)]
+    t = pa.table({"a": pa.array(a, pa.list_(pa.int64())), "b": pa.array(b, pa.list_(pa.list_(pa.int32()))),
+                  "c": pa.array(c, pa.list_(pa.struct([("s", pa.list_(pa.string()))]))),
+                  "m": pa.array(m, pa.map_(pa.string(), pa.int64()))})
+    buf = io.BytesIO()
+    pqa.write_table(t, buf, row_group_size=int(rng.integers(min(200, n), n + 1)),
+                    data_page_size=int(rng.choice([1024, 8192, 1 << 20])), use_dictionary=bool(seed % 3 == 0),
+                    data_page_version="2.0" if seed % 2 else "1.0",
+                    # (pyarrow marks V2 pages with few values uncompressed; the reference decompresses
+                    # every V2 page regardless -- SURVEY.md A.5 -- so SNAPPY V2 files fail there)
+                    compression="NONE" if seed % 2 else "SNAPPY")
+    return buf.getvalue(), n, p_null, p_empty, mean, rng
+
+
+def nest(nseeds):
+    """Random nested files written by pyarrow (lists of lists, lists of structs of lists, maps;
+    random null / empty / length mixes, V1 / V2 pages, small pages) and the writer's deep repeated
+    chains (depth 1-20): every chunk's list offsets, presence per level and leaf validity vs
+    oracle.nest_levels (the Dremel-KAT-pinned restatement)."""
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -220,36 +259,8 @@ def nest(nseeds):
     ctx = pq.native.Context(0)
     total = 0
     for seed in range(5000, 5000 + nseeds):
-        rng = np.random.default_rng(seed)
-        p_null, p_empty, mean = float(rng.uniform(0, 0.5)), float(rng.uniform(0, 0.5)), float(rng.uniform(0.3, 5))
-
-        def lst(f):
-            u = rng.random()
-            if u < p_null:
-                return None
-            if u < p_null + p_empty:
-                return []
-            return [f() for _ in range(rng.poisson(mean))]
-
-        n = int(rng.integers(500, 8000))
-        leaf = lambda: None if rng.random() < p_null else int(rng.integers(-1000, 1000))  # noqa: E731
-        a = [lst(leaf) for _ in range(n)]
-        b = [lst(lambda: lst(leaf)) for _ in range(n)]
-        c = [lst(lambda: {"s": lst(lambda: None if rng.random() < p_null else str(rng.integers(0, 99)))})
-             for _ in range(n)]
-        m = [None if rng.random() < p_null else [(str(rng.integers(0, 50)), leaf()) for _ in range(rng.poisson(mean))]
-             for _ in range(n)]
-        t = pa.table({"a": pa.array(a, pa.list_(pa.int64())), "b": pa.array(b, pa.list_(pa.list_(pa.int32()))),
-                      "c": pa.array(c, pa.list_(pa.struct([("s", pa.list_(pa.string()))]))),
-                      "m": pa.array(m, pa.map_(pa.string(), pa.int64()))})
-        buf = io.BytesIO()
-        pqa.write_table(t, buf, row_group_size=int(rng.integers(200, n + 1)),
-                        data_page_size=int(rng.choice([1024, 8192, 1 << 20])), use_dictionary=bool(seed % 3 == 0),
-                        data_page_version="2.0" if seed % 2 else "1.0",
-                        # (pyarrow marks V2 pages with few values uncompressed; the reference decompresses
-                        # every V2 page regardless -- SURVEY.md A.5 -- so SNAPPY V2 files fail there)
-                        compression="NONE" if seed % 2 else "SNAPPY")
-        checked = T._check_nesting(pq, ctx, buf.getvalue())
+        data, n, p_null, p_empty, mean, rng = _nested_file(seed)
+        checked = T._check_nesting(pq, ctx, data)
         depth = int(rng.integers(1, 21))
         deep, _ = fixtures.deep_repeated(n=int(rng.integers(20, 800)), depth=depth, seed=seed)
         checked += T._check_nesting(pq, ctx, deep)
@@ -319,6 +330,53 @@ def flat(nseeds):
         print(f"seed {seed}: n {n} nulls {nf:.3f}: 2 files in one launch; {c1} + {c2} hinted / wrong-hint "
               f"pages, {c3} mutants ({e3} errors)", flush=True)
     print(f"ok: {one_launch} batches in k_flat's one launch, {total} chunks and cases equal to the oracle", flush=True)
+
+def records(nseeds):
+    """The record API over random nested files (_nested_file, smaller; some with one corrupted page
+    block): every NextRow outcome -- row, load error, or the page error at the row that reaches it --
+    and every ReadRowGroupArrow table equal, call by call, to the assembly over the oracle's pages
+    (tests/test_records.py oracle_next_rows)."""
+    import numpy as np
+
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import test_records as R
+    from oracle import oracle as O
+
+    ctx = pq.native.Context(0)
+    total = rows = errs = 0
+    for seed in range(7000, 7000 + nseeds):
+        data, n, *_ = _nested_file(seed, 100, 1500)
+        rng = np.random.default_rng(seed + 1)
+        if seed % 3 == 0:  # one byte flipped inside a random page block
+            fr = O.FileReader(data)
+            rg, ci = int(rng.integers(0, len(fr.row_groups))), int(rng.integers(0, len(fr.columns)))
+            blocks = R._page_blocks(data, rg, ci)
+            _, start, length = blocks[int(rng.integers(0, len(blocks)))]
+            pos = start + int(rng.integers(0, min(24, length) if rng.random() < 0.5 else length))  # (header or body)
+            data = data[:pos] + bytes([data[pos] ^ (1 << int(rng.integers(0, 8)))]) + data[pos + 1:]
+        want = [R._norm(w) for w in R.oracle_next_rows(data)]
+        fr = pq.reader.FileReader(data, ctx=ctx)
+        got = []
+        while True:
+            try:
+                got.append(R._norm(fr.NextRow()))
+            except EOFError:
+                break
+            except (pq.reader.DecodeError, pq.records.RecordError) as e:
+                got.append(R._norm(R.error_outcome(e)))
+        fr.close()
+        assert got == want, (seed, next(i for i, (g, w) in enumerate(zip(got + [None], want)) if g != w))
+        arrow, paths = R._read_arrow(pq, data)
+        assert [R._norm(g) for g in arrow] == want, seed
+        e = sum(1 for w in want if isinstance(w, tuple))
+        total += 1
+        rows += len(want) - e
+        errs += e
+        print(f"seed {seed}: {n} rows{' (corrupted)' if seed % 3 == 0 else ''}: {len(want) - e} rows, {e} errors; "
+              f"NextRow and ReadRowGroupArrow equal to the oracle {paths}", flush=True)
+    print(f"ok: {total} files, {rows} rows and {errs} error outcomes equal to the oracle's records", flush=True)
 
 
 if __name__ == "__main__":

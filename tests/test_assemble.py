@@ -227,3 +227,17 @@ def test_columnar_selected_columns():
             assert stats.get("fallback")
         if cols in ([0], [1, 2]):
             assert not stats.get("fallback")
+
+
+def test_records_table_fallback():
+    """ReadRowGroupArrow's table for non-columnar row groups (assemble.records_table): every
+    top-level field any record holds becomes a column, not just the first record's (records omit
+    absent fields), and records with no field keep the row count."""
+    A = _pkg().assemble
+    rows = [{"a": {"list": [{"element": 1}, {}]}}, {}, {"c": {"list": [{"element": {"s": {}}}]}, "m": {}},
+            {"b": {"list": [{"element": {"list": [{"element": -3}]}}]}, "a": {}}]
+    t = A.records_table(rows)
+    assert sorted(t.column_names) == ["a", "b", "c", "m"] and t.num_rows == 4
+    assert [A.drop_absent(r) for r in t.to_pylist()] == rows
+    t = A.records_table([{}, {}, {}])
+    assert t.num_rows == 3 and [A.drop_absent(r) for r in t.to_pylist()] == [{}, {}, {}]
