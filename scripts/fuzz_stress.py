@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--delta", type=int, default=0, help="seeds of the DELTA_BINARY_PACKED geometry fuzz instead")
     ap.add_argument("--nest", type=int, default=0, help="seeds of random nested files (nesting outputs) instead")
     ap.add_argument("--records", type=int, default=0, help="seeds of random nested files read by NextRow / Arrow")
+    ap.add_argument("--files", type=int, default=0, help="seeds of random flat pyarrow files (types x encodings)")
     ap.add_argument("--flat", type=int, default=0, help="seeds of random nullable / required k_flat batches instead")
     args = ap.parse_args()
     if args.codecs:
@@ -38,6 +39,8 @@ def main():
         return flat(args.flat)
     if args.records:
         return records(args.records)
+    if args.files:
+        return pyarrow_files(args.files)
     import __graft_entry__ as ge
 
     pq = ge._package()
@@ -377,6 +380,95 @@ def records(nseeds):
         print(f"seed {seed}: {n} rows{' (corrupted)' if seed % 3 == 0 else ''}: {len(want) - e} rows, {e} errors; "
               f"NextRow and ReadRowGroupArrow equal to the oracle {paths}", flush=True)
     print(f"ok: {total} files, {rows} rows and {errs} error outcomes equal to the oracle's records", flush=True)
+
+def _flat_file(seed):
+    """A random flat file written by pyarrow (seeded): 4-9 columns of random types (INT32 / INT64 /
+    FLOAT / DOUBLE / BOOLEAN / BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 timestamps), each required or
+    nullable at a random null fraction, each dictionary / PLAIN / a DELTA encoding / BYTE_STREAM_SPLIT
+    as the type allows; random row group and page sizes; V1 pages UNCOMPRESSED / SNAPPY / GZIP, V2
+    pages uncompressed.  Returns (bytes, rows, description)."""
+    import io
+
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pqa
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 60000))
+    kinds = ["i32", "i64", "f32", "f64", "bool", "str", "bin", "flba", "ts96"]
+    cols, enc, dict_cols, desc = {}, {}, [], []
+    for k in range(int(rng.integers(4, 10))):
+        kind = kinds[int(rng.integers(0, len(kinds)))]
+        name = f"{kind}_{k}"
+        card = int(rng.choice([1, 7, 300, 1 << 20]))
+        if kind in ("i32", "i64"):
+            hi = int(rng.choice([2, 1000, 2**31 - 1]))
+            v = pa.array(rng.integers(-hi, hi, n) % card if card < 1000 else rng.integers(-hi, hi, n),
+                         pa.int32() if kind == "i32" else pa.int64())
+            choices = ["dict", "PLAIN", "DELTA_BINARY_PACKED"]
+        elif kind in ("f32", "f64"):
+            v = pa.array(rng.standard_normal(n)[rng.integers(0, min(card, n), n)] if card < n else rng.standard_normal(n),
+                         pa.float32() if kind == "f32" else pa.float64())
+            choices = ["dict", "PLAIN", "BYTE_STREAM_SPLIT"]
+        elif kind == "bool":
+            v = pa.array(rng.random(n) < rng.random())
+            choices = ["PLAIN"]
+        elif kind in ("str", "bin"):
+            lens = rng.integers(0, int(rng.choice([1, 8, 40, 300])), n)
+            pool = [rng.bytes(int(x)) for x in lens[:min(card, n)]]
+            raw = [pool[int(i)] for i in rng.integers(0, len(pool), n)] if card < n else [rng.bytes(int(x)) for x in lens]
+            v = pa.array([r.hex() for r in raw]) if kind == "str" else pa.array(raw, pa.binary())
+            choices = ["dict", "PLAIN", "DELTA_LENGTH_BYTE_ARRAY", "DELTA_BYTE_ARRAY"]
+        elif kind == "flba":
+            v = pa.array([bytes(r) for r in rng.integers(0, 256, (n, 16), dtype=np.uint8)[rng.integers(0, min(card, n), n)]],
+                         pa.binary(16))
+            choices = ["dict", "PLAIN", "DELTA_BYTE_ARRAY"]
+        else:
+            v = pa.array(rng.integers(0, 2**62, n) % (10**18), pa.timestamp("ns"))
+            choices = ["dict", "PLAIN"]
+        if rng.random() < 0.5:
+            nf = float(rng.choice([0.0, 0.01, rng.random(), 1.0]))
+            v = pa.array(v.to_pylist(), v.type, mask=rng.random(n) < nf)
+        else:
+            nf = None
+        e = choices[int(rng.integers(0, len(choices)))]
+        if e == "dict":
+            dict_cols.append(name)
+        else:
+            enc[name] = e
+        cols[name] = v
+        desc.append(f"{name}:{e}" + ("" if nf is None else f"/nulls {nf:.2f}"))
+    t = pa.table(cols)
+    schema = pa.schema([pa.field(k, c.type, nullable=(k in cols and cols[k].null_count > 0) or rng.random() < 0.5)
+                        for k, c in cols.items()])
+    t = t.cast(schema)
+    v2 = bool(seed % 2)
+    comp = "NONE" if v2 else str(rng.choice(["NONE", "SNAPPY", "GZIP"]))
+    buf = io.BytesIO()
+    pqa.write_table(t, buf, row_group_size=int(rng.integers(max(1, n // 8), n + 1)),
+                    data_page_size=int(rng.choice([1024, 16384, 1 << 20])), use_dictionary=dict_cols or False,
+                    column_encoding=enc or None, data_page_version="2.0" if v2 else "1.0", compression=comp,
+                    use_deprecated_int96_timestamps=True, store_schema=False)
+    return buf.getvalue(), n, f"{'V2' if v2 else 'V1'} {comp}: " + " ".join(desc)
+
+
+def pyarrow_files(nseeds):
+    """Random flat pyarrow files (_flat_file) through decode_chunks: every chunk's status, first
+    error, levels and values vs the oracle (tests/test_gpu_parity.py _run_file; a type / encoding pair
+    the reference rejects must fail the same way, NOT_IMPLEMENTED never)."""
+    import __graft_entry__ as ge
+
+    pq = ge._package()
+    import test_gpu_parity as T
+
+    ctx = pq.native.Context(0)
+    total = 0
+    for seed in range(8000, 8000 + nseeds):
+        data, n, desc = _flat_file(seed)
+        checked, _ = T._run_file(pq, ctx, data)
+        total += checked
+        print(f"seed {seed}: {n} rows, {checked} chunks: {desc}", flush=True)
+    print(f"ok: {total} chunks of random pyarrow files equal to the oracle", flush=True)
 
 
 if __name__ == "__main__":
