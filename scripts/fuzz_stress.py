@@ -5,6 +5,8 @@ many seeds and fixtures, with PQH_FLAT on and off.  Prints one line per (fixture
 the first mismatch (the assertion names the case).
 
   python scripts/fuzz_stress.py [--seeds 40]
+  python scripts/fuzz_stress.py --codecs N | --chains N | --delta N | --nest N | --flat N | --records N | --files N
+(one mode per run; the logs of the round-5 runs are under profiles/r05/fuzz_*.log)
 """
 import argparse
 import os
