@@ -205,12 +205,12 @@ def check_statuses(batch, num_chunks, native, where):
                                f"page {o.error_page} phase {o.error_phase}")
 
 
-def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync, pinned=True):
+def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync, pinned=True, verify=None):
     """Load row groups [rg0, rg1) of f into one HBM-resident batch and time `steps` decode runs
     (graph replays) between barriers; statuses checked before and after the timed runs.
     pinned: the walk writes the page images into the context's pinned pool (False: pageable host
-    memory, for blocks of tens of GB).  Returns (seconds, decoded bytes per run, algorithmic bytes
-    read per run, pages)."""
+    memory, for blocks of tens of GB).  verify(batch): called after the timed runs (outside them).
+    Returns (seconds, decoded bytes per run, algorithmic bytes read per run, pages)."""
     ncols = len(f.columns())
     hb = f.load(rg0, rg1, list(range(ncols)), ctx=ctx if pinned else None)
     b = native.Batch.from_host(ctx, hb)
@@ -229,6 +229,8 @@ def timed_block(ctx, native, f, rg0, rg1, steps, warmup, barrier_sync, pinned=Tr
         el = time.perf_counter() - t0
         b.sync()
         check_statuses(b, hb.num_chunks, native, f"row groups [{rg0}, {rg1}) after the timed runs")
+        if verify is not None:
+            verify(b)
         return el, wr, rd, hb.num_pages
     finally:
         b.close()
@@ -265,6 +267,71 @@ def kernel_table(stats, workload, rows):
                 "frac_of_measured_copy_ceiling": round(ach / 6290.0, 4)}
     all_ms = sum(s.total_ms for s in stats) / max(1, nsteps)
     return kernels, roof, all_ms
+
+
+def mixed_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync):
+    """N > 1: north_star's 1B-row mixed file as strong scaling over the ranks ("near-linear
+    row-group scaling to 8 GPUs"; chunk_reader.go:375-404 readRowGroupData per row group,
+    file_reader.go:187-198 SeekToRowGroup addresses any of them).  Rank 0 writes the file once into
+    /dev/shm (in place, datasets.mixed(path=...)); every rank memory-maps it and decodes its block
+    shard.row_group_block(128, N, rank) HBM-resident; whole-node GB/s = the decoded bytes of all
+    ranks / the slowest rank's time; the blocks are checked to tile the file; each rank's first and
+    last row group (every chunk) is compared with the oracle after its timed runs."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    rows = args.mixed_rows or datasets.MIXED_ROWS
+    desc = datasets.WORKLOADS["mixed"][0]
+    steps = max(3, min(args.steps, 10))
+    warm = max(1, min(args.warmup, 2))
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    path = os.path.join(shm, f"pqh_bench_mixed_50_{os.environ.get('MASTER_PORT', '0')}.parquet")
+    t0 = time.perf_counter()
+    if rank == 0:
+        datasets.mixed(rows=rows, path=path + ".part")
+        os.replace(path + ".part", path)
+    dist.barrier()
+    gen_s = time.perf_counter() - t0
+    f = native.File(path)
+    try:
+        nrg, ncols = f.num_row_groups, len(f.columns())
+        rg0, rg1 = pkg.shard.row_group_block(nrg, world, rank)
+        dev = f"cuda:{local}"
+        checked = []
+
+        def verify(b):  # the rank's first and last row group, every chunk, vs the oracle (untimed)
+            fr = O.FileReader(np.memmap(path, dtype=np.uint8, mode="r"))
+            for rg in sorted({rg0, rg1 - 1}):
+                for ci in range(ncols):
+                    check_chunk(ctx, b, (rg - rg0) * ncols + ci, O.decode_chunk(fr.read_chunk(rg, ci)), np)
+                checked.append(rg)
+
+        el, wr, rd, pages = timed_block(ctx, native, f, rg0, rg1, steps, warm, barrier_sync, pinned=False,
+                                        verify=verify)
+        my_rows = sum(f.row_group_num_rows(g) for g in range(rg0, rg1))
+        el, total = pkg.shard.reduce_step(el, wr, device=dev)
+        blocks = pkg.shard.gather_blocks(rg0, rg1, my_rows, wr, device=dev)
+        pkg.shard.check_cover(blocks, nrg, f.num_rows)
+        t = el / steps
+        return {"workload": desc, "scaling": "strong", "n_gpus": world, "rows_total": f.num_rows,
+                "row_groups": nrg, "file_bytes": os.path.getsize(path), "steps": steps,
+                "ms_per_step": round(t * 1e3, 4), "value": round(total / t / 1e9, 2),
+                "unit": "GB/s (decoded output, whole node)",
+                "per_gpu_gbps_rank0": round(wr / t / 1e9, 2), "pages_rank0": pages,
+                "step_roofline_rank0": {"bound": "hbm", "achieved": round((rd + wr) / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": round((rd + wr) / t / 1e9 / HBM_PEAK_GBS, 4),
+                                        "note": "rank 0's algorithmic bytes / the slowest rank's step time"},
+                "shards": [{"rank": r, "row_groups": [b[0], b[1]], "rows": b[2], "decoded_bytes": b[3]}
+                           for r, b in enumerate(blocks)],
+                "verified": f"rank 0: row groups {checked}: {len(checked) * ncols} chunks bit-exact vs the oracle "
+                            "(every rank checks its first and last row group)",
+                "generate_s": round(gen_s, 2)}
+    finally:
+        f.close()
+        dist.barrier()
+        if rank == 0:
+            os.unlink(path)
 
 
 def mixed_record(args, ctx, native, pkg, datasets, barrier_sync):
@@ -673,10 +740,32 @@ def dry_run(args, world, rank, dist, pkg, datasets, builder, kw, seed, strong, d
                 proxy.append({"n_gpus": n, "rank0_row_groups": [a, b], "rank0_decoded_bytes": decode(fr3, a, b)})
             c3 = {"workload": c3desc, "scaling": "strong", "n_gpus": 1, "rows_total": fr3.num_rows, "row_groups": nrg,
                   "decoded_bytes_total": full, "proxy": proxy}
+    mixed = None
+    if world > 1 and not args.no_mixed and args.workload != "mixed" and args.mixed_rows:
+        # mixed_strong_record's plan: rank 0 writes the file in place into a shared path, every rank
+        # maps it and decodes its block of row_group_block(128, N, rank)
+        import numpy as np
+
+        shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+        mpath = os.path.join(shm, f"pqh_dry_mixed_{os.environ.get('MASTER_PORT', '0')}.parquet")
+        if rank == 0:
+            datasets.mixed(rows=args.mixed_rows, path=mpath + ".part")
+            os.replace(mpath + ".part", mpath)
+        dist.barrier()
+        frm = O.FileReader(np.memmap(mpath, dtype=np.uint8, mode="r"))
+        elm, totalm, shardsm = sharded(frm, True)
+        mixed = {"workload": datasets.WORKLOADS["mixed"][0], "scaling": "strong", "n_gpus": world,
+                 "rows_total": frm.num_rows, "row_groups": len(frm.row_groups), "decoded_bytes_total": totalm,
+                 "max_rank_s": elm, "shards": shardsm}
+        del frm
+        dist.barrier()
+        if rank == 0:
+            os.unlink(mpath)
     if rank == 0:
         print(json.dumps({"dry_run": True, "metric": METRIC, "n_gpus": world, "scaling": "strong" if strong else "weak",
                           "config": {"workload": desc, "rows_total": fr.num_rows if strong else fr.num_rows * world},
-                          "decoded_bytes_total": total, "max_rank_s": el, "shards": shards, "c3_strong": c3}),
+                          "decoded_bytes_total": total, "max_rank_s": el, "shards": shards, "c3_strong": c3,
+                          "mixed_1b": mixed}),
               flush=True)
     if world > 1:
         dist.barrier()
@@ -698,7 +787,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (pinned H2D + decode) pass")
     ap.add_argument("--no-c3", action="store_true", help="skip the c3_strong sub-record")
-    ap.add_argument("--no-mixed", action="store_true", help="skip the mixed_1b sub-record (N=1)")
+    ap.add_argument("--no-mixed", action="store_true", help="skip the mixed_1b sub-record (N=1: the file on one GPU "
+                    "+ the rank-0 proxy; N>1: strong scaling of the file over the ranks)")
     ap.add_argument("--mixed-rows", type=int, default=0, help=argparse.SUPPRESS)  # tests: a smaller mixed file
     ap.add_argument("--e2e-dev-ranges", type=int, default=4,
                     help="end-to-end with device codecs: staged batches (H2D of one overlaps the codec of the last)")
@@ -755,7 +845,10 @@ def main():
         shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
         path = os.path.join(shm, f"pqh_bench_{args.workload}_{seed_kw}_{os.environ.get('MASTER_PORT', '0')}.parquet")
         if rank == 0:
-            builder(seed=seed_kw, **kw).tofile(path + ".part")
+            if args.workload == "mixed":  # (36 GB: written in place, never held in this process)
+                builder(seed=seed_kw, path=path + ".part", **kw)
+            else:
+                builder(seed=seed_kw, **kw).tofile(path + ".part")
             os.replace(path + ".part", path)
         dist.barrier()
         data = None
@@ -977,12 +1070,15 @@ def main():
     c1_x10 = None
     if world == 1 and args.workload == "c1":
         c1_x10 = c1_x10_record(args, ctx, native, datasets, barrier_sync)
-    if world == 1 and not args.no_mixed and args.workload != "mixed":
+    if not args.no_mixed and args.workload != "mixed":
         if hb is not None:
             hb.close()
             hb = None
         data = None  # (the main file: its memory back before the 1B-row file is built)
-        mixed = mixed_record(args, ctx, native, pkg, datasets, barrier_sync)
+        if world > 1:
+            mixed = mixed_strong_record(args, ctx, native, pkg, datasets, world, rank, local, dist, barrier_sync)
+        else:
+            mixed = mixed_record(args, ctx, native, pkg, datasets, barrier_sync)
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PQH_ABI_VERSION 7
+#define PQH_ABI_VERSION 8
 
 /* Bytes of readable slack the device payload buffer must have after its last page image.  The
  * kernels issue (masked) vector loads that may run up to this many bytes past a stream end. */
@@ -117,9 +117,15 @@ typedef enum pqh_status {
   PQH_ERR_DICT_PAGE = 31,             /* second dictionary page / dictionary encoding not PLAIN (chunk_reader.go:197-199, page_dict.go:44-46) */
   PQH_ERR_NO_DEVICE = 32,             /* no HIP device present */
   PQH_ERR_NOT_IMPLEMENTED = 33,       /* decoder kind not (yet) available on the device */
-  PQH_ERR_INTERNAL = 34               /* a device consistency guard fired (an index outside its buffer,
+  PQH_ERR_INTERNAL = 34,              /* a device consistency guard fired (an index outside its buffer,
                                          a look-back that never completed): a bug, never a property of
                                          the input -- the chunk's outputs are undefined */
+  PQH_ERR_UNSUPPORTED_CODEC = 35      /* the chunk's codec is not decoded by this library (ZSTD, LZ4,
+                                         BROTLI, LZO, or any codec a caller registers with
+                                         RegisterBlockCompressor, compress.go:119-129,160,182-187): set by
+                                         the page walker before any page of the chunk is read, never
+                                         a property of the data -- the caller decodes the chunk with the
+                                         reference's own readChunk / pageReader path */
 } pqh_status;
 
 /* Decode phases, in the order the reference runs them for one page (page_v1.go:33-122). */
@@ -350,15 +356,15 @@ int pqh_batch_page_results(const pqh_batch* batch, pqh_page_result* out, int32_t
  * size); def_levels / rep_levels receive num_slots bytes each (NULL = skip); fixed-width values
  * go to `values` (num_non_null * value_size bytes), byte arrays to offsets (num_non_null + 1,
  * relative to the first returned value) + data (num_bytes); value_nil (NULL = skip) receives
- * num_non_null bytes, 1 where the value is the reference's nil (INT96, see pqh_chunk_out), which
- * the shim boxes as a nil interface{}.  With NULL value buffers only the sizes are filled in.  On a readValues error (out->status != PQH_OK) nothing is copied, as the
+ * num_non_null bytes (value_nil_cap bytes available, PQH_ERR_ARG when fewer), 1 where the value is
+ * the reference's nil (INT96, see pqh_chunk_out), which the shim boxes as a nil interface{}.  With NULL value buffers only the sizes are filled in.  On a readValues error (out->status != PQH_OK) nothing is copied, as the
  * reference returns nil slices.  Errors are those of the whole-page call the reference makes
  * (ColumnStore.readNextPage, data_store.go:236-260); a ranged call reports a level error once its
  * range reaches the failing slot and a value error once its values reach the failing value. */
 int pqh_batch_page_read(const pqh_batch* batch, int32_t page, int64_t first, int64_t count, void* values,
                         int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data,
                         int64_t data_cap, uint8_t* def_levels, uint8_t* rep_levels, uint8_t* value_nil,
-                        pqh_page_values* out);
+                        int64_t value_nil_cap, pqh_page_values* out);
 /* Kernel timing accumulated since the last reset (requires PQH_CTX_PROFILE). */
 int pqh_batch_kernel_stats(const pqh_batch* batch, pqh_kernel_stat* out, int32_t max_stats,
                            int32_t* num_stats);
@@ -400,6 +406,16 @@ int32_t pqh_file_schema_name(const pqh_file* f, int32_t i, char* buf, int32_t ca
  * (file_path set, negative offset).  A row group fails at the first column (in schema order)
  * that fails here or whose chunk fails to load. */
 int pqh_file_chunk_check(const pqh_file* f, int32_t rg, int32_t column, int32_t selected);
+
+/* The caller's codec registry (the reference's `compressors` map, compress.go:16-33,160-187; by
+ * default UNCOMPRESSED, GZIP, SNAPPY and ZSTD, as its init registers them).  A chunk whose codec is
+ * registered but not decoded by this library (any codec but UNCOMPRESSED / SNAPPY / GZIP) fails its
+ * load with PQH_ERR_UNSUPPORTED_CODEC before any of its pages is read: the caller decodes that chunk
+ * with the reference's own readChunk / pageReader path.  A codec in no registry fails
+ * as the reference fails it (decompressBlock: "method not supported"): PQH_ERR_DECOMPRESS at the
+ * chunk's first page block, after that page's header and CRC checks.  The cgo shim passes the keys of
+ * GetRegisteredBlockCompressors() (compress.go:164-176). */
+int pqh_file_set_codecs(pqh_file* f, const int32_t* codecs, int32_t num_codecs);
 
 /* The schema as a flat DFS list (FileMetaData.schema, root first), with the levels the reader
  * derives for every node (readGroupSchema / readColumnSchema, schema.go:893-990): what the record

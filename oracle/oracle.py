@@ -563,6 +563,10 @@ def read_schema(schema):
     return leaves
 
 
+# The codecs the reference registers at init (compress.go:182-187).
+DEFAULT_CODECS = (UNCOMPRESSED, GZIP, SNAPPY, ZSTD)
+
+
 def decompress(codec, data, uncompressed_size):
     if codec == UNCOMPRESSED:
         return bytes(data)
@@ -763,8 +767,13 @@ class FileReader:
     (file_meta.go:23-73) + makeSchema (schema.go:1048-1079).  Raises FileError where the reference's
     NewFileReader returns an error."""
 
-    def __init__(self, data):
-        self.data = data.tobytes() if hasattr(data, "tobytes") else bytes(data)
+    def __init__(self, data, codecs=DEFAULT_CODECS):
+        # the reference's compressors registry (compress.go:16-33,160-187): its init registers
+        # UNCOMPRESSED, GZIP, SNAPPY and ZSTD; decompressBlock fails "method not supported" for others
+        self.codecs = frozenset(codecs)
+        # (bytes as given; anything else -- a numpy array, an mmap -- read in place through a
+        # memoryview: a 36 GB file is not copied; page blocks are copied as they are read)
+        self.data = data if isinstance(data, bytes) else memoryview(data).cast("B")
         d = self.data
         if len(d) < 4 or d[:4] != b"PAR1":
             raise FileError("invalid parquet file header")
@@ -848,7 +857,7 @@ class FileReader:
                 nonlocal pos, count, block
                 if csize < 0 or usize < 0:
                     return ERR_PAGE_HEADER
-                block = d[pos:pos + csize]
+                block = bytes(d[pos:pos + csize])
                 pos += len(block)
                 count += len(block)
                 if validate_crc and 4 in ph and (zlib.crc32(block) & 0xFFFFFFFF) != (ph[4] & 0xFFFFFFFF):
@@ -859,6 +868,8 @@ class FileReader:
                 if csz < 0 or usz < 0:
                     return None, ERR_PAGE_HEADER
                 if len(blk) != csz:
+                    return None, ERR_DECOMPRESS
+                if codec not in self.codecs:  # decompressBlock: "method %q is not supported" (:119-129)
                     return None, ERR_DECOMPRESS
                 try:
                     img = decompress(codec, blk, usz)

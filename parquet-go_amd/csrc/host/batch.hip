@@ -81,8 +81,9 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_dba_prefix", "k_delta_spec", "k_delta_page", "k_delta_init",
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
                               "k_ba_wcopy",   "k_gzip",      "k_snap_spec",  "k_snap_stitch",
-                              "k_snap_emit",  "k_snap_fixup", "k_ba_chain",   "k_flat"};
-constexpr int kNumKernels = 31;
+                              "k_snap_emit",  "k_snap_fixup", "k_ba_chain",   "k_flat",
+                              "k_expand_lev"};
+constexpr int kNumKernels = 32;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -108,6 +109,12 @@ bool snappy_page_mode() {
 // (k_ba_wspec / wstitch / wcopy) instead of the fused k_ba_chain.
 bool fuse_enabled() {
   const char* f = getenv("PQH_BA_FUSE");
+  return !(f && f[0] == '0');
+}
+
+// PQH_NEST_EARLY=0 (A/B experiments, tests): one k_expand launch, the nesting kernels after it.
+bool nest_early_enabled() {
+  const char* f = getenv("PQH_NEST_EARLY");
   return !(f && f[0] == '0');
 }
 
@@ -265,6 +272,9 @@ struct pqh_batch {
   std::vector<DevPage> hpages;
   std::vector<DevChunk> hchunks;
   std::vector<Tile> expand_tiles;   // k_expand work list (kinds interleaved)
+  int32_t expand_lev_n = 0;         // its first expand_lev_n tiles: the level tiles of the chunks with
+                                    // nesting outputs, launched first (k_expand_lev) so that the
+                                    // nesting kernels run beside the rest of k_expand
   std::vector<Tile> global_tiles;   // k_dict_global work list
   std::vector<Tile> delta_tiles;    // k_delta_sum work list (the TK_DELTA tiles)
   std::vector<Tile> delta_streams;  // k_delta_page work list: (page, 0, stream) with values
@@ -1009,6 +1019,15 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
     delete b;
     return rc;
   }
+  // the level tiles of the nested chunks first, as their own launch: the nesting branch forks after
+  // it and overlaps the value tiles (and the byte-array chain) instead of following all of k_expand
+  if (!b->nests.empty() && nest_early_enabled()) {
+    auto nest_lev = [&](const Tile& t) {
+      return t.kind == TK_LEVELS && b->chunk_nest[size_t(b->hpages[size_t(t.page)].chunk)] >= 0;
+    };
+    std::stable_partition(b->expand_tiles.begin(), b->expand_tiles.end(), nest_lev);
+    b->expand_lev_n = int32_t(std::count_if(b->expand_tiles.begin(), b->expand_tiles.end(), nest_lev));
+  }
   std::vector<Tile> all(b->expand_tiles);
   all.insert(all.end(), b->global_tiles.begin(), b->global_tiles.end());
   for (const Tile& t : b->expand_tiles) {  // k_flat's records (the chunks' value buffers are known now)
@@ -1109,7 +1128,10 @@ bool flat_batch(const pqh_batch* b) {
   // flat columns, required or nullable (max_def 1: only with V2 pages, whose headers give the
   // speculative notNull and whose levels sit raw at the image's start)
   if (!std::all_of(b->hchunks.begin(), b->hchunks.end(), [](const DevChunk& C) {
-        return C.max_rep == 0 && C.max_def <= 1 && C.value_size > 0 && !C.value_nil;
+        // (INT96 PLAIN chunks too: a page whose short last value is the reference's nil fails the
+        // speculation -- flat_spec wants notNull whole values -- and goes through the three
+        // kernels, which mark it; a dictionary ending with the nil entry marks from any tile)
+        return C.max_rep == 0 && C.max_def <= 1 && C.value_size > 0 && !C.dict_nil;
       }))
     return false;
   return std::all_of(b->hpages.begin(), b->hpages.end(), [&](const DevPage& P) {
@@ -1288,26 +1310,33 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   // byte-array dictionary keys are checked against the dictionary sizes the chain branch found
   if (e == hipSuccess && b->ba_wdict) e = join_chain();
   const int32_t ne = int32_t(b->expand_tiles.size()), ng = int32_t(b->global_tiles.size());
-  if (e == hipSuccess && ne)
-    e = timed(2, ne, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, ne, b->expand_lds, st); });
-  if (e == hipSuccess && ng)
-    e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
+  const int32_t nl = b->expand_lev_n;  // the nested chunks' level tiles (their own launch, first)
   const int32_t nnt = int32_t(b->nest_tiles.size()), nns = int32_t(b->nests.size());
   bool nest_open = false;
-  if (e == hipSuccess && nnt) {  // nesting: the levels are complete
+  auto launch_nesting = [&]() -> hipError_t {  // nesting: the levels are complete
+    hipError_t r = hipSuccess;
     hipStream_t ns = s;
     if (side) {
-      e = dep(s, side, 2);
+      r = dep(s, side, 2);
       ns = side;
       nest_open = true;
     }
     // count / scan / write passes (a one-pass write with look-back bases measured slower: DESIGN §5)
-    if (e == hipSuccess)
-      e = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
-    if (e == hipSuccess) e = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
-    if (e == hipSuccess)
-      e = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
-  }
+    if (r == hipSuccess)
+      r = timed(11, nnt, ns, [&](hipStream_t st) { return launch_nest_count(d, b->d_nest_tiles, nnt, st); });
+    if (r == hipSuccess) r = timed(12, nns, ns, [&](hipStream_t st) { return launch_nest_scan(d, nns, st); });
+    if (r == hipSuccess)
+      r = timed(13, nnt, ns, [&](hipStream_t st) { return launch_nest_write(d, b->d_nest_tiles, nnt, st); });
+    return r;
+  };
+  if (e == hipSuccess && nl)
+    e = timed(31, nl, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles, nl, b->expand_lds, st); });
+  if (e == hipSuccess && nnt && nl) e = launch_nesting();
+  if (e == hipSuccess && ne > nl)
+    e = timed(2, ne - nl, s, [&](hipStream_t st) { return launch_expand(d, b->d_tiles + nl, ne - nl, b->expand_lds, st); });
+  if (e == hipSuccess && ng)
+    e = timed(3, ng, s, [&](hipStream_t st) { return launch_dict_global(d, b->d_tiles + ne, ng, st); });
+  if (e == hipSuccess && nnt && !nl) e = launch_nesting();
   if (e == hipSuccess) e = join_chain();  // byte sums and limits of the PLAIN pages
   if (e == hipSuccess) e = join_delta();  // DELTA_LENGTH lengths
   if (e == hipSuccess && nbt) {
@@ -1509,22 +1538,34 @@ int pqh_batch_sync(pqh_batch* b) {
     if (rc != PQH_OK) return rc;
     return pqh_batch_sync(b);
   }
-  // the reference's nil INT96 values: per page and chunk counts of the value_nil marks
+  // the reference's nil INT96 values: per page and chunk counts of the value_nil marks, among the
+  // values the reference returns (an error page's values before its val_limit; none after a
+  // dictionary key error, which returns 0 values, type_dict.go:52-54).  A PLAIN page holds at most
+  // one, its short last value, which k_scan marks exactly when the page decoded with val_limit =
+  // notNull - 1 -- known from the states; only chunks whose dictionary ends with the nil entry
+  // (dict_nil: any value may index it) read their marks back.
   b->page_nil.assign(b->pages.size(), 0);
   b->chunk_nil.assign(b->chunks.size(), 0);
   for (size_t c = 0; c < b->hchunks.size(); c++) {
     const DevChunk& D = b->hchunks[c];
     if (!D.value_nil || D.values_cap <= 0) continue;
-    std::vector<uint8_t> m(static_cast<size_t>(D.values_cap));
-    HIP_TRY(ctx, bounce_d2h(ctx, m.data(), D.value_nil, m.size()));
     for (int32_t i = 0; i < D.num_pages; i++) {
       const int32_t p = D.first_page + i;
       const PageState& S = b->states[size_t(p)];
-      if (b->hpages[size_t(p)].page_type == PQH_DICTIONARY_PAGE || S.nn <= 0 || S.value_base < 0 ||
-          S.value_base + S.nn > D.values_cap)
+      const DevPage& P = b->hpages[size_t(p)];
+      if (P.page_type == PQH_DICTIONARY_PAGE || S.nn <= 0 || S.value_base < 0 || S.value_base + S.nn > D.values_cap)
         continue;
       int32_t k = 0;
-      for (int64_t v = S.value_base; v < S.value_base + S.nn; v++) k += m[size_t(v)] != 0;
+      if (P.kind == K_PLAIN_INT96) {
+        k = S.err == kNoError && S.val_limit == S.nn - 1 ? 1 : 0;
+      } else if (P.kind == K_DICT && D.dict_nil && (S.err & 0xff) != PQH_ERR_DICT_INDEX) {
+        const int64_t m = S.err == kNoError ? S.nn : std::min<int64_t>(std::max(S.val_limit, 0), S.nn);
+        if (m > 0) {
+          std::vector<uint8_t> marks(static_cast<size_t>(m));
+          HIP_TRY(ctx, bounce_d2h(ctx, marks.data(), D.value_nil + S.value_base, marks.size()));
+          for (uint8_t x : marks) k += x != 0;
+        }
+      }
       b->page_nil[size_t(p)] = k;
       b->chunk_nil[c] += k;
     }
@@ -1564,8 +1605,9 @@ int pqh_batch_sync(pqh_batch* b) {
       double lb = 0;
       if (S.rep_s >= 0) lb += S.rep_e - S.rep_s;
       if (S.def_s >= 0) lb += S.def_e - S.def_s;
-      b->k_read[2] += lb;
-      b->k_written[2] += levels;
+      const int kl = b->expand_lev_n && b->chunk_nest[size_t(P.chunk)] >= 0 ? 31 : 2;  // (k_expand_lev's tiles)
+      b->k_read[kl] += lb;
+      b->k_written[kl] += levels;
     }
     switch (P.kind) {
       case K_PLAIN_FIXED:
@@ -1682,7 +1724,8 @@ int pqh_batch_page_results(const pqh_batch* b, pqh_page_result* out, int32_t num
 // the non-null ones.  Sizes only when the buffers are NULL.
 int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t count, void* values,
                         int64_t values_cap, int64_t* offsets, int64_t offsets_cap, uint8_t* data, int64_t data_cap,
-                        uint8_t* def_levels, uint8_t* rep_levels, uint8_t* value_nil, pqh_page_values* out) {
+                        uint8_t* def_levels, uint8_t* rep_levels, uint8_t* value_nil, int64_t value_nil_cap,
+                        pqh_page_values* out) {
   if (!b || !out || page < 0 || size_t(page) >= b->pages.size() || first < 0 || count < 0)
     return set_err(b ? b->ctx : nullptr, PQH_ERR_ARG, "bad page read arguments");
   if (!b->synced) return set_err(b->ctx, PQH_ERR_ARG, "batch not synced");
@@ -1750,6 +1793,7 @@ int pqh_batch_page_read(const pqh_batch* b, int32_t page, int64_t first, int64_t
   out->num_non_null = nn1;
   out->values_read = nn1;
   const int64_t v0 = S.value_base + nn0;
+  if (value_nil && value_nil_cap < nn1) return set_err(ctx, PQH_ERR_ARG, "value_nil buffer too small");
   if (C.value_nil && nn1 > 0) {  // the reference's nil INT96 values among the returned ones
     std::vector<uint8_t> m(static_cast<size_t>(nn1));
     HIP_TRY(ctx, bounce_d2h(ctx, m.data(), C.value_nil + v0, size_t(nn1)));
@@ -1918,7 +1962,7 @@ int pqh_batch_path_info(const pqh_batch* b, pqh_batch_paths* out) {
   out->ba_fuse_active = b->ba_fuse_on ? 1 : 0;
   out->ba_fuse_fallbacks = b->ba_fuse_fallbacks;
   out->regrows = b->regrows;
-  out->graph_replay = (graphs_enabled() && !b->graph_failed && !flat_batch(b)) ? 1 : 0;
+  out->graph_replay = (graphs_enabled() && !b->graph_failed && !flat_batch(b) && !(b->ctx->flags & PQH_CTX_PROFILE)) ? 1 : 0;
   return PQH_OK;
 }
 

@@ -82,6 +82,9 @@ struct pqh_file {
   int64_t num_rows = 0;
   std::vector<ColumnMeta> columns;
   std::vector<RowGroupMeta> rgs;
+  // the caller's codec registry: the reference's compressors map, UNCOMPRESSED / GZIP / SNAPPY / ZSTD
+  // by default (compress.go:182-187), plus what RegisterBlockCompressor added (pqh_file_set_codecs)
+  std::vector<int32_t> codecs{PQH_CODEC_UNCOMPRESSED, PQH_CODEC_GZIP, PQH_CODEC_SNAPPY, PQH_CODEC_ZSTD};
 };
 
 namespace {
@@ -352,6 +355,14 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
   if (m.has_file_path) return fail(PQH_ERR_IO);  // "nyi: data is in another file"
   if (!m.has_meta) return fail(PQH_ERR_SCHEMA);  // "missing meta data for Column"
   if (m.type != col.col.physical_type) return fail(PQH_ERR_SCHEMA);  // "wrong type in Column chunk metadata"
+  // A codec the caller's registry holds but this library does not decode (the reference's ZSTD, or
+  // one registered through RegisterBlockCompressor: compress.go:119-129,160,182-187) is not a
+  // property of the data: the chunk is handed back before any page is read, never reported as a
+  // corrupt page.  (A codec in no registry fails as the reference fails it: decompressBlock's
+  // "method not supported", at the first page's block -- materialise / decompress_into.)
+  if (m.codec != PQH_CODEC_UNCOMPRESSED && m.codec != PQH_CODEC_SNAPPY && m.codec != PQH_CODEC_GZIP &&
+      std::find(f->codecs.begin(), f->codecs.end(), m.codec) != f->codecs.end())
+    return fail(PQH_ERR_UNSUPPORTED_CODEC);
   int64_t pos = m.has_dict_offset ? m.dict_page_offset : m.data_page_offset;
   if (pos < 0) return fail(PQH_ERR_IO);  // Seek: negative position
   int64_t count = 0;
@@ -754,6 +765,12 @@ int32_t pqh_file_schema_name(const pqh_file* f, int32_t i, char* buf, int32_t ca
   const std::string& n = f->schema[size_t(i)].el.name;
   if (buf && cap > 0) memcpy(buf, n.data(), std::min(n.size(), size_t(cap)));
   return int32_t(n.size());
+}
+
+int pqh_file_set_codecs(pqh_file* f, const int32_t* codecs, int32_t n) {
+  if (!f || n < 0 || (n > 0 && !codecs)) return PQH_ERR_ARG;
+  f->codecs.assign(codecs, codecs + n);
+  return PQH_OK;
 }
 
 int pqh_file_chunk_check(const pqh_file* f, int32_t rg, int32_t column, int32_t selected) {

@@ -40,7 +40,10 @@
 
 struct ChainLds {
   uint32_t win[(kChainWin + 64) / 4];
-  uint64_t mask[kBlock][kChainWords];
+  // segment j's record-start marks as 32-bit words, word-major (mask[k][j]): the 64 lanes of a wave
+  // touch 64 consecutive dwords, one per bank, on every mark / clear / read (a [j][k] layout of 64-bit
+  // words put lanes j, j + 16, j + 32, j + 48 in one bank: 4-way conflicts on each record's mark)
+  uint32_t mask[2 * kChainWords][kBlock];
   int32_t exitv[kBlock];
   uint8_t exitbad[kBlock];
   int32_t first_bad;
@@ -49,6 +52,15 @@ struct ChainLds {
   int32_t pad;
   uint64_t wsum[4];
 };
+
+__device__ __forceinline__ uint64_t seg_mask(const ChainLds& C, int j, int k) {
+  return uint64_t(C.mask[2 * k][j]) | (uint64_t(C.mask[2 * k + 1][j]) << 32);
+}
+
+__device__ __forceinline__ void seg_clear(ChainLds& C, int j) {
+#pragma unroll
+  for (int k = 0; k < 2 * kChainWords; k++) C.mask[k][j] = 0;
+}
 
 // Workgroup sum (every thread gets it).
 __device__ __forceinline__ int64_t block_sum64(int64_t x, int64_t* wsum) {
@@ -98,9 +110,7 @@ __device__ __forceinline__ int32_t seg_end(int j, int32_t wb, int32_t wend) {
 // the error code of the record that stops the walk is taken once, after the loop.
 __device__ void chain_walk(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t e0, int32_t start) {
   const int32_t s0 = wb + j * kChainSeg, s1 = seg_end(j, wb, wend);
-  uint32_t* mw = reinterpret_cast<uint32_t*>(&C.mask[j][0]);
-#pragma unroll
-  for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+  seg_clear(C, j);
   int32_t p = start;
   bool stop = false;
   while (p < s1) {
@@ -110,7 +120,7 @@ __device__ void chain_walk(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t
       break;
     }
     const int q = p - s0;
-    atomicOr(mw + (q >> 5), 1u << (q & 31));
+    atomicOr(&C.mask[q >> 5][j], 1u << (q & 31));
     p = nx;
   }
   uint8_t bad = 0;
@@ -123,7 +133,7 @@ __device__ void chain_walk(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t
 }
 
 __device__ __forceinline__ bool chain_has(const ChainLds& C, int j, int q) {
-  return (C.mask[j][q >> 6] >> (q & 63)) & 1;
+  return (C.mask[q >> 5][j] >> (q & 31)) & 1;
 }
 
 // Is segment j's stored result right for its true entry (the previous segment's exit)?  By
@@ -139,7 +149,7 @@ __device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int32_t wb,
   }
   bool empty = true;
 #pragma unroll
-  for (int k = 0; k < kChainWords; k++) empty = empty && C.mask[j][k] == 0;
+  for (int k = 0; k < 2 * kChainWords; k++) empty = empty && C.mask[k][j] == 0;
   if (pbad) return true;  // the chain ended before j (exactly, if j-1 is right): nothing here counts
   if (T >= s1) return empty && !C.exitbad[j] && C.exitv[j] == T;  // skipped by a long record
   if (empty && C.exitbad[j] && C.exitv[j] == T) return true;       // the record at T itself is invalid
@@ -150,8 +160,7 @@ __device__ __forceinline__ bool chain_good(const ChainLds& C, int j, int32_t wb,
 __device__ void chain_fix(ChainLds& C, int j, int32_t wb, int32_t wend, int32_t e0, int32_t T, uint8_t pbad) {
   const int32_t s0 = wb + j * kChainSeg;
   if (pbad || T >= seg_end(j, wb, wend)) {
-#pragma unroll
-    for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+    seg_clear(C, j);
     C.exitv[j] = T;
     C.exitbad[j] = pbad;
   } else if (!chain_has(C, j, T - s0)) {
@@ -228,8 +237,7 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
     if (s0 <= entry) start = entry;  // the segment holding the entry (segments before it stay empty)
     else if (s0 < s1) start = chain_guess(C, wb, e0, s0, s1, wb + kChainWin);
     if (s1 <= entry) {
-#pragma unroll
-      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      seg_clear(C, j);
       C.exitv[j] = entry;
       C.exitbad[j] = 0;
     } else if (start >= 0) {
@@ -237,13 +245,11 @@ __device__ void chain_resolve(ChainLds& C, int32_t wb, int32_t wend, int32_t e0,
     } else if (s0 >= e0 && s0 < s1) {
       // past the end of the bytes: what a walk from s0 gives (EOF at s0), so that the segments after
       // the chain's end agree at once instead of being fixed one per round
-#pragma unroll
-      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      seg_clear(C, j);
       C.exitv[j] = s0;
       C.exitbad[j] = uint8_t(PQH_ERR_EOF);
     } else {
-#pragma unroll
-      for (int k = 0; k < kChainWords; k++) C.mask[j][k] = 0;
+      seg_clear(C, j);
       C.exitv[j] = s1 > s0 ? s1 : s0;
       C.exitbad[j] = 0;
     }
@@ -275,7 +281,7 @@ __device__ __forceinline__ int chain_marks(const ChainLds& C, int j, int32_t wb,
   int cnt = 0;
 #pragma unroll
   for (int k = 0; k < kChainWords; k++) {
-    m[k] = live ? C.mask[j][k] : 0;
+    m[k] = live ? seg_mask(C, j, k) : 0;
     const int32_t lo = T - s0 - 64 * k;
     if (lo > 0) m[k] = lo >= 64 ? 0 : m[k] & ~((1ull << lo) - 1);
     cnt += __popcll(m[k]);

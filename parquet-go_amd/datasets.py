@@ -11,6 +11,8 @@ reference writer's layout by libpqgen.  Used by bench.py and the tests; nothing 
                   RLE_DICTIONARY pages (dictionary page <= 1 MiB) and falls back to
                   DELTA_LENGTH_BYTE_ARRAY; SNAPPY
 """
+import os
+
 import numpy as np
 
 from . import writer as W
@@ -228,15 +230,19 @@ def mixed_sizes(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS):
     return [min(per, rows - g * per) for g in range(row_groups) if rows - g * per > 0]
 
 
-def mixed(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS, seed=50, batch=4, threads=0):
+def mixed(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS, seed=50, batch=4, threads=0, path=None):
     """The mixed-encoding workload file (BASELINE north_star: "a 1B-row mixed-encoding Parquet
     file"): `row_groups` row groups of ceil(rows / row_groups) records, V2 pages, UNCOMPRESSED, in
     the reference writer's layout, streamed `batch` row groups at a time into one buffer (the
-    columns of all 1B rows never exist at once).  Returns the file as a uint8 array."""
+    columns of all 1B rows never exist at once).  Returns the file as a uint8 array; with `path`,
+    the pages are written in place into that file (memory-mapped, e.g. under /dev/shm for ranks that
+    share it), which is cut to the file's size, and the path is returned."""
     sizes = mixed_sizes(rows, row_groups)
     schema = W.flat_schema(mixed_row_group(0, 0, seed))
     # upper bound: 57 bytes per row of values + levels + page / chunk overheads
-    sw = W.StreamWriter(schema, 57 * rows + (64 << 20), v2=True, threads=threads)
+    cap = 57 * rows + (64 << 20)
+    buf = np.memmap(path, dtype=np.uint8, mode="w+", shape=(cap,)) if path else None  # (sparse until written)
+    sw = W.StreamWriter(schema, cap, v2=True, threads=threads, buf=buf)
     A = _mixed_arrays(sum(sizes[:batch]))
     for g0 in range(0, len(sizes), batch):
         part = sizes[g0:g0 + batch]
@@ -245,7 +251,15 @@ def mixed(rows=MIXED_ROWS, row_groups=MIXED_ROW_GROUPS, seed=50, batch=4, thread
             nn += _mixed_fill(A, r0, nn, g0 + k, n, seed, threads)
             r0 += n
         sw.write([c for _, c, _ in _mixed_columns(A, r0, nn)], part)
-    return sw.finish()
+    out = sw.finish()
+    if path is None:
+        return out
+    n = len(out)
+    del out, sw
+    buf.flush()
+    del buf
+    os.truncate(path, n)
+    return path
 
 
 WORKLOADS = {

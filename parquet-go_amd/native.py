@@ -21,11 +21,12 @@ STATUS = {
     14: "DELTA_BIT_WIDTH", 15: "DELTA_STREAM", 16: "NEGATIVE_LENGTH", 17: "NEGATIVE_DLBA_LENGTH",
     18: "DBA_PREFIX", 19: "DBA_COUNT", 20: "INT96_SHORT", 21: "UNSUPPORTED", 22: "PAGE_HEADER",
     23: "DECOMPRESS", 24: "CRC", 25: "THRIFT", 26: "IO", 27: "ARG", 28: "HIP", 29: "NOMEM", 30: "SCHEMA",
-    31: "DICT_PAGE", 32: "NO_DEVICE", 33: "NOT_IMPLEMENTED", 34: "INTERNAL",
+    31: "DICT_PAGE", 32: "NO_DEVICE", 33: "NOT_IMPLEMENTED", 34: "INTERNAL", 35: "UNSUPPORTED_CODEC",
 }
 OK = 0
 NOT_IMPLEMENTED = 33
 INTERNAL = 34
+UNSUPPORTED_CODEC = 35  # the chunk's codec is not decoded here: the caller routes it to the reference
 # error phases (pqh_phase): page load (readChunk), repetition levels, definition levels, values
 PHASE_LOAD, PHASE_REP, PHASE_DEF, PHASE_VALUES = range(4)
 CTX_PROFILE = 1
@@ -100,7 +101,7 @@ class BatchPaths(ctypes.Structure):
 
 
 # (name, restype, argtypes) for every function of include/pqhip.h
-ABI_VERSION = 7  # include/pqhip.h PQH_ABI_VERSION
+ABI_VERSION = 8  # include/pqhip.h PQH_ABI_VERSION
 
 PROTOTYPES = [
     ("pqh_abi_version", ctypes.c_int, []),
@@ -126,7 +127,7 @@ PROTOTYPES = [
     ("pqh_batch_chunk_out", ctypes.c_int, [vp, i32, ctypes.POINTER(ChunkOut)]),
     ("pqh_batch_nesting", ctypes.c_int, [vp, i32, ctypes.POINTER(NestOut)]),
     ("pqh_batch_page_results", ctypes.c_int, [vp, ctypes.POINTER(PageResult), i32]),
-    ("pqh_batch_page_read", ctypes.c_int, [vp, i32, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp,
+    ("pqh_batch_page_read", ctypes.c_int, [vp, i32, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, i64,
                                            ctypes.POINTER(PageValues)]),
     ("pqh_batch_kernel_stats", ctypes.c_int, [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]),
     ("pqh_batch_path_info", ctypes.c_int, [vp, ctypes.POINTER(BatchPaths)]),
@@ -143,6 +144,7 @@ PROTOTYPES = [
     ("pqh_file_num_columns", i32, [vp]),
     ("pqh_file_column", ctypes.c_int, [vp, i32, ctypes.POINTER(Column), ctypes.c_char_p, i32]),
     ("pqh_file_chunk_check", ctypes.c_int, [vp, i32, i32, i32]),
+    ("pqh_file_set_codecs", ctypes.c_int, [vp, ctypes.POINTER(i32), i32]),
     ("pqh_file_column_path", i32, [vp, i32, ctypes.c_char_p, i32]),
     ("pqh_file_schema_name", i32, [vp, i32, ctypes.c_char_p, i32]),
     ("pqh_file_num_schema_elements", i32, [vp]),
@@ -425,6 +427,13 @@ class File:
         fn(self.h, i, buf, n)
         return buf.raw[:n].decode("utf-8", "surrogateescape")
 
+    def set_codecs(self, codecs):
+        """The caller's codec registry (pqh_file_set_codecs; default UNCOMPRESSED / GZIP / SNAPPY /
+        ZSTD, compress.go:182-187): registered codecs this library does not decode fail their chunks
+        with UNSUPPORTED_CODEC at load, unregistered ones as the reference fails them."""
+        arr = (i32 * max(len(codecs), 1))(*codecs)
+        _check(self.L.pqh_file_set_codecs(self.h, arr, len(codecs)))
+
     def chunk_check(self, rg, column, selected=True):
         """readRowGroupData's checks of a column before its pages (pqh_file_chunk_check): a status."""
         return self.L.pqh_file_chunk_check(self.h, rg, column, int(selected))
@@ -526,7 +535,7 @@ class Batch:
             count = 1 << 62
         pv = PageValues()
         self.ctx.check(self.L.pqh_batch_page_read(self.h, page, first, count, None, 0, None, 0, None, 0, None, None,
-                                                  None, ctypes.byref(pv)))
+                                                  None, 0, ctypes.byref(pv)))
         ns = pv.num_slots
         d = np.empty(ns, np.uint8)
         r = np.empty(ns, np.uint8)
@@ -542,7 +551,7 @@ class Batch:
         self.ctx.check(self.L.pqh_batch_page_read(
             self.h, page, first, count, p(vals), 0 if vals is None else vals.nbytes, p(offs),
             0 if offs is None else len(offs), p(data), 0 if data is None else data.nbytes, p(d), p(r), p(m),
-            ctypes.byref(pv)))
+            0 if m is None else len(m), ctypes.byref(pv)))
         if data is not None:
             data = data[:pv.num_bytes]
         if nil is not None and m is not None:

@@ -31,6 +31,18 @@ class DecodeError(RuntimeError):
         super().__init__(f"{path}: {native.STATUS.get(status, status)} (phase {phase}, index {index}, page {page})")
 
 
+class UnsupportedCodecError(DecodeError):
+    """The chunk's codec is one this library does not decode (ZSTD, or a codec registered with
+    RegisterBlockCompressor, compress.go:119-129,160,182-187).  Not a property of the data: the
+    reference decodes such a chunk with its own readChunk (INTEGRATION.md's loadRowGroupGPU routes
+    it there); here the chunk fails at load, before any of its pages is read."""
+
+
+def decode_error(path, status, phase=0, index=0, page=-1):
+    cls = UnsupportedCodecError if status == native.UNSUPPORTED_CODEC else DecodeError
+    return cls(path, status, phase, index, page)
+
+
 class ColumnData:
     """One decoded column chunk (dense not-null values + level bytes), host copy."""
 
@@ -102,12 +114,12 @@ class ColumnData:
     def raise_for_load(self):
         """readChunk (chunk_reader.go:299-362): only page-load / walker / codec errors fail here."""
         if self.load_error is not None:
-            raise DecodeError(self.path, *self.load_error)
+            raise decode_error(self.path, *self.load_error)
         return self
 
     def raise_for_status(self):
         if self.status != native.OK:
-            raise DecodeError(self.path, self.status, self.error_phase, self.error_index, self.error_page)
+            raise decode_error(self.path, self.status, self.error_phase, self.error_index, self.error_page)
         return self
 
     def to_pylist(self):
@@ -275,7 +287,7 @@ class FileReader:
         (assemble.ColumnarAssembler), else value by value (records.RowAssembler) when the row group
         breaks one of its preconditions (the reference's page-local cursors / getFirstRDLevel
         quirks)."""
-        from . import assemble, records
+        from . import assemble
 
         if self._schema is None:
             self._schema = self.file.schema()
@@ -302,8 +314,17 @@ class FileReader:
                     return ("columnar", rows, errs)
                 except assemble.NotColumnar:
                     pass
-        # readValues errors surface page by page, when the assembly reaches the failing page
-        # (ColumnStore.get -> readNextPage, data_store.go:236-269); rows before it are returned
+        return self._value_by_value()
+
+    def _value_by_value(self):
+        """records.RowAssembler over the current row group: readValues errors surface page by page,
+        when the assembly reaches the failing page (ColumnStore.get -> readNextPage,
+        data_store.go:236-269); rows before it are returned."""
+        from . import records
+
+        if self._schema is None:
+            self._schema = self.file.schema()
+        nrows = self.file.row_group_num_rows(self.row_group_position - 1)
         cols = {self.selected[i]: (c, c.physical_type, c.path) for i, c in enumerate(self._loaded)}
         self.assembled["value_by_value"] += 1
         return ("value_by_value", records.RowAssembler(self._schema, cols, nrows))
@@ -388,13 +409,20 @@ class FileReader:
             a = self._assembler(arrow=True)
             if a[0] == "arrow":
                 asm = a[1]
-                self.assembled["arrow"] = self.assembled.get("arrow", 0) + 1
-                t = asm.arrow()
-                # the cursor after the table's rows: a failing row's error comes from the next call
-                # (NextRow's columnar path raises errs[k - ok_rows] there)
-                self._rows = ("columnar", [None] * asm.ok_rows, asm.errors())
-                self.current_record = asm.ok_rows
-                return t
+                try:
+                    # (runs the assembler's lazy checks -- leaves that disagree, instance counts,
+                    # repeated leaves -- that rows() runs too: a row group that breaks one goes value
+                    # by value, as NextRow does)
+                    t = asm.arrow()
+                except assemble.NotColumnar:
+                    a = self._value_by_value()
+                else:
+                    self.assembled["arrow"] = self.assembled.get("arrow", 0) + 1
+                    # the cursor after the table's rows: a failing row's error comes from the next call
+                    # (NextRow's columnar path raises errs[k - ok_rows] there)
+                    self._rows = ("columnar", [None] * asm.ok_rows, asm.errors())
+                    self.current_record = asm.ok_rows
+                    return t
             self._rows = a
         rows = self.NextBatch(nrows - k)
         return assemble.records_table(rows) if rows else pa.table({})

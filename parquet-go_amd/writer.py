@@ -126,7 +126,7 @@ class StreamWriter:
     is an upper bound of the file size (the buffer is np.empty: pages never written are never
     touched).  The result equals write() of the same rows, byte for byte."""
 
-    def __init__(self, schema, capacity, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0):
+    def __init__(self, schema, capacity, v2=False, codec=UNCOMPRESSED, max_page_size=0, crc=False, threads=0, buf=None):
         L = _lib.gen()
         self.L = L
         self._names = [x[0].encode() for x in schema]
@@ -138,7 +138,9 @@ class StreamWriter:
         self.h = L.pqg_stream_open(self._els, len(schema), ctypes.byref(self._opt), err, 512)
         if not self.h:
             raise ValueError("pqg_stream_open: " + err.value.decode())
-        self.buf = np.empty(int(capacity), dtype=np.uint8)
+        # (buf: a caller's uint8 buffer of >= capacity bytes, e.g. an np.memmap of a file, which the
+        # pages are written into in place)
+        self.buf = np.empty(int(capacity), dtype=np.uint8) if buf is None else buf
         self.pos = ctypes.c_int64(0)
 
     def write(self, columns, rg_rows):

@@ -220,3 +220,21 @@ def deep_repeated(n=3000, depth=10, seed=5, wrap=None, v2=False):
     col = W.Column(W.INT32, np.array(vals, dtype=np.int32), def_levels=np.array(dl, np.uint8),
                    rep_levels=np.array(rl, np.uint8), use_dict=False)
     return W.write(schema, [col], [n // 2, n - n // 2], v2=v2, max_page_size=8 * 1024), D
+
+
+def disagreeing_group(n=4000, seed=9):
+    """optional group g {optional int32 a; optional int32 b} whose two leaves disagree on g's presence
+    in some rows (a writes d = 0 where b writes g present): a file the columnar assembly accepts at
+    construction but whose lazy presence check (assemble.ColumnarAssembler._presence) rejects, so
+    NextRow and ReadRowGroupArrow assemble it value by value.  Two row groups, the second consistent."""
+    rng = np.random.default_rng(seed)
+    da = rng.integers(0, 3, n).astype(np.uint8)
+    db = np.where(da == 0, 0, rng.integers(1, 3, n)).astype(np.uint8)  # mostly consistent ...
+    flip = rng.random(n // 2) < 0.05
+    db[:n // 2][flip & (da[:n // 2] == 0)] = 2  # ... except some rows of the first row group
+    schema = [W.element("schema", repetition=-1, num_children=1),
+              W.element("g", repetition=W.OPTIONAL, num_children=2),
+              W.element("a", W.INT32, W.OPTIONAL), W.element("b", W.INT32, W.OPTIONAL)]
+    cols = [W.Column(W.INT32, rng.integers(-99, 99, int((da == 2).sum())).astype(np.int32), def_levels=da, use_dict=False),
+            W.Column(W.INT32, rng.integers(-99, 99, int((db == 2).sum())).astype(np.int32), def_levels=db, use_dict=False)]
+    return W.write(schema, cols, [n // 2, n - n // 2], max_page_size=4 * 1024)

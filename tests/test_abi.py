@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(pq):
 
 def test_abi_version_and_devices(pq):
     L = pq._lib.hip()
-    assert L.pqh_abi_version() == pq.native.ABI_VERSION == 7
+    assert L.pqh_abi_version() == pq.native.ABI_VERSION == 8
     n = pq.native.device_count()
     assert n >= 0
 

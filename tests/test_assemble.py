@@ -229,6 +229,36 @@ def test_columnar_selected_columns():
             assert not stats.get("fallback")
 
 
+def test_lazy_not_columnar_row_group():
+    """A row group the columnar assembler accepts at construction but whose lazy presence check
+    rejects (two leaves disagreeing on their group's presence): rows() and arrow() both raise
+    NotColumnar (so reader.FileReader's NextRow and ReadRowGroupArrow go value by value), and the
+    assembled rows equal the value-by-value restatement's; the consistent row group stays columnar."""
+    A = _pkg().assemble
+    data = fixtures.disagreeing_group()
+    lazy = []
+
+    class Probe(A.ColumnarAssembler):
+        def arrow(self):
+            try:
+                return super().arrow()
+            except A.NotColumnar as e:
+                lazy.append(str(e))
+                raise
+
+    orig = A.ColumnarAssembler
+    A.ColumnarAssembler = Probe
+    try:
+        stats = {}
+        _same(columnar_next_rows(data, stats=stats), oracle_next_rows(data))
+    finally:
+        A.ColumnarAssembler = orig
+    assert stats == {"fallback": 1, "columnar": 1}, stats
+    # (rows() raised first for the first row group; the second one's arrow() ran clean)
+    fr = O.FileReader(data)
+    assert len(fr.row_groups) == 2 and not lazy
+
+
 def test_records_table_fallback():
     """ReadRowGroupArrow's table for non-columnar row groups (assemble.records_table): every
     top-level field any record holds becomes a column, not just the first record's (records omit

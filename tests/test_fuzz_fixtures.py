@@ -65,6 +65,12 @@ def test_fixture_footer_schema_and_walk(pq, m):
     for k, ch in enumerate(hb.chunks()):
         och = fr.read_chunk(*divmod(k, len(cols)))
         data_pages = [p for p in hb.pages()[ch.first_page:ch.first_page + ch.num_pages] if p.page_type != O.DICTIONARY_PAGE]
+        if ch.host_status == pq.native.UNSUPPORTED_CODEC:
+            # a registered codec the library does not decode (ZSTD): handed back before any page, the
+            # shim's reference readChunk gives the oracle's outcome (test_codec_registry.py)
+            codec = fr.row_groups[k // len(cols)][1][k % len(cols)][3][4]
+            assert codec in O.DEFAULT_CODECS and codec not in (0, 1, 2) and ch.num_pages == 0, (k, codec)
+            continue
         if ch.host_status:  # the walk stopped at a page the oracle cannot read either (or earlier)
             assert och.status != 0 and len(och.pages) <= len(data_pages), (k, ch.host_status, och.status)
             if len(och.pages) == len(data_pages):  # stopped at the same page: the same error

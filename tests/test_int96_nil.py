@@ -258,3 +258,68 @@ def _batch(pq, ctx, hb):
     b.run()
     b.sync()
     return b
+
+
+@pytest.mark.gpu
+def test_gpu_int96_plain_on_flat(pq, ctx):
+    """PLAIN INT96 chunks stay on the one-launch k_flat path: a clean file decodes
+    there (paths()['flat_active'], no fallback) bit for bit as the oracle; a page whose short last
+    value is the reference's nil fails k_flat's speculation, and the three-kernel decode marks the
+    nil (zeros, value_nil, num_nil) as the oracle does."""
+    rng = np.random.default_rng(101)
+    v = _vals(rng, 64).tobytes()
+    clean = pqcraft.int96_file([(None, [(v[:12 * 20], 20, PLAIN, None, None), (v[:12 * 9], 9, PLAIN, None, None)]),
+                                (None, [(v[:12 * 33], 33, PLAIN, None, None)])])
+    short = pqcraft.int96_file([(None, [(v[:12 * 20], 20, PLAIN, None, None), (v[:12 * 8 + 3], 9, PLAIN, None, None)])])
+    for data, nil in ((clean, 0), (short, 1)):
+        f = pq.native.File(data)
+        hb = f.load(0, f.num_row_groups, [0])
+        b = pq.native.Batch.from_host(ctx, hb)
+        b.run()
+        b.sync()
+        paths = b.paths()
+        if nil:
+            assert paths["flat_fallbacks"] == 1 and not paths["flat_active"], paths
+        else:
+            assert paths["flat_active"] == 1 and paths["flat_fallbacks"] == 0, paths
+        fro = O.FileReader(data)
+        for rg in range(f.num_row_groups):
+            o = b.chunk_out(rg)
+            exp = O.decode_chunk(fro.read_chunk(rg, 0))
+            assert all(r.status == 0 for r in exp)
+            want = b"".join(r.values for r in exp)
+            assert ctx.d2h_array(o.values, o.num_non_null * 12).tobytes() == want
+            assert o.num_nil == sum(int(r.nil.sum()) for r in exp if r.nil is not None)
+        assert sum(b.chunk_out(rg).num_nil for rg in range(f.num_row_groups)) == nil
+        b.close()
+        hb.close()
+        f.close()
+
+
+@pytest.mark.gpu
+def test_gpu_int96_nil_entry_with_bad_key(pq, ctx):
+    """A dictionary whose last entry is the reference's nil, and a data page that indexes it before
+    an out-of-range key: the page fails with DICT_INDEX and returns 0 values (type_dict.go:52-54), so
+    no nil counts for it (num_nil only over the values the reference returns); the
+    page before it keeps its nils."""
+    W = _pkg().writer
+    rng = np.random.default_rng(102)
+    v = _vals(rng, 8).tobytes()
+    dpage = (v[:12 * 4 + 2], 5)  # entries 0..3, then the short nil entry 4
+    good = bytes([3]) + W.hybrid_encode(3, np.array([4, 0, 4, 1], np.int32))
+    bad = bytes([4]) + W.hybrid_encode(4, np.array([4, 1, 4, 9, 0], np.int32))  # key 9 >= 5
+    data = pqcraft.int96_file([(dpage, [(good, 4, RLE_DICTIONARY, None, None), (bad, 5, RLE_DICTIONARY, None, None)])])
+    f = pq.native.File(data)
+    hb = f.load(0, 1, [0])
+    b = pq.native.Batch.from_host(ctx, hb)
+    b.run()
+    b.sync()
+    res = b.page_results(hb.num_pages)
+    exp = O.decode_chunk(O.FileReader(data).read_chunk(0, 0))
+    data_res = [r for r, p in zip(res, hb.pages()) if p.page_type != O.DICTIONARY_PAGE]
+    assert [r.status for r in data_res] == [e.status for e in exp] == [0, 10]
+    assert [r.num_nil for r in data_res] == [2, 0]
+    assert b.chunk_out(0).num_nil == 2
+    b.close()
+    hb.close()
+    f.close()

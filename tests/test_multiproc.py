@@ -127,8 +127,8 @@ def test_bench_self_launch_two_ranks():
     scaling).  --dry-run puts the CPU oracle in place of the GPU decode and gloo in place of RCCL, so
     both plans (blocks that tile the file) and the reductions (sum of bytes, max of time) are checked
     here."""
-    rows, c3rows = 20_000, 300_000
-    d = _bench_dry(2, "--rows", str(rows), "--c3-rows", str(c3rows))
+    rows, c3rows, mrows = 20_000, 300_000, 256_000
+    d = _bench_dry(2, "--rows", str(rows), "--c3-rows", str(c3rows), "--mixed-rows", str(mrows))
     assert d["dry_run"] and d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["config"]["workload"].startswith("C2") and d["config"]["rows_total"] == 2 * rows
     sh = d["shards"]
@@ -141,6 +141,14 @@ def test_bench_self_launch_two_ranks():
     assert sh[0]["row_groups"] == [0, 64] and sh[1]["row_groups"] == [64, 128]
     assert sum(s["rows"] for s in sh) == c3rows
     assert c3["decoded_bytes_total"] == 8 * c3rows == sum(s["decoded_bytes"] for s in sh)
+    # mixed_1b at N > 1: north_star's target file (written once, in place, by rank 0) as strong
+    # scaling -- the same blocks of its 128 row groups, the whole file covered
+    m = d["mixed_1b"]
+    assert m["scaling"] == "strong" and m["n_gpus"] == 2 and m["workload"].startswith("mixed")
+    assert m["rows_total"] == mrows and m["row_groups"] == 128
+    assert [s["row_groups"] for s in m["shards"]] == [[0, 64], [64, 128]]
+    assert sum(s["rows"] for s in m["shards"]) == mrows
+    assert m["decoded_bytes_total"] == sum(s["decoded_bytes"] for s in m["shards"]) > 42 * mrows
 
 
 def test_bench_single_gpu_scaling_proxy():

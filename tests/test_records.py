@@ -530,6 +530,19 @@ def test_read_row_group_arrow(pq, ctx):
 
 
 @pytest.mark.gpu
+def test_read_row_group_arrow_lazy_fallback(pq, ctx):
+    """ReadRowGroupArrow on a row group whose columnar assembly fails only in its lazy checks (two
+    leaves disagreeing on their group's presence, fixtures.disagreeing_group): the Arrow export
+    raises NotColumnar inside ReadRowGroupArrow, which then goes value by value (as NextRow does)
+    instead of raising -- the same records as NextRow and the oracle's assembly."""
+    data = fixtures.disagreeing_group()
+    want = [_norm(w) for w in oracle_next_rows(data)]
+    got, paths = _read_arrow(pq, data)
+    assert [_norm(g) for g in got] == want
+    assert paths.get("value_by_value", 0) == 1 and paths.get("arrow", 0) == 1, paths
+
+
+@pytest.mark.gpu
 def test_next_row_many_small_row_groups(pq, ctx):
     """A row group every 100 rows (the reference's column-selection file, filereader_test.go:13-247):
     100 row groups of the all-types file and of a nested LIST / MAP file, NextRow with every column and
