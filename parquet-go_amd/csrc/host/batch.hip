@@ -82,8 +82,8 @@ const char* kKernelNames[] = {"k_prologue", "k_scan", "k_expand", "k_dict_global
                               "k_delta_fused", "k_ba_wstitch", "k_ba_wemit",   "k_snappy",
                               "k_ba_wcopy",   "k_gzip",      "k_snap_spec",  "k_snap_stitch",
                               "k_snap_emit",  "k_snap_fixup", "k_ba_chain",   "k_flat",
-                              "k_expand_lev"};
-constexpr int kNumKernels = 32;
+                              "k_expand_lev", "k_delta_split"};
+constexpr int kNumKernels = 33;
 // Batches with at least this many delta streams decode each stream in one workgroup (k_delta_page);
 // fewer streams go through per-tile sums, a page scan and per-tile expands (more parallelism).
 constexpr size_t kDeltaPageModeMin = 256;
@@ -109,6 +109,13 @@ bool snappy_page_mode() {
 // (k_ba_wspec / wstitch / wcopy) instead of the fused k_ba_chain.
 bool fuse_enabled() {
   const char* f = getenv("PQH_BA_FUSE");
+  return !(f && f[0] == '0');
+}
+
+// PQH_DELTA_SPLIT=0 (A/B experiments, tests): page-mode delta heads by k_delta_fused (one workgroup
+// per stream) instead of k_delta_split (windows of a stream over many workgroups).
+bool split_enabled() {
+  const char* f = getenv("PQH_DELTA_SPLIT");
   return !(f && f[0] == '0');
 }
 
@@ -282,6 +289,18 @@ struct pqh_batch {
   int32_t delta_fused_pages = 0;    // page mode: delta pages / streams through k_delta_fused
   int32_t delta_fused_streams = 0;
   int32_t delta_lens_streams = 0;   // the last of delta_streams: DELTA_LENGTH_BYTE_ARRAY pages
+  // k_delta_split (page mode): the windows of the streams k_delta_fused would take, page-major
+  // (split_wins: (page, window)), and their window-major dispatch order (the DELTA_LENGTH windows'
+  // order last, split_nl of them)
+  bool split_on = false;
+  std::vector<int2> split_wins;
+  std::vector<int32_t> split_order;
+  int32_t split_nl = 0;
+  DeltaSplit* d_dsplit = nullptr;
+  uint32_t* d_dticket = nullptr;
+  uint64_t* d_dwords = nullptr;
+  int2* d_split_wins = nullptr;
+  int32_t* d_split_order = nullptr;
   std::vector<int32_t> delta_pages; // k_delta_walk / k_delta_scan work list
   std::vector<Tile> ba_tiles;       // k_ba_sum / k_ba_expand work list (chunk-contiguous)
   std::vector<int32_t> ba_xlist;    // ba_tiles indices: DELTA_LENGTH tiles, then PLAIN / dictionary, then k_ba_sum's
@@ -376,6 +395,7 @@ struct pqh_batch {
   bool flat_off = false;  // a k_flat speculation failed once: the three kernels from then on
   int32_t flat_fallbacks = 0;
   int32_t regrows = 0;
+  std::vector<DeltaState> hdstates;  // (after sync, batches with byte-array length streams) dstates
   std::vector<int32_t> page_nil;   // (after sync) nil INT96 values per page / chunk (value_nil marks)
   std::vector<int64_t> chunk_nil;
   std::vector<int64_t> flat_base;   // k_flat: page value bases if every page is clean (num_values prefixes)
@@ -821,6 +841,30 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
                             [&](const Tile& t) { return b->hpages[size_t(t.page)].kind != K_DLBA; });
       b->delta_lens_streams = int32_t(std::count_if(b->delta_streams.begin(), b->delta_streams.end(),
                                                     [&](const Tile& t) { return b->hpages[size_t(t.page)].kind == K_DLBA; }));
+      b->split_on = split_enabled();
+      if (b->split_on) {
+        // windows of kSplitStride bytes over each stream k_delta_fused would take (the first stream
+        // of each page), page-major; dispatched window-major (every page's window 0, then every
+        // window 1, ...), the DELTA_LENGTH streams' windows in a launch of their own
+        std::vector<int32_t> ord[2];
+        for (const Tile& t : b->delta_streams) {
+          if (t.kind != 0) continue;
+          const DevPage& P = b->hpages[size_t(t.page)];
+          const int g = P.kind == K_DLBA ? 1 : 0;
+          const int32_t nw = int32_t(std::max<int64_t>(1, ceil_div(std::max<int64_t>(P.image_len, 1), kSplitStride)));
+          for (int32_t w = 0; w < nw; w++) {
+            ord[g].push_back(int32_t(b->split_wins.size()));
+            b->split_wins.push_back(make_int2(t.page, w));
+          }
+        }
+        for (int g = 0; g < 2; g++) {
+          std::stable_sort(ord[g].begin(), ord[g].end(), [&](int32_t x, int32_t y) {
+            return b->split_wins[size_t(x)].y < b->split_wins[size_t(y)].y;
+          });
+          b->split_order.insert(b->split_order.end(), ord[g].begin(), ord[g].end());
+        }
+        b->split_nl = int32_t(ord[1].size());
+      }
     }
   }
 
@@ -896,6 +940,11 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_flat_tiles), sizeof(FlatTile) * b->expand_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_bawords), sizeof(uint64_t) * (b->ba_wins.size() - size_t(b->ba_wins_nf)))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_forder), sizeof(int32_t) * b->ba_forder.size())) ||
+      (b->split_on && (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsplit), sizeof(DeltaSplit) * size_t(num_pages)))) ||
+      (b->split_on && (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dticket), sizeof(uint32_t) * 2))) ||
+      (b->split_on && (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dwords), sizeof(uint64_t) * 3 * b->split_wins.size()))) ||
+      (b->split_on && (rc = dalloc(b, reinterpret_cast<void**>(&b->d_split_wins), sizeof(int2) * b->split_wins.size()))) ||
+      (b->split_on && (rc = dalloc(b, reinterpret_cast<void**>(&b->d_split_order), sizeof(int32_t) * b->split_order.size()))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_chunk_bytes), sizeof(int64_t) * size_t(std::max(num_chunks, 1))))) {
     free_batch(b);
     delete b;
@@ -1082,6 +1131,8 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       {b->d_ba_wlist, b->ba_wlist.data(), sizeof(int2) * b->ba_wlist.size()},
       {b->d_ba_chunks, b->ba_chunks.data(), sizeof(int32_t) * b->ba_chunks.size()},
       {b->d_ba_forder, b->ba_forder.data(), sizeof(int32_t) * b->ba_forder.size()},
+      {b->d_split_wins, b->split_wins.data(), sizeof(int2) * b->split_wins.size()},
+      {b->d_split_order, b->split_order.data(), sizeof(int32_t) * b->split_order.size()},
       {b->d_nests, b->nests.data(), sizeof(DevNest) * b->nests.size()},
       {b->d_nest_tiles, b->nest_tiles.data(), sizeof(Tile) * b->nest_tiles.size()},
       {b->d_flat_base, b->flat_base.data(), sizeof(int64_t) * size_t(num_pages)},
@@ -1144,7 +1195,8 @@ bool flat_batch(const pqh_batch* b) {
 hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
-             b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2, b->d_bafuse, b->d_bawords};
+             b->d_chunk_bytes, b->d_nests, b->d_nsums, b->d_basums2, b->d_bafuse, b->d_bawords,
+             b->split_on ? b->d_dsplit : nullptr, b->d_dticket, b->d_dwords};
   const bool sync_each = sync_each_enabled();
   auto timed = [&](int kind, int32_t items, hipStream_t st, auto&& fn) -> hipError_t {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1285,7 +1337,17 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     ds = b->ctx->side3;
     delta_open = true;
   }
-  if (e == hipSuccess && ni) {
+  if (e == hipSuccess && ni && b->split_on) {
+    const int32_t nw = int32_t(b->split_order.size());
+    e = hipMemsetAsync(b->d_dticket, 0, sizeof(uint32_t) * 2, ds);
+    if (e == hipSuccess) e = hipMemsetAsync(b->d_dwords, 0, sizeof(uint64_t) * 3 * b->split_wins.size(), ds);
+    if (e == hipSuccess)
+      e = timed(32, nw, ds, [&](hipStream_t st) {
+        return launch_delta_split(d, b->d_split_wins, b->d_split_order, nw, b->split_nl, st);
+      });
+    if (e == hipSuccess)
+      e = timed(4, ni, ds, [&](hipStream_t st) { return launch_delta_walk(d, b->d_delta_pages, ni, st); });
+  } else if (e == hipSuccess && ni) {
     const int32_t nis = b->delta_fused_streams;
     e = timed(19, nis, ds, [&](hipStream_t st) { return launch_delta_fused(d, b->d_dtiles, nis, b->delta_lens_streams, st); });
     if (e == hipSuccess)
@@ -1376,6 +1438,14 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     if (e == hipSuccess) e = r;
   }
   return e;
+}
+
+// (after sync) the end of page p's length stream(s): DELTA_LENGTH -> its one stream, DELTA_BYTE_ARRAY
+// -> the suffix lengths that follow the prefix lengths; val_s when unknown
+int64_t dlen_end(const pqh_batch* b, size_t p) {
+  const DevPage& P = b->hpages[p];
+  const size_t i = P.kind == K_DBA ? b->pages.size() + p : p;
+  return i < b->hdstates.size() && b->hdstates[i].end_pos > 0 ? b->hdstates[i].end_pos : b->states[p].val_s;
 }
 
 bool graphs_enabled() {
@@ -1583,6 +1653,15 @@ int pqh_batch_sync(pqh_batch* b) {
   b->event_next = 0;
   // algorithmic bytes of one run: page bytes read once, dictionaries once per
   // chunk, decoded bytes written; attributed to the kernel that moves them.
+  // (where each DELTA_LENGTH / DELTA_BYTE_ARRAY page's length streams end: the byte accounting splits
+  // those pages between the delta kernels and k_ba_expand)
+  const bool lens = std::any_of(b->hpages.begin(), b->hpages.end(),
+                                [](const DevPage& P) { return P.kind == K_DLBA || P.kind == K_DBA; });
+  b->hdstates.clear();
+  if (lens && !b->pages.empty()) {
+    b->hdstates.resize(2 * b->pages.size());
+    HIP_TRY(ctx, bounce_d2h(ctx, b->hdstates.data(), b->d_dstates, sizeof(DeltaState) * b->hdstates.size()));
+  }
   double wr = 0, plain_written = 0;
   auto fused_chunk = [&](int32_t c) { return b->ba_fuse_on && b->hchunks[size_t(c)].ba_fused != 0; };
   std::fill(b->k_read.begin(), b->k_read.end(), 0.0);
@@ -1629,7 +1708,7 @@ int pqh_batch_sync(pqh_batch* b) {
         break;
       case K_DELTA32:
       case K_DELTA64: {  // the walks read block headers; k_delta_expand / k_delta_page read the stream once
-        const int kd = b->delta_page_mode ? 19 : 5;
+        const int kd = b->delta_page_mode ? (b->split_on ? 32 : 19) : 5;
         b->k_read[kd] += S.val_e - S.val_s;
         b->k_written[kd] += vals;
         break;
@@ -1646,9 +1725,13 @@ int pqh_batch_sync(pqh_batch* b) {
         break;
       }
       case K_DLBA:
-      case K_DBA:
-        b->k_read[10] += S.val_e - S.val_s;
+      case K_DBA: {  // the length streams read by the delta kernels, the string bytes by k_ba_expand
+        const int kd = b->delta_page_mode ? (b->split_on ? 32 : 19) : 5;
+        const int64_t le = std::min<int64_t>(std::max<int64_t>(dlen_end(b, p), S.val_s), S.val_e);
+        b->k_read[kd] += le - S.val_s;
+        b->k_read[10] += S.val_e - le;
         break;
+      }
       default:
         break;
     }

@@ -338,6 +338,14 @@ bool snappy_plausible(const uint8_t* p, size_t n, int64_t expected) {
 
 int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
+// Device codecs: pages whose compressed values are at least this fraction of their decompressed
+// size stay on the host-decompressed route (PQH_DEVICE_CODEC_MAX_RATIO overrides it; 0 sends every
+// page of a device-codec chunk to the device, as before ABI 8)
+double device_codec_max_ratio() {
+  const char* v = getenv("PQH_DEVICE_CODEC_MAX_RATIO");
+  return v ? atof(v) : 0.95;
+}
+
 // Plan: readChunk + readPages for one chunk (chunk_reader.go:182-362), page by page in the
 // reference's order of checks.  The walk stops at the first page it cannot read (host_status, with
 // the pages before it listed); the checks of each listed page that belong to the decoders (the
@@ -372,6 +380,7 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
   // some selected chunk's codec is decoded on the device)
   const bool dev = dev_codecs && ((m.codec == PQH_CODEC_SNAPPY && (flags & PQH_LOAD_DEVICE_SNAPPY)) ||
                                   (m.codec == PQH_CODEC_GZIP && (flags & PQH_LOAD_DEVICE_GZIP)));
+  const double max_ratio = device_codec_max_ratio();
   while (m.total_compressed - count > 0) {
     // readThrift(PageHeader): reads past the end of the file fail like any short read
     TReader r(f->data + std::min(pos, f->len), f->data + f->len);
@@ -401,11 +410,15 @@ void plan_chunk(const pqh_file* f, const ColumnMeta& col, const ChunkMeta& m, in
       if (int64_t(h.csize) - levels < 0 || int64_t(h.usize) - levels < 0) return PQH_ERR_PAGE_HEADER;
       if (op.got != h.csize) return PQH_ERR_DECOMPRESS;  // "compressed data must be %d byte"
       if (m.codec == PQH_CODEC_UNCOMPRESSED && h.csize != h.usize) return PQH_ERR_DECOMPRESS;
-      if (dev && m.codec == PQH_CODEC_SNAPPY && !snappy_plausible(op.block + levels, size_t(op.got - levels), int64_t(h.usize) - levels))
+      // a page whose values barely compress (>= 0.95 of their size) saves no PCIe bytes by
+      // travelling compressed: the host decompresses it, the device only copies the image (C5's
+      // random strings: k_snappy's page mode took 32 ms for pages that shrink by 0.2%)
+      const bool raw = dev && (max_ratio <= 0 || double(h.csize - levels) < max_ratio * double(h.usize - levels));
+      if (raw && m.codec == PQH_CODEC_SNAPPY && !snappy_plausible(op.block + levels, size_t(op.got - levels), int64_t(h.usize) - levels))
         return PQH_ERR_DECOMPRESS;
       op.levels = levels;
-      op.raw = dev;
-      op.src_len = dev ? op.got : h.usize;
+      op.raw = raw;
+      op.src_len = raw ? op.got : h.usize;
       op.pg.image_len = h.usize;
       return PQH_OK;
     };

@@ -135,6 +135,22 @@ struct DeltaState {
   uint64_t head_carry;    // value at position head_blocks * block_size (bits)
   int64_t head_neg;       // DELTA_LENGTH: first negative length among the head blocks (INT64_MAX: none)
 };
+// k_delta_split: window w of a page's delta stream owns the blocks whose header lies in
+// [h0 + w * kSplitStride, h0 + (w + 1) * kSplitStride)
+constexpr int kSplitStride = 12288;
+
+// k_delta_split's view of a delta page's first stream (written by k_delta_init, page mode).
+struct DeltaSplit {
+  int64_t h0;      // image offset of block 0's header
+  int64_t e;       // end of the values section (the stream's bytes end at or before it)
+  int64_t vcap;    // positions the head emits
+  int64_t lim;     // DELTA_LENGTH: positions whose lengths count in the byte-array tile sums
+  uint64_t first;  // first value (bits)
+  int32_t R;       // blocks of the head: whole blocks [0, R); 0 = not on the split path
+  int32_t bs, mbc, mbvc;
+};
+static_assert(sizeof(DeltaSplit) == 56, "DeltaSplit layout");
+
 // DELTA_BYTE_ARRAY pages carry two length streams: prefix lengths (state at dstates[page]) and the
 // DELTA_LENGTH suffix lengths that follow (state at dstates[num_pages + page]).
 

@@ -1689,6 +1689,14 @@ hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n,
   return hipGetLastError();
 }
 
+hipError_t launch_delta_split(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, int32_t n_lens,
+                              hipStream_t s) {
+  if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_split, dim3(n - n_lens), dim3(256), 0, s, b, wins, order, n - n_lens);
+  if (n_lens > 0)
+    hipLaunchKernelGGL(k_delta_split_lens, dim3(n_lens), dim3(256), 0, s, b, wins, order + (n - n_lens), n_lens);
+  return hipGetLastError();
+}
+
 hipError_t launch_delta_spec(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_delta_spec, dim3((n + 3) / 4), dim3(256), 0, s, b, delta_pages, n);

@@ -1972,6 +1972,460 @@ __global__ __launch_bounds__(256) void k_delta_fused_lens(DevBatch b, const Tile
   delta_fused_body<true>(b, streams);
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_delta_split (page mode): the head of every DELTA stream decoded by many workgroups per page
+// instead of one (k_delta_fused), so that a page's ~0.16 ms dependent chain of stage -> chase ->
+// expand no longer sets the time of a small shard (C3's N = 8 block: 960 pages for 2048 slots).
+// Reference: deltaBitPackDecoder.next (deltabp_decoder.go:113-174), value[i + 1] = value[i] +
+// delta[i] + minDelta over the chain of blocks (:51-111); byteArrayDeltaLengthDecoder's lengths
+// (type_bytearray.go:98-140).
+//   * a page's stream is cut into windows of kSplitStride bytes from block 0's header h0: window w
+//     owns the blocks whose header lies in [B_w, B_w+1), B_w = h0 + w * kSplitStride;
+//   * one workgroup per window, by ticket window-major (every page's window 0, then every window 1,
+//     ...), stages its bytes (kSplitStage: the stride + room for the block that crosses its end),
+//     takes its entry -- window 0: h0; w > 0: the first position >= B_w where three consecutive
+//     headers parse (a guess) -- and chases its blocks with lds_chase; their sum of delta + minDelta
+//     (the window's aggregate) is computed from the staged bytes;
+//   * decoupled look-back over three 64-bit words per window (relaxed agent-scope atomics, each of
+//     the two carry words tagged with the status word's high half, so that a reader takes only a
+//     consistent triple -- no fence, no L2 write-back): PARTIAL = (blocks, guessed entry, exit,
+//     aggregate), FINAL = (blocks through the window, exit, value after it, ended).  The nearest
+//     FINAL plus the PARTIALs after it give a window its first block and carry when every PARTIAL's
+//     guessed entry is its predecessor's exit; otherwise it waits for its predecessor's FINAL.  A
+//     wrong guess of its own is chased again from the true entry (the bytes are still staged);
+//   * the page's head is the whole blocks [0, R) that k_delta_fused would decode (R from
+//     delta_whole_blocks and the positions to emit); a chain that stops earlier (a header the
+//     common-case parse rejects, the stream end, a block wider than the stage's slack, more than
+//     kSplitMaxBlocks blocks in a window) ends the head there.  The window that ends the head writes
+//     (nblocks, end_pos, head_blocks, head_carry) -- exactly what k_delta_fused leaves -- and
+//     k_delta_walk / k_delta_page continue from it with the reference's exact semantics.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSplitStage = kFusedStage;  // 14848: the stride + 2.5 KiB for the block crossing its end
+constexpr int kSplitMaxBlocks = 1024;     // a window with more blocks (near-constant data) ends the head
+constexpr int kSplitSpinCap = 1 << 22;
+constexpr uint64_t kSpPartial = 1ull << 62, kSpFinal = 2ull << 62, kSpEnded = 1ull << 61;
+
+// The sum of delta + minDelta over the whole blocks [v0, v1) of the staged table (block-aligned v0;
+// wrapping: the 32-bit streams use its low half).  Whole workgroup; every thread gets the total.
+template <class L>
+__device__ uint64_t split_sum(const L& T, int64_t v0, int64_t v1, int lbs, int lmb, uint64_t* wsum) {
+  const int bb0 = int(v0 >> lbs);
+  uint64_t acc = 0;
+  for (int64_t p = v0 + 4 * int64_t(threadIdx.x); p < v1; p += 4 * kBlock) {
+    const int blk = int(p >> lbs) - bb0;
+    const int m = int(p & ((int64_t(1) << lbs) - 1)) >> lmb;
+    if (T.mbw[blk][m] <= 32) {
+      uint32_t u[4];
+      uint64_t md;
+      int bk;
+      staged_u32<4>(T, int32_t(p), bb0, lbs, lmb, u, md, bk);
+      acc += uint64_t(u[0]) + u[1] + u[2] + u[3] + 4 * md;
+    } else {
+      uint64_t d[2], d2[2];
+      staged_delta2(T, p, bb0, lbs, lmb, d);
+      staged_delta2(T, p + 2, bb0, lbs, lmb, d2);
+      acc += d[0] + d[1] + d2[0] + d2[1];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  return wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+struct SplitLds {
+  PageTileLdsT<kSplitStage> T;
+  int16_t hdr[kSplitMaxBlocks + 1];  // stage-relative header offsets of the window's chain
+  int32_t blkbit[kTileBlocks];
+  uint64_t blkw[kTileBlocks];
+  int16_t lst[kChaseCap][64];
+  uint64_t wsum[4];
+  int64_t sh[8];
+  int32_t si[8];
+  unsigned long long neg;
+};
+
+// Wave 0: the first position in [loc, lim) where a header and its two successors parse inside the
+// stage (or the chain reaches the stream's end exactly); lim if none.
+__device__ __forceinline__ int32_t split_guess(const uint32_t* data, int32_t loc, int32_t lim, int32_t eloc, bool is64,
+                                               int mbc, int gbytes) {
+  const int lane = threadIdx.x & 63;
+  const int32_t plim = kSplitStage - 32, dlim = kSplitStage - 16;
+  for (int32_t x0 = loc; x0 < lim; x0 += 64) {
+    const int32_t x = x0 + lane;
+    int32_t d1 = -1, d2 = -1, d3 = -1;
+    bool ok = x < lim && lds_block(data, x, eloc, plim, dlim, is64, mbc, gbytes, d1);
+    ok = ok && (d1 == eloc || lds_block(data, d1, eloc, plim, dlim, is64, mbc, gbytes, d2));
+    ok = ok && (d1 == eloc || d2 == eloc || lds_block(data, d2, eloc, plim, dlim, is64, mbc, gbytes, d3));
+    const uint64_t m = __ballot(ok);
+    if (m) return x0 + __builtin_ctzll(m);
+  }
+  return lim;
+}
+
+// Chase the window's chain from `entry` (stage-relative): headers into S.hdr, the aggregate, the
+// exit (the first header >= wend, or where the chain stops).  Whole workgroup.  Returns the number
+// of blocks; *stop = the chain ends inside the window (*exit is then where it stops).
+__device__ int split_chain(SplitLds& S, int32_t entry, int32_t wend, int32_t eloc, bool is64, int mbc, int mbvc,
+                           int lbs, int lmb, uint64_t* agg, int32_t* exit, bool* stop) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int gbytes = mbvc / 8;
+  int count = 0;
+  uint64_t sum = 0;
+  int32_t loc = entry;
+  int32_t est = 0;
+  bool stopped = false;
+  for (;;) {
+    if (loc >= wend) break;
+    if (count >= kSplitMaxBlocks) {
+      stopped = true;
+      break;
+    }
+    if (tid < 64) {
+      int n;
+      int32_t nxt;
+      bool st;
+      const int nmax = kSplitMaxBlocks - count < kTileBlocks ? kSplitMaxBlocks - count : kTileBlocks;
+      lds_chase(S.T.data, loc, eloc, est, nmax, is64, mbc, gbytes, S.lst, S.blkbit, S.blkw, S.T.md, lane, n, nxt, st,
+                kSplitStage);
+      // headers of the chased blocks; keep those that start before wend
+      int32_t h = -1;
+      if (lane < n) h = lane == 0 ? loc : 0;
+      if (lane >= 1 && lane <= n) {  // header k = the data end of block k - 1
+        h = S.blkbit[lane - 1] / 8 + int32_t(widths_sum(S.blkw[lane - 1])) * gbytes;
+      }
+      const uint64_t inside = __ballot(lane < n && h < wend);
+      const int keep = inside == ~0ull ? 64 : __builtin_ctzll(~inside);  // (headers ascend)
+      if (lane < keep) S.hdr[count + lane] = int16_t(h);
+      int32_t next = keep < n ? __builtin_amdgcn_readlane(h, keep) : nxt;
+      bool stp = keep < n ? false : st;
+      // a block ending past the stage (not a parse failure): the head ends at it
+      if (keep == n && !st && n < nmax && next < wend) stp = true;
+      if (tid == 0) {
+        S.si[0] = keep;
+        S.si[1] = next;
+        S.si[2] = stp;
+      }
+    }
+    __syncthreads();
+    const int keep = S.si[0];
+    const int32_t next = S.si[1];
+    if (keep > 0) {
+      for (int i = tid; i < keep * 8; i += kBlock) {  // miniblock tables of the kept blocks
+        const int blk = i >> 3, m = i & 7;
+        const uint64_t wd = S.blkw[blk];
+        const uint64_t below = m ? wd & ((1ull << (8 * m)) - 1) : 0;
+        S.T.mbbit[blk][m] = S.blkbit[blk] + int32_t(widths_sum(below)) * mbvc;
+        S.T.mbw[blk][m] = uint8_t(m < mbc ? int((wd >> (8 * m)) & 0xff) : 0);
+      }
+      __syncthreads();
+      const int64_t v0 = int64_t(count) << lbs;
+      sum += split_sum(S.T, v0, v0 + (int64_t(keep) << lbs), lbs, lmb, S.wsum);
+      est = (next - loc) / keep;
+    }
+    count += keep;
+    loc = next;
+    const bool stp = S.si[2] != 0;
+    __syncthreads();  // (S.si / tables read by every thread before the next round rewrites them)
+    if (stp) {
+      stopped = true;
+      break;
+    }
+    if (keep == 0) break;
+  }
+  *agg = sum;
+  *exit = loc;
+  *stop = stopped;
+  return count;
+}
+
+// Tables of the window's blocks [k0, k0 + n) (n <= 64) from their headers (stage-relative).
+__device__ __forceinline__ void split_tables(SplitLds& S, int k0, int n, bool is64, int mbc, int mbvc) {
+  const int tid = threadIdx.x;
+  if (tid < n) {
+    int32_t dat;
+    uint64_t md, wd;
+    lds_hdr(S.T.data, S.hdr[k0 + tid], is64, mbc, mbvc / 8, dat, md, wd);
+    S.T.md[tid] = md;
+    S.blkbit[tid] = dat * 8;
+    S.blkw[tid] = wd;
+  }
+  __syncthreads();
+  for (int i = tid; i < n * 8; i += kBlock) {
+    const int blk = i >> 3, m = i & 7;
+    const uint64_t wd = S.blkw[blk];
+    const uint64_t below = m ? wd & ((1ull << (8 * m)) - 1) : 0;
+    S.T.mbbit[blk][m] = S.blkbit[blk] + int32_t(widths_sum(below)) * mbvc;
+    S.T.mbw[blk][m] = uint8_t(m < mbc ? int((wd >> (8 * m)) & 0xff) : 0);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void split_publish(uint64_t* words, int t, uint64_t w0, uint64_t carry) {
+  const uint64_t tag = w0 & 0xffffffff00000000ull;
+  __hip_atomic_store(words + 3 * int64_t(t) + 1, tag | (carry & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(words + 3 * int64_t(t) + 2, tag | (carry >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(words + 3 * int64_t(t), w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A consistent (status, carry) of window j, or status 0 when not (yet) published.
+__device__ __forceinline__ uint64_t split_read(const uint64_t* words, int64_t j, uint64_t* carry) {
+  const uint64_t w0 = __hip_atomic_load(words + 3 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((w0 >> 62) == 0) return 0;
+  const uint64_t w1 = __hip_atomic_load(words + 3 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t w2 = __hip_atomic_load(words + 3 * j + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t tag = w0 & 0xffffffff00000000ull;
+  if ((w1 & 0xffffffff00000000ull) != tag || (w2 & 0xffffffff00000000ull) != tag) return 0;
+  *carry = (w1 & 0xffffffffull) | (w2 << 32);
+  return w0;
+}
+
+// Wave 0: window t (page window w >= 1, the page's window 0 at t - w).  Returns false when the
+// look-back is not decisive (wait for window t - 1's FINAL); otherwise the blocks and the value
+// before window t, the exit of window t - 1 and whether the head already ended.
+__device__ bool split_lookback(const uint64_t* words, int t, int w, int64_t h0, int64_t* pblk, uint64_t* pcarry,
+                               int64_t* pexit, bool* pended, bool* timeout) {
+  const int lane = threadIdx.x & 63;
+  const int first = t - w;
+  int hi = t - 1;
+  int64_t cnt = 0, need = -1, exit1 = -1;
+  uint64_t acc = 0;
+  bool ended1 = false;
+  for (bool round0 = true;; round0 = false) {
+    const int j = hi - lane;
+    const bool in = j >= first;
+    uint64_t v = 0, c = 0;
+    for (int spin = 0;; spin++) {
+      if (in && v == 0) v = split_read(words, j, &c);
+      if (__ballot(in && v == 0) == 0) break;
+      if (spin > kSplitSpinCap) {
+        *timeout = true;
+        return true;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const bool fin = in && (v >> 62) == 2;
+    const uint64_t fm = __ballot(fin);
+    const int f = fm ? __builtin_ctzll(fm) : 64;
+    const int64_t ex = int64_t(uint32_t(v));
+    const bool end = (v & kSpEnded) != 0;
+    // the PARTIAL's guessed entry: its window base + the 16-bit offset
+    const int64_t ent = h0 + int64_t(w - (t - j)) * kSplitStride + int64_t((v >> 45) & 0xffff);
+    int64_t nxt = __shfl_up(ent, 1, 64);  // the entry the next newer window guessed
+    if (lane == 0) nxt = need;
+    if (round0) {
+      exit1 = __shfl(ex, 0, 64);
+      ended1 = __shfl(int(end), 0, 64) != 0;
+    }
+    // a FINAL that ended the head: everything after it is past the head
+    if (f < 64 && __shfl(int(end), f, 64)) {
+      // (consistency of the PARTIALs after it is irrelevant: no window after an ended head writes)
+      const uint64_t vf = __shfl(v, f, 64);
+      *pblk = int64_t((vf >> 32) & 0x1fffffff);
+      *pcarry = 0;
+      *pexit = int64_t(uint32_t(vf));
+      *pended = true;
+      return true;
+    }
+    const bool lead = round0 && lane == 0;
+    // lanes before the FINAL: each exit meets its successor's guess; only window t - 1 may end
+    const bool ok = !in || lane > f || ((nxt < 0 || ex == nxt) && (!end || lead));
+    if (__ballot(!ok)) return false;
+    uint64_t a = (in && lane < f) ? c : 0;
+    int64_t k = (in && lane < f) ? int64_t((v >> 32) & 0x1fff) : 0;
+    for (int off = 32; off > 0; off >>= 1) {
+      a += __shfl_xor(a, off, 64);
+      k += __shfl_xor(k, off, 64);
+    }
+    if (f < 64) {
+      const uint64_t vf = __shfl(v, f, 64);
+      const uint64_t cf = __shfl(c, f, 64);
+      *pblk = int64_t((vf >> 32) & 0x1fffffff) + cnt + k;
+      *pcarry = cf + acc + a;
+      *pexit = exit1;
+      *pended = ended1;
+      return true;
+    }
+    acc += a;
+    cnt += k;
+    need = __shfl(ent, 63, 64);
+    hi -= 64;
+  }
+}
+
+template <bool kLens>
+__device__ __forceinline__ void delta_split_body(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin,
+                                                 uint32_t* ticket) {
+  __shared__ SplitLds S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) S.sh[0] = atomicAdd(ticket, 1u);
+  __syncthreads();
+  if (int(S.sh[0]) >= nwin) return;
+  const int t = order[S.sh[0]];
+  const int2 pw = wins[t];
+  const int p = pw.x, w = pw.y;
+  const DeltaSplit Q = b.dsplit[p];
+  if (Q.R <= 0) return;
+  const int64_t Bw = Q.h0 + int64_t(w) * kSplitStride;
+  if (Bw >= Q.e) return;  // no header starts here (nor in the page's later windows)
+  const DevPage P = b.pages[p];
+  const uint8_t* img = b.payload + P.image_off;
+  const bool is64 = P.kind == K_DELTA64;
+  const int bs = Q.bs, mbc = Q.mbc, mbvc = Q.mbvc;
+  const int lbs = __builtin_ctz(uint32_t(bs)), lmb = __builtin_ctz(uint32_t(mbvc));
+  const int64_t a0 = Bw - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(Bw)) & 15);
+  stage_copy(reinterpret_cast<uint4*>(S.T.data), img + a0, kSplitStage / 16, Q.e - a0);
+  if (tid < 4) S.T.data[kSplitStage / 4 + tid] = 0;
+  __syncthreads();
+  const int32_t eloc = int32_t(Q.e - a0 < kSplitStage ? Q.e - a0 : kSplitStage + 64);  // (past the stage: never reached)
+  const int32_t wend = int32_t(Bw - a0) + kSplitStride;
+  int32_t entry = int32_t(Q.h0 - a0);
+  if (w > 0) {
+    if (tid < 64) {
+      const int32_t g = split_guess(S.T.data, int32_t(Bw - a0), wend, eloc, is64, mbc, mbvc / 8);
+      if (tid == 0) S.si[3] = g;
+    }
+    __syncthreads();
+    entry = S.si[3];
+  }
+  uint64_t agg;
+  int32_t ex;
+  bool stop;
+  int n = entry < wend ? split_chain(S, entry, wend, eloc, is64, mbc, mbvc, lbs, lmb, &agg, &ex, &stop) : 0;
+  if (entry >= wend) {
+    agg = 0;
+    ex = entry;
+    stop = false;
+  }
+  uint64_t* words = b.dwords;
+  int64_t pblk = 0;
+  uint64_t carry = Q.first;
+  bool pended = false;
+  if (w > 0) {
+    if (tid == 0)  // PARTIAL
+      split_publish(words, t, kSpPartial | (stop ? kSpEnded : 0) | (uint64_t(entry - int32_t(Bw - a0)) << 45) |
+                                  (uint64_t(n) << 32) | uint64_t(uint32_t(a0 + ex)),
+                    agg);
+    if (tid < 64) {
+      int64_t pb = 0, pe = 0;
+      uint64_t pc = 0;
+      bool en = false, to = false;
+      if (!split_lookback(words, t, w, Q.h0, &pb, &pc, &pe, &en, &to)) {
+        uint64_t v = 0, c = 0;
+        for (int spin = 0;; spin++) {  // the predecessor's FINAL
+          if (tid == 0) v = split_read(words, t - 1, &c);
+          v = __shfl(v, 0, 64);
+          if ((v >> 62) == 2) break;
+          if (spin > kSplitSpinCap) {
+            to = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        c = __shfl(c, 0, 64);
+        pb = int64_t((v >> 32) & 0x1fffffff);
+        pc = c;
+        pe = int64_t(uint32_t(v));
+        en = (v & kSpEnded) != 0;
+      }
+      if (tid == 0) {
+        if (to) {  // never expected: the page errs instead of hanging (PQH_ERR_INTERNAL)
+          atomicMin(&b.states[p].err, (unsigned long long)err_key(3, 0, PQH_ERR_INTERNAL));
+          en = true;
+        }
+        S.sh[1] = pb;
+        S.sh[2] = int64_t(pc);
+        S.sh[3] = pe;
+        S.sh[4] = en;
+      }
+    }
+    __syncthreads();
+    pblk = S.sh[1];
+    carry = uint64_t(S.sh[2]);
+    const int64_t pexit = S.sh[3];
+    pended = S.sh[4] != 0;
+    if (!pended && pexit != a0 + entry) {
+      // a wrong guess: the true entry is the predecessor's exit (>= B_w)
+      const int32_t te = int32_t(pexit - a0);
+      if (te < wend) {
+        n = split_chain(S, te, wend, eloc, is64, mbc, mbvc, lbs, lmb, &agg, &ex, &stop);
+      } else {
+        n = 0;
+        agg = 0;
+        ex = te;
+        stop = false;
+      }
+    }
+  }
+  if (pended) {
+    if (tid == 0) split_publish(words, t, kSpFinal | kSpEnded | (uint64_t(pblk & 0x1fffffff) << 32), 0);
+    return;
+  }
+  // the head: whole blocks [0, R)
+  const int64_t R = Q.R;
+  const int use = int(pblk + n <= R ? n : (R - pblk > 0 ? R - pblk : 0));
+  bool ended = stop || pblk + use >= R;
+  int64_t hexit = a0 + ex;  // the header after this window's blocks of the head
+  uint64_t after = carry + agg;
+  if (use < n) {
+    hexit = a0 + S.hdr[use];
+    ended = true;
+  }
+  // tables of the blocks in use (the chase left those of its last round: rebuilt unless that round
+  // covered them all), the exact value after them when the head ends inside the window, expansion
+  // FINAL before the expansion, so that the windows after this one need not wait for it (its carry
+  // counts only while the head goes on: when the head ends here, the value after it is computed
+  // below for k_delta_walk / k_delta_page)
+  if (tid == 0)
+    split_publish(words, t, kSpFinal | (ended ? kSpEnded : 0) | (uint64_t((pblk + use) & 0x1fffffff) << 32) |
+                                uint64_t(uint32_t(hexit)),
+                  after);
+  const int64_t vcap = Q.vcap;
+  LenSums ls{b.basums + P.batile_base, Q.lim, INT64_MAX};
+  const DevChunk C = b.chunks[P.chunk];
+  const bool lens = P.kind == K_DLBA || P.kind == K_DBA;
+  int32_t* lp = P.kind == K_DBA ? C.aux2 : C.aux;
+  const PageState PS = b.states[p];
+  uint8_t* out = lens ? reinterpret_cast<uint8_t*>(lp + PS.value_base) : C.values + PS.value_base * P.value_size;
+  uint64_t c = carry;
+  uint64_t partial = 0;  // the sum over the blocks in use (only needed when use < n)
+  for (int k0 = 0; k0 < use; k0 += kTileBlocks) {
+    const int nb = use - k0 < kTileBlocks ? use - k0 : kTileBlocks;
+    __syncthreads();
+    split_tables(S, k0, nb, is64, mbc, mbvc);
+    const int64_t v0 = (pblk + k0) << lbs;
+    if (use < n) partial += split_sum(S.T, v0, v0 + (int64_t(nb) << lbs), lbs, lmb, S.wsum);
+    int64_t v1 = (pblk + k0 + nb) << lbs;
+    if (v1 > vcap) v1 = vcap;
+    if (v0 < v1) {
+      if constexpr (kLens) c = expand_rows<true>(S.T, v0, v1, lbs, lmb, out, false, c, &ls);
+      else c = expand_rows(S.T, v0, v1, lbs, lmb, out, is64, c);
+    }
+  }
+  if (use < n) after = carry + partial;
+  if constexpr (kLens) {
+    if (ls.neg != INT64_MAX) atomicMin(reinterpret_cast<unsigned long long*>(&b.dstates[p].head_neg),
+                                       (unsigned long long)ls.neg);
+  }
+  // the head ends in this window when it ends here and began before it (pblk >= R: the head ended
+  // exactly where this window starts, and the window that reached R wrote it)
+  if (ended && pblk < R && tid == 0) {  // what k_delta_fused leaves for k_delta_walk / k_delta_page
+    b.dstates[p].nblocks = int32_t(pblk + use);
+    b.dstates[p].end_pos = hexit;
+    b.dstates[p].head_blocks = int32_t(pblk + use);
+    b.dstates[p].head_carry = after;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_delta_split(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
+  delta_split_body<false>(b, wins, order, nwin, b.dticket);
+}
+__global__ __launch_bounds__(256) void k_delta_split_lens(DevBatch b, const int2* wins, const int32_t* order,
+                                                          int32_t nwin) {
+  delta_split_body<true>(b, wins, order, nwin, b.dticket + 1);
+}
+
 // k_delta_init (page mode, before k_scan): deltaBitPackDecoder.init of every DELTA_BINARY_PACKED
 // page, so that its load errors (phase 0) are known to the value-offset scan before k_delta_fused
 // decodes into the chunk outputs.  k_delta_walk repeats the init later and finds the same keys.
@@ -1984,16 +2438,47 @@ __global__ __launch_bounds__(256) void k_delta_init(DevBatch b, const int32_t* d
   const int p = delta_pages[idx];
   const DevPage P = b.pages[p];
   const PageState S = b.states[p];
+  DeltaSplit Q;  // k_delta_split's view of the page (R = 0: nothing for it)
+  Q.h0 = Q.e = Q.vcap = Q.lim = 0;
+  Q.first = 0;
+  Q.R = Q.bs = Q.mbc = Q.mbvc = 0;
+  if (lane == 0 && b.dsplit) {  // no head until a k_delta_fused / k_delta_split window writes one
+    b.dstates[p].nblocks = 0;
+    b.dstates[p].end_pos = 0;
+    b.dstates[p].head_blocks = 0;
+    b.dstates[p].head_carry = 0;
+    b.dstates[p].head_neg = INT64_MAX;
+  }
   const bool load_ok = S.err == kNoError || (S.err >> 56) > 0;
-  if (P.host_err != kNoError || !load_ok) return;
-  if (P.kind == K_DLBA)  // k_delta_fused / k_delta_page add the tile byte sums of its lengths
-    for (int k = lane; k < P.batile_n; k += 64) b.basums[P.batile_base + k] = 0;
-  Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
-  win_load(w, S.val_s, lane);
-  DeltaState D;
-  int32_t vc;
-  uint64_t md, widths;
-  int64_t pos = S.val_s;
-  const uint64_t err = delta_init(w, pos, P.kind == K_DELTA64, D, vc, md, widths, lane);
-  if (lane == 0 && err != kNoError) atomicMin(&b.states[p].err, (unsigned long long)err);
+  if (P.host_err == kNoError && load_ok) {
+    if (P.kind == K_DLBA)  // k_delta_fused / k_delta_page add the tile byte sums of its lengths
+      for (int k = lane; k < P.batile_n; k += 64) b.basums[P.batile_base + k] = 0;
+    Win w{b.payload + P.image_off, S.val_e, win_all[wv], 0, 0};
+    win_load(w, S.val_s, lane);
+    DeltaState D;
+    int32_t vc;
+    uint64_t md, widths;
+    int64_t pos = S.val_s, h0 = pos;
+    const uint64_t err = delta_init(w, pos, P.kind == K_DELTA64, D, vc, md, widths, lane, &h0);
+    if (lane == 0 && err != kNoError) atomicMin(&b.states[p].err, (unsigned long long)err);
+    if (err == kNoError && D.mode == DM_FAST) {  // k_delta_fused's head, as whole blocks [0, R)
+      const bool lens = P.kind == K_DLBA || P.kind == K_DBA;
+      const bool before_values = S.err != kNoError && (S.err >> 56) <= 2;
+      const int64_t nn = lens ? vc : (before_values ? 0 : S.nn);
+      const int64_t kmax = delta_whole_blocks(nn, vc, D.block_size, P.dblk_cap);
+      const int lbs = __builtin_ctz(uint32_t(D.block_size));
+      const int64_t vcap = lens ? (before_values ? 0 : int64_t(S.nn)) : kmax << lbs;
+      const int64_t need = (vcap + D.block_size - 1) >> lbs;
+      Q.R = int32_t(kmax < need ? kmax : need);
+      Q.h0 = h0;
+      Q.e = S.val_e;
+      Q.vcap = vcap;
+      Q.lim = P.kind == K_DLBA ? (S.val_limit < vc ? S.val_limit : vc) : 0;
+      Q.first = D.first;
+      Q.bs = D.block_size;
+      Q.mbc = D.mb_count;
+      Q.mbvc = D.mbvc;
+    }
+  }
+  if (lane == 0 && b.dsplit) b.dsplit[p] = Q;
 }

@@ -29,6 +29,9 @@ struct DevBatch {
   int64_t* basums2;      // DELTA_BYTE_ARRAY: per tile suffix-byte sum, then its first suffix byte
   uint32_t* bafuse;      // fused PLAIN chains: [0] window tickets, [1] fallback flag (zeroed per run)
   uint64_t* bawords;     // fused PLAIN chains: per window FINAL word (zeroed per run)
+  DeltaSplit* dsplit;    // page mode: per page, k_delta_split's view of its first delta stream
+  uint32_t* dticket;     // k_delta_split: window tickets (zeroed per run)
+  uint64_t* dwords;      // k_delta_split: three look-back words per window (zeroed per run)
 };
 
 hipError_t launch_prologue(const DevBatch& b, bool wide, hipStream_t s);
@@ -88,6 +91,10 @@ hipError_t launch_delta_expand(const DevBatch& b, const Tile* tiles, int32_t n, 
 // scan; whole blocks chased and decoded in one workgroup per stream (before the exact walk).
 hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int32_t n, hipStream_t s);
 hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, int32_t n_lens, hipStream_t s);
+// k_delta_split: windows wins[order[i]] = (page, window) by ticket; [0, n - n_lens) of DELTA /
+// DELTA_BYTE_ARRAY prefix streams, [n - n_lens, n) of DELTA_LENGTH lengths (two launches)
+hipError_t launch_delta_split(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, int32_t n_lens,
+                              hipStream_t s);
 // Many delta streams: one workgroup per (page, stream), its tiles in order with a running carry.
 hipError_t launch_delta_page(const DevBatch& b, const Tile* streams, int32_t n, hipStream_t s);
 // Byte arrays: PLAIN chains (one wave per page, data and dictionary pages), tile byte sums,

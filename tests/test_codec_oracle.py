@@ -16,6 +16,13 @@ from oracle import oracle as O
 from snappy_blocks import literal, copy1, copy2, copy4, block, sample_blocks
 
 
+
+@pytest.fixture(autouse=True)
+def every_page_on_the_device(monkeypatch):
+    """The layout tests put every page of a device-codec chunk on the device (the walker's default
+    keeps barely compressible pages on the host route; test_gpu_codec.py tests that rule)."""
+    monkeypatch.setenv("PQH_DEVICE_CODEC_MAX_RATIO", "0")
+
 def test_snappy_oracle_matches_pyarrow():
     for raw in sample_blocks():
         comp = pa.compress(raw, codec="snappy", asbytes=True)

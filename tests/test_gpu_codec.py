@@ -31,6 +31,43 @@ def ctx(pq):
     return pq.native.Context(0)
 
 
+@pytest.fixture(autouse=True)
+def every_page_on_the_device(monkeypatch, request):
+    """These tests exercise the device codecs on every page of a device-codec chunk, barely
+    compressible ones included (the walker's default keeps pages whose values compress to >= 0.95
+    of their size on the host route: test_device_codec_skips_incompressible_pages)."""
+    if request.node.name.startswith("test_device_codec_skips"):
+        return
+    monkeypatch.setenv("PQH_DEVICE_CODEC_MAX_RATIO", "0")
+
+
+@pytest.mark.parametrize("codec", [O.SNAPPY, O.GZIP])
+def test_device_codec_skips_incompressible_pages(pq, ctx, codec):
+    """Default routing: with device codecs requested, pages whose compressed
+    values are >= 0.95 of their size travel decompressed (the host decodes them; the device copies
+    the image: codec page codec 0) and the others travel compressed; strings of random bytes are all
+    of the first kind (for SNAPPY, C5's random letters too), URL-like strings of the second.  Every chunk equals the oracle either way."""
+    W = pq.writer
+    rng = np.random.default_rng(11)
+    rand = [bytes(rng.integers(0, 256, int(k)).astype(np.uint8)) for k in rng.integers(8, 40, 6000)]
+    urls = [b"https://www.example.com/news-%d/item%d?id=%d" % (i % 40, i % 500, i) for i in range(6000)]
+    cols = [("r", W.Column(W.BYTE_ARRAY, rand, encoding=W.DELTA_LENGTH_BYTE_ARRAY, use_dict=False), W.REQUIRED),
+            ("u", W.Column(W.BYTE_ARRAY, urls, encoding=W.DELTA_LENGTH_BYTE_ARRAY, use_dict=False), W.REQUIRED)]
+    data = W.flat(cols, 3000, codec=codec, max_page_size=16 * 1024)
+    f = pq.native.File(data)
+    hb = f.load(0, f.num_row_groups, [0, 1], device_snappy=True, device_gzip=True)
+    kinds = {}
+    for cp in hb.codec_pages():
+        kinds.setdefault(cp.chunk % 2, set()).add(cp.codec)
+    assert kinds[0] == {0} and kinds[1] == {codec}, kinds
+    hb.close()
+    res = pq.reader.decode_chunks(ctx, f, 0, f.num_row_groups, [0, 1], device_snappy=True, device_gzip=True)
+    fr = O.FileReader(data)
+    for k, col in enumerate(res):
+        assert_chunk(col, oracle_chunk(fr, *divmod(k, 2)), where=f"chunk {k}")
+    f.close()
+
+
 def _device_decompress(pq, ctx, blocks, sizes, codec=O.SNAPPY):
     """Every block as one codec page; returns [(status, bytes)]."""
     N = pq.native

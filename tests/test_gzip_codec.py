@@ -20,6 +20,13 @@ from oracle import oracle as O
 DECOMPRESS = 23
 
 
+
+@pytest.fixture(autouse=True)
+def every_page_on_the_device(monkeypatch):
+    """The layout tests put every page of a device-codec chunk on the device (the walker's default
+    keeps barely compressible pages on the host route; test_gpu_codec.py tests that rule)."""
+    monkeypatch.setenv("PQH_DEVICE_CODEC_MAX_RATIO", "0")
+
 def expected(stream, size):
     """(status, bytes) the reference's readPageBlock gives a page of `size` bytes."""
     try:
