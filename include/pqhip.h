@@ -283,6 +283,14 @@ typedef struct pqh_ctx pqh_ctx;
 typedef struct pqh_batch pqh_batch;
 
 #define PQH_CTX_PROFILE 1u /* time every kernel launch with HIP events */
+/* A streaming context (creation only; pqh_ctx_set_flags keeps it): one slot of a bounded ring of
+ * end-to-end row-group ranges (reader.RowGroupStream: one context per slot, so that a slot's batch
+ * creation, sync and destruction wait for that slot's own work only).  Its batches allocate from the
+ * device's stream-ordered memory pool (hipMallocAsync / hipFreeAsync: no device-wide hipFree
+ * synchronisation, memory cached for the next range), launch directly (a batch runs once: no graph
+ * capture), and pqh_batch_create_staged defers the first upload to pqh_batch_run_staged (one H2D per
+ * range). */
+#define PQH_CTX_STREAMING 2u
 
 int pqh_abi_version(void);
 /* The build's source hash (sha256 prefix of every source compiled into the library): profiles are
@@ -294,6 +302,9 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out);
  * replay the batch's launch sequence as one captured hipGraph; profiled runs launch each kernel
  * between HIP events. */
 int pqh_ctx_set_flags(pqh_ctx* ctx, uint32_t flags);
+/* Bytes of pinned host memory the context's pool holds (payload blocks in use by host / staged
+ * batches plus the free ones it keeps for reuse): the bound of a streaming ring's pinned staging. */
+int64_t pqh_ctx_pinned_bytes(const pqh_ctx* ctx);
 void pqh_ctx_destroy(pqh_ctx* ctx);
 const char* pqh_last_error(const pqh_ctx* ctx);
 /* The HIP stream every decode of this context is ordered on (a hipStream_t): a run is enqueued on

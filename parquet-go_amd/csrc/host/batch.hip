@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +32,7 @@ struct PinnedPool {
   std::mutex m;
   std::vector<std::pair<uint8_t*, size_t>> free_blocks;
   bool closed = false;
+  std::atomic<int64_t> pinned{0};  // bytes pinned by the pool (blocks in use + free)
 };
 
 struct pqh_ctx {
@@ -112,11 +114,13 @@ bool fuse_enabled() {
   return !(f && f[0] == '0');
 }
 
-// PQH_DELTA_SPLIT=0 (A/B experiments, tests): page-mode delta heads by k_delta_fused (one workgroup
-// per stream) instead of k_delta_split (windows of a stream over many workgroups).
+// PQH_DELTA_SPLIT=1 (opt-in, tests): page-mode delta heads by k_delta_split (12 KiB windows of a
+// stream over many workgroups with a decoupled look-back) instead of k_delta_fused (one workgroup per
+// stream).  Measured slower at every C3 shard size (59 us per window against 26 us per
+// fused tile, 5 vs 8 workgroups per CU), so not the default.
 bool split_enabled() {
   const char* f = getenv("PQH_DELTA_SPLIT");
-  return !(f && f[0] == '0');
+  return f && f[0] == '1';
 }
 
 // PQH_NEST_EARLY=0 (A/B experiments, tests): one k_expand launch, the nesting kernels after it.
@@ -179,7 +183,7 @@ std::shared_ptr<uint8_t> pinned_acquire(pqh_ctx* ctx, size_t bytes) {
   std::shared_ptr<PinnedPool> pool = ctx->pool;
   uint8_t* p = nullptr;
   size_t cap = 0;
-  std::vector<uint8_t*> drop;
+  std::vector<std::pair<uint8_t*, size_t>> drop;
   {
     std::lock_guard<std::mutex> g(pool->m);
     size_t best = SIZE_MAX;
@@ -193,23 +197,36 @@ std::shared_ptr<uint8_t> pinned_acquire(pqh_ctx* ctx, size_t bytes) {
     } else {
       // a miss: the free blocks are all too small for this request; release them rather than keep
       // them pinned for the context's life (payloads that keep growing would pile up otherwise)
-      for (auto& fb : pool->free_blocks) drop.push_back(fb.first);
-      pool->free_blocks.clear();
+      drop.swap(pool->free_blocks);
     }
   }
   if (!drop.empty()) hipSetDevice(ctx->device);
-  for (uint8_t* q : drop) hipHostFree(q);
+  for (auto& fb : drop) {
+    hipHostFree(fb.first);
+    pool->pinned -= int64_t(fb.second);
+  }
   if (!p) {
-    cap = (std::max<size_t>(bytes, 1) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    // 2 MiB granules; a streaming context's ring reuses one block per slot for ranges of similar
+    // but not equal sizes, so its blocks get 1/8 of headroom (and 64 MiB granules past 512 MiB)
+    // instead of being re-pinned whenever a range is a little larger than the last
+    const bool ring = (ctx->flags & PQH_CTX_STREAMING) != 0;
+    const size_t g = ring && bytes > (size_t(512) << 20) ? size_t(64) << 20 : size_t(2) << 20;
+    const size_t want = ring ? bytes + bytes / 8 : bytes;
+    cap = (std::max<size_t>(want, 1) + g - 1) & ~(g - 1);
     hipSetDevice(ctx->device);
     void* q = nullptr;
     if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
     p = static_cast<uint8_t*>(q);
+    pool->pinned += int64_t(cap);
   }
   return std::shared_ptr<uint8_t>(p, [pool, cap](uint8_t* q) {
     std::lock_guard<std::mutex> g(pool->m);
-    if (pool->closed) hipHostFree(q);
-    else pool->free_blocks.emplace_back(q, cap);
+    if (pool->closed) {
+      hipHostFree(q);
+      pool->pinned -= int64_t(cap);
+    } else {
+      pool->free_blocks.emplace_back(q, cap);
+    }
   });
 }
 
@@ -406,11 +423,22 @@ struct pqh_batch {
 
 namespace {
 
+// Device buffers of a batch: hipMalloc, or in a streaming context the stream-ordered pool.
+hipError_t dev_alloc(pqh_ctx* ctx, void** p, size_t bytes) {
+  return (ctx->flags & PQH_CTX_STREAMING) ? hipMallocAsync(p, bytes, ctx->stream) : hipMalloc(p, bytes);
+}
+
+void dev_free(pqh_ctx* ctx, void* p) {
+  if (!p) return;
+  if (ctx->flags & PQH_CTX_STREAMING) hipFreeAsync(p, ctx->stream);
+  else hipFree(p);
+}
+
 void free_batch(pqh_batch* b) {
   for (hipEvent_t e : b->event_pool) hipEventDestroy(e);
-  for (void* p : b->allocations) hipFree(p);
-  if (b->owned_payload) hipFree(b->owned_payload);
-  if (b->d_src) hipFree(b->d_src);
+  for (void* p : b->allocations) dev_free(b->ctx, p);
+  dev_free(b->ctx, b->owned_payload);
+  dev_free(b->ctx, b->d_src);
   if (b->h_staged && !b->h_pinned_ref) hipHostFree(b->h_staged);
   b->h_pinned_ref.reset();
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
@@ -432,7 +460,7 @@ ChunkErr chunk_error(const pqh_batch* b, int32_t chunk);
 // path it takes.
 int dalloc(pqh_batch* b, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc(p, bytes);
+  hipError_t e = dev_alloc(b->ctx, p, bytes);
   if (e != hipSuccess) return set_err(b->ctx, PQH_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   b->allocations.push_back(*p);
   e = hipMemsetAsync(*p, 0, bytes, b->ctx->stream);
@@ -475,6 +503,15 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
   pqh_ctx* c = new pqh_ctx();
   c->device = device;
   c->flags = flags;
+  if (flags & PQH_CTX_STREAMING) {
+    // stream-ordered allocations of this context's batches stay cached in the device's pool (a
+    // ring recycles them range after range) instead of going back to the driver at each sync
+    hipMemPool_t mp = nullptr;
+    if (hipSetDevice(device) == hipSuccess && hipDeviceGetDefaultMemPool(&mp, device) == hipSuccess && mp) {
+      uint64_t keep = UINT64_MAX;
+      hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
@@ -519,9 +556,11 @@ const char* pqh_last_error(const pqh_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 void* pqh_ctx_stream(pqh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
 
+int64_t pqh_ctx_pinned_bytes(const pqh_ctx* ctx) { return ctx ? ctx->pool->pinned.load() : 0; }
+
 int pqh_ctx_set_flags(pqh_ctx* ctx, uint32_t flags) {
   if (!ctx) return set_err(nullptr, PQH_ERR_ARG, "null context");
-  ctx->flags = flags;
+  ctx->flags = (flags & ~PQH_CTX_STREAMING) | (ctx->flags & PQH_CTX_STREAMING);  // (creation only)
   return PQH_OK;
 }
 
@@ -1468,7 +1507,7 @@ int pqh_batch_run(pqh_batch* b) {
   hipError_t e = hipSuccess;
   // a k_flat batch is one kernel: launched directly (C1: 0.0126 ms per step against 0.0178 ms as a
   // one-node graph replay, same box -- the replay adds ~6 us per step)
-  if (!prof && graphs_enabled() && !b->graph_failed && !flat_batch(b)) {
+  if (!prof && graphs_enabled() && !b->graph_failed && !flat_batch(b) && !(ctx->flags & PQH_CTX_STREAMING)) {
     if (!b->gexec) {
       e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
       if (e == hipSuccess) {
@@ -1591,10 +1630,10 @@ int pqh_batch_sync(pqh_batch* b) {
     }
     if (cap <= D.bytes_cap) continue;
     void* np = nullptr;
-    HIP_TRY(ctx, hipMalloc(&np, size_t(cap) + 64));
+    HIP_TRY(ctx, dev_alloc(ctx, &np, size_t(cap) + 64));
     for (auto& a : b->allocations)
       if (a == D.bytes) {
-        hipFree(a);
+        dev_free(ctx, a);
         a = np;
       }
     D.bytes = static_cast<uint8_t*>(np);
@@ -2045,7 +2084,8 @@ int pqh_batch_path_info(const pqh_batch* b, pqh_batch_paths* out) {
   out->ba_fuse_active = b->ba_fuse_on ? 1 : 0;
   out->ba_fuse_fallbacks = b->ba_fuse_fallbacks;
   out->regrows = b->regrows;
-  out->graph_replay = (graphs_enabled() && !b->graph_failed && !flat_batch(b) && !(b->ctx->flags & PQH_CTX_PROFILE)) ? 1 : 0;
+  out->graph_replay = (graphs_enabled() && !b->graph_failed && !flat_batch(b) &&
+                       !(b->ctx->flags & (PQH_CTX_PROFILE | PQH_CTX_STREAMING))) ? 1 : 0;
   return PQH_OK;
 }
 
@@ -2106,17 +2146,17 @@ int snap_plan_alloc(pqh_batch* b, const pqh_codec_page* pages, int32_t n) {
 int create_codec_batch(pqh_ctx* ctx, const pqh_host_batch* hb, void* d_src, pqh_batch** out) {
   void* img = nullptr;
   const size_t ibytes = size_t(hb->image_bytes) + PQH_PAYLOAD_PAD;
-  HIP_TRY(ctx, hipMalloc(&img, ibytes));
+  HIP_TRY(ctx, dev_alloc(ctx, &img, ibytes));
   hipError_t e = hipMemsetAsync(img, 0, ibytes, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
-    hipFree(img);
+    dev_free(ctx, img);
     return set_err(ctx, PQH_ERR_HIP, std::string("image buffer: ") + hipGetErrorString(e));
   }
   int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
                             int32_t(hb->pages.size()), img, hb->image_bytes, out);
   if (rc) {
-    hipFree(img);
+    dev_free(ctx, img);
     return rc;
   }
   pqh_batch* b = *out;
@@ -2156,29 +2196,30 @@ int pqh_batch_create_from_host(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch
   hipSetDevice(ctx->device);
   if (!hb->codec_pages.empty()) {  // source payload to HBM; images rebuilt by every run
     void* src = nullptr;
-    HIP_TRY(ctx, hipMalloc(&src, hb->size()));
+    HIP_TRY(ctx, dev_alloc(ctx, &src, hb->size()));
     hipError_t e = bounce_h2d(ctx, src, hb->data(), hb->size());
     if (e != hipSuccess) {
-      hipFree(src);
+      dev_free(ctx, src);
       return set_err(ctx, PQH_ERR_HIP, std::string("source upload: ") + hipGetErrorString(e));
     }
     const int rc = create_codec_batch(ctx, hb, src, out);
-    if (rc) hipFree(src);
+    if (rc) dev_free(ctx, src);
     return rc;
   }
   void* d = nullptr;
   const size_t bytes = hb->size();
-  HIP_TRY(ctx, hipMalloc(&d, bytes ? bytes : 16));
-  const hipError_t e = hb->pinned ? hipMemcpy(d, hb->data(), bytes, hipMemcpyHostToDevice)
-                                  : bounce_h2d(ctx, d, hb->data(), bytes);
+  HIP_TRY(ctx, dev_alloc(ctx, &d, bytes ? bytes : 16));
+  hipError_t e = hb->pinned ? hipMemcpyAsync(d, hb->data(), bytes, hipMemcpyHostToDevice, ctx->stream)
+                            : bounce_h2d(ctx, d, hb->data(), bytes);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
-    hipFree(d);
+    dev_free(ctx, d);
     return set_err(ctx, PQH_ERR_HIP, std::string("payload upload: ") + hipGetErrorString(e));
   }
   int rc = pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()), hb->pages.data(),
                             int32_t(hb->pages.size()), d, hb->payload_bytes, out);
   if (rc) {
-    hipFree(d);
+    dev_free(ctx, d);
     return rc;
   }
   (*out)->owned_payload = d;
@@ -2203,13 +2244,15 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
     if (!pinned) hipHostFree(h);
   };
   void* d = nullptr;
-  hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
+  const bool streaming = (ctx->flags & PQH_CTX_STREAMING) != 0;
+  hipError_t e = dev_alloc(ctx, &d, bytes ? bytes : 16);
   // the first upload happens here so that planning (which reads nothing from the payload) and the
-  // first plain pqh_batch_run see the same bytes as the staged runs
-  if (e == hipSuccess && bytes) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream);
+  // first plain pqh_batch_run see the same bytes as the staged runs; a streaming context leaves it to
+  // pqh_batch_run_staged (one H2D per range, on the copy stream)
+  if (e == hipSuccess && bytes && !streaming) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
-    if (d) hipFree(d);
+    if (d) dev_free(ctx, d);
     free_h();
     return set_err(ctx, PQH_ERR_HIP, std::string("staged payload: ") + hipGetErrorString(e));
   }
@@ -2218,7 +2261,7 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
                                                        hb->payload_bytes, out)
                                     : create_codec_batch(ctx, hb, d, out);
   if (rc) {
-    hipFree(d);
+    dev_free(ctx, d);
     free_h();
     return rc;
   }

@@ -1493,7 +1493,8 @@ __device__ __forceinline__ uint32_t stage_dw(const uint32_t* stage, int q) {
 constexpr int kChainList = 1024;
 constexpr int kChainLongs = 8;  // records past the stage of kLong bytes or more (at most ~2 per window)
 
-__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
+__global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin,
+                                                  int32_t use_ticket) {
   __shared__ ChainLds C;
   __shared__ uint16_t list[kChainList + 2];
   __shared__ BaWin R;
@@ -1501,7 +1502,7 @@ __global__ __launch_bounds__(256) void k_ba_chain(DevBatch b, const int2* wins, 
   __shared__ int32_t longs[3 * kChainLongs + 1];  // {index, start, end} of long records past the stage; count
   const int tid = threadIdx.x;
   if (tid == 0) {
-    sh[0] = atomicAdd(b.bafuse, 1u);
+    sh[0] = use_ticket ? atomicAdd(b.bafuse, 1u) : blockIdx.x;  // (A/B: the dispatch order itself)
     longs[3 * kChainLongs] = 0;
   }
   __syncthreads();

@@ -1691,9 +1691,12 @@ hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n,
 
 hipError_t launch_delta_split(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, int32_t n_lens,
                               hipStream_t s) {
-  if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_split, dim3(n - n_lens), dim3(256), 0, s, b, wins, order, n - n_lens);
+  const char* tk = getenv("PQH_SPLIT_TICKET");  // (A/B: "0" = dispatch order instead of tickets)
+  const int32_t ticket = !(tk && tk[0] == '0');
+  if (n - n_lens > 0)
+    hipLaunchKernelGGL(k_delta_split, dim3(n - n_lens), dim3(256), 0, s, b, wins, order, n - n_lens, ticket);
   if (n_lens > 0)
-    hipLaunchKernelGGL(k_delta_split_lens, dim3(n_lens), dim3(256), 0, s, b, wins, order + (n - n_lens), n_lens);
+    hipLaunchKernelGGL(k_delta_split_lens, dim3(n_lens), dim3(256), 0, s, b, wins, order + (n - n_lens), n_lens, ticket);
   return hipGetLastError();
 }
 
@@ -1769,7 +1772,12 @@ hipError_t launch_ba_wcopy(const DevBatch& b, const int2* list, int32_t n, const
 
 hipError_t launch_ba_chain(const DevBatch& b, const int2* wins, const int32_t* order, int32_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n);
+  // windows taken in dispatch order (blockIdx.x) rather than by an atomic ticket: C4 k_ba_chain
+  // 0.499 -> 0.481 ms, same box (PQH_CHAIN_TICKET=1 restores the tickets).  Forward progress rests on
+  // the dispatcher's increasing workgroup order; should a look-back ever outwait its spin cap, the
+  // batch falls back to the scratch path (bafuse[1]), never a wrong result
+  const char* tk = getenv("PQH_CHAIN_TICKET");
+  hipLaunchKernelGGL(k_ba_chain, dim3(n), dim3(256), 0, s, b, wins, order, n, int32_t(tk && tk[0] == '1'));
   return hipGetLastError();
 }
 

@@ -2259,7 +2259,8 @@ __device__ __forceinline__ void delta_split_body(DevBatch b, const int2* wins, c
                                                  uint32_t* ticket) {
   __shared__ SplitLds S;
   const int tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) S.sh[0] = atomicAdd(ticket, 1u);
+  // (ticket == nullptr: the dispatch order itself, blockIdx.x -- no contended atomic per window)
+  if (tid == 0) S.sh[0] = ticket ? atomicAdd(ticket, 1u) : blockIdx.x;
   __syncthreads();
   if (int(S.sh[0]) >= nwin) return;
   const int t = order[S.sh[0]];
@@ -2418,12 +2419,13 @@ __device__ __forceinline__ void delta_split_body(DevBatch b, const int2* wins, c
   }
 }
 
-__global__ __launch_bounds__(256) void k_delta_split(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin) {
-  delta_split_body<false>(b, wins, order, nwin, b.dticket);
+__global__ __launch_bounds__(256) void k_delta_split(DevBatch b, const int2* wins, const int32_t* order, int32_t nwin,
+                                                     int32_t use_ticket) {
+  delta_split_body<false>(b, wins, order, nwin, use_ticket ? b.dticket : nullptr);
 }
 __global__ __launch_bounds__(256) void k_delta_split_lens(DevBatch b, const int2* wins, const int32_t* order,
-                                                          int32_t nwin) {
-  delta_split_body<true>(b, wins, order, nwin, b.dticket + 1);
+                                                          int32_t nwin, int32_t use_ticket) {
+  delta_split_body<true>(b, wins, order, nwin, use_ticket ? b.dticket + 1 : nullptr);
 }
 
 // k_delta_init (page mode, before k_scan): deltaBitPackDecoder.init of every DELTA_BINARY_PACKED

@@ -30,6 +30,7 @@ UNSUPPORTED_CODEC = 35  # the chunk's codec is not decoded here: the caller rout
 # error phases (pqh_phase): page load (readChunk), repetition levels, definition levels, values
 PHASE_LOAD, PHASE_REP, PHASE_DEF, PHASE_VALUES = range(4)
 CTX_PROFILE = 1
+CTX_STREAMING = 2  # one slot of a streaming ring (reader.RowGroupStream)
 PAYLOAD_PAD = 256
 MAX_NEST = 32  # include/pqhip.h PQH_MAX_NEST
 
@@ -112,6 +113,7 @@ PROTOTYPES = [
     ("pqh_ctx_set_flags", ctypes.c_int, [vp, u32]),
     ("pqh_last_error", cp, [vp]),
     ("pqh_ctx_stream", vp, [vp]),
+    ("pqh_ctx_pinned_bytes", i64, [vp]),
     ("pqh_malloc", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
     ("pqh_free", ctypes.c_int, [vp, vp]),
     ("pqh_host_alloc", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
@@ -223,11 +225,12 @@ def device_count():
 class Context:
     """One HIP device + stream (pqh_ctx)."""
 
-    def __init__(self, device=0, profile=False):
+    def __init__(self, device=0, profile=False, streaming=False):
         L = _lib.hip()
         self.L = L
         h = vp()
-        rc = L.pqh_ctx_create(device, CTX_PROFILE if profile else 0, ctypes.byref(h))
+        rc = L.pqh_ctx_create(device, (CTX_PROFILE if profile else 0) | (CTX_STREAMING if streaming else 0),
+                              ctypes.byref(h))
         if rc != OK:
             raise PqhError(rc, (L.pqh_last_error(None) or b"").decode())
         self.h = h
@@ -241,6 +244,10 @@ class Context:
 
     def sync(self):
         self.check(self.L.pqh_sync(self.h))
+
+    def pinned_bytes(self):
+        """Pinned host bytes the context's payload pool holds (in use + kept for reuse)."""
+        return int(self.L.pqh_ctx_pinned_bytes(self.h))
 
     def set_profile(self, on):
         """Per-kernel HIP-event timing on (direct launches) or off (graph replay)."""
@@ -559,9 +566,9 @@ class Batch:
         return pv, (vals if pv.value_size > 0 else (offs, data)), d, r
 
     def kernel_stats(self):
-        arr = (KernelStat * 32)()
+        arr = (KernelStat * 64)()
         n = i32()
-        self.ctx.check(self.L.pqh_batch_kernel_stats(self.h, arr, 32, ctypes.byref(n)))
+        self.ctx.check(self.L.pqh_batch_kernel_stats(self.h, arr, 64, ctypes.byref(n)))
         return [arr[i] for i in range(n.value)]
 
     def paths(self):

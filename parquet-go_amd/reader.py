@@ -173,6 +173,82 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
     return out
 
 
+class RowGroupStream:
+    """End-to-end streaming of a file's row groups through a bounded ring (SURVEY.md §8(d)
+    end-to-end mode; north_star: "decompressed page buffers are staged in HBM with pinned
+    hipMemcpyAsync on a side stream").  The reference reads a row group at a time --
+    readRowGroupData (chunk_reader.go:375-404) walks, reads and decompresses every page of the
+    selected chunks (readPageBlock / newBlockReader, chunk_reader.go:161-180, compress.go:131-152)
+    before decoding -- and so does this reader, for ranges of `per_range` row groups, with `slots`
+    ranges in flight:
+
+      * slot s is a streaming context (native.CTX_STREAMING): its own streams, pinned payload pool
+        and stream-ordered device allocations, so nothing a slot waits for belongs to another slot;
+      * range i is walked on the host (thrift headers, CRC, decompression) straight into slot
+        i % slots's pinned block, then its batch copies it to HBM on the slot's copy stream and
+        decodes it on the slot's compute stream (pqh_batch_run_staged): while range i decodes and
+        ranges i+1.. copy, the host walks the next one;
+      * a range's batch is handed to the caller once decoded and stays valid until the next
+        iteration, which releases its slot (pinned block back to the slot's pool, device memory back
+        to the pool) and walks range i + slots into it.
+
+    Pinned host memory is bounded by `slots` blocks (pinned_bytes()); device memory by the
+    batches of `slots` ranges.  Iterating yields (rg_begin, rg_end, native.Batch, host batch)."""
+
+    def __init__(self, file, columns, rg_begin=0, rg_end=None, per_range=4, slots=3, device=0, validate_crc=False):
+        self.file = file
+        self.columns = list(columns)
+        rg_end = file.num_row_groups if rg_end is None else rg_end
+        self.ranges = [(a, min(a + per_range, rg_end)) for a in range(rg_begin, rg_end, per_range)]
+        self.validate_crc = validate_crc
+        self.ctxs = [native.Context(device, streaming=True) for _ in range(max(1, slots))]
+        self.walk_s = 0.0
+
+    def pinned_bytes(self):
+        return sum(c.pinned_bytes() for c in self.ctxs)
+
+    def _submit(self, i):
+        import time
+
+        a, b = self.ranges[i]
+        ctx = self.ctxs[i % len(self.ctxs)]
+        t0 = time.perf_counter()
+        hb = self.file.load(a, b, self.columns, self.validate_crc, ctx=ctx)  # host walk into the slot's block
+        self.walk_s += time.perf_counter() - t0
+        batch = native.Batch.staged(ctx, hb)
+        batch.run_staged()  # H2D on the slot's copy stream, then the decode (asynchronous)
+        return (i, batch, hb)
+
+    def __iter__(self):
+        from collections import deque
+
+        inflight = deque()
+        nxt = 0
+        while nxt < len(self.ranges) and len(inflight) < len(self.ctxs):
+            inflight.append(self._submit(nxt))
+            nxt += 1
+        try:
+            while inflight:
+                i, batch, hb = inflight.popleft()
+                batch.sync()  # the slot's own streams only
+                a, b = self.ranges[i]
+                yield a, b, batch, hb
+                batch.close()
+                hb.close()
+                if nxt < len(self.ranges):
+                    inflight.append(self._submit(nxt))
+                    nxt += 1
+        finally:
+            for _, batch, hb in inflight:
+                batch.close()
+                hb.close()
+
+    def close(self):
+        for c in self.ctxs:
+            c.close()
+        self.ctxs = []
+
+
 def records_error():
     from . import records
 

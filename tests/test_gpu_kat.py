@@ -71,10 +71,11 @@ def _delta_page(w, data, bits):
     return (uvarint(8) + uvarint(1) + uvarint(9) + zigzag(0) + zigzag(0) + bytes([w]) + data + zigzag(0) + bytes([0]))
 
 
-@pytest.mark.parametrize("mode", ["tiles", "streams"])
+@pytest.mark.parametrize("mode", ["tiles", "streams", "split"])
 @pytest.mark.parametrize("bits", [64, 32])
 def test_delta_miniblock_kat(pq, ctx, bits, mode, monkeypatch):
-    monkeypatch.setenv("PQH_DELTA_PAGE_MODE", "1" if mode == "streams" else "0")
+    monkeypatch.setenv("PQH_DELTA_PAGE_MODE", "0" if mode == "tiles" else "1")
+    monkeypatch.setenv("PQH_DELTA_SPLIT", "1" if mode == "split" else "0")
     N = pq.native
     kat = KAT64 if bits == 64 else KAT32
     col = (O.INT64 if bits == 64 else O.INT32, 0, 0, 0)

@@ -21,11 +21,13 @@ def ctx(pq):
     return pq.native.Context(0)
 
 
-@pytest.fixture(params=["tiles", "streams"])
+@pytest.fixture(params=["tiles", "streams", "split"])
 def delta_mode(request, monkeypatch):
-    """Both DELTA decode paths: per-tile sums + page scan + tile expands, and one workgroup per
-    stream (k_delta_page), which the planner picks for batches of >= 1024 delta streams."""
-    monkeypatch.setenv("PQH_DELTA_PAGE_MODE", "1" if request.param == "streams" else "0")
+    """Every DELTA decode path: per-tile sums + page scan + tile expands; one workgroup per stream
+    (k_delta_fused + k_delta_page), which the planner picks for batches of >= 256 delta streams; and
+    the opt-in windowed heads (k_delta_split, PQH_DELTA_SPLIT=1) in page mode."""
+    monkeypatch.setenv("PQH_DELTA_PAGE_MODE", "0" if request.param == "tiles" else "1")
+    monkeypatch.setenv("PQH_DELTA_SPLIT", "1" if request.param == "split" else "0")
     return request.param
 
 
