@@ -285,11 +285,14 @@ typedef struct pqh_batch pqh_batch;
 #define PQH_CTX_PROFILE 1u /* time every kernel launch with HIP events */
 /* A streaming context (creation only; pqh_ctx_set_flags keeps it): one slot of a bounded ring of
  * end-to-end row-group ranges (reader.RowGroupStream: one context per slot, so that a slot's batch
- * creation, sync and destruction wait for that slot's own work only).  Its batches allocate from the
- * device's stream-ordered memory pool (hipMallocAsync / hipFreeAsync: no device-wide hipFree
- * synchronisation, memory cached for the next range), launch directly (a batch runs once: no graph
- * capture), and pqh_batch_create_staged defers the first upload to pqh_batch_run_staged (one H2D per
- * range). */
+ * creation, sync and destruction wait for that slot's own work only).  It has ONE stream: the H2D of
+ * pqh_batch_run_staged, the plan's zero fills and the decode run in order on it (the ring overlaps
+ * slots; extra streams per slot would share the process's few hardware queues with other slots'
+ * streams).  Its batches bump-allocate from the context's device arena, reset when the context's
+ * last batch is destroyed (no driver call per range; PQH_ARENA_GUARD bytes of gap after each buffer,
+ * PQH_ARENA_CHECK=1 verifies them at pqh_batch_sync), launch directly (a batch runs once: no graph
+ * capture), and pqh_batch_create_staged returns without waiting on the GPU: the page images and the
+ * plan tables (from a pinned block of the context's pool) are copied by pqh_batch_run_staged. */
 #define PQH_CTX_STREAMING 2u
 
 int pqh_abi_version(void);

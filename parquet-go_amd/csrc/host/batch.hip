@@ -35,8 +35,34 @@ struct PinnedPool {
   std::atomic<int64_t> pinned{0};  // bytes pinned by the pool (blocks in use + free)
 };
 
+// Device memory of a streaming context (PQH_CTX_STREAMING): one arena, bump-allocated in plan order
+// and reset when the context's last live allocation goes (a ring slot holds one batch at a time, so
+// every range's batch lays its buffers out again from the bottom: no driver call per range, no
+// stream-ordered pool whose cross-stream reuse the copy and side streams would have to be ordered
+// against).  Each allocation is followed by a guard gap (PQH_ARENA_GUARD bytes, default 4 KiB);
+// with PQH_ARENA_CHECK=1 the gaps hold a canary that pqh_batch_sync verifies, naming the allocation
+// a kernel wrote past.
+struct DevArena {
+  struct Chunk {
+    uint8_t* base;
+    size_t cap, used;
+  };
+  struct Guard {
+    uint8_t* p;
+    size_t bytes, alloc_bytes;
+    int32_t index;
+  };
+  std::mutex m;
+  std::vector<Chunk> chunks;
+  std::vector<Guard> guards;
+  int64_t live = 0;    // allocations not yet freed
+  int32_t allocs = 0;  // allocations since the last reset
+  size_t want = 0;     // after the arena grew: the size of the one chunk that replaces its chunks
+};
+
 struct pqh_ctx {
   std::shared_ptr<PinnedPool> pool = std::make_shared<PinnedPool>();
+  DevArena arena;
   int32_t device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
@@ -99,6 +125,10 @@ bool sync_each_enabled() {
   return f && f[0] == '1';
 }
 thread_local const char* g_fail_kernel = nullptr;
+// set by pqh_batch_create_staged in a streaming context around pqh_batch_create: the plan tables are
+// uploaded by pqh_batch_run_staged on the copy stream instead of synchronously (a slot's creation then
+// never waits behind the other slots' payload copies on the DMA engines)
+thread_local bool g_defer_tables = false;
 
 // PQH_SNAPPY_PAGE=1 (A/B experiments): device SNAPPY by k_snappy, one workgroup per page, instead of
 // the multi-workgroup pipeline (k_snap_spec / stitch / emit / fixup).
@@ -373,9 +403,6 @@ struct pqh_batch {
   DeltaState* d_dstates = nullptr;
   DeltaBlock* d_dblocks = nullptr;
   uint64_t* d_dsums = nullptr;
-  uint32_t* d_dflag = nullptr;   // delta look-back: per delta tile flag (+ the ticket counter at the end)
-  uint64_t* d_dagg = nullptr;
-  uint64_t* d_dpre = nullptr;
   Tile* d_batiles = nullptr;
   int32_t* d_ba_xlist = nullptr;
   int32_t* d_ba_pages = nullptr;
@@ -419,18 +446,134 @@ struct pqh_batch {
   std::vector<FlatTile> flat_tiles; // k_flat: expand_tiles with their pages' fields
   int64_t* d_flat_base = nullptr;
   FlatTile* d_flat_tiles = nullptr;
+  // a ring slot's staged batch (streaming context): the plan tables wait in a pinned block and travel
+  // on the copy stream ahead of the range's payload, at its first pqh_batch_run_staged
+  struct TableUp {
+    void* dst;
+    size_t off, bytes;
+  };
+  std::shared_ptr<uint8_t> h_tables;
+  std::vector<TableUp> table_ups;
 };
 
 namespace {
 
-// Device buffers of a batch: hipMalloc, or in a streaming context the stream-ordered pool.
+size_t arena_guard() {
+  static const size_t g = [] {
+    const char* f = getenv("PQH_ARENA_GUARD");
+    const long long v = f ? atoll(f) : 4096;
+    return size_t(v > 0 ? (v + 255) & ~255ll : 0);
+  }();
+  return g;
+}
+
+bool arena_check() {
+  static const bool c = [] {
+    const char* f = getenv("PQH_ARENA_CHECK");
+    return f && f[0] == '1';
+  }();
+  return c;
+}
+
+constexpr uint8_t kCanary = 0xA5;
+
+hipError_t arena_alloc(pqh_ctx* ctx, void** p, size_t bytes) {
+  DevArena& A = ctx->arena;
+  std::lock_guard<std::mutex> g(A.m);
+  const size_t gb = arena_guard();
+  const size_t need = ((bytes + 255) & ~size_t(255)) + gb;
+  if (A.chunks.empty() || A.chunks.back().cap - A.chunks.back().used < need) {
+    size_t cap = std::max({need, A.want, size_t(64) << 20});
+    cap = (cap + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    void* q = nullptr;
+    const hipError_t e = hipMalloc(&q, cap);
+    if (e != hipSuccess) return e;
+    A.want = 0;
+    A.chunks.push_back({static_cast<uint8_t*>(q), cap, 0});
+  }
+  DevArena::Chunk& c = A.chunks.back();
+  uint8_t* r = c.base + c.used;
+  c.used += need;
+  if (gb && arena_check()) {
+    const hipError_t e = hipMemsetAsync(r + need - gb, kCanary, gb, ctx->stream);
+    if (e != hipSuccess) return e;
+    A.guards.push_back({r + need - gb, gb, bytes, A.allocs});
+  }
+  A.allocs++;
+  A.live++;
+  *p = r;
+  return hipSuccess;
+}
+
+// Callers free only after the context's streams have drained (pqh_batch_destroy synchronises them).
+void arena_free(pqh_ctx* ctx) {
+  DevArena& A = ctx->arena;
+  std::lock_guard<std::mutex> g(A.m);
+  if (--A.live > 0) return;
+  A.live = 0;
+  A.allocs = 0;
+  A.guards.clear();
+  if (A.chunks.size() > 1) {  // it grew: one chunk of the peak (+1/8) from the next allocation on
+    size_t used = 0;
+    for (auto& c : A.chunks) {
+      used += c.used;
+      hipFree(c.base);
+    }
+    A.chunks.clear();
+    A.want = used + used / 8;
+  } else if (!A.chunks.empty()) {
+    A.chunks[0].used = 0;
+  }
+}
+
+void arena_release(pqh_ctx* ctx) {
+  DevArena& A = ctx->arena;
+  std::lock_guard<std::mutex> g(A.m);
+  for (auto& c : A.chunks) hipFree(c.base);
+  A.chunks.clear();
+}
+
+// (PQH_ARENA_CHECK=1, after a synchronised run) every guard gap still holds the canary; a kernel that
+// wrote past an allocation is named by the allocation's index (plan order) and size.
+int arena_verify(pqh_ctx* ctx) {
+  DevArena& A = ctx->arena;
+  std::vector<DevArena::Guard> gs;
+  {
+    std::lock_guard<std::mutex> g(A.m);
+    gs = A.guards;
+  }
+  std::vector<uint8_t> h;
+  std::string bad;
+  for (const auto& g : gs) {
+    h.resize(g.bytes);
+    HIP_TRY(ctx, bounce_d2h(ctx, h.data(), g.p, g.bytes));
+    size_t i = 0, n = 0;
+    while (i < h.size() && h[i] == kCanary) i++;
+    for (size_t k = i; k < h.size(); k++) n += h[k] != kCanary;
+    if (i < h.size()) {
+      char m[200];
+      snprintf(m, sizeof(m), "%sallocation #%d (%zu bytes): guard byte +%zu = 0x%02x, %zu of %zu guard bytes overwritten",
+               bad.empty() ? "" : "; ", g.index, g.alloc_bytes, i, h[i], n, h.size());
+      bad += m;
+    }
+  }
+  if (!bad.empty()) {
+    std::string table;
+    for (const auto& g : gs) table += " #" + std::to_string(g.index) + ":" + std::to_string(g.alloc_bytes);
+    fprintf(stderr, "pqhip arena: %s\npqhip arena allocations:%s\n", bad.c_str(), table.c_str());
+    return set_err(ctx, PQH_ERR_INTERNAL, "arena guard overwritten: " + bad);
+  }
+  return PQH_OK;
+}
+
+// Device buffers of a batch: hipMalloc, or in a streaming context the context's arena.
 hipError_t dev_alloc(pqh_ctx* ctx, void** p, size_t bytes) {
-  return (ctx->flags & PQH_CTX_STREAMING) ? hipMallocAsync(p, bytes, ctx->stream) : hipMalloc(p, bytes);
+  return (ctx->flags & PQH_CTX_STREAMING) ? arena_alloc(ctx, p, bytes) : hipMalloc(p, bytes);
 }
 
 void dev_free(pqh_ctx* ctx, void* p) {
   if (!p) return;
-  if (ctx->flags & PQH_CTX_STREAMING) hipFreeAsync(p, ctx->stream);
+  if (ctx->flags & PQH_CTX_STREAMING) arena_free(ctx);
   else hipFree(p);
 }
 
@@ -441,6 +584,7 @@ void free_batch(pqh_batch* b) {
   dev_free(b->ctx, b->d_src);
   if (b->h_staged && !b->h_pinned_ref) hipHostFree(b->h_staged);
   b->h_pinned_ref.reset();
+  b->h_tables.reset();
   if (b->ev_copied) hipEventDestroy(b->ev_copied);
   if (b->ev_done) hipEventDestroy(b->ev_done);
   for (hipEvent_t e : b->ev_dep)
@@ -503,19 +647,15 @@ int pqh_ctx_create(int32_t device, uint32_t flags, pqh_ctx** out) {
   pqh_ctx* c = new pqh_ctx();
   c->device = device;
   c->flags = flags;
-  if (flags & PQH_CTX_STREAMING) {
-    // stream-ordered allocations of this context's batches stay cached in the device's pool (a
-    // ring recycles them range after range) instead of going back to the driver at each sync
-    hipMemPool_t mp = nullptr;
-    if (hipSetDevice(device) == hipSuccess && hipDeviceGetDefaultMemPool(&mp, device) == hipSuccess && mp) {
-      uint64_t keep = UINT64_MAX;
-      hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-  }
+  // A streaming context (a ring slot) is ONE stream: copy, zero fills and decode in order.  The ring
+  // overlaps slots, not a slot's own copy and decode, and every extra stream would share one of the
+  // process's few hardware queues with another slot's stream -- a false dependency that holds one
+  // slot's work behind another slot's copy.
+  const bool one = (flags & PQH_CTX_STREAMING) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side3, hipStreamNonBlocking) != hipSuccess) {
+      (!one && (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&c->side3, hipStreamNonBlocking) != hipSuccess))) {
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->side) hipStreamDestroy(c->side);
     if (c->side2) hipStreamDestroy(c->side2);
@@ -543,6 +683,7 @@ void pqh_ctx_destroy(pqh_ctx* ctx) {
   for (hipEvent_t ev : ctx->bounce_ev)
     if (ev) hipEventDestroy(ev);
   if (ctx->bounce) hipHostFree(ctx->bounce);
+  arena_release(ctx);
   {
     std::lock_guard<std::mutex> g(ctx->pool->m);
     ctx->pool->closed = true;
@@ -958,9 +1099,6 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dstates), sizeof(DeltaState) * 2 * size_t(num_pages))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dblocks), sizeof(DeltaBlock) * size_t(dblk_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dsums), sizeof(uint64_t) * size_t(dtile_cursor))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dflag), sizeof(uint32_t) * size_t(dtile_cursor + 1))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dagg), sizeof(uint64_t) * size_t(dtile_cursor))) ||
-      (rc = dalloc(b, reinterpret_cast<void**>(&b->d_dpre), sizeof(uint64_t) * size_t(dtile_cursor))) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_batiles), sizeof(Tile) * b->ba_tiles.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_xlist), sizeof(int32_t) * b->ba_xlist.size())) ||
       (rc = dalloc(b, reinterpret_cast<void**>(&b->d_ba_pages), sizeof(int32_t) * b->ba_pages.size())) ||
@@ -1179,11 +1317,26 @@ int pqh_batch_create(pqh_ctx* ctx, const pqh_chunk* chunks, int32_t num_chunks, 
   };
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
-  for (const Up& u : ups)
-    if (e == hipSuccess && u.bytes) e = bounce_h2d(ctx, u.dst, u.src, u.bytes);
+  if (g_defer_tables) {
+    size_t total = 0;
+    for (const Up& u : ups) total += (u.bytes + 15) & ~size_t(15);
+    b->h_tables = pinned_acquire(ctx, total ? total : 16);
+    if (!b->h_tables) e = hipErrorOutOfMemory;
+    for (size_t i = 0, off = 0; e == hipSuccess && i < sizeof(ups) / sizeof(ups[0]); i++) {
+      if (!ups[i].bytes) continue;
+      memcpy(b->h_tables.get() + off, ups[i].src, ups[i].bytes);
+      b->table_ups.push_back({ups[i].dst, off, ups[i].bytes});
+      off += (ups[i].bytes + 15) & ~size_t(15);
+    }
+  } else {
+    for (const Up& u : ups)
+      if (e == hipSuccess && u.bytes) e = bounce_h2d(ctx, u.dst, u.src, u.bytes);
+  }
   if (e == hipSuccess && num_chunks) e = hipMemsetAsync(b->d_chunk_bytes, 0, sizeof(int64_t) * size_t(num_chunks), s);
   if (e == hipSuccess) e = hipMemsetAsync(b->d_bafuse, 0, sizeof(uint32_t) * 8, s);  // ([4]: k_flat's flag)
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  // (deferred tables: nothing to wait for here -- the zero fills stay queued on the context stream and
+  // pqh_batch_run_staged orders the copy stream after them; a slot's creation never waits on the GPU)
+  if (e == hipSuccess && !g_defer_tables) e = hipStreamSynchronize(s);
   for (hipEvent_t& ev : b->ev_dep)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -1505,6 +1658,9 @@ int pqh_batch_run(pqh_batch* b) {
   hipStream_t s = ctx->stream;
   b->synced = false;
   hipError_t e = hipSuccess;
+  for (const auto& u : b->table_ups)  // a staged batch run without pqh_batch_run_staged: its tables now
+    HIP_TRY(ctx, hipMemcpyAsync(u.dst, b->h_tables.get() + u.off, u.bytes, hipMemcpyHostToDevice, s));
+  b->table_ups.clear();
   // a k_flat batch is one kernel: launched directly (C1: 0.0126 ms per step against 0.0178 ms as a
   // one-node graph replay, same box -- the replay adds ~6 us per step)
   if (!prof && graphs_enabled() && !b->graph_failed && !flat_batch(b) && !(ctx->flags & PQH_CTX_STREAMING)) {
@@ -1554,6 +1710,10 @@ int pqh_batch_sync(pqh_batch* b) {
   if (b->codec_n)
     HIP_TRY(ctx, bounce_d2h(ctx, b->codec_status.data(), b->d_codec_status, sizeof(int32_t) * size_t(b->codec_n)));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if ((ctx->flags & PQH_CTX_STREAMING) && arena_check()) {
+    const int rc = arena_verify(ctx);
+    if (rc) return rc;
+  }
   // k_flat's speculation failed (a page not clean and simple, a key out of range): decode the batch
   // again through the three kernels, and keep it there
   if (b->flat_on) {
@@ -2230,7 +2390,8 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
   *out = nullptr;
   if (!ctx || !hb) return set_err(ctx, PQH_ERR_ARG, "null argument");
   hipSetDevice(ctx->device);
-  if (!ctx->copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  if (!ctx->copy_stream && !(ctx->flags & PQH_CTX_STREAMING))
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   const size_t bytes = hb->size();
   void* h = nullptr;
   std::shared_ptr<uint8_t> pinned = hb->pinned ? hb->buf : nullptr;  // a pinned payload is adopted, not copied
@@ -2250,16 +2411,18 @@ int pqh_batch_create_staged(pqh_ctx* ctx, const pqh_host_batch* hb, pqh_batch** 
   // first plain pqh_batch_run see the same bytes as the staged runs; a streaming context leaves it to
   // pqh_batch_run_staged (one H2D per range, on the copy stream)
   if (e == hipSuccess && bytes && !streaming) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess && !streaming) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     if (d) dev_free(ctx, d);
     free_h();
     return set_err(ctx, PQH_ERR_HIP, std::string("staged payload: ") + hipGetErrorString(e));
   }
+  g_defer_tables = streaming && hb->codec_pages.empty();
   int rc = hb->codec_pages.empty() ? pqh_batch_create(ctx, hb->chunks.data(), int32_t(hb->chunks.size()),
                                                        hb->pages.data(), int32_t(hb->pages.size()), d,
                                                        hb->payload_bytes, out)
                                     : create_codec_batch(ctx, hb, d, out);
+  g_defer_tables = false;
   if (rc) {
     dev_free(ctx, d);
     free_h();
@@ -2355,13 +2518,28 @@ int pqh_batch_run_staged(pqh_batch* b) {
   pqh_ctx* ctx = b->ctx;
   if (!b->h_staged) return set_err(ctx, PQH_ERR_ARG, "batch was not created by pqh_batch_create_staged");
   hipSetDevice(ctx->device);
+  // a streaming context copies on its one stream (in order with the plan's zero fills and the
+  // decode); otherwise on the copy stream, beside the decode of the previous staged batch
+  const bool one = ctx->copy_stream == nullptr;
+  hipStream_t cs = one ? ctx->stream : ctx->copy_stream;
   // the copy must not overwrite page images a previous decode of this batch still reads
-  if (b->done_recorded) HIP_TRY(ctx, hipStreamWaitEvent(ctx->copy_stream, b->ev_done, 0));
+  if (b->done_recorded && !one) HIP_TRY(ctx, hipStreamWaitEvent(cs, b->ev_done, 0));
+  if (!b->table_ups.empty()) {  // deferred plan tables (first run only): after the plan's zero fills
+    if (!one) {
+      HIP_TRY(ctx, hipEventRecord(b->ev_copied, ctx->stream));
+      HIP_TRY(ctx, hipStreamWaitEvent(cs, b->ev_copied, 0));
+    }
+    for (const auto& u : b->table_ups)
+      HIP_TRY(ctx, hipMemcpyAsync(u.dst, b->h_tables.get() + u.off, u.bytes, hipMemcpyHostToDevice, cs));
+    b->table_ups.clear();
+  }
   if (b->staged_bytes)  // the page images, or with device codecs the source bytes
     HIP_TRY(ctx, hipMemcpyAsync(b->codec_n ? b->d_src : b->owned_payload, b->h_staged, b->staged_bytes,
-                                hipMemcpyHostToDevice, ctx->copy_stream));
-  HIP_TRY(ctx, hipEventRecord(b->ev_copied, ctx->copy_stream));
-  HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->ev_copied, 0));
+                                hipMemcpyHostToDevice, cs));
+  if (!one) {
+    HIP_TRY(ctx, hipEventRecord(b->ev_copied, cs));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, b->ev_copied, 0));
+  }
   int rc = pqh_batch_run(b);
   if (rc) return rc;
   HIP_TRY(ctx, hipEventRecord(b->ev_done, ctx->stream));

@@ -628,8 +628,11 @@ int file_load(pqh_ctx* ctx, pqh_file* f, int32_t rg_begin, int32_t rg_end, const
         dev = (c == PQH_CODEC_SNAPPY && (flags & PQH_LOAD_DEVICE_SNAPPY)) ||
               (c == PQH_CODEC_GZIP && (flags & PQH_LOAD_DEVICE_GZIP));
       }
+  // walker threads: one per hardware thread up to 16 (the host share a GPU box grants), or
+  // PQH_WALK_THREADS (a streaming ring leaves cores to the batch creation beside its walks)
   int nt = int(std::thread::hardware_concurrency());
   if (nt > 16) nt = 16;
+  if (const char* w = getenv("PQH_WALK_THREADS")) nt = atoi(w);
   if (nt < 1) nt = 1;
   auto parallel = [&](int64_t items, auto&& fn) {
     std::atomic<int64_t> next{0};

@@ -17,6 +17,11 @@ FIRST error in decode order) for any failing chunk; the row-group cursor fails a
 readChunk errors (walker, codecs, page load), and NextRow raises a readValues error at the row that
 reaches the failing page (records.py).
 """
+import queue
+import threading
+import time
+from collections import deque
+
 import numpy as np
 
 from . import native
@@ -182,66 +187,184 @@ class RowGroupStream:
     before decoding -- and so does this reader, for ranges of `per_range` row groups, with `slots`
     ranges in flight:
 
-      * slot s is a streaming context (native.CTX_STREAMING): its own streams, pinned payload pool
-        and stream-ordered device allocations, so nothing a slot waits for belongs to another slot;
+      * slot s is a streaming context (native.CTX_STREAMING): one stream of its own (copy, zero
+        fills and decode in order), its own pinned payload pool and device arena, so nothing a slot
+        waits for belongs to another slot;
       * range i is walked on the host (thrift headers, CRC, decompression) straight into slot
-        i % slots's pinned block, then its batch copies it to HBM on the slot's copy stream and
-        decodes it on the slot's compute stream (pqh_batch_run_staged): while range i decodes and
-        ranges i+1.. copy, the host walks the next one;
+        i % slots's pinned block, then its batch copies it to HBM on the slot's stream and
+        decodes it behind the copy on the same stream (pqh_batch_run_staged): while range i decodes
+        and ranges i+1.. copy, the host walks the next one;
       * a range's batch is handed to the caller once decoded and stays valid until the next
-        iteration, which releases its slot (pinned block back to the slot's pool, device memory back
-        to the pool) and walks range i + slots into it.
+        iteration, which releases its slot (pinned block back to the slot's pool, the slot's arena
+        reset) so that range i + slots can be walked into it -- by the caller between hand-outs
+        (threaded=False) or, by default, by a walker and a submitter thread beside the caller.
 
     Pinned host memory is bounded by `slots` blocks (pinned_bytes()); device memory by the
     batches of `slots` ranges.  Iterating yields (rg_begin, rg_end, native.Batch, host batch)."""
 
-    def __init__(self, file, columns, rg_begin=0, rg_end=None, per_range=4, slots=3, device=0, validate_crc=False):
+    def __init__(self, file, columns, rg_begin=0, rg_end=None, per_range=4, slots=3, device=0, validate_crc=False,
+                 threaded=True):
         self.file = file
         self.columns = list(columns)
         rg_end = file.num_row_groups if rg_end is None else rg_end
         self.ranges = [(a, min(a + per_range, rg_end)) for a in range(rg_begin, rg_end, per_range)]
         self.validate_crc = validate_crc
+        self.threaded = threaded
         self.ctxs = [native.Context(device, streaming=True) for _ in range(max(1, slots))]
         self.walk_s = 0.0
+        self.times = {"walk": 0.0, "create": 0.0, "run": 0.0, "sync": 0.0, "close": 0.0}
 
     def pinned_bytes(self):
         return sum(c.pinned_bytes() for c in self.ctxs)
 
-    def _submit(self, i):
-        import time
-
+    def _walk(self, i):
         a, b = self.ranges[i]
-        ctx = self.ctxs[i % len(self.ctxs)]
         t0 = time.perf_counter()
-        hb = self.file.load(a, b, self.columns, self.validate_crc, ctx=ctx)  # host walk into the slot's block
-        self.walk_s += time.perf_counter() - t0
-        batch = native.Batch.staged(ctx, hb)
-        batch.run_staged()  # H2D on the slot's copy stream, then the decode (asynchronous)
+        hb = self.file.load(a, b, self.columns, self.validate_crc, ctx=self.ctxs[i % len(self.ctxs)])
+        dt = time.perf_counter() - t0
+        self.walk_s += dt
+        self.times["walk"] += dt
+        return hb
+
+    def _stage(self, i, hb):
+        t0 = time.perf_counter()
+        try:
+            batch = native.Batch.staged(self.ctxs[i % len(self.ctxs)], hb)
+        except BaseException:
+            hb.close()
+            raise
+        t1 = time.perf_counter()
+        try:
+            batch.run_staged()  # H2D on the slot's stream, then the decode (asynchronous)
+        except BaseException:
+            batch.close()
+            hb.close()
+            raise
+        self.times["create"] += t1 - t0
+        self.times["run"] += time.perf_counter() - t1
         return (i, batch, hb)
 
-    def __iter__(self):
-        from collections import deque
+    def _submit(self, i):
+        return self._stage(i, self._walk(i))
 
+    def __iter__(self):
+        return self._threaded() if self.threaded else self._inline()
+
+    def _try_submit(self, i):
+        try:
+            return self._submit(i)
+        except Exception as e:  # raised when the caller reaches range i (ranges fail in order)
+            return e
+
+    def _inline(self):
+        """Walk + submit on the caller's thread, between the hand-outs."""
         inflight = deque()
         nxt = 0
         while nxt < len(self.ranges) and len(inflight) < len(self.ctxs):
-            inflight.append(self._submit(nxt))
+            inflight.append(self._try_submit(nxt))
             nxt += 1
         try:
             while inflight:
-                i, batch, hb = inflight.popleft()
+                if isinstance(inflight[0], Exception):
+                    raise inflight.popleft()
+                i, batch, hb = inflight[0]  # stays listed (closed by the finally) until released
+                t0 = time.perf_counter()
                 batch.sync()  # the slot's own streams only
+                self.times["sync"] += time.perf_counter() - t0
                 a, b = self.ranges[i]
                 yield a, b, batch, hb
+                t0 = time.perf_counter()
+                inflight.popleft()
                 batch.close()
                 hb.close()
+                self.times["close"] += time.perf_counter() - t0
                 if nxt < len(self.ranges):
-                    inflight.append(self._submit(nxt))
+                    inflight.append(self._try_submit(nxt))
                     nxt += 1
         finally:
-            for _, batch, hb in inflight:
+            for item in inflight:
+                if isinstance(item, tuple):
+                    item[1].close()
+                    item[2].close()
+
+    def _threaded(self):
+        """A two-stage producer beside the caller: a walker thread walks range i into its slot's
+        pinned block as soon as the slot is released, a submitter thread creates the range's batch
+        and starts its H2D + decode, and the caller waits only for decoded ranges (the native calls
+        drop the GIL, so the three overlap: walk of range i+2, batch creation of range i+1, the copies
+        and decodes in flight).  A slot is used by one thread at a time: the walker, then the
+        submitter, then the caller until it releases the slot."""
+        n, k = len(self.ranges), len(self.ctxs)
+        staged, ready = queue.Queue(), queue.Queue()
+        free = [threading.Semaphore(1) for _ in range(k)]
+        stop = threading.Event()
+        done = object()
+
+        def walker():
+            for i in range(n):
+                free[i % k].acquire()
+                if stop.is_set():
+                    break
+                try:
+                    staged.put((i, self._walk(i)))
+                except BaseException as e:  # handed on to the caller, which raises it
+                    staged.put(e)
+                    break
+            staged.put(done)
+
+        def submitter():
+            while True:
+                item = staged.get()
+                if item is done:
+                    return
+                if isinstance(item, BaseException) or stop.is_set():
+                    if isinstance(item, tuple):
+                        item[1].close()
+                    else:
+                        ready.put(item)
+                    continue
+                try:
+                    ready.put(self._stage(*item))
+                except BaseException as e:
+                    ready.put(e)
+
+        threads = [threading.Thread(target=walker, name="RowGroupStream.walk", daemon=True),
+                   threading.Thread(target=submitter, name="RowGroupStream.submit", daemon=True)]
+        for th in threads:
+            th.start()
+        held = None
+        try:
+            for _ in range(n):
+                item = ready.get()
+                if isinstance(item, BaseException):
+                    raise item
+                held = item
+                i, batch, hb = item
+                t0 = time.perf_counter()
+                batch.sync()  # the slot's own streams only
+                self.times["sync"] += time.perf_counter() - t0
+                a, b = self.ranges[i]
+                yield a, b, batch, hb
+                t0 = time.perf_counter()
+                held = None
                 batch.close()
                 hb.close()
+                self.times["close"] += time.perf_counter() - t0
+                free[i % k].release()
+        finally:
+            stop.set()
+            for sem in free:
+                sem.release()
+            for th in threads:
+                th.join()
+            if held is not None:
+                held[1].close()
+                held[2].close()
+            while not ready.empty():
+                item = ready.get_nowait()
+                if isinstance(item, tuple):
+                    item[1].close()
+                    item[2].close()
 
     def close(self):
         for c in self.ctxs:
