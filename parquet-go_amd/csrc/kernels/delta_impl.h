@@ -1907,11 +1907,17 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
     const int64_t vcap = lens ? (before_values ? 0 : int64_t(S.nn)) : int64_t(kmax) << lbs;  // values to emit
     const int64_t img_len = P.image_len;
     int32_t est = 0;  // 0: the first tile measures block 0
+    int64_t a0 = -1;  // the stage's base
     for (;;) {
       __syncthreads();  // the previous tile's readers of T are done
-      const int64_t a0 = h - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(h)) & 15);
-      stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, T.kStageBytes / 16, img_len - a0);
-      __syncthreads();
+      // restage from the next header unless the stage still holds a whole tile's worth of blocks
+      // after it (narrow streams -- DELTA_LENGTH lengths of ~100 bytes per block -- fit 2-6 tiles in
+      // one stage: one HBM round trip instead of one per tile)
+      if (a0 < 0 || h - a0 + int64_t(est) * kTileBlocks + 512 > T.kStageBytes - 64) {
+        a0 = h - int64_t((reinterpret_cast<uintptr_t>(img) + uintptr_t(h)) & 15);
+        stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, T.kStageBytes / 16, img_len - a0);
+        __syncthreads();
+      }
       if (tid < 64) {
         int n;
         int32_t nxt;
