@@ -1003,7 +1003,7 @@ def main():
     # while the previous range decodes on the compute stream.  Host decompression excluded.
     # device codecs: the ranges hold the pages of SNAPPY / GZIP chunks still
     # compressed, so H2D moves compressed bytes and every decode starts with k_snappy / k_gzip.
-    def e2e_pass(device_snappy):
+    def e2e_pass(device_snappy, ranges=None):
         # at most 16 staged batches (contiguous row-group ranges): pipeline depth 16, copies of
         # >= 1/16 of the payload each
         nrg = rg1 - rg0
@@ -1011,7 +1011,7 @@ def main():
         # overlaps the previous range's codec + decode, and every range pays the per-page latency
         # of k_snap_stitch / k_gzip once (a launch takes its slowest page's sequential walk); r04,
         # C5z: 72.4 GB/s with 4 ranges vs 59.6 with 1 (host-decompressed e2e 56-60)
-        groups = min(nrg, max(1, args.e2e_dev_ranges)) if device_snappy else min(nrg, 16)
+        groups = min(nrg, ranges or (max(1, args.e2e_dev_ranges) if device_snappy else 16))
         cuts = [nrg * g // groups for g in range(groups + 1)]
 
         def load_all():
@@ -1085,6 +1085,17 @@ def main():
         dev_codecs = {c.codec for c in probe.codec_pages()} - {0}
         probe.close()
         dev_kernel = "k_gzip" if 2 in dev_codecs else "k_snappy"
+        host = f.load(rg0, rg0 + 1, list(range(ncols)))
+        compressed = host.decompress_seconds() > 0  # the host walk decompressed pages of this file
+        host.close()
+        if compressed and not dev_codecs:
+            # every page compresses to >= PQH_DEVICE_CODEC_MAX_RATIO of its image (C5's random letters):
+            # the device-codec load keeps them all on the host route, so its end-to-end pass is the
+            # host-decompressed one -- measured, not assumed
+            e2e_dev = e2e_pass(True, ranges=16)  # (the host path's ranges: nothing for a codec to overlap)
+            e2e_dev["device_codec"] = {"pages_on_device": 0,
+                                       "note": "no page compresses below PQH_DEVICE_CODEC_MAX_RATIO (0.95) of its image: "
+                                               "all stay on the host-decompressed route (no PCIe bytes to save)"}
         if dev_codecs:
             e2e_dev = e2e_pass(True)
             # the codec kernel alone: HBM-resident batch of the rank's row groups, profiled runs

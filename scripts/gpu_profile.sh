@@ -20,6 +20,7 @@ for w in ${WORKLOADS:-c2 c4 mixed}; do
   case $w in
     c2) A="--steps 10 --warmup 2 $SKIP" ;;
     mixed) A="--workload mixed --steps 5 --warmup 1 $SKIP" ;;
+    c5z_gzip) A="--workload c5z --codec gzip --steps 10 --warmup 2 $SKIP" ;;
     *) A="--workload $w --steps 10 --warmup 2 $SKIP" ;;
   esac
   run prof_${w}_trace 600 "$A" --kernel-trace --stats -T
