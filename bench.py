@@ -1086,7 +1086,7 @@ def main():
         probe.close()
         dev_kernel = "k_gzip" if 2 in dev_codecs else "k_snappy"
         host = f.load(rg0, rg0 + 1, list(range(ncols)))
-        compressed = host.decompress_seconds() > 0  # the host walk decompressed pages of this file
+        compressed = host.decompress_seconds > 0  # the host walk decompressed pages of this file
         host.close()
         if compressed and not dev_codecs:
             # every page compresses to >= PQH_DEVICE_CODEC_MAX_RATIO of its image (C5's random letters):
