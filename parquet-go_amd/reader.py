@@ -141,6 +141,22 @@ class ColumnData:
         return [d[self.offsets[i]:self.offsets[i + 1]] for i in range(len(self.offsets) - 1)]
 
 
+def batch_columns(ctx, file, batch, hb, columns):
+    """ColumnData of every chunk of a synchronised batch, in (row group, column) order."""
+    cols = file.columns()
+    res = batch.page_results(hb.num_pages)
+    pages = hb.pages()
+    out = []
+    for i, ch in enumerate(hb.chunks()):
+        path, pt, tl, md, mr = cols[columns[i % len(columns)]]
+        span = range(ch.first_page, ch.first_page + ch.num_pages)
+        pr = [res[p] for p in span]
+        o = batch.chunk_out(i)  # (its status orders walker, load and readValues errors as the reference)
+        info = [(pages[p].page_type, pages[p].num_values, res[p]) for p in span]
+        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None, info))
+    return out
+
+
 def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, return_batch=False, staged_runs=0,
                   device_snappy=False, device_gzip=False):
     """Walk (host) and decode (GPU) the chunks of `columns` in row groups [rg_begin, rg_end).
@@ -159,18 +175,7 @@ def decode_chunks(ctx, file, rg_begin, rg_end, columns, validate_crc=False, retu
         batch = native.Batch.from_host(ctx, hb)
         batch.run()
     batch.sync()
-    cols = file.columns()
-    res = batch.page_results(hb.num_pages)
-    pages = hb.pages()
-    out = []
-    chunks = hb.chunks()
-    for i, ch in enumerate(chunks):
-        path, pt, tl, md, mr = cols[columns[i % len(columns)]]
-        span = range(ch.first_page, ch.first_page + ch.num_pages)
-        pr = [res[p] for p in span]
-        o = batch.chunk_out(i)  # (its status orders walker, load and readValues errors as the reference)
-        info = [(pages[p].page_type, pages[p].num_values, res[p]) for p in span]
-        out.append(ColumnData(path, (pt, tl, md, mr), o, pr, ctx, batch.nesting(i) if mr > 0 else None, info))
+    out = batch_columns(ctx, file, batch, hb, columns)
     if return_batch:
         return out, batch, hb
     batch.close()
@@ -203,12 +208,13 @@ class RowGroupStream:
     batches of `slots` ranges.  Iterating yields (rg_begin, rg_end, native.Batch, host batch)."""
 
     def __init__(self, file, columns, rg_begin=0, rg_end=None, per_range=4, slots=3, device=0, validate_crc=False,
-                 threaded=True):
+                 threaded=True, device_snappy=False, device_gzip=False):
         self.file = file
         self.columns = list(columns)
         rg_end = file.num_row_groups if rg_end is None else rg_end
         self.ranges = [(a, min(a + per_range, rg_end)) for a in range(rg_begin, rg_end, per_range)]
         self.validate_crc = validate_crc
+        self.load_kw = {"device_snappy": device_snappy, "device_gzip": device_gzip}
         self.threaded = threaded
         self.ctxs = [native.Context(device, streaming=True) for _ in range(max(1, slots))]
         self.walk_s = 0.0
@@ -217,10 +223,14 @@ class RowGroupStream:
     def pinned_bytes(self):
         return sum(c.pinned_bytes() for c in self.ctxs)
 
+    def column_data(self, batch, hb):
+        """The ColumnData of a handed-out range (valid until the next iteration)."""
+        return batch_columns(batch.ctx, self.file, batch, hb, self.columns)
+
     def _walk(self, i):
         a, b = self.ranges[i]
         t0 = time.perf_counter()
-        hb = self.file.load(a, b, self.columns, self.validate_crc, ctx=self.ctxs[i % len(self.ctxs)])
+        hb = self.file.load(a, b, self.columns, self.validate_crc, ctx=self.ctxs[i % len(self.ctxs)], **self.load_kw)
         dt = time.perf_counter() - t0
         self.walk_s += dt
         self.times["walk"] += dt

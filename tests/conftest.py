@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+# every streaming context of the GPU suite verifies its arena's guard gaps at each batch sync (a
+# kernel writing past one of its buffers fails the test with the buffer's index instead of
+# corrupting a neighbour silently); read once, when the library allocates its first arena buffer
+os.environ.setdefault("PQH_ARENA_CHECK", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

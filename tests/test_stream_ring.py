@@ -83,7 +83,7 @@ class FakeFile:
     def __init__(self, book, nrg, fail_at=None):
         self.book, self.num_row_groups, self.fail_at = book, nrg, fail_at
 
-    def load(self, a, b, columns, validate_crc=False, ctx=None):
+    def load(self, a, b, columns, validate_crc=False, ctx=None, device_snappy=False, device_gzip=False):
         if self.fail_at is not None and a == self.fail_at:
             raise native.PqhError(2, "walk failed")
         time.sleep(0.002)
