@@ -186,8 +186,10 @@ def chains(nseeds):
 def delta(nseeds):
     """DELTA_BINARY_PACKED streams of every block geometry the reference accepts (14 geometries,
     int32 / int64, random sizes and value regimes, with the test suite's mutations: counts above /
-    below the stream's, truncations, flipped bytes) over many seeds, alternately in page mode and
-    tile mode: every case vs the oracle."""
+    below the stream's, truncations, flipped bytes) over many seeds, in turn in tile mode, page mode
+    (k_delta_fused) and split page mode (k_delta_split), with one stream of 8K-60K values per size
+    set so that pages span several fused tiles (the stage kept across tiles for narrow blocks):
+    every case vs the oracle."""
     import numpy as np
 
     import __graft_entry__ as ge
@@ -199,12 +201,15 @@ def delta(nseeds):
     total = 0
     for seed in range(4000, 4000 + nseeds):
         rng = np.random.default_rng(seed)
-        os.environ["PQH_DELTA_PAGE_MODE"] = "1" if seed % 2 else "0"
-        sizes = sorted({int(x) for x in rng.integers(1, 5000, 4)} | {int(rng.integers(1, 130))})
+        mode = ("tile", "page", "split")[seed % 3]
+        os.environ["PQH_DELTA_PAGE_MODE"] = "0" if mode == "tile" else "1"
+        os.environ["PQH_DELTA_SPLIT"] = "1" if mode == "split" else "0"
+        sizes = sorted({int(x) for x in rng.integers(1, 5000, 4)} | {int(rng.integers(1, 130))}
+                       | {int(rng.integers(8000, 60000))})
         cases = T._delta_cases(rng, sizes, ["const", "mono", "small", "full", "mixed"], mutate=True)
         compared, errors = T._run_cases(pq, ctx, cases)
         total += compared
-        print(f"seed {seed} ({'page' if seed % 2 else 'tile'} mode): {compared} streams, {errors} errors", flush=True)
+        print(f"seed {seed} ({mode} mode): {compared} streams, {errors} errors", flush=True)
     print(f"ok: {total} DELTA streams equal to the oracle", flush=True)
 
 
