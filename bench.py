@@ -319,7 +319,11 @@ def mixed_strong_record(args, ctx, native, pkg, datasets, world, rank, local, di
         blocks = pkg.shard.gather_blocks(rg0, rg1, my_rows, wr, device=dev)
         pkg.shard.check_cover(blocks, nrg, f.num_rows)
         t = el / steps
-        return {"workload": desc, "scaling": "strong", "n_gpus": world, "rows_total": f.num_rows,
+        e2e = None
+        if not args.no_e2e:
+            e2e = mixed_stream_e2e(ctx, native, pkg, f, ncols, rg_begin=rg0, rg_end=rg1, barrier_sync=barrier_sync,
+                                   device=dev)
+        rec = {"workload": desc, "scaling": "strong", "n_gpus": world, "rows_total": f.num_rows,
                 "row_groups": nrg, "file_bytes": os.path.getsize(path), "steps": steps,
                 "ms_per_step": round(t * 1e3, 4), "value": round(total / t / 1e9, 2),
                 "unit": "GB/s (decoded output, whole node)",
@@ -332,6 +336,9 @@ def mixed_strong_record(args, ctx, native, pkg, datasets, world, rank, local, di
                 "verified": f"rank 0: row groups {checked}: {len(checked) * ncols} chunks bit-exact vs the oracle "
                             "(every rank checks its first and last row group)",
                 "generate_s": round(gen_s, 2)}
+        if e2e is not None:
+            rec["e2e"] = e2e
+        return rec
     finally:
         f.close()
         dist.barrier()
@@ -339,16 +346,21 @@ def mixed_strong_record(args, ctx, native, pkg, datasets, world, rank, local, di
             os.unlink(path)
 
 
-def mixed_stream_e2e(ctx, native, pkg, f, ncols, per_range=4, slots=4, passes=2):
+def mixed_stream_e2e(ctx, native, pkg, f, ncols, per_range=4, slots=4, passes=2, rg_begin=0, rg_end=None,
+                     barrier_sync=None, device=None):
     """End-to-end over the whole 1B-row file through a bounded ring (reader.RowGroupStream): ranges
     of `per_range` row groups walked on the host (thrift headers, page images) straight into pinned
     slot blocks, copied to HBM and decoded in order on each slot's one stream, `slots`
     ranges in flight, so the host walk of the next range overlaps the H2D and decode of the ones
     before it.  Every range's chunks are status-checked as the ring hands them out.  The first pass
     pins the slots' blocks; the second (reported) reuses them.  Host decompression: none (the file
-    is UNCOMPRESSED; the walk copies the page images)."""
+    is UNCOMPRESSED; the walk copies the page images).  N > 1: every rank streams its own block
+    [rg_begin, rg_end) through its own ring (its own host threads, pinned blocks and PCIe link),
+    each pass between barriers; whole-node payload GB/s = the payload of all ranks / the slowest
+    rank's pass."""
     ceiling = pinned_h2d_rate(ctx, native)
-    st = pkg.reader.RowGroupStream(f, list(range(ncols)), per_range=per_range, slots=slots)
+    st = pkg.reader.RowGroupStream(f, list(range(ncols)), rg_begin=rg_begin, rg_end=rg_end, per_range=per_range,
+                                   slots=slots)
     try:
         out = None
         for k in range(passes):
@@ -357,6 +369,8 @@ def mixed_stream_e2e(ctx, native, pkg, f, ncols, per_range=4, slots=4, passes=2)
                 st.times[key] = 0.0
             payload = written = 0
             nr = 0
+            if barrier_sync:
+                barrier_sync()
             t0 = time.perf_counter()
             for a, b, batch, hb in st:
                 check_statuses(batch, hb.num_chunks, native, f"stream e2e: row groups [{a}, {b})")
@@ -364,19 +378,23 @@ def mixed_stream_e2e(ctx, native, pkg, f, ncols, per_range=4, slots=4, passes=2)
                 written += batch.traffic()[1]
                 nr += 1
             el = time.perf_counter() - t0
+            el_max, payload_all = pkg.shard.reduce_step(el, payload, device=device)
+            _, written_all = pkg.shard.reduce_step(el, written, device=device)
             out = {"mode": "streaming ring (reader.RowGroupStream): a walker thread walks each range into its slot's "
                            "pinned block, a submitter thread creates its batch (slot arena) and starts the H2D on the "
                            "slot's stream with the decode behind it, the caller waits for decoded "
                            "ranges; %d slots of %d row groups; the host walk is inside the timed pass; host "
                            "decompression: none (UNCOMPRESSED file)"
                            % (slots, per_range),
-                   "pass": k, "ranges": nr, "seconds": round(el, 3), "payload_bytes": payload,
-                   "payload_h2d_gbps": round(payload / el / 1e9, 2),
-                   "decoded_gbps": round(written / el / 1e9, 2),
+                   "pass": k, "ranges": nr, "seconds": round(el_max, 3), "payload_bytes": int(payload_all),
+                   "payload_h2d_gbps": round(payload_all / el_max / 1e9, 2),
+                   "decoded_gbps": round(written_all / el_max / 1e9, 2),
+                   "rank0_payload_h2d_gbps": round(payload / el / 1e9, 2),
                    "host_walk_s": round(st.walk_s, 3),
                    "host_seconds": {k: round(v, 3) for k, v in st.times.items()},
                    "pinned_h2d_ceiling_gbps": ceiling,
                    "payload_frac_of_pinned_ceiling": round(payload / el / 1e9 / ceiling, 3) if ceiling else None,
+                   "frac_note": "rank 0's payload rate / rank 0's pinned-copy ceiling (one GPU's PCIe link)",
                    "pinned_bytes": st.pinned_bytes(),
                    "pinned_bound_note": f"{slots} pinned blocks (one per slot, reused range after range)"}
         return out
@@ -848,6 +866,9 @@ def main():
     ap.add_argument("--next-row-rows", type=int, default=100_000)
     ap.add_argument("--c3-rows", type=int, default=0, help=argparse.SUPPRESS)  # tests: a smaller C3 file
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    # rehearsal of the N > 1 path on a box with fewer GPUs than ranks: ranks share the visible GPUs
+    # (LOCAL_RANK modulo their count) and reduce over gloo (RCCL refuses two ranks on one GPU)
+    ap.add_argument("--share-gpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -864,9 +885,12 @@ def main():
     except Exception:
         torch = None
     if world > 1:
+        if args.share_gpu:
+            local %= max(1, torch.cuda.device_count())
+            os.environ["LOCAL_RANK"] = str(local)
         if not args.dry_run:
             torch.cuda.set_device(local)
-        dist.init_process_group("gloo" if args.dry_run else "nccl")
+        dist.init_process_group("gloo" if args.dry_run or args.share_gpu else "nccl")
 
     pkg = package()
     from parquet_go_amd import datasets, native
