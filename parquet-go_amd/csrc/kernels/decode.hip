@@ -1686,6 +1686,24 @@ hipError_t launch_delta_init(const DevBatch& b, const int32_t* delta_pages, int3
 hipError_t launch_delta_fused(const DevBatch& b, const Tile* streams, int32_t n, int32_t n_lens, hipStream_t s) {
   if (n - n_lens > 0) hipLaunchKernelGGL(k_delta_fused, dim3(n - n_lens), dim3(256), 0, s, b, streams);
   if (n_lens > 0) hipLaunchKernelGGL(k_delta_fused_lens, dim3(n_lens), dim3(256), 0, s, b, streams + (n - n_lens));
+#ifdef PQH_FUSED_PROF
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
+      hipStreamSynchronize(s) == hipSuccess) {
+    unsigned long long h[2][8], z[2][8] = {};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fprof), sizeof(h)) == hipSuccess) {
+      for (int v = 0; v < 2; v++) {
+        if (!h[v][6]) continue;
+        const double wg = double(h[v][6]), tl = double(h[v][5] ? h[v][5] : 1);
+        fprintf(stderr, "[fused_prof %s] wgs %.0f tiles/wg %.2f | per wg us: body %.2f init %.2f | per tile us: "
+                "stage %.2f chase %.2f tables %.2f expand %.2f\n", v ? "lens" : "values", wg, tl / wg,
+                h[v][7] / wg / 100.0, h[v][0] / wg / 100.0, h[v][1] / tl / 100.0, h[v][2] / tl / 100.0,
+                h[v][3] / tl / 100.0, h[v][4] / tl / 100.0);
+      }
+      hipMemcpyToSymbol(HIP_SYMBOL(g_fprof), z, sizeof(z));
+    }
+  }
+#endif
   return hipGetLastError();
 }
 

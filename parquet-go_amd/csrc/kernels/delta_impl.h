@@ -1805,25 +1805,22 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
   // A chain cut short by a lane that synchronised on a false header (low-entropy packed data reads
   // as plausible headers) ends on a true header: continue from it serially inside the same window
   // (one LDS header parse per block) instead of restaging the window for the next few blocks.
-  while (!stop && n < nmax) {
-    int32_t d;
-    if (!lds_block(data, nxt, eloc, plim, dlim, is64, mbc, gbytes, d)) {
-      int32_t dat;
-      uint64_t md, wd;
-      const int32_t de = nxt < plim ? lds_hdr(data, nxt, is64, mbc, gbytes, dat, md, wd) : 0;
-      stop = nxt + 24 > eloc || (nxt < plim && (de < 0 || de > eloc));
+  while (!stop && n < nmax) {  // (one header parse per block: lds_block's test on the same parse)
+    int32_t dat = 0, dend = -1;
+    uint64_t md = 0, wd = 0;
+    const bool in_reach = nxt < plim && nxt + 24 <= eloc;
+    if (in_reach) dend = lds_hdr(data, nxt, is64, mbc, gbytes, dat, md, wd);
+    if (!in_reach || dend < 0 || dend > dlim || dend > eloc) {
+      stop = nxt + 24 > eloc || (nxt < plim && (dend < 0 || dend > eloc));
       break;
     }
-    int32_t dat;
-    uint64_t md, wd;
-    lds_hdr(data, nxt, is64, mbc, gbytes, dat, md, wd);
     if (lane == 0) {
       blkbit[n] = dat * 8;
       blkw[n] = wd;
       mdt[n] = md;
     }
     n++;
-    nxt = d;
+    nxt = dend;
   }
   n_out = n;
   next_out = nxt;
@@ -1839,8 +1836,23 @@ __device__ void lds_chase(const uint32_t* data, int32_t loc0, int32_t eloc, int3
 // records of the remaining blocks) and k_delta_page decodes the rest.
 // kLens: the DELTA_LENGTH streams' launch (tile byte sums in the row loop); the other streams run
 // the instantiation without them, which keeps its register budget (occupancy) unchanged.
+#ifdef PQH_FUSED_PROF
+// (-DPQH_FUSED_PROF experiments) per phase wall-clock ticks summed over workgroups:
+// [0] init, [1] stage, [2] chase, [3] tables, [4] expand, [5] tiles, [6] workgroups, [7] whole body
+__device__ unsigned long long g_fprof[2][8];
+#define FPROF_T(v) const uint64_t v = wall_clock64()
+#define FPROF_ADD(k, x) prof[k] += (x)
+#else
+#define FPROF_T(v)
+#define FPROF_ADD(k, x)
+#endif
+
 template <bool kLens>
 __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams) {
+#ifdef PQH_FUSED_PROF
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 1, 0};
+  const uint64_t t_begin = wall_clock64();
+#endif
   __shared__ PageTileLdsT<kLens ? kPageStage : kFusedStage> T;
   __shared__ int32_t s_blkbit[kTileBlocks];
   __shared__ uint64_t s_blkw[kTileBlocks];
@@ -1891,6 +1903,10 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
   }
   __syncthreads();
   const int kmax = s_geo[0];
+#ifdef PQH_FUSED_PROF
+  uint64_t t_ph = wall_clock64();
+  FPROF_ADD(0, t_ph - t_begin);
+#endif
   // DELTA_LENGTH: tile byte sums + first negative length of the head (k_delta_init zeroed the sums)
   const bool sums = kLens && P.kind == K_DLBA && kmax > 0;
   LenSums ls{b.basums + P.batile_base, sums ? (S.val_limit < s_geo[4] ? S.val_limit : s_geo[4]) : 0, INT64_MAX};
@@ -1918,6 +1934,9 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
         stage_copy(reinterpret_cast<uint4*>(T.data), img + a0, T.kStageBytes / 16, img_len - a0);
         __syncthreads();
       }
+#ifdef PQH_FUSED_PROF
+      { FPROF_T(t); FPROF_ADD(1, t - t_ph); t_ph = t; FPROF_ADD(5, 1); }
+#endif
       if (tid < 64) {
         int n;
         int32_t nxt;
@@ -1933,6 +1952,9 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
       }
       __syncthreads();
       const int n = s_n;
+#ifdef PQH_FUSED_PROF
+      { FPROF_T(t); FPROF_ADD(2, t - t_ph); t_ph = t; }
+#endif
       if (n == 0) break;
       for (int i = tid; i < n * 8; i += kBlock) {  // miniblock tables
         const int blk = i >> 3, m = i & 7;
@@ -1943,6 +1965,9 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
         T.mbw[blk][m] = uint8_t(wm);
       }
       __syncthreads();
+#ifdef PQH_FUSED_PROF
+      { FPROF_T(t); FPROF_ADD(3, t - t_ph); t_ph = t; }
+#endif
       const int64_t v0 = int64_t(r) << lbs;
       int64_t v1 = int64_t(r + n) << lbs;
       if (v1 > vcap) v1 = vcap;
@@ -1954,6 +1979,10 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
           carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
         }
       }
+#ifdef PQH_FUSED_PROF
+      __syncthreads();
+      { FPROF_T(t); FPROF_ADD(4, t - t_ph); t_ph = t; }
+#endif
       est = int32_t((s_h - h) / n);  // mean block span so far: the next tile's lane segments
       r += n;
       h = s_h;
@@ -1969,6 +1998,11 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
     b.dstates[p].head_carry = carry;
     b.dstates[p].head_neg = int64_t(s_neg);  // counts only if k_delta_walk accepts the head
   }
+#ifdef PQH_FUSED_PROF
+  prof[7] = wall_clock64() - t_begin;
+  if (tid == 0)
+    for (int k = 0; k < 8; k++) atomicAdd(&g_fprof[kLens ? 1 : 0][k], (unsigned long long)prof[k]);
+#endif
 }
 
 __global__ __launch_bounds__(256) PQH_FUSED_ATTR void k_delta_fused(DevBatch b, const Tile* streams) {
