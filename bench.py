@@ -1109,9 +1109,18 @@ def main():
         dev_codecs = {c.codec for c in probe.codec_pages()} - {0}
         probe.close()
         dev_kernel = "k_gzip" if 2 in dev_codecs else "k_snappy"
-        host = f.load(rg0, rg0 + 1, list(range(ncols)))
-        compressed = host.decompress_seconds > 0  # the host walk decompressed pages of this file
-        host.close()
+        # compressed at all?  the same probe with every page eligible for the device codecs
+        keep = os.environ.get("PQH_DEVICE_CODEC_MAX_RATIO")
+        os.environ["PQH_DEVICE_CODEC_MAX_RATIO"] = "0"
+        try:
+            every = f.load(rg0, rg0 + 1, list(range(ncols)), device_snappy=True, device_gzip=True)
+            compressed = len(every.codec_pages()) > 0
+            every.close()
+        finally:
+            if keep is None:
+                del os.environ["PQH_DEVICE_CODEC_MAX_RATIO"]
+            else:
+                os.environ["PQH_DEVICE_CODEC_MAX_RATIO"] = keep
         if compressed and not dev_codecs:
             # every page compresses to >= PQH_DEVICE_CODEC_MAX_RATIO of its image (C5's random letters):
             # the device-codec load keeps them all on the host route, so its end-to-end pass is the
