@@ -1,6 +1,6 @@
 """The end-to-end streaming ring (reader.RowGroupStream): a file several times
 larger than the ring's pinned staging, read range by range -- host walk into a slot's pinned block,
-H2D on the slot's copy stream, decode on its compute stream, `slots` ranges in flight -- and every
+H2D and decode in order on the slot's one stream, `slots` ranges in flight -- and every
 chunk compared with the seeded input it was written from (datasets.mixed: north_star's mixed file
 at a smaller size), two row groups with the oracle bit for bit.  The pinned memory stays bounded
 by the slots, pass after pass."""
