@@ -824,6 +824,22 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
 // Cooperative copy of n bytes by the workgroup: 16-byte aligned stores, each fed by two aligned
 // 16-byte loads of the (arbitrarily aligned) source funnel-shifted into place.  Loads stay inside
 // the source's 16-byte-aligned cover (the payload keeps PQH_PAYLOAD_PAD bytes after the last page).
+#ifndef PQH_BA_COPY_FIRST
+#define PQH_BA_COPY_FIRST 1
+#endif
+#ifndef PQH_BA_COPY_INFLIGHT
+#define PQH_BA_COPY_INFLIGHT 8
+#endif
+#ifndef PQH_BA_COPY_NT
+#define PQH_BA_COPY_NT 0
+#endif
+typedef unsigned int v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
+template <class T>
+__device__ __forceinline__ uint4 nt_load16(const PQH_G T* p) {
+  const v4u_a1 v = __builtin_nontemporal_load(reinterpret_cast<const PQH_G v4u_a1*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <int kIn = 4, int kNt = 0>  // 16-byte loads in flight per thread; 1: streaming stores, 2: + loads
 __device__ __forceinline__ void block_copy(PQH_G uint8_t* dst, const PQH_G uint8_t* src, int64_t n) {
   // destination 16-byte aligned after the head; the source side uses unaligned 16-byte loads
   const int64_t head = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < n
@@ -834,6 +850,45 @@ __device__ __forceinline__ void block_copy(PQH_G uint8_t* dst, const PQH_G uint8
   const PQH_G uint4_u* sp = reinterpret_cast<const PQH_G uint4_u*>(src + head);
   PQH_G uint4* d = reinterpret_cast<PQH_G uint4*>(dst + head);
   int64_t u = threadIdx.x;
+  if constexpr (kIn == 8) {
+    for (; u + 7 * kBlock < units; u += 8 * kBlock) {
+      uint4 x0, x1, x2, x3, x4, x5, x6, x7;
+      if constexpr (kNt == 2) {
+        x0 = nt_load16(sp + u);
+        x1 = nt_load16(sp + u + kBlock);
+        x2 = nt_load16(sp + u + 2 * kBlock);
+        x3 = nt_load16(sp + u + 3 * kBlock);
+        x4 = nt_load16(sp + u + 4 * kBlock);
+        x5 = nt_load16(sp + u + 5 * kBlock);
+        x6 = nt_load16(sp + u + 6 * kBlock);
+        x7 = nt_load16(sp + u + 7 * kBlock);
+      } else {
+        x0 = sp[u], x1 = sp[u + kBlock], x2 = sp[u + 2 * kBlock], x3 = sp[u + 3 * kBlock];
+        x4 = sp[u + 4 * kBlock], x5 = sp[u + 5 * kBlock], x6 = sp[u + 6 * kBlock], x7 = sp[u + 7 * kBlock];
+      }
+      if constexpr (kNt != 0) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        PQH_G v4u* dv = reinterpret_cast<PQH_G v4u*>(d);
+        __builtin_nontemporal_store(v4u{x0.x, x0.y, x0.z, x0.w}, dv + u);
+        __builtin_nontemporal_store(v4u{x1.x, x1.y, x1.z, x1.w}, dv + u + kBlock);
+        __builtin_nontemporal_store(v4u{x2.x, x2.y, x2.z, x2.w}, dv + u + 2 * kBlock);
+        __builtin_nontemporal_store(v4u{x3.x, x3.y, x3.z, x3.w}, dv + u + 3 * kBlock);
+        __builtin_nontemporal_store(v4u{x4.x, x4.y, x4.z, x4.w}, dv + u + 4 * kBlock);
+        __builtin_nontemporal_store(v4u{x5.x, x5.y, x5.z, x5.w}, dv + u + 5 * kBlock);
+        __builtin_nontemporal_store(v4u{x6.x, x6.y, x6.z, x6.w}, dv + u + 6 * kBlock);
+        __builtin_nontemporal_store(v4u{x7.x, x7.y, x7.z, x7.w}, dv + u + 7 * kBlock);
+        continue;
+      }
+      d[u] = x0;
+      d[u + kBlock] = x1;
+      d[u + 2 * kBlock] = x2;
+      d[u + 3 * kBlock] = x3;
+      d[u + 4 * kBlock] = x4;
+      d[u + 5 * kBlock] = x5;
+      d[u + 6 * kBlock] = x6;
+      d[u + 7 * kBlock] = x7;
+    }
+  }
   for (; u + 3 * kBlock < units; u += 4 * kBlock) {
     const uint4 x0 = sp[u], x1 = sp[u + kBlock], x2 = sp[u + 2 * kBlock], x3 = sp[u + 3 * kBlock];
     d[u] = x0;
@@ -845,6 +900,7 @@ __device__ __forceinline__ void block_copy(PQH_G uint8_t* dst, const PQH_G uint8
   const int64_t done = head + units * 16;
   if (int64_t(threadIdx.x) < n - done) dst[done + threadIdx.x] = src[done + threadIdx.x];
 }
+
 
 // Byte copy of one value (unaligned on both sides; values average tens of bytes).
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len);
@@ -1018,6 +1074,24 @@ __device__ __forceinline__ void ba_expand_tile(const DevBatch& b, const Tile& t,
   const BaDict d = is_dict ? ba_dict(b, P) : BaDict{nullptr, 0, 0};
   const int32_t* aux = C.aux + S.value_base + v0;
   const int n = int(v1 - v0), tid = threadIdx.x;
+  // DELTA_LENGTH: the tile's strings are contiguous in the page and in the output, and k_ba_scan's
+  // bases already fix their extent -- [basums[tile], basums[tile + 1]) (the chunk's byte total after
+  // its last tile) -- so the copy is issued first, its loads in flight before the lengths' load and
+  // scan instead of after them.  A tile whose lengths sum past that extent (only an erroneous page
+  // can) copies the rest after the scan.
+  int64_t pre = 0;
+  if constexpr (!kGather) {
+#if PQH_BA_COPY_FIRST
+    const int64_t gi = P.batile_base + t.k, base = b.basums[gi];
+    const int64_t nxt = gi + 1 < C.batile_base + C.batile_n ? b.basums[gi + 1] : b.chunk_bytes[P.chunk];
+    const int64_t ds = b.dstates[t.page].end_pos, rel0 = base - S.byte_base;
+    pre = nxt - base;
+    if (pre > S.val_e - ds - rel0) pre = S.val_e - ds - rel0;
+    if (pre > C.bytes_cap - base) pre = C.bytes_cap - base;
+    if (pre > 0) block_copy<PQH_BA_COPY_INFLIGHT, PQH_BA_COPY_NT>(C.bytes + base, b.payload + P.image_off + ds + rel0, pre);
+    else pre = 0;
+#endif
+  }
   int32_t a[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
@@ -1072,7 +1146,7 @@ __device__ __forceinline__ void ba_expand_tile(const DevBatch& b, const Tile& t,
     int64_t len_all = int64_t(tot);
     if (len_all > data_n - rel0) len_all = data_n - rel0;   // bytes past the page belong to the error
     if (len_all > C.bytes_cap - base) len_all = C.bytes_cap - base;
-    if (len_all > 0) block_copy(C.bytes + base, img + data_s + rel0, len_all);
+    if (len_all > pre) block_copy<PQH_BA_COPY_INFLIGHT, PQH_BA_COPY_NT>(C.bytes + base + pre, img + data_s + rel0 + pre, len_all - pre);
     return;
   } else {
   // source of value idx (nullptr: an out-of-range dictionary key, whose page fails)

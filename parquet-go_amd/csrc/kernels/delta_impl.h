@@ -1171,7 +1171,7 @@ __device__ __forceinline__ void wave_tile_add(WaveTileSum& w, int64_t* tsum, int
 // independent scans).  Returns the carry after the tile.  kSum (int32 DELTA_LENGTH lengths): each
 // lane also sums its lengths of the wave's current kBaTile tile in a register, flushed (one wave
 // reduction + one atomic) when the wave moves on to the next tile.
-template <bool kSum = false, class L>
+template <bool kSum = false, int kRows32 = 1, class L>
 __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, int lbs, int lmb, uint8_t* out,
                                                 bool is64, uint64_t carry, LenSums* ls = nullptr) {
   const int bb0 = int(v0 >> lbs);
@@ -1280,6 +1280,71 @@ __device__ __forceinline__ uint64_t expand_rows(L& T, int64_t v0, int64_t v1, in
   uint32_t c32 = uint32_t(carry);
   WaveTileSum wts{(v0 + 4 * 64 * wv) / kBaTile, 0};
   const int64_t lim_e = kSum ? (v1 < ls->lim ? v1 : ls->lim) : 0;
+  if constexpr (kRows32 > 1) {
+    // kRows32 rows per barrier: every row's LDS reads and wave scan are independent of the other
+    // rows', so they overlap; one barrier publishes the wave totals of all of them (the lengths
+    // kernel runs ~3 workgroups per CU, where each row's dependent LDS reads + scan + barrier set
+    // the time, not HBM)
+    for (int64_t g0 = v0; g0 < v1; g0 += kRows32 * 4 * kBlock, row ^= 1) {
+      uint32_t d[kRows32][4], ts[kRows32], inc[kRows32];
+#pragma unroll
+      for (int rr = 0; rr < kRows32; rr++) {
+        const int64_t p = g0 + rr * 4 * kBlock + 4 * int64_t(threadIdx.x);
+        d[rr][0] = d[rr][1] = d[rr][2] = d[rr][3] = 0;
+        if (p < v1) {
+          uint64_t md;
+          int bk;
+          staged_u32<4>(T, int32_t(p), bb0, lbs, lmb, d[rr], md, bk);
+#pragma unroll
+          for (int j = 0; j < 4; j++) d[rr][j] = p + j < v1 ? d[rr][j] + uint32_t(md) : 0;
+        }
+        ts[rr] = d[rr][0] + d[rr][1] + d[rr][2] + d[rr][3];
+      }
+#pragma unroll
+      for (int rr = 0; rr < kRows32; rr++) inc[rr] = wave_incl_scan32(ts[rr]);
+      if (lane == 63) {
+#pragma unroll
+        for (int rr = 0; rr < kRows32; rr++) T.wt32[row][rr][wv] = inc[rr];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < kRows32; rr++) {
+        const int64_t r0 = g0 + rr * 4 * kBlock;
+        if (r0 >= v1) break;
+        const int64_t p = r0 + 4 * int64_t(threadIdx.x);
+        const uint32_t w0 = T.wt32[row][rr][0], w1 = T.wt32[row][rr][1], w2 = T.wt32[row][rr][2],
+                       w3 = T.wt32[row][rr][3];
+        const uint32_t v = c32 + inc[rr] - ts[rr] + (wv > 0 ? w0 : 0) + (wv > 1 ? w1 : 0) + (wv > 2 ? w2 : 0);
+        const uint32_t o4[4] = {v, v + d[rr][0], v + d[rr][0] + d[rr][1], v + d[rr][0] + d[rr][1] + d[rr][2]};
+        if (p + 4 <= v1) {
+          __builtin_memcpy(o32 + p, o4, 16);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (p + j < v1) o32[p + j] = o4[j];
+        }
+        if constexpr (kSum) {
+          uint64_t rs;
+          if (p + 4 <= lim_e && ((o4[0] | o4[1] | o4[2] | o4[3]) >> 31) == 0) {
+            rs = uint64_t(o4[0] + o4[1]) + uint64_t(o4[2] + o4[3]);
+          } else {
+            rs = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              if (p + j >= lim_e) break;
+              if (int32_t(o4[j]) < 0) ls->neg = p + j < ls->neg ? p + j : ls->neg;
+              else rs += o4[j];
+            }
+          }
+          const int64_t wp = r0 + 4 * 64 * wv;
+          wave_tile_add(wts, ls->tsum, wp, wp + 255, p, rs);
+        }
+        c32 += w0 + w1 + w2 + w3;
+      }
+    }
+    if constexpr (kSum) flush_tile_sum(ls->tsum, wts.tacc, wts.acc);
+    return c32;
+  }
   for (int64_t r0 = v0; r0 < v1; r0 += 4 * kBlock, row ^= 1) {
     const int64_t p = r0 + 4 * int64_t(threadIdx.x);
     uint32_t d[4] = {0, 0, 0, 0};
@@ -1368,8 +1433,13 @@ struct PageTileLdsT {
   int32_t mbbit[kTileBlocks][8];  // first bit of each miniblock's data in `data`
   uint8_t mbw[kTileBlocks][8];
   uint64_t md[kTileBlocks];
-  uint64_t wtot[2][4];
-  uint64_t wtot2[2][4];
+  union {
+    struct {
+      uint64_t wtot[2][4];
+      uint64_t wtot2[2][4];
+    };
+    uint32_t wt32[2][4][4];  // 32-bit rows, kRows32 per barrier: [parity][row][wave]
+  };
   uint64_t mdb[kTileBlocks];
   int64_t a0;
   int32_t nfit;
@@ -1385,6 +1455,10 @@ using PageTileLds = PageTileLdsT<kPageStage>;
 // profiles/r05_exp/c3_probe_*.log).  A block whose bytes do not fit the stage (2048 values wider than
 // ~57 bits) ends the fused head; k_delta_walk / k_delta_page (16 KiB stage) take the rest.
 constexpr int kFusedStage = 14848;
+// DELTA_LENGTH lengths (k_delta_fused_lens, k_delta_page): 1024-value rows expanded per barrier
+#ifndef PQH_LENS_ROWS
+#define PQH_LENS_ROWS 4
+#endif
 #define PQH_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 
 __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* streams) {
@@ -1457,7 +1531,7 @@ __global__ __launch_bounds__(256) void k_delta_page(DevBatch b, const Tile* stre
     const int64_t v0 = blk0 << lbs;
     int64_t v1 = (blk0 + nfit) << lbs;
     if (v1 > vlim) v1 = vlim;
-    if (sums) carry = expand_rows<true>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
+    if (sums) carry = expand_rows<true, PQH_LENS_ROWS>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
     else carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
     blk0 += nfit;
   }
@@ -1973,7 +2047,7 @@ __device__ __forceinline__ void delta_fused_body(DevBatch b, const Tile* streams
       if (v1 > vcap) v1 = vcap;
       if (v0 < v1) {
         if constexpr (kLens) {
-          if (sums) carry = expand_rows<true>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
+          if (sums) carry = expand_rows<true, PQH_LENS_ROWS>(T, v0, v1, lbs, lmb, out, false, carry, &ls);
           else carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
         } else {
           carry = expand_rows(T, v0, v1, lbs, lmb, out, is64, carry);
