@@ -824,8 +824,9 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
 // Cooperative copy of n bytes by the workgroup: 16-byte aligned stores, each fed by one unaligned
 // 16-byte load of the source (the hardware's unaligned dwordx4 load; two aligned loads put
 // together with v_alignbyte measured slower: C5 k_ba_expand 0.53 vs 0.57 of peak).  kIn loads in
-// flight per thread.  DELTA_LENGTH copies (r06): copy first, 8 in flight, and nontemporal loads +
-// stores (kNt = 2: the strings are touched once; C5z k_ba_expand 0.65 -> 0.68 of peak, same box).
+// flight per thread.  DELTA_LENGTH copies (r06): copy first, 8 in flight.  Nontemporal loads +
+// stores (kNt = 2) split the workloads on two boxes: C5z k_ba_expand 0.61-0.65 -> 0.61-0.68 of
+// peak, C5 (the BASELINE config) 0.58-0.62 -> 0.55-0.62; kept off (PQH_BA_COPY_NT=2 builds it).
 #ifndef PQH_BA_COPY_FIRST
 #define PQH_BA_COPY_FIRST 1
 #endif
@@ -833,7 +834,7 @@ __global__ __launch_bounds__(256) void k_ba_scan(DevBatch b, const int32_t* ba_c
 #define PQH_BA_COPY_INFLIGHT 8
 #endif
 #ifndef PQH_BA_COPY_NT
-#define PQH_BA_COPY_NT 2
+#define PQH_BA_COPY_NT 0
 #endif
 typedef unsigned int v4u_a1 __attribute__((ext_vector_type(4), aligned(1)));
 template <class T>
