@@ -392,7 +392,7 @@ struct pqh_batch {
   size_t staged_bytes = 0;
   hipEvent_t ev_copied = nullptr, ev_done = nullptr;
   bool done_recorded = false;
-  hipEvent_t ev_dep[8] = {};       // fork / join points of the side branches
+  hipEvent_t ev_dep[10] = {};      // fork / join points of the side branches
   DevPage* d_pages = nullptr;
   DevChunk* d_chunks = nullptr;
   PageState* d_states = nullptr;
@@ -1384,6 +1384,8 @@ bool flat_batch(const pqh_batch* b) {
   });
 }
 
+bool ba_gather_serial();
+
 hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
   DevBatch d{b->d_payload, b->d_pages, b->d_chunks, b->d_states, b->d_ckpts, int32_t(b->pages.size()),
              int32_t(b->chunks.size()), b->d_dstates, b->d_dblocks, b->d_dsums, b->d_dcum, b->d_basums,
@@ -1600,10 +1602,28 @@ hipError_t enqueue_run(pqh_batch* b, hipStream_t s, bool prof) {
     });
     if (e == hipSuccess)
       e = timed(9, nbc, s, [&](hipStream_t st) { return launch_ba_scan(d, b->d_ba_chunks, nbc, b->d_batiles, st); });
-    if (e == hipSuccess)
+    // k_ba_expand (DELTA_LENGTH / FLBA tiles) and k_ba_gather (dictionary / PLAIN tiles) write
+    // disjoint tiles: with both present the gathers run beside the copies on the third side stream
+    // (free again: the DELTA branch rejoined above) -- C5's dictionary pages no longer wait for its
+    // DELTA_LENGTH copy (0.806 -> 0.792 ms, same box).  Not while the nesting or fused-chain branches
+    // are still open: with four streams busy the step varied (C4 1.22-1.38 vs 1.22 ms)
+    const int32_t ncp = b->ba_ncopy, ngt = b->ba_sum_off - b->ba_ncopy;
+    hipStream_t gs = side && b->ctx->side3 && ncp > 0 && ngt > 0 && !nest_open && !fuse_open && !ba_gather_serial()
+                         ? b->ctx->side3 : nullptr;
+    if (e == hipSuccess && gs) {
+      e = dep(s, gs, 8);
+      if (e == hipSuccess)
+        e = timed(10, ngt, gs, [&](hipStream_t st) {
+          return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist + ncp, 0, ngt, st);
+        });
+      if (e == hipSuccess)
+        e = timed(10, ncp, s, [&](hipStream_t st) { return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, ncp, 0, st); });
+      if (e == hipSuccess) e = dep(gs, s, 9);
+    } else if (e == hipSuccess) {
       e = timed(10, nbt, s, [&](hipStream_t st) {  // k_ba_expand + k_ba_gather
-        return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, b->ba_ncopy, b->ba_sum_off - b->ba_ncopy, st);
+        return launch_ba_expand(d, b->d_batiles, b->d_ba_xlist, ncp, ngt, st);
       });
+    }
     const int32_t nwd = (fuse ? b->ba_wlist_nf : int32_t(b->ba_wlist.size())) - b->ba_wdict;
     if (e == hipSuccess && nwd)
       e = timed(23, nwd, s, [&](hipStream_t st) {
@@ -1638,6 +1658,12 @@ int64_t dlen_end(const pqh_batch* b, size_t p) {
   const DevPage& P = b->hpages[p];
   const size_t i = P.kind == K_DBA ? b->pages.size() + p : p;
   return i < b->hdstates.size() && b->hdstates[i].end_pos > 0 ? b->hdstates[i].end_pos : b->states[p].val_s;
+}
+
+// PQH_BA_GATHER_SERIAL=1: k_ba_gather after k_ba_expand on one stream (the A/B baseline)
+bool ba_gather_serial() {
+  const char* g = getenv("PQH_BA_GATHER_SERIAL");
+  return g && g[0] == '1';
 }
 
 bool graphs_enabled() {
