@@ -1110,18 +1110,22 @@ def test_flba_mixed_chunks(pq, ctx, delta_mode):
         ctx.free(dptr)
 
 
-@pytest.mark.parametrize("mode", ["graph", "direct", "one_stream", "profiled"])
+@pytest.mark.parametrize("mode", ["graph", "direct", "one_stream", "profiled", "gather_serial"])
 def test_launch_modes(pq, mode, monkeypatch):
     """Every launch mode decodes the same bytes: graph replay and direct launches with the side-stream
     branches (PLAIN byte-array chain beside k_scan / k_expand, nesting beside the byte-array copies),
     everything on one stream (PQH_FORK=0), and profiled runs (per-kernel events, one stream).  The
     flat file joins the chain branch before k_expand (byte-array dictionary keys need the dictionary
-    sizes); the nested one joins it before the byte sums."""
+    sizes); the nested one joins it before the byte sums.  The C5-shaped file (dictionary pages, then
+    DELTA_LENGTH fallback pages, no other branch open) runs k_ba_gather beside k_ba_expand on the
+    third side stream in the graph / direct modes and after it with PQH_BA_GATHER_SERIAL=1."""
     W = pq.writer
     if mode == "direct":
         monkeypatch.setenv("PQH_GRAPH", "0")
     if mode == "one_stream":
         monkeypatch.setenv("PQH_FORK", "0")
+    if mode == "gather_serial":
+        monkeypatch.setenv("PQH_BA_GATHER_SERIAL", "1")
     c = pq.native.Context(0, profile=(mode == "profiled"))
     rng = np.random.default_rng(7)
     n = 30000
@@ -1131,7 +1135,7 @@ def test_launch_modes(pq, mode, monkeypatch):
                    ("p", W.Column(W.BYTE_ARRAY, plain, use_dict=False), W.REQUIRED),
                    ("i", W.Column(W.INT64, rng.integers(-2**40, 2**40, n), use_dict=False), W.REQUIRED)],
                   12000, max_page_size=48 * 1024)
-    for data in (flat, pq.datasets.c4(rows=40_000, row_groups=2)):
+    for data in (flat, pq.datasets.c4(rows=40_000, row_groups=2), pq.datasets.c5(rows=400_000, row_groups=2)):
         for _ in range(2):  # a re-run of the same batch (graph replay) too
             checked, skipped = _run_file(pq, c, data)
             assert checked > 0 and skipped == 0
